@@ -1,0 +1,192 @@
+"""Driver benchmark: node-wide videos/s + p50/p99 latency, R(2+1)D-34.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Metric (BASELINE.json): "videos/sec (whole node) + p50/p99 end-to-end
+latency, R(2+1)D-34 8-frame clips". Each rank is one replicated RnB serving
+pipeline on its own MI355X (the r2p1d-whole / aggressive configs: loader +
+whole R(2+1)D-34 per GPU, replication across GPUs): synthetic clips decoded
+on the GPU (clip counts drawn from the reference sampler: 1 clip w.p. 10/11,
+15 clips w.p. 1/11), random-init weights, bf16 compute with fp32
+accumulation, eval-mode BN folded.
+
+One step = ``--videos-per-step`` videos per GPU arriving at once (weak
+scaling), served in batches of ``--video-batch`` videos by ``--replicas``
+concurrent streams (R and B of RnB). Every video goes through the full
+decode -> 72 conv kernels -> head -> per-video argmax chain; the argmax of
+every video is copied back to the host inside the timed region. Latency of a
+video = completion of its batch - arrival (step start).
+
+The reference's only published number is 11.30 videos/s (R(2+1)D-18, fp32,
+one older NVIDIA GPU, load-bound at 11.1 req/s offered).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_VIDEOS_PER_S = 11.30
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--depth", type=int, default=34)
+    ap.add_argument("--videos-per-step", type=int, default=128,
+                    help="videos arriving per GPU per step")
+    ap.add_argument("--video-batch", type=int, default=32,
+                    help="videos per model invocation (RnB batching)")
+    ap.add_argument("--replicas", type=int, default=2,
+                    help="concurrent serving streams per GPU (RnB replication)")
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--no-autotune", action="store_true")
+    ap.add_argument("--json-out", type=str, default=None)
+    return ap.parse_args(argv)
+
+
+def make_workload(n_videos: int, seed: int):
+    """Per-video clip start frames from the reference sampler distribution."""
+    from rnb_amd.models.r2p1d.sampler import R2P1DSampler
+    import random
+    rng = random.Random(seed)
+    sampler = R2P1DSampler(clip_length=8, num_clips_population=(1, 15),
+                           num_clips_weights=(10, 1), seed=seed + 1)
+    videos = []
+    for i in range(n_videos):
+        length = rng.randint(250, 300)          # Kinetics 10-s clips at 25-30 fps
+        videos.append((i, sampler.sample(length)))
+    return videos
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    import torch
+    import torch.distributed as dist
+    import numpy as np
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print("bench.py: --gpus %d needs torch.distributed.run with %d processes"
+                  % (args.gpus, args.gpus), file=sys.stderr)
+            return 2
+    device = torch.device("cuda:%d" % local_rank)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+
+    from rnb_amd.models.r2p1d.fused import FusedR2P1D
+    from rnb_amd.timecard import percentile_stats
+
+    vps, vb = args.videos_per_step, args.video_batch
+    total_steps = args.warmup + args.steps
+    workload = make_workload(vps * total_steps, args.seed + 7919 * rank)
+    batches = [workload[i:i + vb] for i in range(0, len(workload), vb)]
+    max_clips = max(sum(len(s) for _, s in b) for b in batches)
+    eng = FusedR2P1D(device, depth=args.depth, replicas=args.replicas,
+                     max_clips=max(max_clips, 1), max_videos=vb,
+                     autotune=not args.no_autotune, seed=0)
+    t_prep = time.time()
+    eng.prepare([sum(len(s) for _, s in b) for b in batches])
+    prep_s = time.time() - t_prep
+    batches_per_step = (vps + vb - 1) // vb
+
+    def run_step(step):
+        start = torch.cuda.Event(enable_timing=True)
+        start.record(torch.cuda.current_stream(device))
+        for r in eng.replicas:
+            r.stream.wait_stream(torch.cuda.current_stream(device))
+        pending = []
+        bs = batches[step * batches_per_step:(step + 1) * batches_per_step]
+        for i, b in enumerate(bs):
+            rep = eng.replicas[i % len(eng.replicas)]
+            ev_done, out, nvid = rep.submit([(vid, st) for vid, st in b])
+            tev = torch.cuda.Event(enable_timing=True)
+            tev.record(rep.stream)
+            pending.append((tev, out, nvid))
+        for r in eng.replicas:
+            torch.cuda.current_stream(device).wait_stream(r.stream)
+        return start, pending
+
+    for s in range(args.warmup):
+        run_step(s)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    lat_ms, preds = [], 0
+    step_records = []
+    for s in range(args.warmup, total_steps):
+        step_records.append(run_step(s))
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    elapsed = t1 - t0
+    for start, pending in step_records:
+        for tev, out, nvid in pending:
+            t = start.elapsed_time(tev)
+            lat_ms.extend([t] * nvid)
+            preds += int((out >= 0).sum())
+    n_videos = args.steps * vps
+    clips = sum(len(st) for b in batches[args.warmup * batches_per_step:]
+                for _, st in b)
+    stats = percentile_stats(np.asarray(lat_ms) / 1e3)
+    if world > 1:
+        t = torch.tensor([elapsed, stats["p50_ms"], stats["p99_ms"]], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, p50, p99 = t.tolist()
+        c = torch.tensor([float(clips), float(preds)], device=device)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        clips_all, preds_all = c.tolist()
+    else:
+        p50, p99 = stats["p50_ms"], stats["p99_ms"]
+        clips_all, preds_all = float(clips), float(preds)
+    total_videos = n_videos * world
+    value = total_videos / elapsed
+    flops = eng.flops_per_clip() * clips_all / elapsed
+    if rank == 0:
+        rec = {
+            "metric": "videos/sec (whole node) + p50/p99 end-to-end latency, "
+                      "R(2+1)D-34 8-frame clips",
+            "value": round(value, 2), "unit": "videos/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_VIDEOS_PER_S, 2),
+            "dtype": "bf16", "data": "synthetic clips (GPU-decoded), random-init weights",
+            "p50_ms": round(p50, 3), "p99_ms": round(p99, 3),
+            "clips_per_s": round(clips_all / elapsed, 1),
+            "effective_tflops": round(flops / 1e12, 1),
+            "videos_ok": int(preds_all),
+            "config": {"model": "R(2+1)D-%d" % args.depth,
+                       "global_batch": vps * world, "seq_len": 8,
+                       "parallelism": "dp%d (replicated runners)" % world,
+                       "pipeline": "r2p1d-whole (loader+model per GPU, fused)",
+                       "video_batch": vb, "replicas_per_gpu": args.replicas,
+                       "clip": "8x112x112", "clips_dist": "1 w.p. 10/11, 15 w.p. 1/11",
+                       "prepare_s": round(prep_s, 1)},
+        }
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

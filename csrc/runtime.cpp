@@ -1,0 +1,108 @@
+// Native runtime services for the rnb_amd engine (host code, HIP runtime API).
+//
+//  * HIP IPC export/import of producer-owned slot buffers and events -- the
+//    MI355X replacement for the reference's CUDA-IPC shared TensorEvents
+//    (reference: control.py:19-46, 151-157).
+//  * async / peer copies (hipMemcpyAsync with hipMemcpyDefault routes a
+//    cross-GPU copy over xGMI through the SDMA engines).
+//  * a small device allocator wrapper so slot memory is a dedicated
+//    allocation (IPC handles then map exactly one slot).
+//
+// Exposed with a C ABI and loaded through ctypes (rnb_amd/ops/native.py).
+#include <hip/hip_runtime.h>
+#include <cstring>
+#include <cstdint>
+
+extern "C" {
+
+const char* rnb_error_string(int err) { return hipGetErrorString((hipError_t)err); }
+
+int rnb_set_device(int dev) { return (int)hipSetDevice(dev); }
+
+int rnb_get_device(int* dev) { return (int)hipGetDevice(dev); }
+
+int rnb_device_count(int* n) { return (int)hipGetDeviceCount(n); }
+
+int rnb_malloc(void** ptr, size_t bytes) { return (int)hipMalloc(ptr, bytes); }
+
+int rnb_free(void* ptr) { return (int)hipFree(ptr); }
+
+int rnb_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+int rnb_ipc_get_mem_handle(void* ptr, void* out_handle) {
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, ptr);
+  if (e != hipSuccess) return (int)e;
+  std::memcpy(out_handle, &h, sizeof(h));
+  return 0;
+}
+
+int rnb_ipc_open_mem_handle(const void* handle, void** ptr) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+int rnb_ipc_close_mem_handle(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+
+// interprocess events: created with hipEventInterprocess | hipEventDisableTiming
+int rnb_ipc_event_create(void** ev) {
+  hipEvent_t e;
+  hipError_t r = hipEventCreateWithFlags(&e, hipEventInterprocess | hipEventDisableTiming);
+  *ev = (void*)e;
+  return (int)r;
+}
+
+int rnb_ipc_event_handle_size() { return (int)sizeof(hipIpcEventHandle_t); }
+
+int rnb_ipc_get_event_handle(void* ev, void* out_handle) {
+  hipIpcEventHandle_t h;
+  hipError_t e = hipIpcGetEventHandle(&h, (hipEvent_t)ev);
+  if (e != hipSuccess) return (int)e;
+  std::memcpy(out_handle, &h, sizeof(h));
+  return 0;
+}
+
+int rnb_ipc_open_event_handle(const void* handle, void** ev) {
+  hipIpcEventHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  hipEvent_t e;
+  hipError_t r = hipIpcOpenEventHandle(&e, h);
+  *ev = (void*)e;
+  return (int)r;
+}
+
+int rnb_event_record(void* ev, void* stream) {
+  return (int)hipEventRecord((hipEvent_t)ev, (hipStream_t)stream);
+}
+
+int rnb_stream_wait_event(void* stream, void* ev) {
+  return (int)hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0);
+}
+
+int rnb_event_synchronize(void* ev) { return (int)hipEventSynchronize((hipEvent_t)ev); }
+
+int rnb_event_destroy(void* ev) { return (int)hipEventDestroy((hipEvent_t)ev); }
+
+int rnb_memcpy_async(void* dst, const void* src, size_t bytes, void* stream) {
+  return (int)hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, (hipStream_t)stream);
+}
+
+int rnb_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  return (int)hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+}
+
+int rnb_memcpy_peer_async(void* dst, int dst_dev, const void* src, int src_dev, size_t bytes,
+                          void* stream) {
+  return (int)hipMemcpyPeerAsync(dst, dst_dev, src, src_dev, bytes, (hipStream_t)stream);
+}
+
+int rnb_stream_synchronize(void* stream) { return (int)hipStreamSynchronize((hipStream_t)stream); }
+
+int rnb_can_access_peer(int dev, int peer, int* out) {
+  return (int)hipDeviceCanAccessPeer(out, dev, peer);
+}
+
+int rnb_mem_get_info(size_t* free_b, size_t* total_b) { return (int)hipMemGetInfo(free_b, total_b); }
+
+}  // extern "C"

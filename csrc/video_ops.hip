@@ -1,0 +1,204 @@
+// Video-side and head kernels for the R(2+1)D pipeline on CDNA4.
+//
+//  * rnb_clipgen_u8     synthetic "decoder surface": 8-frame clips of
+//                        HxWx3 uint8 pixels, deterministic per (video, frame)
+//                        -- stands in for the rocDecode/VCN output (SURVEY.md
+//                        K30; no decoder or dataset on the target machines).
+//  * rnb_preprocess      uint8 NFHWC3 -> normalised bf16 NDHWC8 (channels 3..7
+//                        zero), the fused form of the reference's
+//                        .float().permute() + slot copy.
+//  * rnb_head            AdaptiveAvgPool3d(1) + Linear(512 -> classes) fused
+//                        into one kernel per clip.
+//  * rnb_video_reduce    per-video sum of clip logits + argmax, the GPU form
+//                        of R2P1DAggregator's reduction.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+static __device__ __forceinline__ uint32_t pixel_hash(uint32_t vid, uint32_t frame,
+                                                      uint32_t pix, uint32_t c) {
+  uint32_t h = vid * 0x9E3779B1u + frame * 0x85EBCA77u + pix * 0xC2B2AE3Du + c * 0x27D4EB2Fu;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return h >> 24;
+}
+
+// out[clip][f][y][x][c], 16 bytes per thread
+__global__ void clipgen_u8_kernel(uint8_t* __restrict__ out, const int* __restrict__ vids,
+                                  const int* __restrict__ starts, int nclips, int F, int H,
+                                  int W) {
+  const long long clip_bytes = (long long)F * H * W * 3;
+  const long long total = clip_bytes * nclips;
+  const long long i16 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (i16 >= total) return;
+  uint32_t words[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const long long idx = i16 + w * 4 + b;
+      uint32_t v = 0;
+      if (idx < total) {
+        const int clip = (int)(idx / clip_bytes);
+        const long long r = idx - (long long)clip * clip_bytes;
+        const int c = (int)(r % 3);
+        const long long pixf = r / 3;
+        const int pix = (int)(pixf % ((long long)H * W));
+        const int f = (int)(pixf / ((long long)H * W));
+        v = pixel_hash((uint32_t)vids[clip], (uint32_t)(starts[clip] + f), (uint32_t)pix,
+                       (uint32_t)c);
+      }
+      word |= v << (8 * b);
+    }
+    words[w] = word;
+  }
+  if (i16 + 16 <= total) {
+    *(uint4*)(out + i16) = make_uint4(words[0], words[1], words[2], words[3]);
+  } else {
+    for (int b = 0; b < 16 && i16 + b < total; ++b)
+      out[i16 + b] = (uint8_t)(words[b >> 2] >> (8 * (b & 3)));
+  }
+}
+
+struct NormParams {
+  float scale[3];   // 1 / (255 * std)
+  float shift[3];   // -mean / std
+};
+
+static __device__ __forceinline__ uint32_t f2bf_bits(float f) {
+  // round-to-nearest-even (inputs are finite)
+  uint32_t u = __float_as_uint(f);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+
+// one thread per pixel: 3 bytes in, 8 bf16 (16 B) out
+__global__ void preprocess_kernel(const uint8_t* __restrict__ in, uint16_t* __restrict__ out,
+                                  long long npix, NormParams np) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix) return;
+  const uint8_t* px = in + i * 3;
+  uint32_t r = f2bf_bits(px[0] * np.scale[0] + np.shift[0]);
+  uint32_t g = f2bf_bits(px[1] * np.scale[1] + np.shift[1]);
+  uint32_t b = f2bf_bits(px[2] * np.scale[2] + np.shift[2]);
+  *(uint4*)(out + i * 8) = make_uint4(r | (g << 16), b, 0u, 0u);
+}
+
+// x: [N][S][Cs] bf16 (NDHWC, S = T*H*W), wgt: [ncls][C] f32, out: [N][ncls] f32.
+// One block per clip: 256 threads pool the clip into LDS, then each wave
+// computes a strided subset of the classes with a 64-lane dot + shuffle reduce.
+__global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ x,
+                                                   const float* __restrict__ wgt,
+                                                   const float* __restrict__ bias,
+                                                   float* __restrict__ out, int S, int C,
+                                                   int Cs, int ncls) {
+  extern __shared__ float pooled[];
+  const int n = blockIdx.x;
+  const uint16_t* xc = x + (size_t)n * S * Cs;
+  const float inv = 1.0f / (float)S;
+  for (int c = threadIdx.x * 2; c < C; c += 512) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int s = 0; s < S; ++s) {
+      const uint32_t v = *(const uint32_t*)(xc + (size_t)s * Cs + c);
+      s0 += __uint_as_float(v << 16);
+      s1 += __uint_as_float(v & 0xFFFF0000u);
+    }
+    pooled[c] = s0 * inv;
+    if (c + 1 < C) pooled[c + 1] = s1 * inv;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  for (int o = wave; o < ncls; o += 4) {
+    const float* wr = wgt + (size_t)o * C;
+    float acc = 0.f;
+    for (int c = lane; c < C; c += 64) acc += wr[c] * pooled[c];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+    if (lane == 0) out[(size_t)n * ncls + o] = acc + bias[o];
+  }
+}
+
+// logits: [nclips][ncls]; offsets: [nvid+1] clip ranges; sums: [nvid][ncls]; arg: [nvid]
+__global__ __launch_bounds__(256) void video_reduce_kernel(const float* __restrict__ logits,
+                                                           const int* __restrict__ offsets,
+                                                           float* __restrict__ sums,
+                                                           int* __restrict__ argmax, int ncls) {
+  __shared__ float bv[256];
+  __shared__ int bi[256];
+  const int v = blockIdx.x;
+  const int c0 = offsets[v], c1 = offsets[v + 1];
+  float best = -INFINITY;
+  int besti = 0x7FFFFFFF;
+  for (int o = threadIdx.x; o < ncls; o += 256) {
+    float s = 0.f;
+    for (int c = c0; c < c1; ++c) s += logits[(size_t)c * ncls + o];
+    if (sums) sums[(size_t)v * ncls + o] = s;
+    if (s > best || (s == best && o < besti)) { best = s; besti = o; }
+  }
+  bv[threadIdx.x] = best;
+  bi[threadIdx.x] = besti;
+  __syncthreads();
+  for (int step = 128; step > 0; step >>= 1) {
+    if (threadIdx.x < step) {
+      const float ov = bv[threadIdx.x + step];
+      const int oi = bi[threadIdx.x + step];
+      if (ov > bv[threadIdx.x] || (ov == bv[threadIdx.x] && oi < bi[threadIdx.x])) {
+        bv[threadIdx.x] = ov;
+        bi[threadIdx.x] = oi;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) argmax[v] = (c1 > c0) ? bi[0] : -1;
+}
+
+extern "C" {
+
+int rnb_clipgen_u8(void* out, const int* vids, const int* starts, int nclips, int F, int H,
+                   int W, hipStream_t stream) {
+  if (nclips <= 0) return 0;
+  const long long total = (long long)nclips * F * H * W * 3;
+  const long long threads = (total + 15) / 16;
+  const int block = 256;
+  const long long grid = (threads + block - 1) / block;
+  hipLaunchKernelGGL(clipgen_u8_kernel, dim3((unsigned)grid), dim3(block), 0, stream,
+                     (uint8_t*)out, vids, starts, nclips, F, H, W);
+  return (int)hipGetLastError();
+}
+
+int rnb_preprocess(const void* in, void* out, long long npix, const float* mean,
+                   const float* stdv, hipStream_t stream) {
+  if (npix <= 0) return 0;
+  NormParams np;
+  for (int c = 0; c < 3; ++c) {
+    np.scale[c] = 1.0f / (255.0f * stdv[c]);
+    np.shift[c] = -mean[c] / stdv[c];
+  }
+  const int block = 256;
+  const long long grid = (npix + block - 1) / block;
+  hipLaunchKernelGGL(preprocess_kernel, dim3((unsigned)grid), dim3(block), 0, stream,
+                     (const uint8_t*)in, (uint16_t*)out, npix, np);
+  return (int)hipGetLastError();
+}
+
+int rnb_head(const void* x, const float* w, const float* b, float* out, int N, int S, int C,
+             int Cs, int ncls, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (C % 2 != 0 || Cs % 2 != 0 || Cs < C) return -2;
+  hipLaunchKernelGGL(head_kernel, dim3(N), dim3(256), C * sizeof(float), stream,
+                     (const uint16_t*)x, w, b, out, S, C, Cs, ncls);
+  return (int)hipGetLastError();
+}
+
+int rnb_video_reduce(const float* logits, const int* offsets, float* sums, int* argmax,
+                     int nvid, int ncls, hipStream_t stream) {
+  if (nvid <= 0) return 0;
+  hipLaunchKernelGGL(video_reduce_kernel, dim3(nvid), dim3(256), 0, stream, logits, offsets,
+                     sums, argmax, ncls);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,74 @@
+"""Cross-request batching stage (reference: batcher.py:5-34).
+
+Stacks ``batch`` incoming tensors along dim 0 and emits them with a
+``TimeCardList``; ``batch <= 1`` passes items through. rnb_amd additions:
+
+* ``max_rows`` (default 15, the slot capacity): if the next item would push
+  the stack past the capacity of the output slot, the current stack is
+  emitted first and the item starts the next batch (the reference would
+  overflow its 15-row slot when batching multi-clip videos);
+* ``max_wait_ms``: a partial batch older than this is flushed at the next
+  arrival (the reference's batcher has no flush at all).
+"""
+import time
+
+import torch
+
+from .runner_model import RunnerModel
+from .timecard import TimeCardList
+
+
+class Batcher(RunnerModel):
+    def __init__(self, device, batch=1, max_rows=15, max_wait_ms=None, **unused):
+        super().__init__(device)
+        self.batch = int(batch)
+        self.max_rows = int(max_rows)
+        self.max_wait_ms = max_wait_ms
+        self.stacked_tensors = []
+        self.stacked_time_cards = []
+        self.first_ts = None
+
+    @staticmethod
+    def output_shape():
+        return ((15, 8, 112, 112, 8),)
+
+    @classmethod
+    def output_shape_for(cls, max_rows=15, **kwargs):
+        return ((int(max_rows), 8, 112, 112, 8),)
+
+    @classmethod
+    def output_dtypes_for(cls, **kwargs):
+        return (torch.bfloat16,)
+
+    def input_shape(self):
+        return ((self.max_rows, 8, 112, 112, 8),)
+
+    def _rows(self):
+        return sum(t.shape[0] for t in self.stacked_tensors)
+
+    def _emit(self):
+        batch = torch.cat(self.stacked_tensors, dim=0)
+        cards = TimeCardList(self.stacked_time_cards)
+        self.stacked_tensors, self.stacked_time_cards = [], []
+        self.first_ts = None
+        return (batch,), None, cards
+
+    def __call__(self, tensors, non_tensors, time_card):
+        if self.batch <= 1:
+            return tensors, non_tensors, time_card
+        tensor = tensors[0]
+        out = None
+        if self.stacked_tensors and self._rows() + tensor.shape[0] > self.max_rows:
+            out = self._emit()
+        # tensors may be views of a reused input placeholder: keep a copy
+        self.stacked_tensors.append(tensor.clone())
+        self.stacked_time_cards.append(time_card)
+        if self.first_ts is None:
+            self.first_ts = time.time()
+        if out is not None:
+            return out
+        expired = (self.max_wait_ms is not None and
+                   (time.time() - self.first_ts) * 1000.0 >= self.max_wait_ms)
+        if len(self.stacked_tensors) >= self.batch or expired:
+            return self._emit()
+        return None, None, None

@@ -1,0 +1,89 @@
+"""In-tree build of the native HIP/C++ libraries for gfx950.
+
+``python -m rnb_amd.build [--force] [-j N]`` compiles every library below with
+``hipcc --offload-arch=gfx950`` into ``rnb_amd/_native/``. The libraries are
+plain C-ABI shared objects loaded with ctypes (``rnb_amd/ops/native.py``), so
+they do not depend on the PyTorch C++ ABI and build in seconds. A library is
+rebuilt only when one of its sources (or this file) is newer than the .so.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+OUT = os.path.join(ROOT, "rnb_amd", "_native")
+ARCH = os.environ.get("RNB_OFFLOAD_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+# name -> (sources, extra flags, extra link libs)
+LIBRARIES = {
+    "librnb_kernels.so": (["conv_igemm.hip", "video_ops.hip"], [], []),
+    "librnb_runtime.so": (["runtime.cpp"], [], []),
+    "librnb_tracer.so": (["tracer.cpp"], [], ["-L%s/lib" % ROCM, "-lroctracer64",
+                                               "-Wl,-rpath,%s/lib" % ROCM]),
+}
+
+
+def hipcc() -> str:
+    exe = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+    if not os.path.exists(exe):
+        raise RuntimeError("hipcc not found (ROCM_PATH=%s)" % ROCM)
+    return exe
+
+
+def _stale(target: str, sources) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    deps = list(sources) + [os.path.abspath(__file__)]
+    return any(os.path.getmtime(s) > t for s in deps)
+
+
+def build_one(name: str, force: bool = False, verbose: bool = False) -> str:
+    srcs, flags, libs = LIBRARIES[name]
+    srcs = [os.path.join(CSRC, s) for s in srcs]
+    missing = [s for s in srcs if not os.path.exists(s)]
+    if missing:
+        raise FileNotFoundError("missing sources for %s: %s" % (name, missing))
+    target = os.path.join(OUT, name)
+    if not force and not _stale(target, srcs):
+        return target
+    os.makedirs(OUT, exist_ok=True)
+    tmp = target + ".tmp.%d" % os.getpid()
+    cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC",
+           "-shared", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+           "-Wno-unused-result"] + flags + srcs + ["-o", tmp] + libs
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("building %s failed:\n%s\n%s" % (name, res.stdout, res.stderr))
+    os.replace(tmp, target)
+    return target
+
+
+def build_all(force: bool = False, jobs: int = 4, verbose: bool = False):
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        futs = {n: ex.submit(build_one, n, force, verbose) for n in LIBRARIES}
+        return {n: f.result() for n, f in futs.items()}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=4)
+    ap.add_argument("-v", "--verbose", action="store_true")
+    args = ap.parse_args(argv)
+    for name, path in build_all(args.force, args.jobs, args.verbose).items():
+        print("built %-22s -> %s" % (name, os.path.relpath(path, ROOT)))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,172 @@
+"""Control plane: termination FSM, signals, queue/slot wiring.
+
+Reference: control.py:1-209. The queue wiring (one filename queue, one output
+queue per distinct out-queue index per step, consumers reading the slot rings
+of every producer group that feeds their in-queue) and the segment-shape rule
+are behaviourally identical. What differs, deliberately:
+
+* Slot rings are ``rnb_amd.parallel.transport`` objects instead of bare CUDA
+  tensors allocated by the main process. GPU rings are allocated by the
+  *producer* (HIP IPC export, ``parallel/transport.py``), so the main process
+  never creates a context on every GPU; CPU consumers
+  or CPU producers get host shared-memory rings (the reference crashed on a
+  CPU producer: ``cuda:-1`` at control.py:153).
+* Slot sizes come from ``output_shape_for(**step_kwargs)`` so a partial
+  R(2+1)D runner advertises its real boundary shape (fixes TODO #69).
+* ``TerminationFlag`` gains ``CHILD_FAILED`` and ``BARRIER_TIMEOUT``, set by
+  the launcher's watchdog.
+"""
+from __future__ import annotations
+
+import math
+from collections import namedtuple
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from .config import PipelineSpec, CPU_DEVICE
+from .utils.class_utils import load_class
+
+DEFAULT_NUM_SHARED_TENSORS = 10
+NUM_EXIT_MARKERS = 10
+
+
+class TerminationFlag:
+    """Job termination states (control.py:11-16 plus failure states)."""
+    UNSET = -1
+    TARGET_NUM_VIDEOS_REACHED = 0
+    FILENAME_QUEUE_FULL = 1
+    FRAME_QUEUE_FULL = 2
+    CHILD_FAILED = 3
+    BARRIER_TIMEOUT = 4
+
+    NAMES = {-1: "UNSET", 0: "TARGET_NUM_VIDEOS_REACHED",
+             1: "FILENAME_QUEUE_FULL", 2: "FRAME_QUEUE_FULL",
+             3: "CHILD_FAILED", 4: "BARRIER_TIMEOUT"}
+
+
+# (group_idx, instance_idx, tensor_idx) like control.py:209; ``ring`` carries
+# the producer ring's import descriptor (HIP IPC handles) for GPU transports.
+Signal = namedtuple("Signal", ["group_idx", "instance_idx", "tensor_idx", "ring"],
+                    defaults=(None,))
+
+
+def segment_bounds(batch: int, num_segments: int, segment_idx: int) -> Tuple[int, int]:
+    """Row range of one segment (runner.py:149-151): remainders go first."""
+    q, r = divmod(batch, num_segments)
+    start = q * segment_idx + min(segment_idx, r)
+    end = q * (segment_idx + 1) + min(segment_idx + 1, r)
+    return start, end
+
+
+def get_segmented_shapes(shapes, num_segments: int):
+    """Slot shapes when a step splits outputs into segments (control.py:49-69)."""
+    if shapes is None or num_segments == 1:
+        return shapes
+    new_shapes = []
+    for shape in shapes:
+        batch = shape[0]
+        if num_segments > batch:
+            raise ValueError("num_segments %d must be <= tensor batch size %d"
+                             % (num_segments, batch))
+        new_shapes.append((math.ceil(batch / num_segments), *shape[1:]))
+    return tuple(new_shapes)
+
+
+def step_output_spec(step, group=None):
+    """(shapes, dtypes) that a step's producers write into their slots."""
+    import torch
+    cls = load_class(step.model)
+    kwargs = dict(group.kwargs if group is not None else step.kwargs)
+    shapes = cls.output_shape_for(**kwargs)
+    dtypes = cls.output_dtypes_for(**kwargs)
+    if shapes is None:
+        return None, None
+    shapes = tuple(tuple(s) for s in shapes)
+    if step.slot_dtype is not None:
+        dtypes = tuple(getattr(torch, step.slot_dtype) for _ in shapes)
+    if dtypes is None:
+        dtypes = tuple(torch.float32 for _ in shapes)
+    return get_segmented_shapes(shapes, step.num_segments), tuple(dtypes)
+
+
+class SharedQueuesAndTensors:
+    """Creates all queues and slot-ring control blocks of a pipeline.
+
+    Args:
+      spec: validated ``PipelineSpec``.
+      queue_class: queue factory, e.g. ``ctx.Queue``.
+      queue_size: max items per queue.
+      ctx: multiprocessing context providing Event/Array (spawn context).
+    """
+
+    def __init__(self, spec: PipelineSpec, queue_class, queue_size: int, ctx):
+        from .parallel.transport import make_ring
+        self.spec = spec
+        self.filename_queue = queue_class(queue_size)
+        self.num_steps = len(spec.steps)
+        self.queue_indices: List[List[Tuple[Optional[int], Optional[List[int]]]]] = []
+        self.queues: List[Dict[int, object]] = []
+        self.rings: List[List[List[object]]] = []
+        for step_idx, step in enumerate(spec.steps):
+            final = step_idx == self.num_steps - 1
+            step_qi, step_qs, step_rings = [], {}, []
+            for group_idx, group in enumerate(step.groups):
+                step_qi.append((group.in_queue, group.out_queues))
+                if final:
+                    continue
+                for q in group.out_queues:
+                    if q not in step_qs:
+                        step_qs[q] = queue_class(queue_size)
+                shapes, dtypes = step_output_spec(step, group)
+                consumers_cpu = self._consumers_use_cpu(step_idx, group)
+                group_rings = []
+                for instance_idx, gpu in enumerate(group.gpus):
+                    if shapes is None:
+                        group_rings.append(None)
+                        continue
+                    group_rings.append(make_ring(
+                        ctx=ctx, shapes=shapes, dtypes=dtypes,
+                        num_slots=step.num_shared_tensors,
+                        producer_gpu=gpu, consumers_cpu=consumers_cpu,
+                        transport=group.transport,
+                        name="s%dg%di%d" % (step_idx, group_idx, instance_idx)))
+                step_rings.append(group_rings)
+            self.queue_indices.append(step_qi)
+            self.queues.append(step_qs)
+            self.rings.append(step_rings)
+
+    def _consumers_use_cpu(self, step_idx: int, group) -> bool:
+        nxt = self.spec.steps[step_idx + 1]
+        outs = set(group.out_queues)
+        for g in nxt.groups:
+            if g.in_queue in outs and any(x == CPU_DEVICE for x in g.gpus):
+                return True
+        return False
+
+    def get_filename_queue(self):
+        return self.filename_queue
+
+    def get_queues(self, step_idx: int, group_idx: int):
+        in_idx, out_idx = self.queue_indices[step_idx][group_idx]
+        in_queue = self.filename_queue if step_idx == 0 \
+            else self.queues[step_idx - 1][in_idx]
+        out_queues = None if step_idx == self.num_steps - 1 \
+            else [self.queues[step_idx][q] for q in out_idx]
+        return in_queue, out_queues
+
+    def get_tensors(self, step_idx: int, group_idx: int, instance_idx: int):
+        """(input rings by producer group, this instance's output ring)."""
+        in_idx, _ = self.queue_indices[step_idx][group_idx]
+        if step_idx == 0:
+            in_rings = None
+        else:
+            in_rings = {}
+            for pg, (_, pouts) in enumerate(self.queue_indices[step_idx - 1]):
+                if in_idx in pouts:
+                    rings = self.rings[step_idx - 1][pg]
+                    if any(r is not None for r in rings):
+                        in_rings[pg] = rings
+            if not in_rings:
+                in_rings = None
+        out_ring = None if step_idx == self.num_steps - 1 \
+            else self.rings[step_idx][group_idx][instance_idx]
+        return in_rings, out_ring

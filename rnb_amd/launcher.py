@@ -1,0 +1,286 @@
+"""``benchmark.py`` CLI: validate config, spawn client + runners, time, report.
+
+Same flags and flow as reference benchmark.py:127-305 (``-mi -b -v -qs -c
+--check``; spawn start method; barriers around the timed window; log-meta and
+a copy of the config in ``logs/<job_id>/``). Additions:
+
+* a watchdog thread aborts the barriers and raises ``CHILD_FAILED`` as soon as
+  any child exits abnormally (the reference hangs forever on ``fin_bar``);
+* ``--barrier-timeout`` bounds every barrier wait;
+* the final-step runners send their TimeCard summaries back, so the launcher
+  prints node-wide videos/s and p50/p90/p99 end-to-end latency, and
+  ``--json-out`` writes them as one JSON record;
+* ``-b/--batch_size`` is applied as the default ``batch`` of ``Batcher``
+  steps that do not set one (in the reference it only named the job).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import threading
+import time
+from datetime import datetime
+
+from .utils.arg_utils import nonnegative_int, positive_int
+
+RESERVED_CHILD_EXIT_GRACE_S = 30.0
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="RnB video-inference benchmark (MI355X)")
+    p.add_argument("-mi", "--mean_interval_ms", type=nonnegative_int, default=3,
+                   help="Mean event interval time (Poisson), milliseconds; 0 = bulk")
+    p.add_argument("-b", "--batch_size", type=positive_int, default=1,
+                   help="Default 'batch' for Batcher steps that do not set one")
+    p.add_argument("-v", "--videos", type=positive_int, default=2000,
+                   help="Total number of videos to run")
+    p.add_argument("-qs", "--queue_size", type=positive_int, default=50000,
+                   help="Maximum queue size for inter-process queues")
+    p.add_argument("-c", "--config_file_path", type=str,
+                   default=os.path.join(os.path.dirname(os.path.dirname(
+                       os.path.abspath(__file__))), "configs", "r2p1d-whole.json"),
+                   help="File path of the pipeline configuration file")
+    p.add_argument("--check", action="store_true",
+                   help="Quick check if all imports are working correctly")
+    p.add_argument("--barrier-timeout", type=float, default=None,
+                   help="Seconds before a barrier wait gives up (default: none)")
+    p.add_argument("--seed", type=int, default=None, help="Client arrival seed")
+    p.add_argument("--json-out", type=str, default=None,
+                   help="Write the run's metrics as JSON to this path")
+    p.add_argument("--log-root", type=str, default=None, help="Log directory root")
+    return p
+
+
+def _apply_batch_default(spec, batch_size: int) -> None:
+    for step in spec.steps:
+        if step.model.endswith("Batcher"):
+            for g in step.groups:
+                g.kwargs.setdefault("batch", batch_size)
+
+
+class Watchdog(threading.Thread):
+    """Aborts the job when a child process dies abnormally."""
+
+    def __init__(self, procs, flag, barriers):
+        super().__init__(daemon=True)
+        self.procs, self.flag, self.barriers = procs, flag, barriers
+        self.stop = threading.Event()
+        self.failed = None
+
+    def run(self):
+        from .control import TerminationFlag
+        while not self.stop.wait(0.2):
+            for name, p in self.procs:
+                code = p.exitcode
+                if code is not None and code != 0:
+                    self.failed = (name, code)
+                    with self.flag.get_lock():
+                        if self.flag.value in (TerminationFlag.UNSET,
+                                               TerminationFlag.TARGET_NUM_VIDEOS_REACHED):
+                            self.flag.value = TerminationFlag.CHILD_FAILED
+                    for b in self.barriers:
+                        try:
+                            b.abort()
+                        except Exception:
+                            pass
+                    return
+
+
+def _assign_rccl_ranks(spec, qt, job_id):
+    """One torch.distributed world for every runner touching an RCCL ring."""
+    import tempfile
+    from .config import ConfigError
+    from .parallel.rccl_channel import DistInfo
+    rccl = {}
+    for s, step_rings in enumerate(qt.rings):
+        for g, rings in enumerate(step_rings):
+            for i, r in enumerate(rings):
+                if r is not None and r.kind == "rccl":
+                    rccl[(s, g, i)] = r
+    if not rccl:
+        return {}
+    backend = os.environ.get("RNB_RCCL_BACKEND", "nccl")
+    members = set(rccl)
+    for (s, g, i), ring in rccl.items():
+        outs = set(spec.steps[s].groups[g].out_queues)
+        for cg, grp in enumerate(spec.steps[s + 1].groups):
+            if grp.in_queue in outs:
+                for ci, gpu in enumerate(grp.gpus):
+                    if backend == "nccl" and (gpu < 0 or gpu == ring.producer_gpu):
+                        raise ConfigError(
+                            "rccl transport needs producer and consumer on different "
+                            "GPUs (step %d group %d gpu %d -> gpu %d); use 'ipc' for "
+                            "same-GPU edges" % (s, g, ring.producer_gpu, gpu))
+                    members.add((s + 1, cg, ci))
+    order = sorted(members)
+    store = os.path.join(tempfile.gettempdir(), "rnb-rccl-%s-%d" % (job_id, os.getpid()))
+    if os.path.exists(store):
+        os.remove(store)
+    infos = {key: DistInfo(rank, len(order), store, backend)
+             for rank, key in enumerate(order)}
+    for key, ring in rccl.items():
+        ring.producer_rank = infos[key].rank
+    return infos
+
+
+def _client_main(fn, *args, **kwargs):
+    from threading import BrokenBarrierError
+    try:
+        fn(*args, **kwargs)
+    except BrokenBarrierError:
+        sys.exit(2)
+
+
+def run(args) -> dict:
+    import torch.multiprocessing as tmp
+    from .config import load_pipeline, check_gpus
+    from .control import TerminationFlag, SharedQueuesAndTensors
+    from .client import poisson_client, bulk_client
+    from .runner import runner
+    from .timecard import TimeCardSummary, logmeta, logroot, LOG_ROOT_ENV
+
+    if args.log_root:
+        os.environ[LOG_ROOT_ENV] = args.log_root
+    spec = load_pipeline(args.config_file_path)
+    check_gpus(spec)
+    _apply_batch_default(spec, args.batch_size)
+
+    ctx = tmp.get_context("spawn")
+    job_id = "%s-mi%d-b%d-v%d-qs%d" % (datetime.today().strftime("%y%m%d_%H%M%S"),
+                                       args.mean_interval_ms, args.batch_size,
+                                       args.videos, args.queue_size)
+    num_runners = spec.num_runners
+    sta_bar = ctx.Barrier(num_runners + 2)
+    fin_bar = ctx.Barrier(num_runners + 2)
+    counter = ctx.Value("i", 0)
+    flag = ctx.Value("i", TerminationFlag.UNSET)
+    queue_size = args.queue_size if args.mean_interval_ms > 0 \
+        else args.videos + num_runners + 1
+    qt = SharedQueuesAndTensors(spec, ctx.Queue, queue_size, ctx)
+    result_queue = ctx.Queue()
+    it_kwargs = spec.iterator_kwargs
+    if args.mean_interval_ms > 0:
+        client = ctx.Process(target=_client_main, name="client",
+                             args=(poisson_client, spec.video_path_iterator,
+                                   qt.get_filename_queue(), args.mean_interval_ms, flag,
+                                   sta_bar, fin_bar),
+                             kwargs=dict(seed=args.seed,
+                                         barrier_timeout=args.barrier_timeout,
+                                         iterator_kwargs=it_kwargs))
+    else:
+        client = ctx.Process(target=_client_main, name="client",
+                             args=(bulk_client, spec.video_path_iterator,
+                                   qt.get_filename_queue(), args.videos, flag, sta_bar,
+                                   fin_bar),
+                             kwargs=dict(seed=args.seed,
+                                         barrier_timeout=args.barrier_timeout,
+                                         iterator_kwargs=it_kwargs))
+    procs = [("client", client)]
+    last = len(spec.steps) - 1
+    dist_infos = _assign_rccl_ranks(spec, qt, job_id)
+    for step_idx, step in enumerate(spec.steps):
+        for group_idx, group in enumerate(step.groups):
+            for instance_idx, gpu in enumerate(group.gpus):
+                in_q, out_qs = qt.get_queues(step_idx, group_idx)
+                in_r, out_r = qt.get_tensors(step_idx, group_idx, instance_idx)
+                first_final = step_idx == last and group_idx == 0 and instance_idx == 0
+                p = ctx.Process(
+                    target=runner,
+                    name="runner-s%d-g%d-i%d" % (step_idx, group_idx, instance_idx),
+                    args=(in_q, out_qs, group.queue_selector, first_final, job_id, gpu,
+                          group_idx, instance_idx, counter, args.videos, flag, step_idx,
+                          sta_bar, fin_bar, step.model, step.num_segments, in_r, out_r),
+                    kwargs=dict(group.kwargs, result_queue=result_queue,
+                                barrier_timeout=args.barrier_timeout,
+                                dist_info=dist_infos.get((step_idx, group_idx,
+                                                          instance_idx))))
+                procs.append((p.name, p))
+    for _, p in procs:
+        p.start()
+    dog = Watchdog(procs, flag, [sta_bar, fin_bar])
+    dog.start()
+
+    from threading import BrokenBarrierError
+    time_start = time_end = None
+    broken = False
+    try:
+        sta_bar.wait(args.barrier_timeout)
+        time_start = time.time()
+        print("START! %f" % time_start, flush=True)
+        fin_bar.wait(args.barrier_timeout)
+        time_end = time.time()
+        print("FINISH! %f" % time_end, flush=True)
+    except BrokenBarrierError:
+        broken = True
+        with flag.get_lock():
+            if flag.value == TerminationFlag.UNSET:
+                flag.value = TerminationFlag.BARRIER_TIMEOUT
+        print("[ERROR] job aborted: %s" % (dog.failed or "barrier timeout"), flush=True)
+
+    summaries = TimeCardSummary()
+    n_final = sum(len(g.gpus) for g in spec.steps[-1].groups)
+    got = 0
+    deadline = time.time() + (60.0 if not broken else 5.0)
+    while got < n_final and time.time() < deadline:
+        try:
+            msg = result_queue.get(timeout=0.5)
+        except Exception:
+            if all(p.exitcode is not None for _, p in procs):
+                break
+            continue
+        if msg[0] == "summary":
+            summaries.merge_from(msg[4])
+            got += 1
+    for _, p in procs:
+        p.join(RESERVED_CHILD_EXIT_GRACE_S if not broken else 5.0)
+        if p.exitcode is None:
+            p.terminate()
+            p.join(5.0)
+    dog.stop.set()
+
+    result = {"job_id": job_id, "config": os.path.basename(args.config_file_path),
+              "termination_flag": TerminationFlag.NAMES.get(flag.value, flag.value),
+              "videos_target": args.videos, "videos_done": counter.value,
+              "mean_interval_ms": args.mean_interval_ms, "ok": False}
+    if time_start is not None and time_end is not None:
+        total = time_end - time_start
+        done = min(counter.value, args.videos)
+        print("Time: %f sec" % total)
+        print("Number of videos: %d videos" % args.videos)
+        lat = summaries.latency_stats(num_skips=min(10, max(0, len(summaries) - 1)))
+        result.update({"time_s": total, "videos_per_s": done / total if total > 0 else 0.0,
+                       "latency": lat, "ok": flag.value ==
+                       TerminationFlag.TARGET_NUM_VIDEOS_REACHED})
+        print("Throughput: %.2f videos/s; latency p50 %.2f ms p99 %.2f ms (%d requests)"
+              % (result["videos_per_s"], lat["p50_ms"], lat["p99_ms"], lat["count"]),
+              flush=True)
+    with open(logmeta(job_id), "w") as f:
+        f.write("Args: %s\n" % str(args))
+        f.write("%f %f\n" % (time_start or 0.0, time_end or 0.0))
+        f.write("Termination flag: %d\n" % flag.value)
+    shutil.copyfile(args.config_file_path,
+                    os.path.join(logroot(job_id), os.path.basename(args.config_file_path)))
+    if args.json_out:
+        with open(args.json_out, "w") as f:
+            json.dump(result, f, indent=2)
+    return result
+
+
+def main(argv=None) -> int:
+    args = build_parser().parse_args(argv)
+    if args.check:
+        import rnb_amd.runner  # noqa: F401  (import smoke, benchmark.py:164-171)
+        import rnb_amd.control  # noqa: F401
+        print("RnB is ready to go!")
+        return 0
+    print("Args:", args, flush=True)
+    from .config import ConfigError
+    try:
+        res = run(args)
+    except ConfigError as err:
+        print("[ERROR] %s" % err, flush=True)
+        return 2
+    return 0 if res.get("ok") else 1

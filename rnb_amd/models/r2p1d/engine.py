@@ -1,0 +1,290 @@
+"""R(2+1)D inference engine: folded-BN plan over the HIP conv kernels.
+
+``R2P1DEngine`` compiles an ``R2Plus1DLayerWrapper`` (any layer range
+[start, end], the layer-partitioned pipeline of reference model.py:20-84) into
+a flat plan of fused ops:
+
+* every ``SpatioTemporalConv`` becomes two ``ConvLayer``s: the spatial conv
+  with its inner BN + ReLU folded in (K23), and the temporal conv with the
+  following block BN folded in (bn1 + ReLU: K24; bn2 + residual add + ReLU in
+  the epilogue: K25; downsamplebn: K26);
+* layer 5 ends in the fused pool + linear head (K28).
+
+Activations are NDHWC bf16 with channels padded to 8. Execution backends:
+
+``hip``    the CDNA4 kernels (default on GPU);
+``torch``  the same folded plan through ``F.conv3d`` (CPU path, and the
+           oracle that isolates the kernels from the folding in tests);
+``module`` the unfolded ``nn.Module`` in NCDHW fp32 -- the only backend that
+           can reproduce the reference's training-mode BN (``bn_mode=batch``,
+           SURVEY.md §2.3 "BatchNorm mode").
+
+``GraphedEngine`` wraps a ``hip`` engine with one HIP graph per clip-count
+bucket (torch.cuda.CUDAGraph capture of the ctypes launches, shared memory
+pool), which removes the ~80 kernel launches per forward from the host path
+(SURVEY.md §7.1). Clip rows are independent in eval mode, so a batch is padded
+up to its bucket and the padded rows are discarded.
+"""
+from __future__ import annotations
+
+import bisect
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ...ops.conv import ConvGeom, ConvLayer, fold_bn, pad_to, CH_ALIGN
+from ...ops.video import Head, IN_CHANNELS_P, ndhwc_to_ncdhw, ncdhw_to_ndhwc
+from .network import (LAYER_CHANNELS, LAYER_INPUT_CTHW, LAYER_OUTPUT_CTHW,
+                      R2Plus1DLayerWrapper, SpatioTemporalConv)
+
+DEFAULT_BUCKETS = (1, 2, 3, 4, 5, 6, 8, 10, 12, 15, 16, 20, 24, 30, 32, 40, 45, 48,
+                   60, 64, 80, 96, 128)
+
+
+def boundary_channels_p(layer_idx: int) -> int:
+    """Channels (padded) of the NDHWC tensor entering layer ``layer_idx``."""
+    if layer_idx == 1:
+        return IN_CHANNELS_P
+    return pad_to(LAYER_INPUT_CTHW[layer_idx][0], CH_ALIGN)
+
+
+def boundary_shape(layer_idx: int, n: int) -> Tuple[int, ...]:
+    c, t, h, w = LAYER_INPUT_CTHW[layer_idx]
+    return (n, t, h, w, boundary_channels_p(layer_idx))
+
+
+class PlanOp:
+    __slots__ = ("kind", "layer", "src", "dst", "res")
+
+    def __init__(self, kind, layer, src, dst, res=None):
+        self.kind, self.layer, self.src, self.dst, self.res = kind, layer, src, dst, res
+
+
+class R2P1DEngine:
+    def __init__(self, net: R2Plus1DLayerWrapper, device: torch.device,
+                 backend: str = "hip", bn_mode: str = "eval"):
+        if backend not in ("hip", "torch", "module"):
+            raise ValueError("unknown backend %r" % backend)
+        if bn_mode not in ("eval", "batch"):
+            raise ValueError("bn_mode must be 'eval' or 'batch'")
+        if bn_mode == "batch" and backend != "module":
+            raise ValueError("bn_mode='batch' (reference training-mode BN) needs "
+                             "backend='module'")
+        self.net = net
+        self.device = device
+        self.backend = backend
+        self.bn_mode = bn_mode
+        self.start_idx, self.end_idx = net.start_idx, net.end_idx
+        self.num_classes = getattr(net, "num_classes", 400)
+        self.ops: List[PlanOp] = []
+        self.head: Optional[Head] = None
+        self._n = 0
+        if backend == "module":
+            self.module = net.to(device)
+            self.module.train(bn_mode == "batch")
+        else:
+            self._build(net.res2plus1d)
+            if self.end_idx == 5:
+                self.head = Head(net.linear, device)
+
+    # ---------------------------------------------------------------- build
+    def _name(self) -> str:
+        self._n += 1
+        return "t%d" % self._n
+
+    def _conv(self, conv: torch.nn.Conv3d, bn, relu: bool, name: str) -> ConvLayer:
+        w, b = fold_bn(conv.weight, conv.bias, bn)
+        geom = ConvGeom(cin=conv.in_channels, cout=conv.out_channels,
+                        kernel=tuple(conv.kernel_size), stride=tuple(conv.stride),
+                        padding=tuple(conv.padding))
+        return ConvLayer(w, b, geom, relu, self.device, name)
+
+    def _stconv(self, st: SpatioTemporalConv, src: str, post_bn, relu: bool,
+                res: Optional[str], name: str) -> str:
+        mid = self._name()
+        self.ops.append(PlanOp("conv", self._conv(st.spatial_conv, st.bn, True,
+                                                  name + ".spatial"), src, mid))
+        dst = self._name()
+        self.ops.append(PlanOp("conv", self._conv(st.temporal_conv, post_bn, relu,
+                                                  name + ".temporal"), mid, dst, res))
+        return dst
+
+    def _block(self, blk, src: str, name: str) -> str:
+        if blk.downsample:
+            res = self._stconv(blk.downsampleconv, src, blk.downsamplebn, False, None,
+                               name + ".downsample")
+        else:
+            res = src
+        h = self._stconv(blk.conv1, src, blk.bn1, True, None, name + ".conv1")
+        return self._stconv(blk.conv2, h, blk.bn2, True, res, name + ".conv2")
+
+    def _build(self, body):
+        cur = "x"
+        for idx in range(self.start_idx, self.end_idx + 1):
+            if idx == 1:
+                cur = self._stconv(body.conv1, cur, None, False, None, "conv1")
+            else:
+                layer = getattr(body, "conv%d" % idx)
+                cur = self._block(layer.block1, cur, "conv%d.block1" % idx)
+                for j, blk in enumerate(layer.blocks):
+                    cur = self._block(blk, cur, "conv%d.blocks.%d" % (idx, j))
+        self.out_name = cur
+
+    # ------------------------------------------------------------- metadata
+    @property
+    def in_channels_p(self) -> int:
+        return boundary_channels_p(self.start_idx)
+
+    def input_shape(self, n: int) -> Tuple[int, ...]:
+        return boundary_shape(self.start_idx, n)
+
+    def output_shape(self, n: int) -> Tuple[int, ...]:
+        if self.end_idx == 5:
+            return (n, self.num_classes)
+        return boundary_shape(self.end_idx + 1, n)
+
+    def output_dtype(self):
+        return torch.float32 if self.end_idx == 5 else torch.bfloat16
+
+    def flops_per_clip(self) -> int:
+        """Useful FLOPs for one 8x112x112 clip through this layer range."""
+        total = 0
+        c, t, h, w = LAYER_INPUT_CTHW[self.start_idx]
+        shapes = {"x": (t, h, w)}
+        for op in self.ops:
+            g = op.layer.geom
+            T, H, W = shapes[op.src]
+            total += g.flops(1, T, H, W)
+            shapes[op.dst] = g.out_thw(T, H, W)
+        if self.head is not None:
+            total += 2 * self.head.channels * self.head.num_classes
+        return total
+
+    def conv_layers(self) -> List[ConvLayer]:
+        return [op.layer for op in self.ops if op.kind == "conv"]
+
+    # -------------------------------------------------------------- forward
+    def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """x: NDHWC bf16 boundary tensor (or NCDHW fp32 for backend=module)."""
+        if self.backend == "module":
+            if x.dim() == 5 and x.shape[-1] == self.in_channels_p and x.dtype == torch.bfloat16:
+                x = ndhwc_to_ncdhw(x, LAYER_INPUT_CTHW[self.start_idx][0])
+            y = self.module(x.to(self.device))
+            if self.end_idx == 5:
+                return y.float()
+            return ncdhw_to_ndhwc(y, boundary_channels_p(self.end_idx + 1))
+        if x.shape[0] == 0:
+            return torch.zeros(self.output_shape(0), dtype=self.output_dtype(),
+                               device=x.device)
+        hip = self.backend == "hip"
+        bufs: Dict[str, torch.Tensor] = {"x": x}
+        for op in self.ops:
+            src = bufs[op.src]
+            res = bufs[op.res] if op.res is not None else None
+            if hip:
+                y = op.layer.forward_hip(src, res)
+            else:
+                y = op.layer.forward_torch(src, res)
+            bufs[op.dst] = y
+        y = bufs[self.out_name]
+        if self.head is not None:
+            y = self.head.forward(y, out) if hip else self.head.forward_torch(y)
+        elif out is not None:
+            out.copy_(y)
+            y = out
+        return y
+
+    __call__ = forward
+
+    def autotune(self, n: int, reps: int = 3) -> Dict[str, int]:
+        """Pick the fastest tile per conv for ``n`` clips (GPU only)."""
+        assert self.backend == "hip"
+        x = torch.randn(self.input_shape(n), device=self.device).to(torch.bfloat16)
+        bufs = {"x": x}
+        chosen = {}
+        for op in self.ops:
+            src = bufs[op.src]
+            res = bufs[op.res] if op.res is not None else None
+            chosen[op.layer.name] = op.layer.autotune(src, res, reps)
+            bufs[op.dst] = op.layer.forward_hip(src, res)
+        torch.cuda.synchronize(self.device)
+        return chosen
+
+
+class GraphedEngine:
+    """HIP-graph replay of a ``hip`` engine, one graph per clip bucket."""
+
+    def __init__(self, engine: R2P1DEngine, max_clips: int,
+                 buckets: Sequence[int] = DEFAULT_BUCKETS, autotune: bool = True,
+                 warmup: int = 2):
+        assert engine.backend == "hip"
+        self.engine = engine
+        self.device = engine.device
+        self.buckets = sorted({b for b in buckets if b < max_clips} | {max_clips})
+        self.autotune = autotune
+        self.warmup = warmup
+        self.graphs: Dict[int, Tuple[torch.cuda.CUDAGraph, torch.Tensor, torch.Tensor]] = {}
+        self.pool = None
+        self.capture_s = 0.0
+
+    def bucket_for(self, n: int) -> int:
+        i = bisect.bisect_left(self.buckets, n)
+        if i == len(self.buckets):
+            raise ValueError("batch of %d clips exceeds max_clips %d"
+                             % (n, self.buckets[-1]))
+        return self.buckets[i]
+
+    def _capture(self, b: int):
+        t0 = time.time()
+        eng = self.engine
+        if self.autotune:
+            eng.autotune(b)
+        static_in = torch.zeros(eng.input_shape(b), dtype=torch.bfloat16, device=self.device)
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(self.warmup):
+                eng.forward(static_in)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        torch.cuda.synchronize(self.device)
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self.pool):
+            static_out = eng.forward(static_in)
+        torch.cuda.synchronize(self.device)
+        self.graphs[b] = (g, static_in, static_out)
+        self.capture_s += time.time() - t0
+        return self.graphs[b]
+
+    def prepare(self, sizes: Optional[Sequence[int]] = None):
+        for b in (self.buckets if sizes is None else sorted({self.bucket_for(s) for s in sizes})):
+            if b not in self.graphs:
+                self._capture(b)
+
+    def input_buffer(self, n: int) -> Tuple[torch.Tensor, int]:
+        """Static input of the bucket for n clips (write rows [:n] in place)."""
+        b = self.bucket_for(n)
+        if b not in self.graphs:
+            self._capture(b)
+        return self.graphs[b][1], b
+
+    def replay(self, n: int) -> torch.Tensor:
+        """Replay the bucket graph whose input was filled via input_buffer."""
+        b = self.bucket_for(n)
+        g, static_in, static_out = self.graphs[b]
+        # rows >= n hold stale (finite) inputs; clip rows are independent in
+        # eval mode, so their outputs are simply not returned
+        g.replay()
+        return static_out[:n]
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        n = x.shape[0]
+        if n == 0:
+            return self.engine.forward(x)
+        static_in, b = self.input_buffer(n)
+        static_in[:n].copy_(x)
+        return self.replay(n)
+
+    __call__ = forward

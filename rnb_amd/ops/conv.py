@@ -1,0 +1,221 @@
+"""Channels-last (NDHWC) bf16 3-D convolution layer backed by the HIP kernel.
+
+``ConvLayer`` owns one convolution of the R(2+1)D plan with eval-mode
+BatchNorm already folded in. It stores the weight as the GEMM matrix the
+kernel streams (``[Cout_p + 256][K_pad]`` bf16, K ordered (dt, dh, dw, c) with
+c padded to ``Cin_p``; the 256 zero rows let any channel tile read past
+``Cout_p`` safely) and picks a tile configuration per input shape, either by a
+cost heuristic or by timing every instantiated tile on the GPU
+(``autotune``; the analogue of ``cudnn.benchmark = True`` in
+reference runner.py:25).
+
+``forward_torch`` computes the same op with ``torch.nn.functional.conv3d``
+in fp32 on the bf16-rounded weights: the numerics reference for tests and the
+CPU execution path.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+CH_ALIGN = 8        # channel padding of every NDHWC activation
+BK = 64             # K step of the kernel
+W_ROW_SLACK = 256   # extra zero weight rows (>= largest channel tile)
+
+
+def pad_to(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+@dataclass(frozen=True)
+class ConvGeom:
+    cin: int
+    cout: int
+    kernel: Tuple[int, int, int]
+    stride: Tuple[int, int, int]
+    padding: Tuple[int, int, int]
+
+    @property
+    def cin_p(self) -> int:
+        return pad_to(self.cin, CH_ALIGN)
+
+    @property
+    def cout_p(self) -> int:
+        return pad_to(self.cout, CH_ALIGN)
+
+    @property
+    def k_total(self) -> int:
+        kt, kh, kw = self.kernel
+        return kt * kh * kw * self.cin_p
+
+    @property
+    def k_pad(self) -> int:
+        return pad_to(self.k_total, BK)
+
+    def out_thw(self, T: int, H: int, W: int) -> Tuple[int, int, int]:
+        (kt, kh, kw), (st, sh, sw), (pt, ph, pw) = self.kernel, self.stride, self.padding
+        return ((T + 2 * pt - kt) // st + 1, (H + 2 * ph - kh) // sh + 1,
+                (W + 2 * pw - kw) // sw + 1)
+
+    def flops(self, n: int, T: int, H: int, W: int) -> int:
+        """Useful (unpadded) FLOPs for n clips."""
+        To, Ho, Wo = self.out_thw(T, H, W)
+        kt, kh, kw = self.kernel
+        return 2 * n * To * Ho * Wo * self.cout * self.cin * kt * kh * kw
+
+
+def fold_bn(weight: torch.Tensor, bias: Optional[torch.Tensor], bn) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Fold an eval-mode BatchNorm into the preceding conv's weight/bias."""
+    w = weight.detach().double()
+    b = bias.detach().double() if bias is not None else torch.zeros(w.shape[0], dtype=torch.float64)
+    if bn is None:
+        return w.float(), b.float()
+    s = bn.weight.detach().double() / torch.sqrt(bn.running_var.detach().double() + bn.eps)
+    w = w * s.view(-1, *([1] * (w.dim() - 1)))
+    b = (b - bn.running_mean.detach().double()) * s + bn.bias.detach().double()
+    return w.float(), b.float()
+
+
+class ConvLayer:
+    """One folded conv (+ optional residual add and ReLU) of the plan."""
+
+    def __init__(self, weight: torch.Tensor, bias: torch.Tensor, geom: ConvGeom,
+                 relu: bool, device: torch.device, name: str = ""):
+        assert weight.shape == (geom.cout, geom.cin) + tuple(geom.kernel), \
+            (weight.shape, geom)
+        self.geom = geom
+        self.relu = bool(relu)
+        self.name = name
+        self.device = device
+        kt, kh, kw = geom.kernel
+        cin_p, cout_p = geom.cin_p, geom.cout_p
+        # GEMM matrix [rows][K_pad] with k = ((dt*KH + dh)*KW + dw)*cin_p + c
+        w = torch.zeros(geom.cout, kt, kh, kw, cin_p, dtype=torch.float32)
+        w[..., :geom.cin] = weight.detach().float().permute(0, 2, 3, 4, 1)
+        wmat = torch.zeros(cout_p + W_ROW_SLACK, geom.k_pad, dtype=torch.float32)
+        wmat[:geom.cout, :geom.k_total] = w.reshape(geom.cout, -1)
+        self.wmat = wmat.to(torch.bfloat16).to(device).contiguous()
+        b = torch.zeros(cout_p + W_ROW_SLACK, dtype=torch.float32)
+        b[:geom.cout] = bias.detach().float()
+        self.bias = b.to(device).contiguous()
+        # the bf16-rounded weight in conv layout, for the torch path
+        self.w_ref = (weight.detach().to(torch.bfloat16).float().to(device))
+        self.b_ref = bias.detach().float().to(device)
+        self._config: Dict[Tuple[int, int], int] = {}
+
+    # ------------------------------------------------------------------
+    def out_shape(self, x_shape) -> Tuple[int, int, int, int, int]:
+        N, T, H, W, _ = x_shape
+        To, Ho, Wo = self.geom.out_thw(T, H, W)
+        return (N, To, Ho, Wo, self.geom.cout_p)
+
+    def params(self, x: torch.Tensor, y: torch.Tensor, residual: Optional[torch.Tensor]):
+        from .native import ConvParams
+        g = self.geom
+        N, T, H, W, C = x.shape
+        if C != g.cin_p:
+            raise ValueError("%s: input has %d channels, expected %d" % (self.name, C, g.cin_p))
+        _, To, Ho, Wo, Co = y.shape
+        p = ConvParams()
+        p.x, p.w, p.bias = x.data_ptr(), self.wmat.data_ptr(), self.bias.data_ptr()
+        p.res = residual.data_ptr() if residual is not None else None
+        p.y = y.data_ptr()
+        p.N, p.T, p.H, p.W, p.Cin_p = N, T, H, W, g.cin_p
+        p.To, p.Ho, p.Wo = To, Ho, Wo
+        p.KT, p.KH, p.KW = g.kernel
+        p.ST, p.SH, p.SW = g.stride
+        p.PT, p.PH, p.PW = g.padding
+        p.Cout_p = g.cout_p
+        p.y_stride = Co
+        p.res_stride = residual.shape[-1] if residual is not None else 0
+        p.K_total, p.K_pad = g.k_total, g.k_pad
+        p.M = N * To * Ho * Wo
+        p.relu = 1 if self.relu else 0
+        p.w_rows = self.wmat.shape[0]
+        return p
+
+    def heuristic_config(self, M: int) -> int:
+        from .native import kernels
+        best, best_cost = 0, None
+        cp = self.geom.cout_p
+        for cid, (pt, ct) in enumerate(kernels().configs):
+            nblk = math.ceil(M / pt) * math.ceil(cp / ct)
+            work = math.ceil(M / pt) * pt * math.ceil(cp / ct) * ct
+            # per-element overhead of small tiles (operand re-reads) and the
+            # quantisation of the grid into waves of 2 blocks x 256 CUs
+            waves = math.ceil(nblk / 512.0)
+            cost = work * (1.0 + 16.0 / pt + 16.0 / ct) * (waves * 512.0 / max(nblk, 1)) ** 0.5
+            if best_cost is None or cost < best_cost:
+                best, best_cost = cid, cost
+        return best
+
+    def config_for(self, x_shape) -> int:
+        key = tuple(x_shape[:4])
+        cid = self._config.get(key)
+        if cid is None:
+            N, T, H, W, _ = x_shape
+            To, Ho, Wo = self.geom.out_thw(T, H, W)
+            cid = self.heuristic_config(N * To * Ho * Wo)
+            self._config[key] = cid
+        return cid
+
+    def autotune(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                 reps: int = 5) -> int:
+        """Time every tile config on this input shape; keep the fastest."""
+        from .native import kernels
+        kern = kernels()
+        y = torch.empty(self.out_shape(x.shape), dtype=torch.bfloat16, device=x.device)
+        stream = torch.cuda.current_stream(x.device)
+        best, best_t = None, None
+        for cid in range(len(kern.configs)):
+            p = self.params(x, y, residual)
+            kern.conv(p, cid, stream.cuda_stream)          # warm
+            start = torch.cuda.Event(enable_timing=True)
+            end = torch.cuda.Event(enable_timing=True)
+            start.record(stream)
+            for _ in range(reps):
+                kern.conv(p, cid, stream.cuda_stream)
+            end.record(stream)
+            end.synchronize()
+            t = start.elapsed_time(end) / reps
+            if best_t is None or t < best_t:
+                best, best_t = cid, t
+        self._config[tuple(x.shape[:4])] = best
+        return best
+
+    # ------------------------------------------------------------------
+    def forward_hip(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                    out: Optional[torch.Tensor] = None, config: Optional[int] = None):
+        from .native import kernels
+        if x.dtype != torch.bfloat16 or not x.is_contiguous():
+            raise ValueError("%s: expected contiguous bf16 NDHWC input" % self.name)
+        y = out if out is not None else torch.empty(self.out_shape(x.shape),
+                                                    dtype=torch.bfloat16, device=x.device)
+        if residual is not None:
+            if residual.shape[:4] != y.shape[:4] or residual.dtype != torch.bfloat16:
+                raise ValueError("%s: residual %s does not match output %s"
+                                 % (self.name, tuple(residual.shape), tuple(y.shape)))
+        cid = self.config_for(x.shape) if config is None else config
+        p = self.params(x, y, residual)
+        kernels().conv(p, cid, torch.cuda.current_stream(x.device).cuda_stream)
+        return y
+
+    def forward_torch(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                      out_dtype=torch.bfloat16):
+        """fp32 reference of the same op on NDHWC tensors."""
+        g = self.geom
+        xin = x[..., :g.cin].float().permute(0, 4, 1, 2, 3)
+        y = F.conv3d(xin, self.w_ref.to(x.device), self.b_ref.to(x.device),
+                     stride=g.stride, padding=g.padding)
+        y = y.permute(0, 2, 3, 4, 1)
+        if residual is not None:
+            y = y + residual[..., :g.cout].float()
+        if self.relu:
+            y = torch.relu(y)
+        if g.cout_p != g.cout:
+            y = F.pad(y, (0, g.cout_p - g.cout))
+        return y.to(out_dtype).contiguous()

@@ -1,0 +1,286 @@
+"""ctypes bindings for the in-tree native libraries (rnb_amd/_native/*.so).
+
+Design note: the HIP libraries export a plain C ABI and are loaded with
+ctypes instead of being compiled as PyTorch C++ extensions. They build with a
+single ``hipcc`` call in seconds, carry no PyTorch-ABI coupling, and launch on
+whatever ``hipStream_t`` the caller passes (``torch.cuda.current_stream()
+.cuda_stream``), which is what HIP-graph capture needs.
+
+Loading policy: on a machine with a visible GPU a missing or stale library is
+a hard error (``NativeUnavailable``) -- the GPU path never silently falls
+back to PyTorch. On a CPU-only machine callers may probe ``available()``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+NATIVE_DIR = os.path.join(os.path.dirname(_HERE), "_native")
+
+_lock = threading.Lock()
+_libs = {}
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+def _lib_path(name: str) -> str:
+    return os.path.join(NATIVE_DIR, name)
+
+
+def _load(name: str, build_if_missing: bool = True) -> ctypes.CDLL:
+    with _lock:
+        lib = _libs.get(name)
+        if lib is not None:
+            return lib
+        path = _lib_path(name)
+        if not os.path.exists(path) and build_if_missing and \
+                os.environ.get("RNB_NO_AUTOBUILD") != "1":
+            from .. import build
+            try:
+                build.build_one(name)
+            except Exception as err:  # pragma: no cover - reported below
+                raise NativeUnavailable("could not build %s: %s" % (name, err))
+        if not os.path.exists(path):
+            raise NativeUnavailable("%s not built; run `python -m rnb_amd.build`"
+                                    % path)
+        try:
+            lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        except OSError as err:
+            raise NativeUnavailable("failed to load %s: %s" % (path, err))
+        _libs[name] = lib
+        return lib
+
+
+def available(name: str = "librnb_kernels.so") -> bool:
+    try:
+        _load(name)
+        return True
+    except NativeUnavailable:
+        return False
+
+
+def loaded_paths():
+    """Paths of the native libraries loaded into this process."""
+    return sorted(_lib_path(n) for n in _libs)
+
+
+def _check(rc: int, what: str, lib: Optional[ctypes.CDLL] = None) -> None:
+    if rc == 0:
+        return
+    if rc < 0:
+        raise RuntimeError("%s: shape/contract check failed (code %d)" % (what, rc))
+    msg = ""
+    try:
+        rt = _load("librnb_runtime.so")
+        rt.rnb_error_string.restype = ctypes.c_char_p
+        msg = rt.rnb_error_string(rc).decode()
+    except Exception:
+        pass
+    raise RuntimeError("%s failed: hipError %d %s" % (what, rc, msg))
+
+
+# ---------------------------------------------------------------------------
+# kernels
+# ---------------------------------------------------------------------------
+class ConvParams(ctypes.Structure):
+    """Mirror of ``struct ConvParams`` in csrc/conv_igemm.hip."""
+    _fields_ = [
+        ("x", ctypes.c_void_p), ("w", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+        ("res", ctypes.c_void_p), ("y", ctypes.c_void_p),
+        ("N", ctypes.c_int), ("T", ctypes.c_int), ("H", ctypes.c_int),
+        ("W", ctypes.c_int), ("Cin_p", ctypes.c_int),
+        ("To", ctypes.c_int), ("Ho", ctypes.c_int), ("Wo", ctypes.c_int),
+        ("KT", ctypes.c_int), ("KH", ctypes.c_int), ("KW", ctypes.c_int),
+        ("ST", ctypes.c_int), ("SH", ctypes.c_int), ("SW", ctypes.c_int),
+        ("PT", ctypes.c_int), ("PH", ctypes.c_int), ("PW", ctypes.c_int),
+        ("Cout_p", ctypes.c_int), ("y_stride", ctypes.c_int),
+        ("res_stride", ctypes.c_int), ("K_total", ctypes.c_int),
+        ("K_pad", ctypes.c_int), ("M", ctypes.c_int), ("relu", ctypes.c_int),
+        ("n_ptiles", ctypes.c_int), ("n_ctiles", ctypes.c_int),
+        ("x_bytes", ctypes.c_uint32), ("w_rows", ctypes.c_int),
+    ]
+
+
+class Kernels:
+    """Typed wrappers over librnb_kernels.so."""
+
+    def __init__(self):
+        lib = _load("librnb_kernels.so")
+        self.lib = lib
+        lib.rnb_conv_num_configs.restype = ctypes.c_int
+        lib.rnb_conv_config_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                             ctypes.POINTER(ctypes.c_int)]
+        lib.rnb_conv_params_size.restype = ctypes.c_int
+        lib.rnb_conv_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
+                                        ctypes.c_void_p]
+        lib.rnb_conv_launch.restype = ctypes.c_int
+        lib.rnb_clipgen_u8.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_void_p]
+        lib.rnb_preprocess.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
+                                       ctypes.POINTER(ctypes.c_float),
+                                       ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
+        lib.rnb_head.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        lib.rnb_video_reduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_void_p]
+        if lib.rnb_conv_params_size() != ctypes.sizeof(ConvParams):
+            raise NativeUnavailable("ConvParams layout mismatch (%d vs %d): rebuild"
+                                    % (lib.rnb_conv_params_size(),
+                                       ctypes.sizeof(ConvParams)))
+        self.configs = []
+        for i in range(lib.rnb_conv_num_configs()):
+            p, c = ctypes.c_int(), ctypes.c_int()
+            lib.rnb_conv_config_info(i, ctypes.byref(p), ctypes.byref(c))
+            self.configs.append((p.value, c.value))
+
+    def conv(self, params: ConvParams, config_id: int, stream: int) -> None:
+        _check(self.lib.rnb_conv_launch(ctypes.byref(params), config_id, stream),
+               "conv (config %d)" % config_id)
+
+    def clipgen_u8(self, out_ptr, vids_ptr, starts_ptr, nclips, F, H, W, stream):
+        _check(self.lib.rnb_clipgen_u8(out_ptr, vids_ptr, starts_ptr, nclips, F, H, W,
+                                       stream), "clipgen_u8")
+
+    def preprocess(self, in_ptr, out_ptr, npix, mean, std, stream):
+        m = (ctypes.c_float * 3)(*mean)
+        s = (ctypes.c_float * 3)(*std)
+        _check(self.lib.rnb_preprocess(in_ptr, out_ptr, npix, m, s, stream), "preprocess")
+
+    def head(self, x_ptr, w_ptr, b_ptr, out_ptr, N, S, C, Cs, ncls, stream):
+        _check(self.lib.rnb_head(x_ptr, w_ptr, b_ptr, out_ptr, N, S, C, Cs, ncls, stream),
+               "head")
+
+    def video_reduce(self, logits_ptr, offsets_ptr, sums_ptr, argmax_ptr, nvid, ncls,
+                     stream):
+        _check(self.lib.rnb_video_reduce(logits_ptr, offsets_ptr, sums_ptr, argmax_ptr,
+                                         nvid, ncls, stream), "video_reduce")
+
+
+class Runtime:
+    """Typed wrappers over librnb_runtime.so (IPC, copies, device info)."""
+
+    def __init__(self):
+        lib = _load("librnb_runtime.so")
+        self.lib = lib
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        lib.rnb_error_string.restype = ctypes.c_char_p
+        lib.rnb_malloc.argtypes = [ctypes.POINTER(vp), sz]
+        lib.rnb_free.argtypes = [vp]
+        lib.rnb_ipc_get_mem_handle.argtypes = [vp, vp]
+        lib.rnb_ipc_open_mem_handle.argtypes = [vp, ctypes.POINTER(vp)]
+        lib.rnb_ipc_close_mem_handle.argtypes = [vp]
+        lib.rnb_memcpy_async.argtypes = [vp, vp, sz, vp]
+        lib.rnb_memcpy_d2h.argtypes = [vp, vp, sz]
+        lib.rnb_memcpy_peer_async.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, sz, vp]
+        lib.rnb_stream_synchronize.argtypes = [vp]
+        lib.rnb_ipc_event_create.argtypes = [ctypes.POINTER(vp)]
+        lib.rnb_ipc_get_event_handle.argtypes = [vp, vp]
+        lib.rnb_ipc_open_event_handle.argtypes = [vp, ctypes.POINTER(vp)]
+        lib.rnb_event_record.argtypes = [vp, vp]
+        lib.rnb_stream_wait_event.argtypes = [vp, vp]
+        lib.rnb_event_synchronize.argtypes = [vp]
+        lib.rnb_event_destroy.argtypes = [vp]
+        lib.rnb_can_access_peer.argtypes = [ctypes.c_int, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_int)]
+        lib.rnb_mem_get_info.argtypes = [ctypes.POINTER(sz), ctypes.POINTER(sz)]
+        self.handle_size = lib.rnb_ipc_handle_size()
+        self.event_handle_size = lib.rnb_ipc_event_handle_size()
+
+    def set_device(self, dev: int) -> None:
+        _check(self.lib.rnb_set_device(dev), "hipSetDevice")
+
+    def ipc_malloc(self, nbytes: int) -> int:
+        p = ctypes.c_void_p()
+        _check(self.lib.rnb_malloc(ctypes.byref(p), nbytes), "hipMalloc(%d)" % nbytes)
+        return p.value
+
+    def free(self, ptr: int) -> None:
+        _check(self.lib.rnb_free(ptr), "hipFree")
+
+    def ipc_get_handle(self, ptr: int) -> bytes:
+        buf = ctypes.create_string_buffer(self.handle_size)
+        _check(self.lib.rnb_ipc_get_mem_handle(ptr, buf), "hipIpcGetMemHandle")
+        return buf.raw
+
+    def ipc_open_handle(self, handle: bytes) -> int:
+        p = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(handle, len(handle))
+        _check(self.lib.rnb_ipc_open_mem_handle(buf, ctypes.byref(p)),
+               "hipIpcOpenMemHandle")
+        return p.value
+
+    def ipc_close_handle(self, ptr: int) -> None:
+        _check(self.lib.rnb_ipc_close_mem_handle(ptr), "hipIpcCloseMemHandle")
+
+    def event_create_ipc(self) -> int:
+        p = ctypes.c_void_p()
+        _check(self.lib.rnb_ipc_event_create(ctypes.byref(p)), "hipEventCreate")
+        return p.value
+
+    def event_get_handle(self, ev: int) -> bytes:
+        buf = ctypes.create_string_buffer(self.event_handle_size)
+        _check(self.lib.rnb_ipc_get_event_handle(ev, buf), "hipIpcGetEventHandle")
+        return buf.raw
+
+    def event_open_handle(self, handle: bytes) -> int:
+        p = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(handle, len(handle))
+        _check(self.lib.rnb_ipc_open_event_handle(buf, ctypes.byref(p)),
+               "hipIpcOpenEventHandle")
+        return p.value
+
+    def event_record(self, ev: int, stream: int) -> None:
+        _check(self.lib.rnb_event_record(ev, stream), "hipEventRecord")
+
+    def stream_wait_event(self, stream: int, ev: int) -> None:
+        _check(self.lib.rnb_stream_wait_event(stream, ev), "hipStreamWaitEvent")
+
+    def memcpy_async(self, dst: int, src: int, nbytes: int, stream: int) -> None:
+        _check(self.lib.rnb_memcpy_async(dst, src, nbytes, stream), "hipMemcpyAsync")
+
+    def memcpy_d2h(self, dst: int, src: int, nbytes: int) -> None:
+        _check(self.lib.rnb_memcpy_d2h(dst, src, nbytes), "hipMemcpy D2H")
+
+    def memcpy_peer_async(self, dst, dst_dev, src, src_dev, nbytes, stream) -> None:
+        _check(self.lib.rnb_memcpy_peer_async(dst, dst_dev, src, src_dev, nbytes, stream),
+               "hipMemcpyPeerAsync")
+
+    def stream_synchronize(self, stream: int) -> None:
+        _check(self.lib.rnb_stream_synchronize(stream), "hipStreamSynchronize")
+
+    def can_access_peer(self, dev: int, peer: int) -> bool:
+        out = ctypes.c_int()
+        _check(self.lib.rnb_can_access_peer(dev, peer, ctypes.byref(out)),
+               "hipDeviceCanAccessPeer")
+        return bool(out.value)
+
+    def mem_info(self):
+        f, t = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(self.lib.rnb_mem_get_info(ctypes.byref(f), ctypes.byref(t)), "hipMemGetInfo")
+        return f.value, t.value
+
+
+_kernels: Optional[Kernels] = None
+_runtime: Optional[Runtime] = None
+
+
+def kernels() -> Kernels:
+    global _kernels
+    if _kernels is None:
+        _kernels = Kernels()
+    return _kernels
+
+
+def runtime() -> Runtime:
+    global _runtime
+    if _runtime is None:
+        _runtime = Runtime()
+    return _runtime

@@ -1,0 +1,138 @@
+"""Loader, head and reduction ops: HIP kernels + bit-exact/fp32 torch mirrors.
+
+GPU tensors dispatch to ``librnb_kernels.so``; CPU tensors run the torch
+mirror (the mirrors are what the numerics tests compare the kernels with).
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+# Kinetics-400 normalisation used by R(2+1)D
+KINETICS_MEAN = (0.43216, 0.394666, 0.37645)
+KINETICS_STD = (0.22803, 0.22145, 0.216989)
+IN_CHANNELS_P = 8   # RGB padded to 8 channels (16-byte NDHWC pixels)
+
+_M32 = 0xFFFFFFFF
+
+
+def _pixel_hash_torch(vid: torch.Tensor, frame: torch.Tensor, pix: torch.Tensor,
+                      c: torch.Tensor) -> torch.Tensor:
+    h = (vid * 0x9E3779B1 + frame * 0x85EBCA77 + pix * 0xC2B2AE3D + c * 0x27D4EB2F) & _M32
+    h = h ^ (h >> 15)
+    h = (h * 0x2C1B3C6D) & _M32
+    h = h ^ (h >> 12)
+    h = (h * 0x297A2D39) & _M32
+    h = h ^ (h >> 15)
+    return (h >> 24).to(torch.uint8)
+
+
+def clipgen_u8(vids: torch.Tensor, starts: torch.Tensor, F: int, H: int, W: int,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Synthetic decoded clips: uint8 [n, F, H, W, 3], deterministic."""
+    n = int(vids.numel())
+    if vids.is_cuda:
+        from .native import kernels
+        if out is None:
+            out = torch.empty((n, F, H, W, 3), dtype=torch.uint8, device=vids.device)
+        vids = vids.to(torch.int32).contiguous()
+        starts = starts.to(torch.int32).contiguous()
+        kernels().clipgen_u8(out.data_ptr(), vids.data_ptr(), starts.data_ptr(), n, F, H, W,
+                             torch.cuda.current_stream(vids.device).cuda_stream)
+        return out
+    v = vids.to(torch.int64).view(n, 1, 1, 1, 1)
+    f = starts.to(torch.int64).view(n, 1, 1, 1, 1) + torch.arange(F).view(1, F, 1, 1, 1)
+    pix = torch.arange(H * W, dtype=torch.int64).view(1, 1, H, W, 1)
+    c = torch.arange(3, dtype=torch.int64).view(1, 1, 1, 1, 3)
+    res = _pixel_hash_torch(v, f, pix, c)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res.contiguous()
+
+
+def preprocess(frames_u8: torch.Tensor, mean=KINETICS_MEAN, std=KINETICS_STD,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """uint8 [n, F, H, W, 3] -> normalised bf16 [n, F, H, W, 8] (NDHWC)."""
+    n, F, H, W, C = frames_u8.shape
+    assert C == 3
+    if frames_u8.is_cuda:
+        from .native import kernels
+        if out is None:
+            out = torch.empty((n, F, H, W, IN_CHANNELS_P), dtype=torch.bfloat16,
+                              device=frames_u8.device)
+        kernels().preprocess(frames_u8.contiguous().data_ptr(), out.data_ptr(),
+                             n * F * H * W, mean, std,
+                             torch.cuda.current_stream(frames_u8.device).cuda_stream)
+        return out
+    scale = torch.tensor([1.0 / (255.0 * s) for s in std], dtype=torch.float32)
+    shift = torch.tensor([-m / s for m, s in zip(mean, std)], dtype=torch.float32)
+    y = frames_u8.float() * scale + shift
+    res = torch.zeros((n, F, H, W, IN_CHANNELS_P), dtype=torch.bfloat16)
+    res[..., :3] = y.to(torch.bfloat16)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+def ndhwc_to_ncdhw(x: torch.Tensor, channels: int) -> torch.Tensor:
+    """Boundary tensor -> reference NCDHW float32 layout."""
+    return x[..., :channels].permute(0, 4, 1, 2, 3).float().contiguous()
+
+
+def ncdhw_to_ndhwc(x: torch.Tensor, channels_p: int, dtype=torch.bfloat16) -> torch.Tensor:
+    """Reference NCDHW tensor -> NDHWC with channels padded to ``channels_p``."""
+    y = x.permute(0, 2, 3, 4, 1)
+    if y.shape[-1] != channels_p:
+        y = torch.nn.functional.pad(y, (0, channels_p - y.shape[-1]))
+    return y.to(dtype).contiguous()
+
+
+class Head:
+    """AdaptiveAvgPool3d(1) + Linear(C -> classes) on an NDHWC bf16 tensor."""
+
+    def __init__(self, linear: torch.nn.Linear, device: torch.device):
+        self.weight = linear.weight.detach().float().to(device).contiguous()
+        self.bias = linear.bias.detach().float().to(device).contiguous()
+        self.num_classes, self.channels = self.weight.shape
+
+    def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        N, T, H, W, Cs = x.shape
+        if x.is_cuda:
+            from .native import kernels
+            if out is None:
+                out = torch.empty((N, self.num_classes), dtype=torch.float32, device=x.device)
+            kernels().head(x.data_ptr(), self.weight.data_ptr(), self.bias.data_ptr(),
+                           out.data_ptr(), N, T * H * W, self.channels, Cs, self.num_classes,
+                           torch.cuda.current_stream(x.device).cuda_stream)
+            return out
+        return self.forward_torch(x)
+
+    def forward_torch(self, x: torch.Tensor) -> torch.Tensor:
+        pooled = x[..., :self.channels].float().mean(dim=(1, 2, 3))
+        return pooled @ self.weight.to(x.device).t() + self.bias.to(x.device)
+
+
+def video_reduce(logits: torch.Tensor, offsets: torch.Tensor,
+                 sums: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Sum clip logits per video ([offsets[v], offsets[v+1]) rows) + argmax."""
+    nvid = offsets.numel() - 1
+    ncls = logits.shape[1]
+    if logits.is_cuda:
+        from .native import kernels
+        if sums is None:
+            sums = torch.empty((nvid, ncls), dtype=torch.float32, device=logits.device)
+        arg = torch.empty((nvid,), dtype=torch.int32, device=logits.device)
+        kernels().video_reduce(logits.contiguous().data_ptr(),
+                               offsets.to(torch.int32).contiguous().data_ptr(),
+                               sums.data_ptr(), arg.data_ptr(), nvid, ncls,
+                               torch.cuda.current_stream(logits.device).cuda_stream)
+        return sums, arg
+    off = offsets.tolist()
+    out = torch.stack([logits[off[v]:off[v + 1]].sum(0) for v in range(nvid)]) \
+        if nvid else torch.zeros((0, ncls))
+    arg = torch.tensor([int(torch.argmax(out[v])) if off[v + 1] > off[v] else -1
+                        for v in range(nvid)], dtype=torch.int32)
+    return out, arg

@@ -1,0 +1,180 @@
+"""RCCL send/recv slot ring for cross-GPU pipeline edges.
+
+The BASELINE north star moves inter-stage clip tensors GPU-to-GPU with RCCL
+send/recv over xGMI instead of host-side queues. Pipeline queues are dynamic
+(any consumer replica may dequeue any item: reference control.py:167-205),
+while RCCL point-to-point needs both peers to know each other. ``RcclRing``
+bridges that with a *claim handshake* (SURVEY.md §7.4 item 3):
+
+1. the producer writes its output into a local HBM slot and enqueues a
+   ``Signal`` on the pipeline queue (control plane unchanged);
+2. the consumer that dequeues it posts ``(slot, my_rank)`` on the ring's claim
+   queue and immediately posts ``recv`` from the producer's rank;
+3. the producer's sender thread pops claims in order and issues ``send`` of
+   the slot's valid rows to the claimer, waits for completion, then frees the
+   slot.
+
+Per (src, dst) pair the claims are served in the order the consumer posted
+them, so sends and receives match. All participating runners form one
+``torch.distributed`` world (backend ``nccl`` = RCCL on ROCm; ``gloo`` for the
+CPU tests) created by the launcher-assigned ``DistInfo``. RCCL cannot put two
+ranks of one communicator on the same GPU, so the launcher only allows this
+transport on edges whose producer and consumers sit on different GPUs.
+"""
+from __future__ import annotations
+
+import os
+import queue
+import threading
+from typing import Optional
+
+import torch
+
+from .transport import RingBase
+
+_state = {"rank": None, "world": None, "backend": None}
+
+
+class DistInfo:
+    """Picklable description of this process's place in the RCCL world."""
+
+    def __init__(self, rank: int, world_size: int, store_path: str, backend: str):
+        self.rank, self.world_size = rank, world_size
+        self.store_path, self.backend = store_path, backend
+
+
+def init_dist(info: Optional[DistInfo], device: torch.device) -> None:
+    if info is None or _state["rank"] is not None:
+        return
+    import torch.distributed as dist
+    store = dist.FileStore(info.store_path, info.world_size)
+    kwargs = {}
+    if info.backend == "nccl":
+        kwargs["device_id"] = device
+    dist.init_process_group(info.backend, store=store, rank=info.rank,
+                            world_size=info.world_size, **kwargs)
+    _state.update(rank=info.rank, world=info.world_size, backend=info.backend)
+
+
+def shutdown_dist() -> None:
+    if _state["rank"] is None:
+        return
+    import torch.distributed as dist
+    try:
+        dist.destroy_process_group()
+    finally:
+        _state.update(rank=None, world=None, backend=None)
+
+
+def my_rank() -> int:
+    if _state["rank"] is None:
+        raise RuntimeError("RCCL transport used before the process joined the world")
+    return _state["rank"]
+
+
+class RcclRing(RingBase):
+    kind = "rccl"
+
+    def __init__(self, ctx, shapes, dtypes, num_slots, name, producer_gpu):
+        super().__init__(ctx, shapes, dtypes, num_slots, name, producer_gpu)
+        self.claims = ctx.Queue()
+        self.producer_rank = None          # assigned by the launcher
+        self._slots = None
+        self._thread = None
+        self._stop = None
+        self._error = None
+
+    def __getstate__(self):
+        st = dict(self.__dict__)
+        st["_slots"] = None
+        st["_thread"] = None
+        st["_stop"] = None
+        return st
+
+    # ---- producer ----
+    def producer_attach(self, device):
+        self.device = device
+        self._slots = [tuple(torch.empty(s, dtype=d, device=device)
+                             for s, d in zip(self.shapes, self.dtypes))
+                       for _ in range(self.num_slots)]
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._serve, name="rccl-send-" + self.name,
+                                        daemon=True)
+        self._thread.start()
+
+    def _serve(self):
+        import torch.distributed as dist
+        stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
+        with ctx:
+            while not self._stop.is_set():
+                try:
+                    claim = self.claims.get(timeout=0.1)
+                except queue.Empty:
+                    continue
+                if claim is None:
+                    break
+                idx, dst = claim
+                try:
+                    for t, rows in zip(self._slots[idx], self.valid_rows(idx)):
+                        if rows:
+                            dist.send(t[:rows], dst)
+                    if stream is not None:
+                        stream.synchronize()
+                except Exception as err:  # surfaced on the producer's next write
+                    self._error = err
+                    break
+                self.events[idx].set()
+
+    def write(self, idx, tensors):
+        if self._error is not None:
+            raise RuntimeError("RCCL sender failed: %s" % self._error)
+        rows = []
+        for dst, src in zip(self._slots[idx], tensors):
+            b = src.shape[0]
+            if b > dst.shape[0]:
+                raise ValueError("output of %d rows exceeds slot capacity %d (%s)"
+                                 % (b, dst.shape[0], self.name))
+            if b:
+                dst[:b].copy_(src)
+            rows.append(b)
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        self._set_valid(idx, rows)
+        self.events[idx].clear()
+
+    def descriptor(self):
+        return self.producer_rank
+
+    def close(self):
+        if self._thread is not None:
+            self._stop.set()
+            self.claims.put(None)
+            self._thread.join(timeout=10.0)
+            self._thread = None
+
+    # ---- consumer ----
+    def read_into(self, idx, placeholders, descriptor=None):
+        import torch.distributed as dist
+        src = self.producer_rank if descriptor is None else descriptor
+        self.claims.put((idx, my_rank()))
+        out = []
+        for ph, rows in zip(placeholders, self.valid_rows(idx)):
+            if rows:
+                dist.recv(ph[:rows], src)
+            out.append(ph[:rows])
+        if placeholders and placeholders[0].is_cuda:
+            torch.cuda.current_stream(placeholders[0].device).synchronize()
+        return out
+
+    def release(self, idx):
+        # the producer frees the slot once its send has completed
+        pass
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False

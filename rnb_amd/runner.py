@@ -1,0 +1,276 @@
+"""Per-replica runner process: the pipeline's hot loop.
+
+Behaviour follows reference runner.py:5-271 step for step (dequeue ->
+pull input slot -> model -> segment/push output slots -> enqueue signals, or
+count + record on the final step; exit markers and slot release on shutdown)
+with these MI355X-first changes:
+
+* one private HIP stream per runner (``torch.cuda.Stream``), the model and
+  all slot traffic run on it; the GPU engine replays HIP graphs;
+* slot hand-off is race-free: pulls/pushes complete before a slot is released
+  or marked full (``parallel/transport.py``), fixing SURVEY.md §5.2 races 1-2;
+* every blocking wait is bounded and re-checks the termination flag, barriers
+  carry timeouts, and an exception in any runner sets ``CHILD_FAILED`` and
+  aborts the barriers instead of leaving the job hung;
+* empty segments are forwarded as 0-row slots (the consumer model returns a
+  0-row output) so segment counts stay consistent for the aggregator;
+* the final step reports its ``TimeCardSummary`` to the launcher so p50/p99
+  can be computed over the whole node.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+import traceback
+from queue import Empty, Full
+
+NUM_EXIT_MARKERS = 10
+NUM_SUMMARY_SKIPS = 10
+QUEUE_POLL_S = 0.1
+
+
+def _set_flag(flag, value, only_if_unset=True):
+    from .control import TerminationFlag
+    with flag.get_lock():
+        if not only_if_unset or flag.value == TerminationFlag.UNSET:
+            flag.value = value
+
+
+def runner(input_queue, output_queues, queue_selector_path, print_summary,
+           job_id, g_idx, group_idx, instance_idx,
+           global_inference_counter, num_videos,
+           termination_flag, step_idx,
+           sta_bar, fin_bar,
+           model_module_path, num_segments,
+           shared_input_rings, shared_output_ring,
+           result_queue=None, barrier_timeout=None, dist_info=None,
+           **model_kwargs):
+    """Entry point of one runner process (spawned by the launcher)."""
+    from threading import BrokenBarrierError
+    from .control import TerminationFlag
+    try:
+        _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
+                     job_id, g_idx, group_idx, instance_idx, global_inference_counter,
+                     num_videos, termination_flag, step_idx, sta_bar, fin_bar,
+                     model_module_path, num_segments, shared_input_rings,
+                     shared_output_ring, result_queue, barrier_timeout, dist_info,
+                     model_kwargs)
+    except BrokenBarrierError:
+        _set_flag(termination_flag, TerminationFlag.BARRIER_TIMEOUT)
+        print("[runner %d/%d/%d] barrier broken or timed out" % (step_idx, group_idx,
+                                                                instance_idx),
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    except BaseException:
+        _set_flag(termination_flag, TerminationFlag.CHILD_FAILED)
+        traceback.print_exc()
+        for bar in (sta_bar, fin_bar):
+            try:
+                bar.abort()
+            except Exception:
+                pass
+        sys.stderr.flush()
+        sys.exit(1)
+
+
+def _runner_body(input_queue, output_queues, queue_selector_path, print_summary, job_id,
+                 g_idx, group_idx, instance_idx, global_inference_counter, num_videos,
+                 termination_flag, step_idx, sta_bar, fin_bar, model_module_path,
+                 num_segments, shared_input_rings, shared_output_ring, result_queue,
+                 barrier_timeout, dist_info, model_kwargs):
+    import contextlib
+    import torch
+    from .control import TerminationFlag, Signal, segment_bounds
+    from .timecard import TimeCardSummary, TimeCardList, logname
+    from .utils.class_utils import load_class
+
+    fault = os.environ.get("RNB_FAULT_INJECT", "")
+    if fault == "runner%d_init" % step_idx:
+        raise RuntimeError("injected fault in runner%d init" % step_idx)
+
+    use_gpu = g_idx >= 0
+    if use_gpu:
+        torch.cuda.set_device(g_idx)
+        device = torch.device("cuda:%d" % g_idx)
+        stream = torch.cuda.Stream(device=device)
+        stream_ctx = torch.cuda.stream(stream)
+    else:
+        device = torch.device("cpu")
+        stream = None
+        stream_ctx = contextlib.nullcontext()
+        torch.set_num_threads(max(1, int(os.environ.get("RNB_CPU_THREADS", "2"))))
+
+    if dist_info is not None:
+        from .parallel.rccl_channel import init_dist
+        init_dist(dist_info, device)
+
+    is_final_step = output_queues is None
+    with stream_ctx, torch.no_grad():
+        model = load_class(model_module_path)(device, **model_kwargs)
+        if is_final_step:
+            summary = TimeCardSummary()
+            selector = None
+        else:
+            sel_cls = load_class(queue_selector_path)
+            selector = sel_cls(len(output_queues))
+        out_counter = 0
+
+        if shared_output_ring is not None:
+            shared_output_ring.producer_attach(device)
+
+        placeholders = None
+        if shared_input_rings is not None:
+            shapes, dtypes = None, None
+            for rings in shared_input_rings.values():
+                for ring in rings:
+                    if ring is None:
+                        continue
+                    ring.consumer_attach(device)
+                    if shapes is None:
+                        shapes, dtypes = ring.shapes, ring.dtypes
+                    else:
+                        shapes = tuple(tuple(max(a, b) for a, b in zip(s1, s2))
+                                       for s1, s2 in zip(shapes, ring.shapes))
+            placeholders = tuple(torch.zeros(s, dtype=d, device=device)
+                                 for s, d in zip(shapes, dtypes))
+
+        def aborted():
+            return termination_flag.value != TerminationFlag.UNSET
+
+        sta_bar.wait(barrier_timeout)
+        progress = None
+        if print_summary and os.environ.get("RNB_NO_TQDM") != "1":
+            try:
+                from tqdm import tqdm
+                progress = tqdm(total=num_videos, file=sys.stdout, mininterval=1.0)
+            except Exception:
+                progress = None
+        last_count = 0
+        items = 0
+
+        while termination_flag.value == TerminationFlag.UNSET:
+            try:
+                tpl = input_queue.get(timeout=QUEUE_POLL_S)
+            except Empty:
+                continue
+            if tpl is None:
+                break
+            signal, non_tensor_inputs, time_card = tpl
+            time_card.add_gpu(g_idx)
+            time_card.record("runner%d_start" % step_idx)
+
+            if signal is not None:
+                ring = shared_input_rings[signal.group_idx][signal.instance_idx]
+                if ring.is_free(signal.tensor_idx) and aborted():
+                    break
+                tensor_inputs = ring.read_into(signal.tensor_idx, placeholders, signal.ring)
+                ring.release(signal.tensor_idx)
+            else:
+                tensor_inputs = None
+
+            time_card.record("inference%d_start" % step_idx)
+            items += 1
+            if fault == "runner%d_item%d" % (step_idx, items):
+                raise RuntimeError("injected fault in runner%d at item %d"
+                                   % (step_idx, items))
+            tensor_outputs, non_tensor_outputs, time_card = \
+                model(tensor_inputs, non_tensor_inputs, time_card)
+            if stream is not None:
+                stream.synchronize()
+            if time_card is None:
+                continue
+            time_card.record("inference%d_finish" % step_idx)
+
+            if is_final_step:
+                n_inf = len(time_card.time_cards) if isinstance(time_card, TimeCardList) else 1
+                stop = False
+                with global_inference_counter.get_lock():
+                    prev = global_inference_counter.value
+                    global_inference_counter.value = prev + n_inf
+                    now = global_inference_counter.value
+                if now >= num_videos:
+                    if prev < num_videos:
+                        print("Finished processing %d videos" % num_videos, flush=True)
+                        _set_flag(termination_flag,
+                                  TerminationFlag.TARGET_NUM_VIDEOS_REACHED)
+                    else:
+                        stop = True
+                if progress is not None and now > last_count:
+                    progress.update(min(now, num_videos) - min(last_count, num_videos))
+                    last_count = now
+                if stop:
+                    break
+                cards = time_card.time_cards if isinstance(time_card, TimeCardList) \
+                    else [time_card]
+                for tc in cards:
+                    summary.register(tc)
+                continue
+
+            # ---- non-final step: push segments into slots, enqueue signals
+            out_q = output_queues[selector.select(tensor_outputs, non_tensor_outputs,
+                                                  time_card)]
+            msgs = []
+            for seg in range(num_segments):
+                signal_out = None
+                if shared_output_ring is not None:
+                    seg_tensors = []
+                    for t in tensor_outputs:
+                        a, b = segment_bounds(t.shape[0], num_segments, seg)
+                        seg_tensors.append(t[a:b])
+                    slot = out_counter % len(shared_output_ring)
+                    if not shared_output_ring.wait_free(slot, aborted):
+                        break
+                    shared_output_ring.write(slot, seg_tensors)
+                    signal_out = Signal(group_idx, instance_idx, slot,
+                                        shared_output_ring.descriptor())
+                    out_counter = (out_counter + 1) % len(shared_output_ring)
+                tc = time_card.fork(seg) if num_segments > 1 else time_card
+                msgs.append((signal_out, non_tensor_outputs, tc))
+            if len(msgs) != num_segments:
+                break
+            try:
+                for m in msgs:
+                    out_q.put_nowait(m)
+            except Full:
+                print("[WARNING] Queue between runner step %d and %d is full. "
+                      "Aborting..." % (step_idx, step_idx + 1), flush=True)
+                _set_flag(termination_flag, TerminationFlag.FRAME_QUEUE_FULL)
+                break
+
+        # ---- shutdown
+        if not is_final_step:
+            try:
+                for _ in range(NUM_EXIT_MARKERS):
+                    for q in output_queues:
+                        q.put_nowait(None)
+            except Full:
+                pass
+        if shared_input_rings is not None:
+            for rings in shared_input_rings.values():
+                for ring in rings:
+                    if ring is not None:
+                        ring.release_all()
+
+    fin_bar.wait(barrier_timeout)
+    if output_queues is not None:
+        for q in output_queues:
+            q.cancel_join_thread()
+    if is_final_step:
+        with open(logname(job_id, g_idx, group_idx, instance_idx), "w") as f:
+            summary.save_full_report(f)
+        if result_queue is not None:
+            result_queue.put(("summary", step_idx, group_idx, instance_idx, summary))
+        if print_summary:
+            if progress is not None:
+                progress.close()
+            summary.print_summary(NUM_SUMMARY_SKIPS)
+    if shared_output_ring is not None and hasattr(shared_output_ring, "close"):
+        # consumers have passed fin_bar, so no one still reads these slots
+        try:
+            shared_output_ring.close()
+        except Exception:
+            pass
+    if dist_info is not None:
+        from .parallel.rccl_channel import shutdown_dist
+        shutdown_dist()

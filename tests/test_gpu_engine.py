@@ -1,0 +1,143 @@
+"""End-to-end GPU tests: engine, graphs, fused serving path, IPC, tracer."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+def _engines(start, end, depth=18):
+    from rnb_amd.models.r2p1d.model import build_network
+    from rnb_amd.models.r2p1d.engine import R2P1DEngine
+    net = build_network(start, end, depth=depth, seed=3)
+    return (R2P1DEngine(net, DEV, backend="hip"), R2P1DEngine(net, DEV, backend="torch"),
+            R2P1DEngine(net, DEV, backend="module"))
+
+
+@pytest.mark.parametrize("rng", [(1, 5), (1, 2), (3, 5), (2, 4)])
+def test_engine_hip_matches_torch_plan(rng):
+    hip, ref, mod = _engines(*rng)
+    x = torch.randn(hip.input_shape(3), device=DEV).to(torch.bfloat16)
+    if rng[0] == 1:
+        x[..., 3:] = 0
+    y = hip.forward(x).float()
+    r = ref.forward(x).float()
+    m = mod.forward(x).float()
+    torch.cuda.synchronize()
+    scale = r.abs().max().item()
+    assert (y - r).abs().max().item() <= 3e-2 * scale + 3e-2
+    # folded bf16 plan vs the unfolded fp32 nn.Module
+    assert (r - m).abs().max().item() <= 5e-2 * scale + 5e-2
+
+
+def test_r34_full_forward_close_to_module():
+    hip, ref, mod = _engines(1, 5, depth=34)
+    from rnb_amd.models.r2p1d.decoder import SyntheticDecoder
+    x = SyntheticDecoder(DEV).decode(11, [0, 100, 200])
+    y = hip.forward(x)
+    m = mod.forward(x)
+    torch.cuda.synchronize()
+    rel = (y - m).abs().max().item() / m.abs().max().item()
+    assert rel < 5e-2, rel
+    assert torch.equal(y.argmax(1), m.argmax(1)) or rel < 1e-2
+
+
+def test_graphed_engine_matches_eager():
+    from rnb_amd.models.r2p1d.engine import GraphedEngine
+    hip, _, _ = _engines(1, 5)
+    ge = GraphedEngine(hip, max_clips=6, buckets=(1, 2, 4), autotune=False)
+    for n in (1, 3, 6):
+        x = torch.randn(hip.input_shape(n), device=DEV).to(torch.bfloat16)
+        x[..., 3:] = 0
+        a = ge(x).clone()
+        b = hip.forward(x)
+        torch.cuda.synchronize()
+        assert torch.allclose(a, b, atol=1e-3, rtol=1e-3)
+
+
+def test_fused_serving_matches_stepwise():
+    from rnb_amd.models.r2p1d.fused import FusedR2P1D
+    from rnb_amd.models.r2p1d.decoder import SyntheticDecoder
+    from rnb_amd.ops import video as vops
+    f = FusedR2P1D(DEV, depth=18, replicas=2, max_clips=32, max_videos=4,
+                   buckets=(4, 16, 32), autotune=False)
+    videos = [(5, [0, 50]), (9, [3]), (12, list(range(0, 120, 8))), (20, [7])]
+    ev, out, nvid = f.replicas[1].submit(videos)
+    ev.synchronize()
+    got = out.tolist()
+    dec = SyntheticDecoder(DEV)
+    want = []
+    for vid, st in videos:
+        logits = f.engine.forward(dec.decode(vid, st))
+        want.append(int(logits.float().sum(0).argmax()))
+    assert got == want
+
+
+def test_autotune_picks_valid_config():
+    hip, _, _ = _engines(1, 5)
+    chosen = hip.autotune(2, reps=1)
+    from rnb_amd.ops.native import kernels
+    assert all(0 <= c < len(kernels().configs) for c in chosen.values())
+
+
+def _ipc_child(q_in, q_out):
+    import torch
+    from rnb_amd.ops import native
+    rt = native.runtime()
+    torch.cuda.set_device(0)
+    handle, nbytes = q_in.get()
+    ptr = rt.ipc_open_handle(handle)
+    dst = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda:0")
+    s = torch.cuda.current_stream()
+    rt.memcpy_async(dst.data_ptr(), ptr, nbytes, s.cuda_stream)
+    s.synchronize()
+    q_out.put(dst.sum().item())
+    rt.ipc_close_handle(ptr)
+
+
+def test_hip_ipc_roundtrip_two_processes():
+    import torch.multiprocessing as mp
+    from rnb_amd.ops import native
+    rt = native.runtime()
+    torch.cuda.set_device(0)
+    n = 1 << 12
+    ptr = rt.ipc_malloc(n * 4)
+    src = torch.arange(n, dtype=torch.float32, device=DEV)
+    rt.memcpy_async(ptr, src.data_ptr(), n * 4, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ctx = mp.get_context("spawn")
+    q_in, q_out = ctx.Queue(), ctx.Queue()
+    p = ctx.Process(target=_ipc_child, args=(q_in, q_out))
+    p.start()
+    q_in.put((rt.ipc_get_handle(ptr), n * 4))
+    total = q_out.get(timeout=120)
+    p.join(60)
+    rt.free(ptr)
+    assert p.exitcode == 0
+    assert total == float(n * (n - 1) // 2)
+
+
+def test_tracer_reports_kernels():
+    from rnb_amd.profiling import tracer
+    hip, _, _ = _engines(1, 5)
+    x = torch.zeros(hip.input_shape(1), device=DEV, dtype=torch.bfloat16)
+    tracer.initialize()
+    hip.forward(x)
+    torch.cuda.synchronize()
+    tracer.flush()
+    recs = tracer.report()
+    names = [r[0] for r in recs]
+    assert len(recs) >= 40, len(recs)
+    assert any("conv_igemm" in n for n in names), names[:5]
+    assert all(e >= s for _, s, e in recs)
+
+
+def test_native_libraries_loaded_from_tree():
+    from rnb_amd.ops import native
+    native.kernels()
+    paths = native.loaded_paths()
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    assert any(p.startswith(here) for p in paths)

@@ -1,0 +1,131 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references (GPU only)."""
+import pytest
+import torch
+
+from rnb_amd.ops.conv import ConvGeom, ConvLayer
+from rnb_amd.ops import video as vops
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+# (cin, cout, kernel, stride, padding, (T, H, W)) covering SURVEY.md K1..K22 roles
+CONV_CASES = [
+    (3, 83, (1, 7, 7), (1, 2, 2), (0, 3, 3), (8, 112, 112)),     # K1 stem spatial
+    (83, 64, (3, 1, 1), (1, 1, 1), (1, 0, 0), (8, 56, 56)),      # K2 stem temporal
+    (64, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1), (8, 56, 56)),     # K3
+    (144, 64, (3, 1, 1), (1, 1, 1), (1, 0, 0), (8, 56, 56)),     # K4
+    (64, 230, (1, 3, 3), (1, 2, 2), (0, 1, 1), (8, 56, 56)),     # K5
+    (230, 128, (3, 1, 1), (2, 1, 1), (1, 0, 0), (8, 28, 28)),    # K6
+    (64, 42, (1, 1, 1), (1, 2, 2), (0, 0, 0), (8, 56, 56)),      # K9
+    (42, 128, (1, 1, 1), (2, 1, 1), (0, 0, 0), (8, 28, 28)),     # K10
+    (256, 576, (1, 3, 3), (1, 1, 1), (0, 1, 1), (2, 14, 14)),    # K13
+    (256, 921, (1, 3, 3), (1, 2, 2), (0, 1, 1), (2, 14, 14)),    # K17
+    (921, 512, (3, 1, 1), (2, 1, 1), (1, 0, 0), (2, 7, 7)),      # K18
+    (512, 1152, (1, 3, 3), (1, 1, 1), (0, 1, 1), (1, 7, 7)),     # K19
+    (1152, 512, (3, 1, 1), (1, 1, 1), (1, 0, 0), (1, 7, 7)),     # K20
+]
+
+
+def _layer(cin, cout, k, s, p, relu=True, seed=0, integer=False):
+    g = torch.Generator().manual_seed(seed)
+    if integer:
+        w = torch.randint(-2, 3, (cout, cin) + k, generator=g).float()
+        b = torch.randint(-4, 5, (cout,), generator=g).float()
+    else:
+        fan = cin * k[0] * k[1] * k[2]
+        w = torch.randn((cout, cin) + k, generator=g) * (2.0 / fan) ** 0.5
+        b = torch.randn(cout, generator=g) * 0.1
+    geom = ConvGeom(cin, cout, k, s, p)
+    return ConvLayer(w, b, geom, relu, DEV, "test")
+
+
+def _input(n, thw, cin_p, cin, integer=False, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    if integer:
+        x = torch.randint(-3, 4, (n,) + thw + (cin_p,), generator=g).float()
+    else:
+        x = torch.randn((n,) + thw + (cin_p,), generator=g)
+    x[..., cin:] = 0
+    return x.to(torch.bfloat16).to(DEV)
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: "%dx%d_k%s_s%s" % (c[0], c[1], "".join(map(str, c[2])), "".join(map(str, c[3]))))
+def test_conv_matches_torch(case):
+    cin, cout, k, s, p, thw = case
+    layer = _layer(cin, cout, k, s, p)
+    x = _input(2, thw, layer.geom.cin_p, cin)
+    y = layer.forward_hip(x)
+    ref = layer.forward_torch(x, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    err = (y.float() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= 1e-2 * scale + 1e-2, (err, scale)
+
+
+@pytest.mark.parametrize("cfg", range(14))
+def test_conv_every_tile_config_exact_integers(cfg):
+    """Small-integer data is exact in bf16/fp32: any layout bug shows up."""
+    from rnb_amd.ops.native import kernels
+    if cfg >= len(kernels().configs):
+        pytest.skip("config not built")
+    layer = _layer(64, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False, integer=True)
+    x = _input(1, (2, 15, 13), 64, 64, integer=True)
+    y = layer.forward_hip(x, config=cfg)
+    ref = layer.forward_torch(x, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert torch.equal(y.float(), ref), (y.float() - ref).abs().max().item()
+
+
+def test_conv_residual_relu_epilogue():
+    layer = _layer(144, 64, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=True, integer=True)
+    x = _input(3, (4, 9, 11), 144, 144, integer=True)
+    res = _input(3, (4, 9, 11), 64, 64, integer=True, seed=5)
+    y = layer.forward_hip(x, residual=res)
+    ref = layer.forward_torch(x, residual=res, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert torch.equal(y.float(), ref)
+
+
+def test_conv_odd_m_tail_and_padding_channels():
+    layer = _layer(42, 85, (1, 1, 1), (2, 2, 2), (0, 0, 0), integer=True)
+    x = _input(1, (3, 5, 7), layer.geom.cin_p, 42, integer=True)
+    y = layer.forward_hip(x)
+    ref = layer.forward_torch(x, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert y.shape[-1] == 88
+    assert torch.equal(y.float(), ref)
+    assert torch.count_nonzero(y[..., 85:]) == 0
+
+
+def test_head_matches_torch():
+    lin = torch.nn.Linear(512, 400)
+    head = vops.Head(lin, DEV)
+    x = torch.randn(5, 1, 7, 7, 512).to(torch.bfloat16).to(DEV)
+    y = head.forward(x)
+    ref = head.forward_torch(x)
+    torch.cuda.synchronize()
+    assert torch.allclose(y, ref, atol=1e-4, rtol=1e-4)
+
+
+def test_video_reduce_matches_torch():
+    logits = torch.randn(11, 400, device=DEV)
+    offs = torch.tensor([0, 1, 1, 6, 11], dtype=torch.int32, device=DEV)
+    sums, arg = vops.video_reduce(logits, offs)
+    rs, ra = vops.video_reduce(logits.cpu(), offs.cpu())
+    torch.cuda.synchronize()
+    assert torch.allclose(sums.cpu(), rs, atol=1e-4)
+    assert arg.cpu().tolist() == ra.tolist()
+    assert arg.cpu().tolist()[1] == -1
+
+
+def test_clipgen_and_preprocess_bit_exact():
+    vids = torch.tensor([3, 3, 17], dtype=torch.int32)
+    starts = torch.tensor([0, 40, 9], dtype=torch.int32)
+    g = vops.clipgen_u8(vids.to(DEV), starts.to(DEV), 8, 112, 112)
+    c = vops.clipgen_u8(vids, starts, 8, 112, 112)
+    assert torch.equal(g.cpu(), c)
+    pg = vops.preprocess(g)
+    pc = vops.preprocess(c)
+    torch.cuda.synchronize()
+    assert torch.equal(pg.cpu().float(), pc.float())
