@@ -9,7 +9,11 @@ Same three-call API as the reference's CUPTI bridge::
     for name, start_ns, end_ns in tracer.report():   # report() also clears
         ...
 
-plus ``report_full()`` (op kind and device per record) and ``summary()``
+``initialize()`` must run before the process initialises the HIP runtime
+(before the first ``torch.cuda`` call): roctracer registers its activity
+callbacks with the HIP runtime at start-up through rocprofiler-register.
+
+Also ``report_full()`` (op kind and device per record) and ``summary()``
 (per-kernel count / total / mean time) for quick breakdowns inside a runner.
 Backed by ``librnb_tracer.so`` (csrc/tracer.cpp).
 """

@@ -1,0 +1,78 @@
+"""Per-layer timing of the R(2+1)D HIP engine (eager, HIP events).
+
+    python scripts/profile_layers.py --depth 34 --clips 64 [--autotune]
+
+Prints, for every conv of the plan, its GEMM shape, chosen tile, time and
+achieved TFLOP/s (useful FLOPs; padding excluded), then the totals. Writes the
+table as JSON with --json-out.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from rnb_amd.models.r2p1d.model import build_network  # noqa: E402
+from rnb_amd.models.r2p1d.engine import R2P1DEngine  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--depth", type=int, default=34)
+    ap.add_argument("--clips", type=int, default=64)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--autotune", action="store_true")
+    ap.add_argument("--json-out", default=None)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    eng = R2P1DEngine(build_network(1, 5, depth=args.depth), dev, backend="hip")
+    n = args.clips
+    if args.autotune:
+        eng.autotune(n)
+    x = torch.randn(eng.input_shape(n), device=dev).to(torch.bfloat16)
+    x[..., 3:] = 0
+    bufs = {"x": x}
+    rows = []
+    from rnb_amd.ops.native import kernels
+    cfgs = kernels().configs
+    for op in eng.ops:
+        src = bufs[op.src]
+        res = bufs[op.res] if op.res is not None else None
+        y = op.layer.forward_hip(src, res)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(args.reps):
+            op.layer.forward_hip(src, res, out=y)
+        e.record()
+        e.synchronize()
+        ms = s.elapsed_time(e) / args.reps
+        g = op.layer.geom
+        N, T, H, W, _ = src.shape
+        flops = g.flops(N, T, H, W)
+        To, Ho, Wo = g.out_thw(T, H, W)
+        cid = op.layer.config_for(src.shape)
+        rows.append({"name": op.layer.name, "M": N * To * Ho * Wo, "N": g.cout,
+                     "K": g.cin * g.kernel[0] * g.kernel[1] * g.kernel[2],
+                     "tile": "%dx%d" % cfgs[cid], "ms": ms,
+                     "tflops": flops / ms / 1e9, "gflop": flops / 1e9})
+        bufs[op.dst] = y
+    tot_ms = sum(r["ms"] for r in rows)
+    tot_gf = sum(r["gflop"] for r in rows)
+    for r in rows:
+        print("%-34s M=%8d N=%5d K=%5d tile=%-8s %8.3f ms %7.1f TF (%4.1f%%)"
+              % (r["name"], r["M"], r["N"], r["K"], r["tile"], r["ms"], r["tflops"],
+                 100 * r["ms"] / tot_ms))
+    print("TOTAL %d convs: %.3f ms for %d clips = %.1f TFLOP/s, %.1f clips/s"
+          % (len(rows), tot_ms, n, tot_gf / tot_ms, n / tot_ms * 1e3))
+    if args.json_out:
+        with open(args.json_out, "w") as f:
+            json.dump({"clips": n, "depth": args.depth, "rows": rows,
+                       "total_ms": tot_ms, "tflops": tot_gf / tot_ms}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -4,16 +4,17 @@ Runs a Conv2d(3, 64, k=11, s=4) like the reference and prints each kernel's
 name and start/end timestamps, then a per-kernel summary of one R(2+1)D-18
 forward through the HIP engine.
 """
-import torch
-
 from rnb_amd.profiling import tracer
+
+tracer.initialize()     # roctracer must register before the HIP runtime starts
+import torch  # noqa: E402
 
 
 def main():
     dev = torch.device("cuda:0")
     model = torch.nn.Conv2d(3, 64, kernel_size=11, stride=4, padding=2).to(dev)
     x = torch.randn(4, 3, 224, 224, device=dev)
-    tracer.initialize()
+    tracer.report()
     model(x)
     torch.cuda.synchronize()
     tracer.flush()

@@ -120,19 +120,36 @@ def test_hip_ipc_roundtrip_two_processes():
     assert total == float(n * (n - 1) // 2)
 
 
+_TRACER_CHILD = r"""
+import sys
+sys.path.insert(0, %r)
+from rnb_amd.profiling import tracer
+tracer.initialize()            # must precede HIP runtime initialisation
+import torch
+from rnb_amd.models.r2p1d.model import build_network
+from rnb_amd.models.r2p1d.engine import R2P1DEngine
+dev = torch.device("cuda:0")
+hip = R2P1DEngine(build_network(1, 5, depth=18), dev, backend="hip")
+x = torch.zeros(hip.input_shape(1), device=dev, dtype=torch.bfloat16)
+hip.forward(x)
+torch.cuda.synchronize()
+tracer.flush()
+recs = tracer.report()
+names = [r[0] for r in recs]
+assert len(recs) >= 40, len(recs)
+assert any("conv_igemm" in n for n in names), names[:5]
+assert all(e >= s for _, s, e in recs)
+print("TRACER_OK", len(recs))
+"""
+
+
 def test_tracer_reports_kernels():
-    from rnb_amd.profiling import tracer
-    hip, _, _ = _engines(1, 5)
-    x = torch.zeros(hip.input_shape(1), device=DEV, dtype=torch.bfloat16)
-    tracer.initialize()
-    hip.forward(x)
-    torch.cuda.synchronize()
-    tracer.flush()
-    recs = tracer.report()
-    names = [r[0] for r in recs]
-    assert len(recs) >= 40, len(recs)
-    assert any("conv_igemm" in n for n in names), names[:5]
-    assert all(e >= s for _, s, e in recs)
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, "-c", _TRACER_CHILD % here],
+                         capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0 and "TRACER_OK" in res.stdout, res.stdout + res.stderr
 
 
 def test_native_libraries_loaded_from_tree():
