@@ -17,10 +17,8 @@
 // (TP*16 pixels) x (TC*16 channels). BK = 64: an LDS row is 128 B = 8 chunks
 // of 16 B, XOR-swizzled (chunk ^ (row & 7)) so the ds_read_b128 fragment
 // reads are bank-conflict free (cdna_hip_programming.md T2). The K loop is
-// register-staged and double-buffered with one barrier per K-step: the next
-// step's global loads are issued before the MFMAs of the current step.
-// Activation gathers use buffer loads whose out-of-range offset returns zero,
-// which implements the conv zero padding and the M/K tails without branches.
+// staged by LDS-DMA and double-buffered with one barrier per K-step (details
+// at the kernel below).
 // Block ids are remapped so consecutive tiles share an XCD's L2 (T1).
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
@@ -51,6 +49,15 @@ struct ConvParams {
   int n_ptiles, n_ctiles;
   uint32_t x_bytes;       // buffer range of x for the zero-fill gathers
   int w_rows;             // allocated weight/bias rows (>= n_ctiles * C_TILE)
+  const int2* ktab;       // [K_pad/8] per 16-B K chunk: {byte delta, required mask}
+  // magic-number division by Wo, Ho, To (set by the launcher): q = umulhi(n, m) >> s
+  uint32_t mWo, sWo, mHo, sHo, mTo, sTo;
+  // row order: 0 = raster (n, t, h, w); 1 = time-major groups of 16 output
+  // pixels: m = ((n * ngroups + g) * To + t) * 16 + j, pixel hw = 16 g + j, so a
+  // tile holds every output frame of its pixels and the temporal taps of the
+  // input are reused on chip instead of being re-fetched from HBM.
+  int row_mode, ngroups;
+  uint32_t mG, sG;
 };
 
 #define INVALID_OFF 0xFFFFFFF0u
@@ -59,8 +66,61 @@ static __device__ __forceinline__ uint16_t f2bf(float f) {
   __hip_bfloat16 h = __float2bfloat16(f);
   return __builtin_bit_cast(uint16_t, h);
 }
+// n / d for 0 <= n < 2^31 with a host-computed (m, s); m == 0 encodes d == 1
+static __device__ __forceinline__ int fast_div(int n, uint32_t m, uint32_t s) {
+  return m ? (int)(__umulhi((uint32_t)n, m) >> s) : n;
+}
+// bits [lo, hi) of the taps d in [0, K) with 0 <= o + d < S
+static __device__ __forceinline__ int range_mask(int o, int K, int S) {
+  const int lo = max(0, -o);
+  const int hi = min(K, S - o);
+  return hi > lo ? (int)(((1u << hi) - 1u) ^ ((1u << lo) - 1u)) : 0;
+}
 static __device__ __forceinline__ float bf2f(uint32_t u16) {
   return __uint_as_float(u16 << 16);
+}
+
+// ---------------------------------------------------------------------------
+// Main loop. Both operands are staged with buffer_load ... lds (LDS-DMA, no
+// VGPR round trip). One wave instruction writes 1 KiB = 8 LDS rows of 128 B,
+// lane-linear, so the XOR swizzle is applied on the SOURCE side: lane l of an
+// instruction fills row r = row0 + (l >> 3), physical chunk (l & 7), and
+// therefore fetches logical chunk kc = (l & 7) ^ (r & 7) = (l & 7) ^ (l >> 3)
+// (cdna_hip_programming.md rule 21). Out-of-range activation offsets return
+// zero into LDS, which implements the conv padding and the M/K tails.
+//
+// Gather addressing costs ~5 VALU per row per K-step: the host precomputes,
+// for every 16-B K chunk, the byte offset of its tap relative to the output
+// pixel's origin and a "required bits" mask (bit dt, 8+dh, 16+dw); each row
+// holds a validity bitmask of the taps that stay inside the input (built once
+// per block), so a chunk is valid iff (rowmask & req) == req. A K chunk past
+// K_total gets req = bit 31, which no row mask has.
+//
+// Double-buffered: the next step's DMA is issued before the current step's
+// MFMAs and retired by vmcnt(0) + barrier at the end of the step.
+// Decode GEMM row m into output coordinates; returns false for padding rows.
+static __device__ __forceinline__ bool decode_row(const ConvParams& p, int m, int& n, int& to,
+                                                  int& ho, int& wo) {
+  if (m >= p.M) return false;
+  if (p.row_mode == 0) {
+    const int t1 = fast_div(m, p.mWo, p.sWo);
+    wo = m - t1 * p.Wo;
+    const int t2 = fast_div(t1, p.mHo, p.sHo);
+    ho = t1 - t2 * p.Ho;
+    n = fast_div(t2, p.mTo, p.sTo);
+    to = t2 - n * p.To;
+    return true;
+  }
+  const int j = m & 15;
+  const int t2 = m >> 4;
+  const int gi = fast_div(t2, p.mTo, p.sTo);
+  to = t2 - gi * p.To;
+  n = fast_div(gi, p.mG, p.sG);
+  const int hw = (gi - n * p.ngroups) * 16 + j;
+  if (hw >= p.Ho * p.Wo) return false;
+  ho = fast_div(hw, p.mWo, p.sWo);
+  wo = hw - ho * p.Wo;
+  return true;
 }
 
 template <int TP, int TC, int WP, int WC>
@@ -69,12 +129,13 @@ void conv_igemm_kernel(const ConvParams p) {
   constexpr int P_TILE = WP * TP * 16;
   constexpr int C_TILE = WC * TC * 16;
   constexpr int BK = 64;
-  constexpr int A_ROWS = P_TILE / 32;                 // gathered rows / thread / step
-  constexpr int W_ITERS = (C_TILE * 8 + 255) / 256;   // weight chunks / thread / step
+  constexpr int A_INSTR = P_TILE / 32;            // act DMA instructions per wave
+  constexpr int W_INSTR_TOTAL = C_TILE / 8;       // weight DMA instructions per block
+  constexpr int W_INSTR = (W_INSTR_TOTAL + 3) / 4;
   constexpr int ACT_BYTES = P_TILE * BK * 2;
   constexpr int BUF_BYTES = (P_TILE + C_TILE) * BK * 2;
   static_assert(WP * WC == 4, "4 waves per block");
-  static_assert(P_TILE % 32 == 0, "pixel tile must be a multiple of 32");
+  static_assert(C_TILE % 16 == 0 && P_TILE % 32 == 0, "tile shape");
 
   __shared__ __attribute__((aligned(16))) char lds[2 * BUF_BYTES];
 
@@ -94,76 +155,50 @@ void conv_igemm_kernel(const ConvParams p) {
   const int p0 = ptile * P_TILE;
   const int c0 = ctile * C_TILE;
 
-  // ---- per-row gather state ----
-  const int kc = tid & 7;
-  const int rsub = tid >> 3;
-  int rbase[A_ROWS], rt[A_ROWS], rh[A_ROWS], rw[A_ROWS];
+  const int lrow = lane >> 3;                      // row within an instruction
+  const int kc = (lane & 7) ^ lrow;                // logical 16-B chunk this lane fetches
+  int rbase[A_INSTR], rmask[A_INSTR];
 #pragma unroll
-  for (int i = 0; i < A_ROWS; ++i) {
-    const int m = p0 + rsub + 32 * i;
-    if (m < p.M) {
-      int wo = m % p.Wo;
-      int t1 = m / p.Wo;
-      int ho = t1 % p.Ho;
-      int t2 = t1 / p.Ho;
-      int to = t2 % p.To;
-      int n = t2 / p.To;
-      rt[i] = to * p.ST - p.PT;
-      rh[i] = ho * p.SH - p.PH;
-      rw[i] = wo * p.SW - p.PW;
-      rbase[i] = (((n * p.T + rt[i]) * p.H + rh[i]) * p.W + rw[i]) * p.Cin_p;
-    } else {
-      rt[i] = -(1 << 28);
-      rh[i] = 0;
-      rw[i] = 0;
-      rbase[i] = 0;
+  for (int i = 0; i < A_INSTR; ++i) {
+    const int m = p0 + (wave * A_INSTR + i) * 8 + lrow;
+    int mask = 0, base = 0;
+    int n, to, ho, wo;
+    if (decode_row(p, m, n, to, ho, wo)) {
+      const int t0 = to * p.ST - p.PT, h0 = ho * p.SH - p.PH, w0 = wo * p.SW - p.PW;
+      mask = range_mask(t0, p.KT, p.T) | (range_mask(h0, p.KH, p.H) << 8) |
+             (range_mask(w0, p.KW, p.W) << 16);
+      base = ((((n * p.T + t0) * p.H + h0) * p.W + w0) * p.Cin_p) * 2;
     }
+    rbase[i] = base;
+    rmask[i] = mask;
   }
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+  const uint32_t w_bytes = (uint32_t)p.w_rows * (uint32_t)p.K_pad * 2u;
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, w_bytes, 0x00020000);
+  const uint32_t wrow_off = ((uint32_t)c0 * (uint32_t)p.K_pad + (uint32_t)kc * 8u) * 2u;
 
-  i32x4 av[A_ROWS];
-  i32x4 wv[W_ITERS];
-
-  auto gload = [&](int s) {
-    const int k = s * BK + kc * 8;
-    const bool kvalid = k < p.K_total;
-    const int tap = k / p.Cin_p;
-    const int c = k - tap * p.Cin_p;
-    const int dw = tap % p.KW;
-    const int tq = tap / p.KW;
-    const int dh = tq % p.KH;
-    const int dt = tq / p.KH;
-    const int delta = ((dt * p.H + dh) * p.W + dw) * p.Cin_p + c;
-#pragma unroll
-    for (int i = 0; i < A_ROWS; ++i) {
-      const int ti = rt[i] + dt, hi = rh[i] + dh, wi = rw[i] + dw;
-      const bool ok = kvalid && (unsigned)ti < (unsigned)p.T &&
-                      (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
-      const uint32_t off = ok ? (uint32_t)(rbase[i] + delta) * 2u : INVALID_OFF;
-      av[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
-    }
-    const uint16_t* wsrc = p.w + (size_t)c0 * p.K_pad + s * BK + kc * 8;
-#pragma unroll
-    for (int j = 0; j < W_ITERS; ++j) {
-      const int row = rsub + 32 * j;
-      if (C_TILE % 32 == 0 || row < C_TILE)
-        wv[j] = *(const i32x4*)(wsrc + (size_t)row * p.K_pad);
-    }
-  };
-
-  auto lstore = [&](int buf) {
+  auto issue = [&](int s, int buf, int2 e) {
     char* base = lds + buf * BUF_BYTES;
 #pragma unroll
-    for (int i = 0; i < A_ROWS; ++i) {
-      const int row = rsub + 32 * i;
-      *(i32x4*)(base + row * 128 + ((kc ^ (row & 7)) << 4)) = av[i];
+    for (int i = 0; i < A_INSTR; ++i) {
+      const bool ok = (rmask[i] & e.y) == e.y;
+      const uint32_t off = ok ? (uint32_t)(rbase[i] + e.x) : INVALID_OFF;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xr, (__attribute__((address_space(3))) void*)(base + (wave * A_INSTR + i) * 1024),
+          16, off, 0, 0, 0);
     }
 #pragma unroll
-    for (int j = 0; j < W_ITERS; ++j) {
-      const int row = rsub + 32 * j;
-      if (C_TILE % 32 == 0 || row < C_TILE)
-        *(i32x4*)(base + ACT_BYTES + row * 128 + ((kc ^ (row & 7)) << 4)) = wv[j];
+    for (int j = 0; j < W_INSTR; ++j) {
+      const int instr = wave + 4 * j;
+      if (W_INSTR_TOTAL % 4 == 0 || instr < W_INSTR_TOTAL) {
+        const uint32_t off = wrow_off + ((uint32_t)(instr * 8 + lrow) * (uint32_t)p.K_pad +
+                                         (uint32_t)(s * BK)) * 2u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            wr, (__attribute__((address_space(3))) void*)(base + ACT_BYTES + instr * 1024), 16,
+            off, 0, 0, 0);
+      }
     }
   };
 
@@ -174,15 +209,21 @@ void conv_igemm_kernel(const ConvParams p) {
     for (int b = 0; b < TC; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nsteps = p.K_pad / BK;
-  gload(0);
-  lstore(0);
+  const int2* ktab = p.ktab + kc;
+  int2 e_next = ktab[0];
+  issue(0, 0, e_next);
+  if (nsteps > 1) e_next = ktab[8];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const int frow = lane & 15;
   const int fq = lane >> 4;
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s & 1;
-    if (s + 1 < nsteps) gload(s + 1);
+    if (s + 1 < nsteps) {
+      issue(s + 1, cur ^ 1, e_next);
+      if (s + 2 < nsteps) e_next = ktab[(s + 2) * 8];
+    }
     const char* abase = lds + cur * BUF_BYTES;
     const char* wbase = abase + ACT_BYTES;
 #pragma unroll
@@ -205,15 +246,21 @@ void conv_igemm_kernel(const ConvParams p) {
         for (int tc = 0; tc < TC; ++tc)
           acc[tp][tc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tc], af[tp], acc[tp][tc], 0, 0, 0);
     }
-    if (s + 1 < nsteps) lstore(cur ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
   // ---- epilogue: bias (+ residual) (+ ReLU) -> bf16, 4 channels per lane ----
 #pragma unroll
   for (int tp = 0; tp < TP; ++tp) {
-    const int m = p0 + wp * TP * 16 + tp * 16 + frow;
-    if (m >= p.M) continue;
+    int m = p0 + wp * TP * 16 + tp * 16 + frow;
+    if (p.row_mode == 1) {            // GEMM row -> output pixel index
+      int n, to, ho, wo;
+      if (!decode_row(p, m, n, to, ho, wo)) continue;
+      m = ((n * p.To + to) * p.Ho + ho) * p.Wo + wo;
+    } else if (m >= p.M) {
+      continue;
+    }
 #pragma unroll
     for (int tc = 0; tc < TC; ++tc) {
       const int c = c0 + wc * TC * 16 + tc * 16 + fq * 4;
@@ -251,22 +298,22 @@ struct ConvConfig {
 };
 
 #define CFG(TP, TC, WP, WC) {WP * TP * 16, WC * TC * 16, conv_igemm_kernel<TP, TC, WP, WC>}
-static const ConvConfig kConfigs[] = {
-    CFG(4, 4, 2, 2),   // 0: 128 px x 128 ch
-    CFG(4, 4, 4, 1),   // 1: 256 px x  64 ch
-    CFG(2, 9, 4, 1),   // 2: 128 px x 144 ch
-    CFG(2, 6, 4, 1),   // 3: 128 px x  96 ch
-    CFG(2, 3, 4, 1),   // 4: 128 px x  48 ch
-    CFG(4, 2, 1, 4),   // 5:  64 px x 128 ch
-    CFG(2, 2, 2, 2),   // 6:  64 px x  64 ch
-    CFG(4, 4, 1, 4),   // 7:  64 px x 256 ch
-    CFG(2, 4, 4, 1),   // 8: 128 px x  64 ch
-    CFG(2, 8, 4, 1),   // 9: 128 px x 128 ch
-    CFG(2, 5, 4, 1),   // 10: 128 px x 80 ch
-    CFG(4, 3, 4, 1),   // 11: 256 px x 48 ch
-    CFG(2, 4, 2, 2),   // 12:  64 px x 128 ch
-    CFG(4, 6, 2, 2),   // 13: 128 px x 192 ch
-};
+#define TILES(X) \
+    X(4, 4, 2, 2),   /* 128 px x 128 ch */ \
+    X(4, 4, 4, 1),   /* 256 px x  64 ch */ \
+    X(2, 9, 4, 1),   /* 128 px x 144 ch */ \
+    X(2, 6, 4, 1),   /* 128 px x  96 ch */ \
+    X(2, 3, 4, 1),   /* 128 px x  48 ch */ \
+    X(4, 2, 1, 4),   /*  64 px x 128 ch */ \
+    X(2, 2, 2, 2),   /*  64 px x  64 ch */ \
+    X(4, 4, 1, 4),   /*  64 px x 256 ch */ \
+    X(2, 4, 4, 1),   /* 128 px x  64 ch */ \
+    X(2, 8, 4, 1),   /* 128 px x 128 ch */ \
+    X(2, 5, 4, 1),   /* 128 px x  80 ch */ \
+    X(4, 3, 4, 1),   /* 256 px x  48 ch */ \
+    X(2, 4, 2, 2),   /*  64 px x 128 ch */ \
+    X(4, 6, 2, 2)    /* 128 px x 192 ch */
+static const ConvConfig kConfigs[] = {TILES(CFG)};
 static const int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
 extern "C" {
@@ -282,6 +329,17 @@ int rnb_conv_config_info(int id, int* p_tile, int* c_tile) {
 
 int rnb_conv_params_size() { return (int)sizeof(ConvParams); }
 
+// (m, s) with n / d == umulhi(n, m) >> s for all 0 <= n < 2^31 (d >= 2);
+// m = 0 encodes d == 1.
+static void magic_div(uint32_t d, uint32_t* m, uint32_t* s) {
+  if (d <= 1) { *m = 0; *s = 0; return; }
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;                 // ceil(log2 d)
+  const uint64_t p = 31 + l;
+  *m = (uint32_t)(((1ull << p) + d - 1) / d);
+  *s = (uint32_t)(p - 32);
+}
+
 // Validates the shape contract the kernel relies on, then launches.
 // Returns 0 on success, a negative code for a contract violation, or the
 // positive hipError_t of the launch.
@@ -293,14 +351,26 @@ int rnb_conv_launch(const ConvParams* pp, int config_id, hipStream_t stream) {
   if (p.K_total > p.K_pad) return -3;
   if (p.M <= 0) return 0;
   if (p.y_stride < p.Cout_p || (p.res && p.res_stride < p.Cout_p)) return -4;
-  if ((long long)p.N * p.T * p.H * p.W * p.Cin_p * 2 > 0xFFFFFF00LL) return -5;
+  if ((long long)p.N * p.T * p.H * p.W * p.Cin_p * 2 > 0x7FFFFF00LL) return -5;
   if ((long long)p.M * p.y_stride >= (1LL << 31)) return -6;
   p.x_bytes = (uint32_t)((long long)p.N * p.T * p.H * p.W * p.Cin_p * 2);
+  magic_div((uint32_t)p.Wo, &p.mWo, &p.sWo);
+  magic_div((uint32_t)p.Ho, &p.mHo, &p.sHo);
+  magic_div((uint32_t)p.To, &p.mTo, &p.sTo);
+  if (p.row_mode == 1) {
+    p.ngroups = (p.Ho * p.Wo + 15) / 16;
+    p.M = p.N * p.ngroups * p.To * 16;
+    magic_div((uint32_t)p.ngroups, &p.mG, &p.sG);
+  } else {
+    p.row_mode = 0;
+  }
+  if (p.KT > 8 || p.KH > 8 || p.KW > 8) return -10;
   p.n_ptiles = (p.M + cfg.p_tile - 1) / cfg.p_tile;
   p.n_ctiles = (p.Cout_p + cfg.c_tile - 1) / cfg.c_tile;
   const long long blocks = (long long)p.n_ptiles * p.n_ctiles;
   if (blocks > 0x7FFFFFFF) return -7;
   if (p.n_ctiles * cfg.c_tile > p.w_rows) return -8;
+  if (!p.ktab) return -9;
   hipLaunchKernelGGL(cfg.kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
 }

@@ -106,12 +106,44 @@ class ConvLayer:
         self.w_ref = (weight.detach().to(torch.bfloat16).float().to(device))
         self.b_ref = bias.detach().float().to(device)
         self._config: Dict[Tuple[int, int], int] = {}
+        self._ktab: Dict[Tuple[int, int, int], torch.Tensor] = {}
+        self.time_major = False   # time-major rows for temporal convs (measured: no gain)
 
     # ------------------------------------------------------------------
     def out_shape(self, x_shape) -> Tuple[int, int, int, int, int]:
         N, T, H, W, _ = x_shape
         To, Ho, Wo = self.geom.out_thw(T, H, W)
         return (N, To, Ho, Wo, self.geom.cout_p)
+
+    def ktab(self, T: int, H: int, W: int, device) -> torch.Tensor:
+        """Per-16-B-K-chunk gather table for input spatial shape (T, H, W).
+
+        Entry q (k = 8q) = (byte offset of k's tap/channel relative to the
+        output pixel's input origin, required validity bits): bit dt, 8 + dh,
+        16 + dw. Chunks past K_total require bit 31, which no row has.
+        """
+        key = (T, H, W)
+        tab = self._ktab.get(key)
+        if tab is None:
+            g = self.geom
+            kt, kh, kw = g.kernel
+            if max(kt, kh, kw) > 8:
+                raise ValueError("kernel extent > 8 not supported by the gather table")
+            q = torch.arange(g.k_pad // 8, dtype=torch.int64)
+            k = q * 8
+            tap = k // g.cin_p
+            c = k % g.cin_p
+            dw = tap % kw
+            dh = (tap // kw) % kh
+            dt = tap // (kw * kh)
+            delta = (((dt * H + dh) * W + dw) * g.cin_p + c) * 2
+            req = (1 << dt) | (1 << (8 + dh)) | (1 << (16 + dw))
+            valid = k < g.k_total
+            delta = torch.where(valid, delta, torch.zeros_like(delta))
+            req = torch.where(valid, req, torch.full_like(req, -(1 << 31)))
+            tab = torch.stack([delta, req], dim=1).to(torch.int32).contiguous().to(device)
+            self._ktab[key] = tab
+        return tab
 
     def params(self, x: torch.Tensor, y: torch.Tensor, residual: Optional[torch.Tensor]):
         from .native import ConvParams
@@ -136,6 +168,9 @@ class ConvLayer:
         p.M = N * To * Ho * Wo
         p.relu = 1 if self.relu else 0
         p.w_rows = self.wmat.shape[0]
+        p.ktab = self.ktab(T, H, W, x.device).data_ptr()
+        # temporal convs: tiles hold all output frames of 16-pixel groups
+        p.row_mode = 1 if (self.time_major and g.kernel[0] > 1) else 0
         return p
 
     def heuristic_config(self, M: int) -> int:

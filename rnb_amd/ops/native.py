@@ -103,6 +103,12 @@ class ConvParams(ctypes.Structure):
         ("K_pad", ctypes.c_int), ("M", ctypes.c_int), ("relu", ctypes.c_int),
         ("n_ptiles", ctypes.c_int), ("n_ctiles", ctypes.c_int),
         ("x_bytes", ctypes.c_uint32), ("w_rows", ctypes.c_int),
+        ("ktab", ctypes.c_void_p),
+        ("mWo", ctypes.c_uint32), ("sWo", ctypes.c_uint32),
+        ("mHo", ctypes.c_uint32), ("sHo", ctypes.c_uint32),
+        ("mTo", ctypes.c_uint32), ("sTo", ctypes.c_uint32),
+        ("row_mode", ctypes.c_int), ("ngroups", ctypes.c_int),
+        ("mG", ctypes.c_uint32), ("sG", ctypes.c_uint32),
     ]
 
 

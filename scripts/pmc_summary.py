@@ -1,0 +1,28 @@
+"""Summarise rocprofv3 counter CSVs (one dir per pass) for the conv kernel."""
+import collections
+import csv
+import glob
+import os
+import sys
+
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+vals = collections.OrderedDict()
+for d in sorted(glob.glob(os.path.join(root, "p*"))):
+    f = os.path.join(d, "run_counter_collection.csv")
+    if not os.path.exists(f):
+        continue
+    per = collections.defaultdict(list)
+    for r in csv.DictReader(open(f)):
+        if "conv_igemm" in r["Kernel_Name"]:
+            per[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, v in per.items():
+        vals[k] = v[-1]
+for k, v in vals.items():
+    print("%-32s %16.0f" % (k, v))
+if "SQ_INSTS_MFMA" in vals and vals["SQ_INSTS_MFMA"]:
+    print("VALU/MFMA = %.2f" % (vals.get("SQ_INSTS_VALU", 0) / vals["SQ_INSTS_MFMA"]))
+if "SQ_WAVE_CYCLES" in vals:
+    w = vals["SQ_WAVE_CYCLES"]
+    for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+        if k in vals:
+            print("%s / WAVE_CYCLES = %.2f" % (k, vals[k] / w))

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--autotune", action="store_true")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--compare", action="store_true",
+                    help="time every tile config per layer; report best per family")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     eng = R2P1DEngine(build_network(1, 5, depth=args.depth), dev, backend="hip")
@@ -59,13 +61,30 @@ def main():
                      "K": g.cin * g.kernel[0] * g.kernel[1] * g.kernel[2],
                      "tile": "%dx%d" % cfgs[cid], "ms": ms,
                      "tflops": flops / ms / 1e9, "gflop": flops / 1e9})
+        if args.compare:
+            best = {}
+            for c in range(len(cfgs)):
+                s.record()
+                for _ in range(args.reps):
+                    op.layer.forward_hip(src, res, out=y, config=c)
+                e.record()
+                e.synchronize()
+                t = s.elapsed_time(e) / args.reps
+                fam = "best"
+                if fam not in best or t < best[fam][1]:
+                    best[fam] = (c, t)
+            rows[-1]["best"] = {k: ("%dx%d" % cfgs[v[0]], v[1]) for k, v in best.items()}
         bufs[op.dst] = y
     tot_ms = sum(r["ms"] for r in rows)
     tot_gf = sum(r["gflop"] for r in rows)
     for r in rows:
-        print("%-34s M=%8d N=%5d K=%5d tile=%-8s %8.3f ms %7.1f TF (%4.1f%%)"
+        extra = ""
+        if "best" in r:
+            extra = "  " + " ".join("%s:%s %.3f" % (k, v[0], v[1])
+                                    for k, v in sorted(r["best"].items()))
+        print("%-34s M=%8d N=%5d K=%5d tile=%-8s %8.3f ms %7.1f TF (%4.1f%%)%s"
               % (r["name"], r["M"], r["N"], r["K"], r["tile"], r["ms"], r["tflops"],
-                 100 * r["ms"] / tot_ms))
+                 100 * r["ms"] / tot_ms, extra))
     print("TOTAL %d convs: %.3f ms for %d clips = %.1f TFLOP/s, %.1f clips/s"
           % (len(rows), tot_ms, n, tot_gf / tot_ms, n / tot_ms * 1e3))
     if args.json_out:

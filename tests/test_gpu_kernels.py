@@ -72,9 +72,9 @@ def test_conv_every_tile_config_exact_integers(cfg):
     layer = _layer(64, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False, integer=True)
     x = _input(1, (2, 15, 13), 64, 64, integer=True)
     y = layer.forward_hip(x, config=cfg)
-    ref = layer.forward_torch(x, out_dtype=torch.float32)
+    ref = layer.forward_torch(x, out_dtype=torch.bfloat16)
     torch.cuda.synchronize()
-    assert torch.equal(y.float(), ref), (y.float() - ref).abs().max().item()
+    assert torch.equal(y, ref), (y.float() - ref.float()).abs().max().item()
 
 
 def test_conv_residual_relu_epilogue():
@@ -82,19 +82,19 @@ def test_conv_residual_relu_epilogue():
     x = _input(3, (4, 9, 11), 144, 144, integer=True)
     res = _input(3, (4, 9, 11), 64, 64, integer=True, seed=5)
     y = layer.forward_hip(x, residual=res)
-    ref = layer.forward_torch(x, residual=res, out_dtype=torch.float32)
+    ref = layer.forward_torch(x, residual=res, out_dtype=torch.bfloat16)
     torch.cuda.synchronize()
-    assert torch.equal(y.float(), ref)
+    assert torch.equal(y, ref)
 
 
 def test_conv_odd_m_tail_and_padding_channels():
     layer = _layer(42, 85, (1, 1, 1), (2, 2, 2), (0, 0, 0), integer=True)
     x = _input(1, (3, 5, 7), layer.geom.cin_p, 42, integer=True)
     y = layer.forward_hip(x)
-    ref = layer.forward_torch(x, out_dtype=torch.float32)
+    ref = layer.forward_torch(x, out_dtype=torch.bfloat16)
     torch.cuda.synchronize()
     assert y.shape[-1] == 88
-    assert torch.equal(y.float(), ref)
+    assert torch.equal(y, ref)
     assert torch.count_nonzero(y[..., 85:]) == 0
 
 
@@ -129,3 +129,20 @@ def test_clipgen_and_preprocess_bit_exact():
     pc = vops.preprocess(c)
     torch.cuda.synchronize()
     assert torch.equal(pg.cpu().float(), pc.float())
+
+
+@pytest.mark.parametrize("thw,cin,cout,stride", [((8, 14, 14), 144, 64, 1), ((4, 7, 7), 288, 128, 2),
+                                                 ((2, 5, 3), 64, 96, 1)])
+def test_time_major_rows_exact(thw, cin, cout, stride):
+    """Temporal convs use the time-major row order; both orders must agree."""
+    layer = _layer(cin, cout, (3, 1, 1), (stride, 1, 1), (1, 0, 0), integer=True)
+    x = _input(3, thw, layer.geom.cin_p, cin, integer=True)
+    res_shape = layer.out_shape(x.shape)
+    res = _input(res_shape[0], res_shape[1:4], res_shape[4], cout, integer=True, seed=9)
+    ref = layer.forward_torch(x, residual=res, out_dtype=torch.bfloat16)
+    for mode in (True, False):
+        layer.time_major = mode
+        for cfg in (0, 5, 8):
+            y = layer.forward_hip(x, residual=res, config=cfg)
+            torch.cuda.synchronize()
+            assert torch.equal(y, ref), (mode, cfg)
