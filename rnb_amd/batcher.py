@@ -8,7 +8,9 @@ Stacks ``batch`` incoming tensors along dim 0 and emits them with a
   emitted first and the item starts the next batch (the reference would
   overflow its 15-row slot when batching multi-clip videos);
 * ``max_wait_ms``: a partial batch older than this is flushed at the next
-  arrival (the reference's batcher has no flush at all).
+  arrival (the reference's batcher has no flush at all);
+* ``flush()``: the runner calls it at end of stream, so a trailing partial
+  batch is emitted instead of held forever.
 """
 import time
 
@@ -52,6 +54,12 @@ class Batcher(RunnerModel):
         self.stacked_tensors, self.stacked_time_cards = [], []
         self.first_ts = None
         return (batch,), None, cards
+
+    def flush(self):
+        """End of stream: emit a partial batch (None when nothing is held)."""
+        if not self.stacked_tensors:
+            return None
+        return self._emit()
 
     def __call__(self, tensors, non_tensors, time_card):
         if self.batch <= 1:

@@ -25,7 +25,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 LIBRARIES = {
     "librnb_kernels.so": (["conv_igemm.hip", "video_ops.hip"], [], []),
     "librnb_runtime.so": (["runtime.cpp"], [], []),
-    "librnb_tracer.so": (["tracer.cpp"], [], ["-L%s/lib" % ROCM, "-lroctracer64",
+    "librnb_tracer.so": (["tracer.cpp"], [], ["-L%s/lib" % ROCM, "-lrocprofiler-sdk",
                                                "-Wl,-rpath,%s/lib" % ROCM]),
 }
 

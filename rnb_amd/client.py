@@ -61,7 +61,8 @@ def poisson_client(video_path_iterator, filename_queue, beta, termination_flag,
 
 
 def bulk_client(video_path_iterator, filename_queue, num_videos, termination_flag,
-                sta_bar, fin_bar, seed=None, barrier_timeout=None, iterator_kwargs=None):
+                sta_bar, fin_bar, seed=None, barrier_timeout=None, iterator_kwargs=None,
+                done_counter=None):
     from queue import Full
     from .control import TerminationFlag
     from .timecard import TimeCard
@@ -84,5 +85,13 @@ def bulk_client(video_path_iterator, filename_queue, num_videos, termination_fla
                     termination_flag.value = TerminationFlag.FILENAME_QUEUE_FULL
             break
     _push_exit_markers(filename_queue)
+    if done_counter is not None and termination_flag.value == TerminationFlag.UNSET:
+        filename_queue.close()
+        filename_queue.join_thread()          # every path is in the pipe
+        with done_counter.get_lock():
+            done_counter.value += 1
     fin_bar.wait(barrier_timeout)
-    filename_queue.cancel_join_thread()
+    try:
+        filename_queue.cancel_join_thread()
+    except Exception:
+        pass

@@ -1,4 +1,4 @@
-"""Control plane: termination FSM, signals, queue/slot wiring.
+"""Control plane: termination FSM, signals, queue/slot wiring, end of stream.
 
 Reference: control.py:1-209. The queue wiring (one filename queue, one output
 queue per distinct out-queue index per step, consumers reading the slot rings
@@ -15,6 +15,13 @@ are behaviourally identical. What differs, deliberately:
   R(2+1)D runner advertises its real boundary shape (fixes TODO #69).
 * ``TerminationFlag`` gains ``CHILD_FAILED`` and ``BARRIER_TIMEOUT``, set by
   the launcher's watchdog.
+* End of stream is explicit. The reference lets a consumer exit on the first
+  ``None`` marker it dequeues (runner.py:81-83), so when two replicas feed
+  one queue the first replica to finish can stop the consumer before the
+  other replica's last item arrives. Here every producer flushes its queue
+  feeder and then increments the queue's ``done`` counter; a consumer exits
+  only once ``done == #producers`` and the queue is drained (markers merely
+  wake it up).
 """
 from __future__ import annotations
 
@@ -106,9 +113,15 @@ class SharedQueuesAndTensors:
         self.queue_indices: List[List[Tuple[Optional[int], Optional[List[int]]]]] = []
         self.queues: List[Dict[int, object]] = []
         self.rings: List[List[List[object]]] = []
+        # end-of-stream accounting: per queue, how many producer instances
+        # feed it and how many have finished (flushed their last item)
+        self.filename_done = ctx.Value("i", 0)
+        self.done: List[Dict[int, object]] = []
+        self.num_producers: List[Dict[int, int]] = []
         for step_idx, step in enumerate(spec.steps):
             final = step_idx == self.num_steps - 1
             step_qi, step_qs, step_rings = [], {}, []
+            step_done, step_np = {}, {}
             for group_idx, group in enumerate(step.groups):
                 step_qi.append((group.in_queue, group.out_queues))
                 if final:
@@ -116,6 +129,9 @@ class SharedQueuesAndTensors:
                 for q in group.out_queues:
                     if q not in step_qs:
                         step_qs[q] = queue_class(queue_size)
+                        step_done[q] = ctx.Value("i", 0)
+                        step_np[q] = 0
+                    step_np[q] += len(group.gpus)
                 shapes, dtypes = step_output_spec(step, group)
                 consumers_cpu = self._consumers_use_cpu(step_idx, group)
                 group_rings = []
@@ -133,6 +149,8 @@ class SharedQueuesAndTensors:
             self.queue_indices.append(step_qi)
             self.queues.append(step_qs)
             self.rings.append(step_rings)
+            self.done.append(step_done)
+            self.num_producers.append(step_np)
 
     def _consumers_use_cpu(self, step_idx: int, group) -> bool:
         nxt = self.spec.steps[step_idx + 1]
@@ -152,6 +170,18 @@ class SharedQueuesAndTensors:
         out_queues = None if step_idx == self.num_steps - 1 \
             else [self.queues[step_idx][q] for q in out_idx]
         return in_queue, out_queues
+
+    def get_stream_state(self, step_idx: int, group_idx: int):
+        """End-of-stream handles: ((in done counter, #producers), [out counters])."""
+        in_idx, out_idx = self.queue_indices[step_idx][group_idx]
+        if step_idx == 0:
+            in_state = (self.filename_done, 1)
+        else:
+            in_state = (self.done[step_idx - 1][in_idx],
+                        self.num_producers[step_idx - 1][in_idx])
+        outs = None if step_idx == self.num_steps - 1 \
+            else [self.done[step_idx][q] for q in out_idx]
+        return in_state, outs
 
     def get_tensors(self, step_idx: int, group_idx: int, instance_idx: int):
         """(input rings by producer group, this instance's output ring)."""

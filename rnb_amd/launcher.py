@@ -177,7 +177,8 @@ def run(args) -> dict:
                                    fin_bar),
                              kwargs=dict(seed=args.seed,
                                          barrier_timeout=args.barrier_timeout,
-                                         iterator_kwargs=it_kwargs))
+                                         iterator_kwargs=it_kwargs,
+                                         done_counter=qt.filename_done))
     procs = [("client", client)]
     last = len(spec.steps) - 1
     dist_infos = _assign_rccl_ranks(spec, qt, job_id)
@@ -196,7 +197,8 @@ def run(args) -> dict:
                     kwargs=dict(group.kwargs, result_queue=result_queue,
                                 barrier_timeout=args.barrier_timeout,
                                 dist_info=dist_infos.get((step_idx, group_idx,
-                                                          instance_idx))))
+                                                          instance_idx)),
+                                stream_state=qt.get_stream_state(step_idx, group_idx)))
                 procs.append((p.name, p))
     for _, p in procs:
         p.start()

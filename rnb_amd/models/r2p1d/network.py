@@ -228,12 +228,17 @@ def R2Plus1DClassifier(num_classes=400, layer_sizes=(2, 2, 2, 2),
 def init_random_(model: nn.Module, seed: int = 0) -> nn.Module:
     """Deterministic random init with non-trivial BN statistics.
 
-    Weights are Kaiming-normal (fan-in), BN gamma/beta/running stats are
+    Every module draws from its own generator seeded by (seed, module name),
+    so a layer-range runner holds exactly the weights of the same layers of
+    the whole model: split pipelines compute the same function as one runner.
+    Weights are Kaiming-normal (fan-in); BN gamma/beta/running stats are
     randomised around identity so eval-mode folding is actually exercised.
     """
-    g = torch.Generator().manual_seed(seed)
+    import zlib
     with torch.no_grad():
-        for m in model.modules():
+        for name, m in model.named_modules():
+            g = torch.Generator().manual_seed(
+                (zlib.crc32(name.encode()) * 1000003 + int(seed)) & 0x7FFFFFFFFFFF)
             if isinstance(m, (nn.Conv3d, nn.Linear)):
                 fan_in = m.weight[0].numel()
                 m.weight.copy_(torch.randn(m.weight.shape, generator=g)

@@ -1,4 +1,4 @@
-"""Kernel timestamps via roctracer (reference: utils/cupti.cpp, test_cupti.py).
+"""Kernel timestamps via rocprofiler-sdk (reference: utils/cupti.cpp, test_cupti.py).
 
 Same three-call API as the reference's CUPTI bridge::
 
@@ -10,8 +10,10 @@ Same three-call API as the reference's CUPTI bridge::
         ...
 
 ``initialize()`` must run before the process initialises the HIP runtime
-(before the first ``torch.cuda`` call): roctracer registers its activity
-callbacks with the HIP runtime at start-up through rocprofiler-register.
+(before the first ``torch.cuda`` call): it registers ``librnb_tracer.so`` as a
+rocprofiler-sdk tool (``rocprofiler_force_configure``), and tools are set up
+when the runtime starts. (roctracer, the legacy interface, delivers no
+activity records on ROCm 7.2.)
 
 Also ``report_full()`` (op kind and device per record) and ``summary()``
 (per-kernel count / total / mean time) for quick breakdowns inside a runner.
@@ -47,15 +49,20 @@ def initialize(buffer_bytes: int = 4 << 20) -> None:
     lib = _load()
     rc = lib.rnb_tracer_initialize(buffer_bytes)
     if rc != 0:
-        raise RuntimeError("roctracer init failed (%d): %s"
-                           % (rc, (lib.rnb_tracer_error() or b"").decode()))
+        raise RuntimeError("rocprofiler-sdk tool registration failed (%d)" % rc)
+
+
+def started() -> bool:
+    """True once the runtime has initialised and the tool context is running."""
+    return bool(_load().rnb_tracer_started())
 
 
 def flush() -> None:
     lib = _load()
     rc = lib.rnb_tracer_flush()
     if rc != 0:
-        raise RuntimeError("roctracer flush failed (%d)" % rc)
+        raise RuntimeError("tracer flush failed (%d, status %d): was initialize() called "
+                           "before the HIP runtime started?" % (rc, lib.rnb_tracer_status()))
 
 
 def report_full(clear: bool = True) -> List[Tuple[str, int, int, str, int]]:

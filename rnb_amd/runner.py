@@ -45,7 +45,7 @@ def runner(input_queue, output_queues, queue_selector_path, print_summary,
            model_module_path, num_segments,
            shared_input_rings, shared_output_ring,
            result_queue=None, barrier_timeout=None, dist_info=None,
-           **model_kwargs):
+           stream_state=None, **model_kwargs):
     """Entry point of one runner process (spawned by the launcher)."""
     from threading import BrokenBarrierError
     from .control import TerminationFlag
@@ -55,7 +55,7 @@ def runner(input_queue, output_queues, queue_selector_path, print_summary,
                      num_videos, termination_flag, step_idx, sta_bar, fin_bar,
                      model_module_path, num_segments, shared_input_rings,
                      shared_output_ring, result_queue, barrier_timeout, dist_info,
-                     model_kwargs)
+                     stream_state, model_kwargs)
     except BrokenBarrierError:
         _set_flag(termination_flag, TerminationFlag.BARRIER_TIMEOUT)
         print("[runner %d/%d/%d] barrier broken or timed out" % (step_idx, group_idx,
@@ -78,7 +78,7 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                  g_idx, group_idx, instance_idx, global_inference_counter, num_videos,
                  termination_flag, step_idx, sta_bar, fin_bar, model_module_path,
                  num_segments, shared_input_rings, shared_output_ring, result_queue,
-                 barrier_timeout, dist_info, model_kwargs):
+                 barrier_timeout, dist_info, stream_state, model_kwargs):
     import contextlib
     import torch
     from .control import TerminationFlag, Signal, segment_bounds
@@ -114,8 +114,6 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         else:
             sel_cls = load_class(queue_selector_path)
             selector = sel_cls(len(output_queues))
-        out_counter = 0
-
         if shared_output_ring is not None:
             shared_output_ring.producer_attach(device)
 
@@ -146,16 +144,92 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 progress = tqdm(total=num_videos, file=sys.stdout, mininterval=1.0)
             except Exception:
                 progress = None
-        last_count = 0
         items = 0
+
+        state = {"out_counter": 0, "last_count": 0}
+
+        def emit(outputs):
+            """Route one model output; False means stop the runner loop."""
+            tensor_outputs, non_tensor_outputs, time_card = outputs
+            if stream is not None:
+                stream.synchronize()
+            if time_card is None:
+                return True
+            time_card.record("inference%d_finish" % step_idx)
+            if is_final_step:
+                n_inf = len(time_card.time_cards) if isinstance(time_card, TimeCardList) else 1
+                with global_inference_counter.get_lock():
+                    prev = global_inference_counter.value
+                    global_inference_counter.value = prev + n_inf
+                    now = global_inference_counter.value
+                if now >= num_videos:
+                    if prev < num_videos:
+                        print("Finished processing %d videos" % num_videos, flush=True)
+                        _set_flag(termination_flag,
+                                  TerminationFlag.TARGET_NUM_VIDEOS_REACHED)
+                    else:
+                        return False
+                if progress is not None and now > state["last_count"]:
+                    progress.update(min(now, num_videos) - min(state["last_count"], num_videos))
+                    state["last_count"] = now
+                cards = time_card.time_cards if isinstance(time_card, TimeCardList) \
+                    else [time_card]
+                for tc in cards:
+                    summary.register(tc)
+                return True
+            # non-final step: push segments into slots, enqueue signals
+            out_q = output_queues[selector.select(tensor_outputs, non_tensor_outputs,
+                                                  time_card)]
+            msgs = []
+            for seg in range(num_segments):
+                signal_out = None
+                if shared_output_ring is not None:
+                    seg_tensors = []
+                    for t in tensor_outputs:
+                        a, b = segment_bounds(t.shape[0], num_segments, seg)
+                        seg_tensors.append(t[a:b])
+                    slot = state["out_counter"] % len(shared_output_ring)
+                    if not shared_output_ring.wait_free(slot, aborted):
+                        return False
+                    shared_output_ring.write(slot, seg_tensors)
+                    signal_out = Signal(group_idx, instance_idx, slot,
+                                        shared_output_ring.descriptor())
+                    state["out_counter"] = (state["out_counter"] + 1) % len(shared_output_ring)
+                tc = time_card.fork(seg) if num_segments > 1 else time_card
+                msgs.append((signal_out, non_tensor_outputs, tc))
+            try:
+                for m in msgs:
+                    out_q.put_nowait(m)
+            except Full:
+                print("[WARNING] Queue between runner step %d and %d is full. "
+                      "Aborting..." % (step_idx, step_idx + 1), flush=True)
+                _set_flag(termination_flag, TerminationFlag.FRAME_QUEUE_FULL)
+                return False
+            return True
+
+        in_state, out_states = stream_state if stream_state else (None, None)
+
+        def upstream_finished():
+            # without accounting (direct callers) fall back to marker semantics
+            return in_state is None or in_state[0].value >= in_state[1]
 
         while termination_flag.value == TerminationFlag.UNSET:
             try:
                 tpl = input_queue.get(timeout=QUEUE_POLL_S)
             except Empty:
+                if in_state is not None and upstream_finished():
+                    break          # every producer flushed and the queue is drained
                 continue
             if tpl is None:
-                break
+                if upstream_finished():
+                    try:           # drain whatever is still queued behind markers
+                        tpl = input_queue.get(timeout=QUEUE_POLL_S)
+                    except Empty:
+                        break
+                    if tpl is None:
+                        continue
+                else:
+                    continue
             signal, non_tensor_inputs, time_card = tpl
             time_card.add_gpu(g_idx)
             time_card.record("runner%d_start" % step_idx)
@@ -174,69 +248,15 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             if fault == "runner%d_item%d" % (step_idx, items):
                 raise RuntimeError("injected fault in runner%d at item %d"
                                    % (step_idx, items))
-            tensor_outputs, non_tensor_outputs, time_card = \
-                model(tensor_inputs, non_tensor_inputs, time_card)
-            if stream is not None:
-                stream.synchronize()
-            if time_card is None:
-                continue
-            time_card.record("inference%d_finish" % step_idx)
-
-            if is_final_step:
-                n_inf = len(time_card.time_cards) if isinstance(time_card, TimeCardList) else 1
-                stop = False
-                with global_inference_counter.get_lock():
-                    prev = global_inference_counter.value
-                    global_inference_counter.value = prev + n_inf
-                    now = global_inference_counter.value
-                if now >= num_videos:
-                    if prev < num_videos:
-                        print("Finished processing %d videos" % num_videos, flush=True)
-                        _set_flag(termination_flag,
-                                  TerminationFlag.TARGET_NUM_VIDEOS_REACHED)
-                    else:
-                        stop = True
-                if progress is not None and now > last_count:
-                    progress.update(min(now, num_videos) - min(last_count, num_videos))
-                    last_count = now
-                if stop:
-                    break
-                cards = time_card.time_cards if isinstance(time_card, TimeCardList) \
-                    else [time_card]
-                for tc in cards:
-                    summary.register(tc)
-                continue
-
-            # ---- non-final step: push segments into slots, enqueue signals
-            out_q = output_queues[selector.select(tensor_outputs, non_tensor_outputs,
-                                                  time_card)]
-            msgs = []
-            for seg in range(num_segments):
-                signal_out = None
-                if shared_output_ring is not None:
-                    seg_tensors = []
-                    for t in tensor_outputs:
-                        a, b = segment_bounds(t.shape[0], num_segments, seg)
-                        seg_tensors.append(t[a:b])
-                    slot = out_counter % len(shared_output_ring)
-                    if not shared_output_ring.wait_free(slot, aborted):
-                        break
-                    shared_output_ring.write(slot, seg_tensors)
-                    signal_out = Signal(group_idx, instance_idx, slot,
-                                        shared_output_ring.descriptor())
-                    out_counter = (out_counter + 1) % len(shared_output_ring)
-                tc = time_card.fork(seg) if num_segments > 1 else time_card
-                msgs.append((signal_out, non_tensor_outputs, tc))
-            if len(msgs) != num_segments:
+            outputs = model(tensor_inputs, non_tensor_inputs, time_card)
+            if not emit(outputs):
                 break
-            try:
-                for m in msgs:
-                    out_q.put_nowait(m)
-            except Full:
-                print("[WARNING] Queue between runner step %d and %d is full. "
-                      "Aborting..." % (step_idx, step_idx + 1), flush=True)
-                _set_flag(termination_flag, TerminationFlag.FRAME_QUEUE_FULL)
-                break
+        if termination_flag.value == TerminationFlag.UNSET and hasattr(model, "flush"):
+            # natural end of stream: let batching/aggregating stages emit what
+            # they still hold (the reference's Batcher would hold it forever)
+            outputs = model.flush()
+            if outputs is not None:
+                emit(outputs)
 
         # ---- shutdown
         if not is_final_step:
@@ -246,6 +266,14 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                         q.put_nowait(None)
             except Full:
                 pass
+            if out_states is not None and termination_flag.value == TerminationFlag.UNSET:
+                # natural end of stream: make sure every item is in the pipe,
+                # then tell consumers this producer is done
+                for q, done in zip(output_queues, out_states):
+                    q.close()
+                    q.join_thread()
+                    with done.get_lock():
+                        done.value += 1
         if shared_input_rings is not None:
             for rings in shared_input_rings.values():
                 for ring in rings:
@@ -255,7 +283,10 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
     fin_bar.wait(barrier_timeout)
     if output_queues is not None:
         for q in output_queues:
-            q.cancel_join_thread()
+            try:
+                q.cancel_join_thread()
+            except Exception:
+                pass
     if is_final_step:
         with open(logname(job_id, g_idx, group_idx, instance_idx), "w") as f:
             summary.save_full_report(f)

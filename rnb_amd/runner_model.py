@@ -14,6 +14,10 @@ A pipeline step is a ``RunnerModel``:
   time_card)``. Returning ``None`` as the time card means "no output yet"
   (batching / aggregation).
 
+``flush()`` (optional, rnb_amd addition) is called once at the natural end
+of the input stream and may return one last ``(tensors, non_tensors,
+time_card)`` (e.g. a partial batch), or ``None``.
+
 ``output_shape_for(**kwargs)`` (rnb_amd addition) may be overridden when the
 slot shape depends on step kwargs, which fixes the reference's TODO #69
 (model.py:76-80: partial R(2+1)D runners always advertised ``(10, 400)``).

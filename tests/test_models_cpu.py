@@ -1,0 +1,136 @@
+"""R(2+1)D network / engine / decoder numerics on CPU (torch oracle paths)."""
+import pytest
+import torch
+
+from rnb_amd.models.r2p1d.network import (R2Plus1DClassifier, R2Plus1DLayerWrapper,
+                                          intermediate_channels, normalize_layer_sizes,
+                                          init_random_, load_reference_state_dict)
+from rnb_amd.models.r2p1d.model import build_network, R2P1DRunner, R2P1DLoader, R2P1DSingleStep
+from rnb_amd.models.r2p1d.engine import R2P1DEngine, boundary_shape
+from rnb_amd.models.r2p1d.decoder import SyntheticDecoder
+from rnb_amd.ops.video import ncdhw_to_ndhwc, ndhwc_to_ncdhw, video_reduce
+from rnb_amd.timecard import TimeCard
+
+CPU = torch.device("cpu")
+
+
+def test_intermediate_widths_match_survey():
+    assert intermediate_channels(3, 64, (3, 7, 7)) == 83
+    assert intermediate_channels(64, 64, 3) == 144
+    assert intermediate_channels(64, 128, 3) == 230
+    assert intermediate_channels(64, 128, 1) == 42
+    assert intermediate_channels(256, 512, 3) == 921
+
+
+def test_param_counts_and_flops():
+    r18 = R2Plus1DClassifier(400, (2, 2, 2, 2))
+    r34 = R2Plus1DClassifier(400, (3, 4, 6, 3))
+    assert abs(sum(p.numel() for p in r18.parameters()) / 1e6 - 33.4) < 0.1
+    assert abs(sum(p.numel() for p in r34.parameters()) / 1e6 - 63.7) < 0.1
+    e18 = R2P1DEngine(build_network(1, 5, depth=18), CPU, backend="torch")
+    assert abs(e18.flops_per_clip() / 1e9 - 42.17) < 0.01
+    assert len(e18.conv_layers()) == 40
+
+
+def test_state_dict_keys_follow_upstream_tree():
+    keys = set(R2Plus1DClassifier().state_dict())
+    assert "res2plus1d.conv1.spatial_conv.weight" in keys
+    assert "res2plus1d.conv3.block1.downsampleconv.temporal_conv.bias" in keys
+    assert "res2plus1d.conv5.blocks.0.bn2.running_var" in keys
+    assert "linear.weight" in keys
+
+
+def test_partial_runner_loads_filtered_checkpoint():
+    full = init_random_(R2Plus1DClassifier(), seed=4)
+    part = R2Plus1DLayerWrapper(3, 5, 400, normalize_layer_sizes(3, 5, None, 18))
+    load_reference_state_dict(part, full.state_dict())
+    a = part.state_dict()["res2plus1d.conv4.block1.conv1.spatial_conv.weight"]
+    b = full.state_dict()["res2plus1d.conv4.block1.conv1.spatial_conv.weight"]
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("args,expect", [
+    ((1, 5, None, 34), {2: 3, 3: 4, 4: 6, 5: 3}),
+    ((1, 5, [2, 2, 2, 2], None), {2: 2, 3: 2, 4: 2, 5: 2}),
+    ((1, 5, [9, 1, 2, 3, 4], None), {2: 1, 3: 2, 4: 3, 5: 4}),   # runner convention
+    ((3, 4, [5, 6], None), {3: 5, 4: 6}),
+])
+def test_layer_size_conventions(args, expect):
+    got = normalize_layer_sizes(*args)
+    assert {k: got[k] for k in expect} == expect
+
+
+def test_folded_plan_matches_module_and_boundary_shapes():
+    net = build_network(1, 5, depth=10, seed=2)
+    plan = R2P1DEngine(net, CPU, backend="torch")
+    mod = R2P1DEngine(net, CPU, backend="module")
+    x = ncdhw_to_ndhwc(torch.randn(1, 3, 8, 112, 112), 8)
+    y1, y2 = plan(x), mod(x)
+    assert y1.shape == (1, 400)
+    assert (y1 - y2).abs().max() <= 0.03 * y2.abs().max() + 0.03
+    assert boundary_shape(3, 2) == (2, 8, 56, 56, 64)
+    assert boundary_shape(5, 1) == (1, 2, 14, 14, 256)
+
+
+def test_layer_split_composes_to_whole():
+    torch.manual_seed(0)
+    whole = R2P1DEngine(build_network(1, 5, depth=10, seed=7), CPU, backend="torch")
+    a = R2P1DEngine(build_network(1, 2, depth=10, seed=7), CPU, backend="torch")
+    b = R2P1DEngine(build_network(3, 5, depth=10, seed=7), CPU, backend="torch")
+    assert len(a.ops) + len(b.ops) == len(whole.ops)
+    x = ncdhw_to_ndhwc(torch.randn(2, 3, 8, 112, 112), 8)
+    mid = a(x)
+    assert mid.shape == (2, 8, 56, 56, 64) and mid.dtype == torch.bfloat16
+    assert torch.allclose(b(mid), whole(x), atol=1e-3, rtol=1e-3)
+
+
+def test_batch_mode_bn_only_on_module_backend():
+    net = build_network(1, 5, depth=10)
+    with pytest.raises(ValueError):
+        R2P1DEngine(net, CPU, backend="torch", bn_mode="batch")
+    eng = R2P1DEngine(net, CPU, backend="module", bn_mode="batch")
+    assert eng.module.training
+
+
+def test_runner_accepts_reference_layout_and_empty_batch():
+    r = R2P1DRunner(CPU, 4, 5, depth=10, warmup=0)
+    x = torch.randn(2, 128, 4, 28, 28)                  # reference NCDHW fp32
+    (y,), _, tc = r((x,), None, TimeCard(1))
+    assert y.shape == (2, 400)
+    (y0,), _, _ = r((torch.zeros(0, 4, 28, 28, 128, dtype=torch.bfloat16),), None, TimeCard(2))
+    assert y0.shape == (0, 400)
+    assert R2P1DRunner.output_shape_for(start_index=1, end_index=3) == ((15, 4, 28, 28, 128),)
+    with pytest.raises(ValueError):
+        R2P1DRunner(CPU, 0, 5)
+
+
+def test_synthetic_decoder_and_loader():
+    dec = SyntheticDecoder(CPU)
+    a = dec.decode(3, [0, 16])
+    b = dec.decode(3, [0, 16])
+    assert a.shape == (2, 8, 112, 112, 8) and torch.equal(a, b)
+    assert torch.count_nonzero(a[..., 3:]) == 0
+    assert not torch.equal(a[0], a[1])
+    loader = R2P1DLoader(CPU, num_clips_population=[15], num_clips_weights=[1], seed=0,
+                         warmup=0)
+    tc = TimeCard(1)
+    (frames,), nt, tc = loader(None, "synthetic://5?frames=300", tc)
+    assert frames.shape[0] == 15 and tc.num_clips == 15 and nt is None
+    (frames,), _, tc = loader(None, "synthetic://6?frames=20", TimeCard(2))
+    assert frames.shape[0] == 2                        # 8 * 2 <= 20 < 8 * 3
+
+
+def test_single_step_end_to_end_cpu():
+    s = R2P1DSingleStep(CPU, depth=10, num_clips_population=[2], num_clips_weights=[1],
+                        seed=1, warmup=0)
+    (logits,), _, tc = s(None, "synthetic://1?frames=100", TimeCard(1))
+    assert logits.shape == (2, 400) and tc.num_clips == 2
+    sums, arg = video_reduce(logits, torch.tensor([0, 2]))
+    assert int(arg[0]) == int(logits.sum(0).argmax())
+
+
+def test_layout_converters_roundtrip():
+    x = torch.randn(2, 3, 4, 5, 6)
+    y = ncdhw_to_ndhwc(x, 8, dtype=torch.float32)
+    assert y.shape == (2, 4, 5, 6, 8)
+    assert torch.equal(ndhwc_to_ncdhw(y, 3), x)

@@ -1,0 +1,145 @@
+"""Multi-process pipelines end to end on CPU (spawned runners, host rings).
+
+These run the real launcher (client + runner processes + barriers + queues)
+with ``gpus: [-1]`` everywhere and a tiny R(2+1)D-10 so they finish in
+seconds: the CPU plumbing configuration of BASELINE.json (config #1) plus the
+topologies of the reference configs (two-stage, segment + aggregator,
+replicate + batch, layer split) and failure handling.
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+IT = "rnb_amd.models.r2p1d.model.R2P1DVideoPathIterator"
+M = "rnb_amd.models.r2p1d.model."
+SMALL = {"depth": 10, "num_clips_population": [1, 3], "num_clips_weights": [2, 1],
+         "warmup": 0}
+
+
+def run_cfg(tmp_path, cfg, *args, env=None, timeout=240):
+    path = tmp_path / "cfg.json"
+    path.write_text(json.dumps(cfg))
+    out = tmp_path / "res.json"
+    e = dict(os.environ, RNB_NO_TQDM="1", RNB_CPU_THREADS="1", PYTHONPATH=ROOT)
+    if env:
+        e.update(env)
+    cmd = [sys.executable, os.path.join(ROOT, "benchmark.py"), "-c", str(path),
+           "--log-root", str(tmp_path / "logs"), "--json-out", str(out),
+           "--barrier-timeout", "200"] + list(args)
+    t0 = time.time()
+    proc = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e)
+    res = json.loads(out.read_text()) if out.exists() else None
+    return proc, res, time.time() - t0
+
+
+def test_check_flag():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "benchmark.py"), "--check"],
+                         capture_output=True, text=True, timeout=120,
+                         env=dict(os.environ, PYTHONPATH=ROOT))
+    assert out.returncode == 0 and "RnB is ready to go!" in out.stdout
+
+
+def test_nopipeline_single_step_bulk(tmp_path):
+    cfg = {"video_path_iterator": IT, "defaults": SMALL, "pipeline": [
+        {"model": M + "R2P1DSingleStep", "queue_groups": [{"gpus": [-1, -1]}]}]}
+    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "6", "-mi", "0")
+    assert proc.returncode == 0, proc.stdout + proc.stderr
+    assert res["termination_flag"] == "TARGET_NUM_VIDEOS_REACHED"
+    assert res["videos_done"] >= 6 and res["videos_per_s"] > 0
+    assert res["latency"]["count"] >= 1
+    logdir = tmp_path / "logs" / res["job_id"]
+    assert (logdir / "log-meta.txt").exists() and (logdir / "cfg.json").exists()
+    assert (logdir / "g-1-group0-0.txt").exists()
+    header = (logdir / "g-1-group0-0.txt").read_text().splitlines()[0]
+    assert header.split() == ["enqueue_filename", "runner0_start", "inference0_start",
+                              "inference0_finish", "gpu0"]
+
+
+def test_two_stage_host_ring_poisson(tmp_path):
+    cfg = {"video_path_iterator": IT, "defaults": SMALL, "pipeline": [
+        {"model": M + "R2P1DLoader", "queue_groups": [{"gpus": [-1], "out_queues": [0]}],
+         "num_shared_tensors": 4},
+        {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [-1], "in_queue": 0}]}]}
+    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "12", "-mi", "20", "--seed", "3")
+    assert proc.returncode == 0, proc.stdout + proc.stderr
+    assert res["ok"] and "Average time between inference0_finish and runner1_start" in proc.stdout
+
+
+def test_segment_parallel_with_aggregator(tmp_path):
+    cfg = {"video_path_iterator": IT, "defaults": SMALL, "pipeline": [
+        {"model": M + "R2P1DLoader", "queue_groups": [{"gpus": [-1], "out_queues": [0]}],
+         "num_shared_tensors": 8, "num_segments": 2},
+        {"model": M + "R2P1DRunner",
+         "queue_groups": [{"gpus": [-1, -1], "in_queue": 0, "out_queues": [0]}],
+         "num_shared_tensors": 4},
+        {"model": M + "R2P1DAggregator", "queue_groups": [{"gpus": [-1], "in_queue": 0}],
+         "aggregate": 2}]}
+    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "5", "-mi", "0")
+    assert proc.returncode == 0, proc.stdout + proc.stderr
+    assert res["ok"]
+    log = tmp_path / "logs" / res["job_id"] / "g-1-group0-0.txt"
+    header = log.read_text().splitlines()[0].split()
+    # merged TimeCards: post-fork keys suffixed per segment; both segments ran
+    # on "GPU" -1, so merge collapses their gpu column (rnb_logging.py:113-121)
+    assert "runner1_start-0" in header and "runner1_start-1" in header
+    assert "gpu1" in header and "gpu2" in header
+    rows = log.read_text().splitlines()[1:]
+    assert len(rows) >= 4
+
+
+def test_replicate_and_batch_rnb_topology(tmp_path):
+    cfg = {"video_path_iterator": IT, "defaults": dict(SMALL, num_clips_population=[1, 15],
+                                                       num_clips_weights=[4, 1]),
+           "pipeline": [
+               {"model": M + "R2P1DLoader",
+                "queue_groups": [{"gpus": [-1, -1], "out_queues": [0, 1],
+                                  "queue_selector": M + "LargeSmallSelector"}],
+                "num_shared_tensors": 6},
+               {"model": "batcher.Batcher",
+                "queue_groups": [{"gpus": [-1], "in_queue": 0, "out_queues": [0], "batch": 2},
+                                 {"gpus": [-1], "in_queue": 1, "out_queues": [0]}],
+                "num_shared_tensors": 6},
+               {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [-1], "in_queue": 0}]}]}
+    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "6", "-mi", "0")
+    assert proc.returncode == 0, proc.stdout + proc.stderr
+    assert res["videos_done"] >= 6
+
+
+def test_layer_split_pipeline(tmp_path):
+    cfg = {"video_path_iterator": IT, "defaults": SMALL, "pipeline": [
+        {"model": M + "R2P1DLoader", "queue_groups": [{"gpus": [-1], "out_queues": [0]}],
+         "num_shared_tensors": 4},
+        {"model": M + "R2P1DRunner",
+         "queue_groups": [{"gpus": [-1], "in_queue": 0, "out_queues": [0]}],
+         "start_index": 1, "end_index": 2, "num_shared_tensors": 3},
+        {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [-1], "in_queue": 0}],
+         "start_index": 3, "end_index": 5}]}
+    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "3", "-mi", "0")
+    assert proc.returncode == 0, proc.stdout + proc.stderr
+    assert res["ok"]
+
+
+def test_child_failure_aborts_instead_of_hanging(tmp_path):
+    cfg = {"video_path_iterator": IT, "defaults": SMALL, "pipeline": [
+        {"model": M + "R2P1DLoader", "queue_groups": [{"gpus": [-1], "out_queues": [0]}],
+         "num_shared_tensors": 4},
+        {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [-1], "in_queue": 0}]}]}
+    proc, res, dt = run_cfg(tmp_path, cfg, "-v", "50", "-mi", "0",
+                            env={"RNB_FAULT_INJECT": "runner1_item2"})
+    assert proc.returncode != 0
+    assert res["termination_flag"] in ("CHILD_FAILED", "BARRIER_TIMEOUT")
+    assert "injected fault" in proc.stderr
+    assert dt < 150
+
+
+def test_malformed_config_clean_error(tmp_path):
+    cfg = {"video_path_iterator": IT, "pipeline": [
+        {"model": M + "R2P1DLoader", "queue_groups": [{"gpus": [-1], "out_queues": [0]}]},
+        {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [-1], "in_queue": 3}]}]}
+    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "2")
+    assert proc.returncode == 2 and "do not match" in proc.stdout

@@ -1,0 +1,240 @@
+"""TimeCards, sampler, selectors, Batcher, Aggregator, host ring (CPU)."""
+import collections
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from rnb_amd.timecard import TimeCard, TimeCardList, TimeCardSummary, percentile_stats
+from rnb_amd.models.r2p1d.sampler import R2P1DSampler
+from rnb_amd.selector import RoundRobinSelector, ShortestQueueSelector
+from rnb_amd.models.r2p1d.model import LargeSmallSelector, R2P1DAggregator
+from rnb_amd.batcher import Batcher
+
+
+# ---------------------------------------------------------------- TimeCard
+def test_timecard_fork_merge_suffixes_and_gpus():
+    tc = TimeCard(7)
+    tc.record("enqueue_filename")
+    tc.add_gpu(0)
+    tc.record("inference0_finish")
+    kids = [tc.fork(i) for i in range(3)]
+    for i, k in enumerate(kids):
+        k.add_gpu(i + 1)
+        k.record("runner1_start")
+    merged = TimeCard.merge(list(reversed(kids)))
+    assert list(merged.timings) == ["enqueue_filename", "inference0_finish",
+                                    "runner1_start-0", "runner1_start-1", "runner1_start-2"]
+    assert merged.gpus == [(0,), (1, 2, 3)]
+    assert merged.id == 7
+
+
+def test_timecard_fork_rules():
+    tc = TimeCard(1)
+    tc.record("a")
+    child = tc.fork(0)
+    with pytest.raises(RuntimeError):
+        child.fork(1)
+    other = TimeCard(1)
+    other.record("a")
+    other = other.fork(1)
+    other.record("b")
+    with pytest.raises(RuntimeError):
+        TimeCard.merge([child, other])
+
+
+def test_timecardlist_records_all():
+    lst = TimeCardList([TimeCard(1), TimeCard(2)])
+    lst.record("x")
+    lst.add_gpu(4)
+    assert all("x" in tc.timings and tc.gpus == [(4,)] for tc in lst.time_cards)
+    with pytest.raises(NotImplementedError):
+        lst.fork(0)
+
+
+def test_summary_percentiles_and_report(tmp_path):
+    s = TimeCardSummary()
+    for i in range(100):
+        tc = TimeCard(i)
+        tc.record("enqueue_filename", 100.0 + i)
+        tc.record("runner0_start", 100.0 + i + 0.001)
+        tc.record("inference0_finish", 100.0 + i + 0.001 * (i + 1))
+        tc.add_gpu(0)
+        s.register(tc)
+    st = s.latency_stats()
+    assert st["count"] == 100
+    assert abs(st["p50_ms"] - 50.5) < 0.6 and abs(st["max_ms"] - 100.0) < 1e-6
+    assert st["p99_ms"] >= st["p90_ms"] >= st["p50_ms"]
+    deltas = s.mean_deltas(10)
+    assert abs(deltas["enqueue_filename -> runner0_start"] - 1.0) < 1e-6
+    with open(tmp_path / "r.txt", "w") as f:
+        s.save_full_report(f)
+    lines = open(tmp_path / "r.txt").read().splitlines()
+    assert lines[0] == "enqueue_filename runner0_start inference0_finish gpu0"
+    assert len(lines) == 101
+    other = TimeCardSummary()
+    other.merge_from(s)
+    other.merge_from(s)
+    assert len(other) == 200
+    with pytest.raises(AssertionError):
+        bad = TimeCard(0)
+        bad.record("zzz")
+        s.register(bad)
+
+
+def test_percentile_stats_empty():
+    st = percentile_stats([])
+    assert st["count"] == 0 and np.isnan(st["p50_ms"])
+
+
+# ---------------------------------------------------------------- sampler
+def test_sampler_distribution_and_spacing():
+    s = R2P1DSampler(seed=0)
+    counts = collections.Counter()
+    for _ in range(4400):
+        starts = s.sample(300)
+        counts[len(starts)] += 1
+        if len(starts) > 1:
+            d = np.diff(starts)
+            assert (d == d[0]).all() and d[0] == 300 // len(starts)
+        assert starts[0] >= 0 and starts[-1] + 8 <= 300
+    assert set(counts) == {1, 15}
+    assert abs(counts[15] / 4400 - 1 / 11) < 0.02
+    assert abs(s.expected_clips() - 25 / 11) < 1e-9
+
+
+def test_sampler_caps_clips_to_length():
+    s = R2P1DSampler(num_clips_population=[15], num_clips_weights=[1], seed=1)
+    assert len(s.sample(60)) == 7          # 8 * 7 = 56 <= 60
+    assert s.sample(5) is None             # not even one clip fits
+
+
+# ---------------------------------------------------------------- selectors
+def test_round_robin_starts_at_one():
+    s = RoundRobinSelector(3)
+    assert [s.select(None, None, None) for _ in range(5)] == [1, 2, 0, 1, 2]
+
+
+def test_large_small_selector():
+    s = LargeSmallSelector(2)
+    tc = TimeCard(1)
+    tc.num_clips = 15
+    assert s.select(None, None, tc) == 1
+    tc.num_clips = 1
+    assert s.select(None, None, tc) == 0
+    with pytest.raises(ValueError):
+        LargeSmallSelector(3)
+
+
+def test_shortest_queue_selector():
+    class Q:
+        def __init__(self, n):
+            self.n = n
+
+        def qsize(self):
+            return self.n
+    s = ShortestQueueSelector(3, [Q(5), Q(1), Q(3)])
+    assert s.select(None, None, None) == 1
+
+
+# ---------------------------------------------------------------- batcher
+def _item(i, rows=1):
+    tc = TimeCard(i)
+    tc.num_clips = rows
+    return (torch.full((rows, 2), float(i)),), None, tc
+
+
+def test_batcher_stacks_copies_not_views():
+    b = Batcher(torch.device("cpu"), batch=3)
+    buf = torch.zeros(1, 2)
+    outs = []
+    for i in range(3):
+        buf.fill_(i)                       # the runner reuses one placeholder
+        outs.append(b((buf[:1],), None, _item(i)[2]))
+    assert outs[0][2] is None and outs[1][2] is None
+    (t,), _, cards = outs[2]
+    assert t[:, 0].tolist() == [0.0, 1.0, 2.0]
+    assert [c.id for c in cards.time_cards] == [0, 1, 2]
+
+
+def test_batcher_passthrough_and_capacity_flush():
+    assert Batcher(torch.device("cpu"), batch=1)(*_item(5))[2].id == 5
+    b = Batcher(torch.device("cpu"), batch=4, max_rows=15)
+    assert b(*_item(1, 1))[2] is None
+    out = b(*_item(2, 15))                 # would overflow the 15-row slot
+    assert out[0][0].shape[0] == 1 and len(out[2]) == 1
+    assert b._rows() == 15
+
+
+def test_batcher_max_wait_flush():
+    b = Batcher(torch.device("cpu"), batch=8, max_wait_ms=1)
+    b(*_item(1))
+    time.sleep(0.01)
+    out = b(*_item(2))
+    assert out[2] is not None and len(out[2]) == 2
+
+
+# ---------------------------------------------------------------- aggregator
+def test_aggregator_segments_rejoin():
+    agg = R2P1DAggregator(torch.device("cpu"), aggregate=3)
+    tc = TimeCard(9)
+    tc.record("enqueue_filename")
+    kids = [tc.fork(i) for i in range(3)]
+    logits = torch.zeros(6, 400)
+    logits[4, 123] = 10.0
+    res = []
+    for i, k in enumerate(kids):
+        k.record("inference1_finish")
+        res.append(agg((logits[2 * i:2 * i + 2],), None, k))
+    assert res[0] == (None, None, None) and res[1] == (None, None, None)
+    _, pred, merged = res[2]
+    assert pred == 123
+    assert "inference1_finish-2" in merged.timings
+    assert agg.results == {}
+
+
+def test_aggregator_empty_segment_and_single():
+    agg = R2P1DAggregator(torch.device("cpu"), aggregate=1)
+    _, pred, tc = agg((torch.zeros(0, 400),), None, TimeCard(1))
+    assert pred == 0 and tc.id == 1
+
+
+def test_aggregator_timecardlist():
+    agg = R2P1DAggregator(torch.device("cpu"))
+    a, b = TimeCard(1), TimeCard(2)
+    a.num_clips, b.num_clips = 1, 2
+    logits = torch.zeros(3, 400)
+    logits[0, 5] = 1
+    logits[1, 7] = 1
+    logits[2, 7] = 1
+    _, preds, cards = agg((logits,), None, TimeCardList([a, b]))
+    assert preds == [5, 7]
+
+
+# ---------------------------------------------------------------- host ring
+def test_host_ring_roundtrip():
+    import torch.multiprocessing as mp
+    from rnb_amd.parallel.transport import make_ring
+    ctx = mp.get_context("spawn")
+    ring = make_ring(ctx, ((4, 3),), (torch.float32,), 2, producer_gpu=-1,
+                     consumers_cpu=True, name="t")
+    assert ring.kind == "host"
+    ring.producer_attach(torch.device("cpu"))
+    assert ring.wait_free(0)
+    ring.write(0, (torch.arange(6.).view(2, 3),))
+    assert not ring.is_free(0)
+    ph = (torch.zeros(4, 3),)
+    out = ring.read_into(0, ph, ring.descriptor())
+    assert out[0].shape == (2, 3) and out[0][1, 2] == 5
+    ring.release(0)
+    assert ring.is_free(0)
+    with pytest.raises(ValueError):
+        ring.write(1, (torch.zeros(5, 3),))
+    flag = {"n": 0}
+    ring.write(1, (torch.zeros(1, 3),))
+
+    def abort():
+        flag["n"] += 1
+        return flag["n"] > 2
+    assert ring.wait_free(1, abort) is False
