@@ -41,8 +41,12 @@ def parse_args(argv=None):
     ap.add_argument("--depth", type=int, default=34)
     ap.add_argument("--videos-per-step", type=int, default=128,
                     help="videos arriving per GPU per step")
-    ap.add_argument("--video-batch", type=int, default=32,
-                    help="videos per model invocation (RnB batching)")
+    ap.add_argument("--video-batch", type=int, default=64,
+                    help="max videos per model invocation (RnB batching)")
+    ap.add_argument("--clips-per-batch", type=int, default=128,
+                    help="clip budget per model invocation: videos are packed in "
+                         "arrival order until the next one would exceed it, so "
+                         "batches fill a captured graph bucket exactly")
     ap.add_argument("--replicas", type=int, default=2,
                     help="concurrent serving streams per GPU (RnB replication)")
     ap.add_argument("--seed", type=int, default=1234)
@@ -90,23 +94,37 @@ def main(argv=None) -> int:
     vps, vb = args.videos_per_step, args.video_batch
     total_steps = args.warmup + args.steps
     workload = make_workload(vps * total_steps, args.seed + 7919 * rank)
-    batches = [workload[i:i + vb] for i in range(0, len(workload), vb)]
-    max_clips = max(sum(len(s) for _, s in b) for b in batches)
+    # per step: pack the step's videos (arrival order) into batches of at most
+    # --clips-per-batch clips and --video-batch videos
+    step_batches = []
+    for st in range(total_steps):
+        vids, cur, cur_clips, out = workload[st * vps:(st + 1) * vps], [], 0, []
+        for v in vids:
+            n = len(v[1])
+            if cur and (cur_clips + n > args.clips_per_batch or len(cur) >= vb):
+                out.append(cur)
+                cur, cur_clips = [], 0
+            cur.append(v)
+            cur_clips += n
+        if cur:
+            out.append(cur)
+        step_batches.append(out)
+    batches = [b for sb in step_batches for b in sb]
+    max_clips = max(max(sum(len(s) for _, s in b) for b in batches), args.clips_per_batch)
+    buckets = sorted({8, 16, 32, 48, 64, 96, args.clips_per_batch, max_clips})
     eng = FusedR2P1D(device, depth=args.depth, replicas=args.replicas,
-                     max_clips=max(max_clips, 1), max_videos=vb,
+                     max_clips=max(max_clips, 1), max_videos=vb, buckets=buckets,
                      autotune=not args.no_autotune, seed=0)
     t_prep = time.time()
     eng.prepare([sum(len(s) for _, s in b) for b in batches])
     prep_s = time.time() - t_prep
-    batches_per_step = (vps + vb - 1) // vb
-
     def run_step(step):
         start = torch.cuda.Event(enable_timing=True)
         start.record(torch.cuda.current_stream(device))
         for r in eng.replicas:
             r.stream.wait_stream(torch.cuda.current_stream(device))
         pending = []
-        bs = batches[step * batches_per_step:(step + 1) * batches_per_step]
+        bs = step_batches[step]
         for i, b in enumerate(bs):
             rep = eng.replicas[i % len(eng.replicas)]
             ev_done, out, nvid = rep.submit([(vid, st) for vid, st in b])
@@ -140,8 +158,7 @@ def main(argv=None) -> int:
             lat_ms.extend([t] * nvid)
             preds += int((out >= 0).sum())
     n_videos = args.steps * vps
-    clips = sum(len(st) for b in batches[args.warmup * batches_per_step:]
-                for _, st in b)
+    clips = sum(len(st) for sb in step_batches[args.warmup:] for b in sb for _, st in b)
     stats = percentile_stats(np.asarray(lat_ms) / 1e3)
     if world > 1:
         t = torch.tensor([elapsed, stats["p50_ms"], stats["p99_ms"]], device=device)
@@ -174,7 +191,8 @@ def main(argv=None) -> int:
                        "global_batch": vps * world, "seq_len": 8,
                        "parallelism": "dp%d (replicated runners)" % world,
                        "pipeline": "r2p1d-whole (loader+model per GPU, fused)",
-                       "video_batch": vb, "replicas_per_gpu": args.replicas,
+                       "video_batch": vb, "clips_per_batch": args.clips_per_batch,
+                       "replicas_per_gpu": args.replicas,
                        "clip": "8x112x112", "clips_dist": "1 w.p. 10/11, 15 w.p. 1/11",
                        "prepare_s": round(prep_s, 1)},
         }

@@ -1,0 +1,295 @@
+// Halo-tiled 1x3x3 stride-1 spatial convolution (R(2+1)D K3/K7/K13/K19 --
+// ~70 % of R(2+1)D-34's FLOPs) on CDNA4.
+//
+// Why a second kernel: the generic implicit-GEMM kernel (conv_igemm.hip)
+// gathers every input pixel once per tap through LDS-DMA, i.e. 9x for a 3x3
+// conv, and rocprof shows that DMA path -- not MFMA -- bounds it. Here a
+// block owns R full image rows of one frame (R * W <= 224 output pixels) x
+// 144 output channels and, per 64-channel input chunk, DMAs the input PATCH
+// those pixels touch exactly once: image rows [h0-1, h0+R] x columns
+// [-1, W], the padding border coming back as zeros from out-of-range buffer
+// offsets. The 9 taps are then 9 K-steps that read B fragments from the same
+// patch at a shifted row (dh * (W+2) + dw): only the 144 x 64 weight slice
+// streams per step (double-buffered). A first version with 256-pixel tiles
+// spanning frames needed up to 72 KB patches, ran one block per CU with the
+// patch prologue exposed, and was 1.5x slower than the generic kernel.
+//
+// Geometry: up to 7 waves; wave w computes output pixels [32w, 32w+32) of the
+// tile (two 16-pixel MFMA sub-tiles) x all 144 channels (9 sub-tiles) with
+// v_mfma_f32_16x16x32_bf16, A = weights, B = patch rows,
+// so each lane ends with 4 consecutive channels of one pixel (8-byte stores),
+// exactly like the generic kernel's epilogue (bias + residual + ReLU fused).
+// LDS rows are 128 B (64 bf16 channels) with the chunk XOR swizzle
+// (chunk ^ (row & 7)) applied on the DMA source side.
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+
+#define HALO_INVALID 0xFFFFFFF0u
+#define HALO_MAX_PI 8           // patch DMA instructions per wave
+#define HALO_MAX_PX 224         // output pixels per tile (7 waves x 32)
+
+struct HaloParams {
+  const uint16_t* x;   // NDHWC input, Cin channels (multiple of 64)
+  const uint16_t* w;   // [w_rows][K_pad], k = tap * Cin + c, tap = dh * 3 + dw
+  const float* bias;
+  const uint16_t* res;
+  uint16_t* y;
+  int frames, H, W, Cin;
+  int Cout_p, y_stride, res_stride;
+  int K_pad, M, relu, w_rows;
+  int n_ptiles, n_ctiles;
+  int R;               // image rows per tile (R * W <= 224)
+  int bands;           // ceil(H / R) tiles per frame
+  int np;              // patch pixels = (R + 2) * (W + 2)
+  uint32_t x_bytes;
+  uint32_t mB, sB, mW, sW;   // magic division by bands, W
+};
+
+static __device__ __forceinline__ int hdiv(int n, uint32_t m, uint32_t s) {
+  return m ? (int)(__umulhi((uint32_t)n, m) >> s) : n;
+}
+static __device__ __forceinline__ uint16_t hf2bf(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);
+  return __builtin_bit_cast(uint16_t, h);
+}
+static __device__ __forceinline__ float hbf2f(uint32_t u16) { return __uint_as_float(u16 << 16); }
+
+// One block = one tile of R full image rows of one frame (row-aligned, so the
+// patch is a fixed (R+2) x (W+2) box whose border rows/columns are the conv
+// zero padding) x 144 output channels. blockDim = 64 * ceil(R*W / 32) waves;
+// each wave owns 32 output pixels (2 MFMA sub-tiles) x 144 channels. LDS =
+// one patch + 2 weight stages (<= 80 KB), so two blocks share a CU and hide
+// each other's patch prologue.
+template <int TC>
+__global__ __launch_bounds__(448, 2)
+void conv_halo_kernel(const HaloParams p) {
+  constexpr int C_TILE = TC * 16;
+  constexpr int W_INSTR_TOTAL = C_TILE / 8;            // weight DMA instructions / step
+  constexpr int WBUF = C_TILE * 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwaves = blockDim.x >> 6;
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int ctile = wgid % p.n_ctiles;
+  const int ptile = wgid / p.n_ctiles;
+  const int c0 = ctile * C_TILE;
+  const int f = hdiv(ptile, p.mB, p.sB);
+  const int band = ptile - f * p.bands;
+  const int h0 = band * p.R;
+  const int nrows = min(p.R, p.H - h0);
+  const int npx = nrows * p.W;                        // valid output pixels
+  const int p0 = (f * p.H + h0) * p.W;                // first output pixel (raster)
+  const int W2 = p.W + 2;
+
+  const int lrow = lane >> 3;
+  const int kc = (lane & 7) ^ lrow;
+  const int n_instr = (p.np + 7) >> 3;
+  // patch pixel q <-> image (h0 - 1 + q / W2, q % W2 - 1) of frame f
+  uint32_t poff[HALO_MAX_PI];
+#pragma unroll
+  for (int i = 0; i < HALO_MAX_PI; ++i) {
+    const int instr = wave + nwaves * i;
+    const int q = instr * 8 + lrow;
+    uint32_t off = HALO_INVALID;
+    if (instr < n_instr && q < p.np) {
+      const int j = q / W2;
+      const int col = q - j * W2;
+      const int h = h0 - 1 + j, wc = col - 1;
+      if ((unsigned)h < (unsigned)p.H && (unsigned)wc < (unsigned)p.W)
+        off = (uint32_t)((((f * p.H + h) * p.W + wc) * p.Cin + kc * 8) * 2);
+    }
+    poff[i] = off;
+  }
+
+  const int frow = lane & 15;
+  const int fq = lane >> 4;
+  int center[2];
+#pragma unroll
+  for (int tp = 0; tp < 2; ++tp) {
+    const int i = wave * 32 + tp * 16 + frow;          // pixel within the tile
+    const int hh = hdiv(min(i, npx - 1), p.mW, p.sW);
+    const int ww = min(i, npx - 1) - hh * p.W;
+    center[tp] = (hh + 1) * W2 + (ww + 1);
+  }
+
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+  const uint32_t w_bytes = (uint32_t)p.w_rows * (uint32_t)p.K_pad * 2u;
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, w_bytes, 0x00020000);
+  const uint32_t wrow_off = ((uint32_t)c0 * (uint32_t)p.K_pad + (uint32_t)kc * 8u) * 2u;
+
+  char* pbuf = smem;
+  char* wbase = smem + ((p.np + 7) & ~7) * 128;
+
+  auto issue_patch = [&](int chunk) {
+    const uint32_t coff = (uint32_t)chunk * 128u;
+#pragma unroll
+    for (int i = 0; i < HALO_MAX_PI; ++i) {
+      const int instr = wave + nwaves * i;
+      if (instr < n_instr) {
+        const uint32_t off = poff[i] == HALO_INVALID ? HALO_INVALID : poff[i] + coff;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            xr, (__attribute__((address_space(3))) void*)(pbuf + instr * 1024), 16, off, 0, 0,
+            0);
+      }
+    }
+  };
+  auto issue_w = [&](int s, int buf) {
+    const int chunk = s / 9, tap = s - chunk * 9;
+    const uint32_t kofs = (uint32_t)(tap * p.Cin + chunk * 64);
+    for (int instr = wave; instr < W_INSTR_TOTAL; instr += nwaves) {
+      const uint32_t off =
+          wrow_off + ((uint32_t)(instr * 8 + lrow) * (uint32_t)p.K_pad + kofs) * 2u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wr, (__attribute__((address_space(3))) void*)(wbase + buf * WBUF + instr * 1024), 16,
+          off, 0, 0, 0);
+    }
+  };
+
+  f32x4 acc[2][TC];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < TC; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nchunks = p.Cin >> 6;
+  issue_w(0, 0);
+  for (int chunk = 0; chunk < nchunks; ++chunk) {
+    // the previous chunk's last step ended with a barrier: the patch is free
+    issue_patch(chunk);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int tap = 0; tap < 9; ++tap) {
+      const int s = chunk * 9 + tap;
+      if (s + 1 < nchunks * 9) issue_w(s + 1, (s + 1) & 1);
+      const char* wb = wbase + (s & 1) * WBUF;
+      const int dh = tap / 3, dw = tap - dh * 3;
+      const int shift = (dh - 1) * W2 + (dw - 1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ch = kk * 4 + fq;
+        bf16x8 af[2], wf[TC];
+#pragma unroll
+        for (int tc = 0; tc < TC; ++tc) {
+          const int row = tc * 16 + frow;
+          wf[tc] = *(const bf16x8*)(wb + row * 128 + ((ch ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int tp = 0; tp < 2; ++tp) {
+          const int row = center[tp] + shift;
+          af[tp] = *(const bf16x8*)(pbuf + row * 128 + ((ch ^ (row & 7)) << 4));
+        }
+#pragma unroll
+        for (int tp = 0; tp < 2; ++tp)
+#pragma unroll
+          for (int tc = 0; tc < TC; ++tc)
+            acc[tp][tc] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tc], af[tp], acc[tp][tc], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
+#pragma unroll
+  for (int tp = 0; tp < 2; ++tp) {
+    const int i = wave * 32 + tp * 16 + frow;
+    if (i >= npx) continue;
+    const int m = p0 + i;
+#pragma unroll
+    for (int tc = 0; tc < TC; ++tc) {
+      const int c = c0 + tc * 16 + fq * 4;
+      if (c >= p.Cout_p) continue;
+      const float4 b4 = *(const float4*)(p.bias + c);
+      float v0 = acc[tp][tc][0] + b4.x, v1 = acc[tp][tc][1] + b4.y;
+      float v2 = acc[tp][tc][2] + b4.z, v3 = acc[tp][tc][3] + b4.w;
+      if (p.res) {
+        const i32x2 r = *(const i32x2*)(p.res + (size_t)m * p.res_stride + c);
+        v0 += hbf2f((uint32_t)r[0] & 0xFFFFu);
+        v1 += hbf2f((uint32_t)r[0] >> 16);
+        v2 += hbf2f((uint32_t)r[1] & 0xFFFFu);
+        v3 += hbf2f((uint32_t)r[1] >> 16);
+      }
+      if (p.relu) {
+        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f);
+        v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+      }
+      i32x2 o;
+      o[0] = (int)((uint32_t)hf2bf(v0) | ((uint32_t)hf2bf(v1) << 16));
+      o[1] = (int)((uint32_t)hf2bf(v2) | ((uint32_t)hf2bf(v3) << 16));
+      *(i32x2*)(p.y + (size_t)m * p.y_stride + c) = o;
+    }
+  }
+}
+
+static void halo_magic(uint32_t d, uint32_t* m, uint32_t* s) {
+  if (d <= 1) { *m = 0; *s = 0; return; }
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t p = 31 + l;
+  *m = (uint32_t)(((1ull << p) + d - 1) / d);
+  *s = (uint32_t)(p - 32);
+}
+
+static int halo_rows(int H, int W) {
+  int R = HALO_MAX_PX / W;
+  return R < 1 ? 0 : (R > H ? H : R);
+}
+
+extern "C" {
+
+int rnb_halo_params_size() { return (int)sizeof(HaloParams); }
+
+// LDS bytes a launch on this shape requests (-1: shape not supported).
+int rnb_halo_lds_bytes(int frames, int H, int W, int Cin) {
+  const int R = halo_rows(H, W);
+  if (R == 0 || Cin % 64 != 0) return -1;
+  const int np = (R + 2) * (W + 2);
+  if ((np + 7) / 8 > 7 * HALO_MAX_PI) return -1;
+  return ((np + 7) & ~7) * 128 + 2 * 144 * 128;
+}
+
+int rnb_halo_launch(const HaloParams* pp, hipStream_t stream) {
+  HaloParams p = *pp;
+  if (p.Cin % 64 != 0 || p.K_pad != 9 * p.Cin || p.Cout_p % 4 != 0) return -2;
+  if (p.M <= 0) return 0;
+  if ((long long)p.M * p.Cin * 2 > 0x7FFFFF00LL) return -5;
+  p.R = halo_rows(p.H, p.W);
+  if (p.R == 0) return -3;
+  p.bands = (p.H + p.R - 1) / p.R;
+  p.np = (p.R + 2) * (p.W + 2);
+  const int lds = rnb_halo_lds_bytes(p.frames, p.H, p.W, p.Cin);
+  if (lds < 0 || lds > 160 * 1024) return -6;
+  const int waves = (p.R * p.W + 31) / 32;
+  if ((p.np + 7) / 8 > waves * HALO_MAX_PI) return -4;
+  p.x_bytes = (uint32_t)((long long)p.M * p.Cin * 2);
+  halo_magic((uint32_t)p.bands, &p.mB, &p.sB);
+  halo_magic((uint32_t)p.W, &p.mW, &p.sW);
+  p.n_ptiles = p.frames * p.bands;
+  p.n_ctiles = (p.Cout_p + 143) / 144;
+  if (p.n_ctiles * 144 > p.w_rows) return -8;
+  if (p.y_stride < p.Cout_p || (p.res && p.res_stride < p.Cout_p)) return -9;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)conv_halo_kernel<9>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(conv_halo_kernel<9>, dim3((unsigned)(p.n_ptiles * p.n_ctiles)),
+                     dim3(64 * waves), lds, stream, p);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

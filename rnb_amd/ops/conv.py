@@ -25,6 +25,8 @@ import torch.nn.functional as F
 CH_ALIGN = 8        # channel padding of every NDHWC activation
 BK = 64             # K step of the kernel
 W_ROW_SLACK = 256   # extra zero weight rows (>= largest channel tile)
+HALO = 100          # config id of the halo-tiled 1x3x3 stride-1 kernel (conv_halo.hip)
+LDS_LIMIT = 160 * 1024
 
 
 def pad_to(x: int, m: int) -> int:
@@ -108,6 +110,7 @@ class ConvLayer:
         self._config: Dict[Tuple[int, int], int] = {}
         self._ktab: Dict[Tuple[int, int, int], torch.Tensor] = {}
         self.time_major = False   # time-major rows for temporal convs (measured: no gain)
+        self.use_halo = True      # allow the halo-tiled kernel for 1x3x3 stride-1 convs
 
     # ------------------------------------------------------------------
     def out_shape(self, x_shape) -> Tuple[int, int, int, int, int]:
@@ -173,6 +176,38 @@ class ConvLayer:
         p.row_mode = 1 if (self.time_major and g.kernel[0] > 1) else 0
         return p
 
+    def halo_eligible(self, x_shape) -> bool:
+        """1x3x3 / stride 1 / pad (0,1,1) with Cin % 64 == 0 and the patch fits LDS."""
+        g = self.geom
+        if not (g.kernel == (1, 3, 3) and g.stride == (1, 1, 1) and g.padding == (0, 1, 1)
+                and g.cin_p % 64 == 0 and self.use_halo):
+            return False
+        from .native import kernels
+        N, T, H, W, _ = x_shape
+        key = ("halo", N * T, H, W)
+        ok = self._config.get(key)
+        if ok is None:
+            nb = kernels().halo_lds_bytes(N * T, H, W, g.cin_p)
+            ok = 0 < nb <= LDS_LIMIT
+            self._config[key] = ok
+        return bool(ok)
+
+    def halo_params(self, x, y, residual):
+        from .native import HaloParams
+        g = self.geom
+        N, T, H, W, C = x.shape
+        p = HaloParams()
+        p.x, p.w, p.bias = x.data_ptr(), self.wmat.data_ptr(), self.bias.data_ptr()
+        p.res = residual.data_ptr() if residual is not None else None
+        p.y = y.data_ptr()
+        p.frames, p.H, p.W, p.Cin = N * T, H, W, C
+        p.Cout_p, p.y_stride = g.cout_p, y.shape[-1]
+        p.res_stride = residual.shape[-1] if residual is not None else 0
+        p.K_pad, p.M = g.k_pad, N * T * H * W
+        p.relu = 1 if self.relu else 0
+        p.w_rows = self.wmat.shape[0]
+        return p
+
     def heuristic_config(self, M: int) -> int:
         from .native import kernels
         best, best_cost = 0, None
@@ -191,6 +226,8 @@ class ConvLayer:
     def config_for(self, x_shape) -> int:
         key = tuple(x_shape[:4])
         cid = self._config.get(key)
+        if cid is None and self.halo_eligible(x_shape):
+            cid = self._config[key] = HALO
         if cid is None:
             N, T, H, W, _ = x_shape
             To, Ho, Wo = self.geom.out_thw(T, H, W)
@@ -206,14 +243,17 @@ class ConvLayer:
         y = torch.empty(self.out_shape(x.shape), dtype=torch.bfloat16, device=x.device)
         stream = torch.cuda.current_stream(x.device)
         best, best_t = None, None
-        for cid in range(len(kern.configs)):
+        cands = list(range(len(kern.configs)))
+        if self.halo_eligible(x.shape):
+            cands.append(HALO)
+        for cid in cands:
             p = self.params(x, y, residual)
-            kern.conv(p, cid, stream.cuda_stream)          # warm
+            self._launch(p, cid, x, y, residual, stream)    # warm
             start = torch.cuda.Event(enable_timing=True)
             end = torch.cuda.Event(enable_timing=True)
             start.record(stream)
             for _ in range(reps):
-                kern.conv(p, cid, stream.cuda_stream)
+                self._launch(p, cid, x, y, residual, stream)
             end.record(stream)
             end.synchronize()
             t = start.elapsed_time(end) / reps
@@ -221,6 +261,13 @@ class ConvLayer:
                 best, best_t = cid, t
         self._config[tuple(x.shape[:4])] = best
         return best
+
+    def _launch(self, p, cid, x, y, residual, stream):
+        from .native import kernels
+        if cid == HALO:
+            kernels().halo(self.halo_params(x, y, residual), stream.cuda_stream)
+        else:
+            kernels().conv(p, cid, stream.cuda_stream)
 
     # ------------------------------------------------------------------
     def forward_hip(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
@@ -235,8 +282,11 @@ class ConvLayer:
                 raise ValueError("%s: residual %s does not match output %s"
                                  % (self.name, tuple(residual.shape), tuple(y.shape)))
         cid = self.config_for(x.shape) if config is None else config
-        p = self.params(x, y, residual)
-        kernels().conv(p, cid, torch.cuda.current_stream(x.device).cuda_stream)
+        stream = torch.cuda.current_stream(x.device)
+        if cid == HALO:
+            kernels().halo(self.halo_params(x, y, residual), stream.cuda_stream)
+        else:
+            kernels().conv(self.params(x, y, residual), cid, stream.cuda_stream)
         return y
 
     def forward_torch(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,

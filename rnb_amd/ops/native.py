@@ -112,6 +112,22 @@ class ConvParams(ctypes.Structure):
     ]
 
 
+class HaloParams(ctypes.Structure):
+    """Mirror of ``struct HaloParams`` in csrc/conv_halo.hip."""
+    _fields_ = [
+        ("x", ctypes.c_void_p), ("w", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+        ("res", ctypes.c_void_p), ("y", ctypes.c_void_p),
+        ("frames", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+        ("Cin", ctypes.c_int), ("Cout_p", ctypes.c_int), ("y_stride", ctypes.c_int),
+        ("res_stride", ctypes.c_int), ("K_pad", ctypes.c_int), ("M", ctypes.c_int),
+        ("relu", ctypes.c_int), ("w_rows", ctypes.c_int), ("n_ptiles", ctypes.c_int),
+        ("n_ctiles", ctypes.c_int), ("R", ctypes.c_int), ("bands", ctypes.c_int),
+        ("np", ctypes.c_int), ("x_bytes", ctypes.c_uint32),
+        ("mB", ctypes.c_uint32), ("sB", ctypes.c_uint32), ("mW", ctypes.c_uint32),
+        ("sW", ctypes.c_uint32),
+    ]
+
+
 class Kernels:
     """Typed wrappers over librnb_kernels.so."""
 
@@ -137,6 +153,11 @@ class Kernels:
         lib.rnb_video_reduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_void_p]
+        lib.rnb_halo_launch.argtypes = [ctypes.POINTER(HaloParams), ctypes.c_void_p]
+        lib.rnb_halo_launch.restype = ctypes.c_int
+        lib.rnb_halo_lds_bytes.argtypes = [ctypes.c_int] * 4
+        if lib.rnb_halo_params_size() != ctypes.sizeof(HaloParams):
+            raise NativeUnavailable("HaloParams layout mismatch: rebuild")
         if lib.rnb_conv_params_size() != ctypes.sizeof(ConvParams):
             raise NativeUnavailable("ConvParams layout mismatch (%d vs %d): rebuild"
                                     % (lib.rnb_conv_params_size(),
@@ -150,6 +171,12 @@ class Kernels:
     def conv(self, params: ConvParams, config_id: int, stream: int) -> None:
         _check(self.lib.rnb_conv_launch(ctypes.byref(params), config_id, stream),
                "conv (config %d)" % config_id)
+
+    def halo(self, params: HaloParams, stream: int) -> None:
+        _check(self.lib.rnb_halo_launch(ctypes.byref(params), stream), "conv_halo")
+
+    def halo_lds_bytes(self, frames: int, H: int, W: int, cin: int) -> int:
+        return self.lib.rnb_halo_lds_bytes(frames, H, W, cin)
 
     def clipgen_u8(self, out_ptr, vids_ptr, starts_ptr, nclips, F, H, W, stream):
         _check(self.lib.rnb_clipgen_u8(out_ptr, vids_ptr, starts_ptr, nclips, F, H, W,

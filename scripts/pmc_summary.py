@@ -13,7 +13,7 @@ for d in sorted(glob.glob(os.path.join(root, "p*"))):
         continue
     per = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
-        if "conv_igemm" in r["Kernel_Name"]:
+        if os.environ.get("KNAME", "conv_") in r["Kernel_Name"]:
             per[r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, v in per.items():
         vals[k] = v[-1]

@@ -59,11 +59,13 @@ def main():
         cid = op.layer.config_for(src.shape)
         rows.append({"name": op.layer.name, "M": N * To * Ho * Wo, "N": g.cout,
                      "K": g.cin * g.kernel[0] * g.kernel[1] * g.kernel[2],
-                     "tile": "%dx%d" % cfgs[cid], "ms": ms,
+                     "tile": "halo" if cid >= len(cfgs) else "%dx%d" % cfgs[cid], "ms": ms,
                      "tflops": flops / ms / 1e9, "gflop": flops / 1e9})
         if args.compare:
             best = {}
-            for c in range(len(cfgs)):
+            from rnb_amd.ops.conv import HALO
+            cands = list(range(len(cfgs))) + ([HALO] if op.layer.halo_eligible(src.shape) else [])
+            for c in cands:
                 s.record()
                 for _ in range(args.reps):
                     op.layer.forward_hip(src, res, out=y, config=c)
@@ -73,7 +75,8 @@ def main():
                 fam = "best"
                 if fam not in best or t < best[fam][1]:
                     best[fam] = (c, t)
-            rows[-1]["best"] = {k: ("%dx%d" % cfgs[v[0]], v[1]) for k, v in best.items()}
+            rows[-1]["best"] = {k: ("halo" if v[0] >= len(cfgs) else "%dx%d" % cfgs[v[0]], v[1])
+                                for k, v in best.items()}
         bufs[op.dst] = y
     tot_ms = sum(r["ms"] for r in rows)
     tot_gf = sum(r["gflop"] for r in rows)

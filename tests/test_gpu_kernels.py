@@ -146,3 +146,33 @@ def test_time_major_rows_exact(thw, cin, cout, stride):
             y = layer.forward_hip(x, residual=res, config=cfg)
             torch.cuda.synchronize()
             assert torch.equal(y, ref), (mode, cfg)
+
+
+@pytest.mark.parametrize("n,thw,cin,cout", [
+    (2, (8, 56, 56), 64, 144),      # conv2 spatial (K3): tiles span frames, 1 chunk
+    (2, (4, 28, 28), 128, 288),     # conv3 spatial (K7): 2 chunks, 2 channel tiles
+    (3, (2, 14, 14), 256, 576),     # conv4 spatial (K13): tiles span 2-3 frames
+    (1, (3, 5, 7), 64, 96),         # tiny frames, partial channel tile
+    (1, (1, 9, 40), 192, 144),      # 3 chunks, single frame, M tail
+])
+def test_halo_kernel_exact(n, thw, cin, cout):
+    from rnb_amd.ops.conv import HALO
+    layer = _layer(cin, cout, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=True, integer=True)
+    x = _input(n, thw, cin, cin, integer=True)
+    assert layer.halo_eligible(x.shape)
+    res_shape = layer.out_shape(x.shape)
+    res = _input(res_shape[0], res_shape[1:4], res_shape[4], cout, integer=True, seed=3)
+    ref = layer.forward_torch(x, residual=res, out_dtype=torch.bfloat16)
+    y = layer.forward_hip(x, residual=res, config=HALO)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref), (y.float() - ref.float()).abs().max().item()
+
+
+def test_halo_kernel_random_matches_generic():
+    from rnb_amd.ops.conv import HALO
+    layer = _layer(64, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1))
+    x = _input(2, (8, 56, 56), 64, 64)
+    a = layer.forward_hip(x, config=HALO).float()
+    b = layer.forward_hip(x, config=2).float()
+    torch.cuda.synchronize()
+    assert (a - b).abs().max().item() <= 2e-2 * b.abs().max().item()
