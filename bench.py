@@ -39,7 +39,7 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--depth", type=int, default=34)
-    ap.add_argument("--videos-per-step", type=int, default=128,
+    ap.add_argument("--videos-per-step", type=int, default=256,
                     help="videos arriving per GPU per step")
     ap.add_argument("--video-batch", type=int, default=64,
                     help="max videos per model invocation (RnB batching)")
@@ -47,11 +47,14 @@ def parse_args(argv=None):
                     help="clip budget per model invocation: videos are packed in "
                          "arrival order until the next one would exceed it, so "
                          "batches fill a captured graph bucket exactly")
-    ap.add_argument("--replicas", type=int, default=2,
+    ap.add_argument("--replicas", type=int, default=3,
                     help="concurrent serving streams per GPU (RnB replication)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-autotune", action="store_true")
     ap.add_argument("--json-out", type=str, default=None)
+    ap.add_argument("--trace", type=str, default=None,
+                    help="write a per-kernel time table of the timed steps (rocprofiler-"
+                         "sdk tracer, rnb_amd.profiling.tracer) to this path")
     return ap.parse_args(argv)
 
 
@@ -71,6 +74,9 @@ def make_workload(n_videos: int, seed: int):
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    if args.trace:
+        from rnb_amd.profiling import tracer
+        tracer.initialize()            # before the HIP runtime starts
     import torch
     import torch.distributed as dist
     import numpy as np
@@ -141,6 +147,9 @@ def main(argv=None) -> int:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
+    if args.trace:
+        tracer.flush()
+        tracer.report()                # drop warm-up / autotune records
     t0 = time.perf_counter()
     lat_ms, preds = [], 0
     step_records = []
@@ -152,6 +161,21 @@ def main(argv=None) -> int:
         dist.barrier()
     torch.cuda.synchronize(device)
     elapsed = t1 - t0
+    if args.trace and rank == 0:
+        tracer.flush()
+        recs = tracer.report()
+        summ = tracer.summary(recs)
+        busy = sum(v["total_us"] for v in summ.values())
+        with open(args.trace, "w") as f:
+            f.write("# per-kernel GPU time over %d timed steps (%.1f ms wall, %.1f ms "
+                    "kernel busy summed over streams)\n" % (args.steps, elapsed * 1e3,
+                                                            busy / 1e3))
+            f.write("%-70s %7s %11s %9s %6s\n" % ("kernel", "calls", "total_us",
+                                                   "mean_us", "pct"))
+            for name, st in summ.items():
+                f.write("%-70s %7d %11.1f %9.1f %5.1f%%\n"
+                        % (name[:70], st["count"], st["total_us"], st["mean_us"],
+                           100.0 * st["total_us"] / max(busy, 1e-9)))
     for start, pending in step_records:
         for tev, out, nvid in pending:
             t = start.elapsed_time(tev)

@@ -8,7 +8,7 @@
 //                        zero), the fused form of the reference's
 //                        .float().permute() + slot copy.
 //  * rnb_head            AdaptiveAvgPool3d(1) + Linear(512 -> classes) fused
-//                        into one kernel per clip.
+//                        into one kernel, 16 clips per block.
 //  * rnb_video_reduce    per-video sum of clip logits + argmax, the GPU form
 //                        of R2P1DAggregator's reduction.
 #include <hip/hip_runtime.h>
@@ -25,41 +25,41 @@ static __device__ __forceinline__ uint32_t pixel_hash(uint32_t vid, uint32_t fra
   return h >> 24;
 }
 
-// out[clip][f][y][x][c], 16 bytes per thread
+// out[clip][f][y][x][c]; one thread = 16 consecutive pixels (48 bytes) of one
+// frame (H*W is a multiple of 16 for the 112x112 clips; a tail is handled).
 __global__ void clipgen_u8_kernel(uint8_t* __restrict__ out, const int* __restrict__ vids,
                                   const int* __restrict__ starts, int nclips, int F, int H,
                                   int W) {
-  const long long clip_bytes = (long long)F * H * W * 3;
-  const long long total = clip_bytes * nclips;
-  const long long i16 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 16;
-  if (i16 >= total) return;
-  uint32_t words[4];
+  const long long hw = (long long)H * W;
+  const long long total_px = hw * F * nclips;
+  const long long px0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (px0 >= total_px) return;
+  const long long frame = px0 / hw;                  // clip * F + f
+  const int clip = (int)(frame / F);
+  const uint32_t vid = (uint32_t)vids[clip];
+  const uint32_t fr = (uint32_t)(starts[clip] + (int)(frame - (long long)clip * F));
+  const uint32_t pix0 = (uint32_t)(px0 - frame * hw);
+  const int n = (int)min(16LL, min(total_px - px0, hw - (long long)pix0));
+  uint32_t words[12];
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    uint32_t word = 0;
+  for (int w = 0; w < 12; ++w) words[w] = 0;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const long long idx = i16 + w * 4 + b;
-      uint32_t v = 0;
-      if (idx < total) {
-        const int clip = (int)(idx / clip_bytes);
-        const long long r = idx - (long long)clip * clip_bytes;
-        const int c = (int)(r % 3);
-        const long long pixf = r / 3;
-        const int pix = (int)(pixf % ((long long)H * W));
-        const int f = (int)(pixf / ((long long)H * W));
-        v = pixel_hash((uint32_t)vids[clip], (uint32_t)(starts[clip] + f), (uint32_t)pix,
-                       (uint32_t)c);
-      }
-      word |= v << (8 * b);
+  for (int i = 0; i < 16; ++i) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int b = i * 3 + c;
+      const uint32_t v = i < n ? pixel_hash(vid, fr, pix0 + i, c) : 0u;
+      words[b >> 2] |= v << (8 * (b & 3));
     }
-    words[w] = word;
   }
-  if (i16 + 16 <= total) {
-    *(uint4*)(out + i16) = make_uint4(words[0], words[1], words[2], words[3]);
+  uint8_t* dst = out + px0 * 3;
+  if (n == 16) {
+    uint4* d4 = (uint4*)dst;                         // 48 * t bytes: 16-B aligned
+    d4[0] = make_uint4(words[0], words[1], words[2], words[3]);
+    d4[1] = make_uint4(words[4], words[5], words[6], words[7]);
+    d4[2] = make_uint4(words[8], words[9], words[10], words[11]);
   } else {
-    for (int b = 0; b < 16 && i16 + b < total; ++b)
-      out[i16 + b] = (uint8_t)(words[b >> 2] >> (8 * (b & 3)));
+    for (int b = 0; b < n * 3; ++b) dst[b] = (uint8_t)(words[b >> 2] >> (8 * (b & 3)));
   }
 }
 
@@ -86,38 +86,55 @@ __global__ void preprocess_kernel(const uint8_t* __restrict__ in, uint16_t* __re
   *(uint4*)(out + i * 8) = make_uint4(r | (g << 16), b, 0u, 0u);
 }
 
-// x: [N][S][Cs] bf16 (NDHWC, S = T*H*W), wgt: [ncls][C] f32, out: [N][ncls] f32.
-// One block per clip: 256 threads pool the clip into LDS, then each wave
-// computes a strided subset of the classes with a 64-lane dot + shuffle reduce.
+// x: [N][S][Cs] bf16 (NDHWC, S = T*H*W), wt: [C][ncls] f32 (TRANSPOSED linear
+// weight), out: [N][ncls] f32. Grid = (ceil(ncls / 64), ceil(N / 16)): a block
+// pools its 16 clips into LDS, then lane l of every wave computes class
+// 64 * blockIdx.x + l for 4 of the clips, reading wt[c][class] coalesced (each
+// wave one 256-B row segment per c) and the pooled features as LDS broadcasts.
+#define HEAD_CLIPS 16
+#define HEAD_CLS 64
 __global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ x,
-                                                   const float* __restrict__ wgt,
+                                                   const float* __restrict__ wt,
                                                    const float* __restrict__ bias,
-                                                   float* __restrict__ out, int S, int C,
-                                                   int Cs, int ncls) {
-  extern __shared__ float pooled[];
-  const int n = blockIdx.x;
-  const uint16_t* xc = x + (size_t)n * S * Cs;
+                                                   float* __restrict__ out, int N, int S,
+                                                   int C, int Cs, int ncls) {
+  extern __shared__ float pooled[];                  // [HEAD_CLIPS][C]
+  const int n0 = blockIdx.y * HEAD_CLIPS;
+  const int nb = min(HEAD_CLIPS, N - n0);
   const float inv = 1.0f / (float)S;
-  for (int c = threadIdx.x * 2; c < C; c += 512) {
+  for (int idx = threadIdx.x; idx < HEAD_CLIPS * (C / 2); idx += blockDim.x) {
+    const int j = idx / (C / 2);
+    const int c = (idx - j * (C / 2)) * 2;
     float s0 = 0.f, s1 = 0.f;
-    for (int s = 0; s < S; ++s) {
-      const uint32_t v = *(const uint32_t*)(xc + (size_t)s * Cs + c);
-      s0 += __uint_as_float(v << 16);
-      s1 += __uint_as_float(v & 0xFFFF0000u);
+    if (j < nb) {
+      const uint16_t* xc = x + (size_t)(n0 + j) * S * Cs + c;
+      for (int s = 0; s < S; ++s) {
+        const uint32_t v = *(const uint32_t*)(xc + (size_t)s * Cs);
+        s0 += __uint_as_float(v << 16);
+        s1 += __uint_as_float(v & 0xFFFF0000u);
+      }
     }
-    pooled[c] = s0 * inv;
-    if (c + 1 < C) pooled[c + 1] = s1 * inv;
+    pooled[j * C + c] = s0 * inv;
+    pooled[j * C + c + 1] = s1 * inv;
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  for (int o = wave; o < ncls; o += 4) {
-    const float* wr = wgt + (size_t)o * C;
-    float acc = 0.f;
-    for (int c = lane; c < C; c += 64) acc += wr[c] * pooled[c];
+  const int wave = threadIdx.x >> 6;                 // clips 4*wave .. 4*wave+3
+  const int o = blockIdx.x * HEAD_CLS + lane;
+  if (o >= ncls) return;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const float* pj = pooled + (wave * 4) * C;
+#pragma unroll 8
+  for (int c = 0; c < C; ++c) {
+    const float w = wt[(size_t)c * ncls + o];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
-    if (lane == 0) out[(size_t)n * ncls + o] = acc + bias[o];
+    for (int j = 0; j < 4; ++j) acc[j] += w * pj[j * C + c];
+  }
+  const float b = bias[o];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int clip = wave * 4 + j;
+    if (clip < nb) out[(size_t)(n0 + clip) * ncls + o] = acc[j] + b;
   }
 }
 
@@ -160,7 +177,8 @@ extern "C" {
 int rnb_clipgen_u8(void* out, const int* vids, const int* starts, int nclips, int F, int H,
                    int W, hipStream_t stream) {
   if (nclips <= 0) return 0;
-  const long long total = (long long)nclips * F * H * W * 3;
+  if (((long long)H * W) % 16 != 0) return -2;      // 16-pixel runs must not cross frames
+  const long long total = (long long)nclips * F * H * W;
   const long long threads = (total + 15) / 16;
   const int block = 256;
   const long long grid = (threads + block - 1) / block;
@@ -184,12 +202,15 @@ int rnb_preprocess(const void* in, void* out, long long npix, const float* mean,
   return (int)hipGetLastError();
 }
 
+// w: TRANSPOSED linear weight [C][ncls]
 int rnb_head(const void* x, const float* w, const float* b, float* out, int N, int S, int C,
              int Cs, int ncls, hipStream_t stream) {
   if (N <= 0) return 0;
   if (C % 2 != 0 || Cs % 2 != 0 || Cs < C) return -2;
-  hipLaunchKernelGGL(head_kernel, dim3(N), dim3(256), C * sizeof(float), stream,
-                     (const uint16_t*)x, w, b, out, S, C, Cs, ncls);
+  if ((size_t)HEAD_CLIPS * C * sizeof(float) > 64 * 1024) return -3;
+  const dim3 grid((ncls + HEAD_CLS - 1) / HEAD_CLS, (N + HEAD_CLIPS - 1) / HEAD_CLIPS);
+  hipLaunchKernelGGL(head_kernel, grid, dim3(256), HEAD_CLIPS * C * sizeof(float), stream,
+                     (const uint16_t*)x, w, b, out, N, S, C, Cs, ncls);
   return (int)hipGetLastError();
 }
 

@@ -95,6 +95,8 @@ class Head:
 
     def __init__(self, linear: torch.nn.Linear, device: torch.device):
         self.weight = linear.weight.detach().float().to(device).contiguous()
+        # the kernel reads the transposed [C][classes] matrix (coalesced per class)
+        self.weight_t = self.weight.t().contiguous()
         self.bias = linear.bias.detach().float().to(device).contiguous()
         self.num_classes, self.channels = self.weight.shape
 
@@ -104,7 +106,7 @@ class Head:
             from .native import kernels
             if out is None:
                 out = torch.empty((N, self.num_classes), dtype=torch.float32, device=x.device)
-            kernels().head(x.data_ptr(), self.weight.data_ptr(), self.bias.data_ptr(),
+            kernels().head(x.data_ptr(), self.weight_t.data_ptr(), self.bias.data_ptr(),
                            out.data_ptr(), N, T * H * W, self.channels, Cs, self.num_classes,
                            torch.cuda.current_stream(x.device).cuda_stream)
             return out

@@ -176,3 +176,21 @@ def test_halo_kernel_random_matches_generic():
     b = layer.forward_hip(x, config=2).float()
     torch.cuda.synchronize()
     assert (a - b).abs().max().item() <= 2e-2 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("n", [1, 16, 37])
+def test_head_many_clips(n):
+    lin = torch.nn.Linear(512, 400)
+    head = vops.Head(lin, DEV)
+    x = torch.randn(n, 1, 7, 7, 512).to(torch.bfloat16).to(DEV)
+    y = head.forward(x)
+    torch.cuda.synchronize()
+    assert torch.allclose(y, head.forward_torch(x), atol=1e-4, rtol=1e-4)
+
+
+def test_clipgen_partial_and_many_clips():
+    vids = torch.arange(5, dtype=torch.int32) * 7
+    starts = torch.arange(5, dtype=torch.int32) * 3
+    g = vops.clipgen_u8(vids.to(DEV), starts.to(DEV), 8, 112, 112)
+    torch.cuda.synchronize()
+    assert torch.equal(g.cpu(), vops.clipgen_u8(vids, starts, 8, 112, 112))
