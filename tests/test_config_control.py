@@ -124,6 +124,26 @@ def test_check_gpus_rejects_missing_gpu(monkeypatch):
     check_gpus(cpu, num_devices=0)
 
 
+def test_check_gpus_free_vram_threshold(monkeypatch):
+    """amdsmi VRAM check (benchmark.py:97-125 used NVML memory.used == 0)."""
+    import rnb_amd.config as config
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    spec = load_pipeline(os.path.join(CONFIGS, "r2p1d-whole.json"))   # GPU 0
+    monkeypatch.setattr(config, "gpu_memory_used_bytes", lambda: [5 << 30, 0])
+    monkeypatch.delenv("RNB_GPU_FREE_MB", raising=False)
+    check_gpus(spec, num_devices=2)                       # check off by default
+    with pytest.raises(ConfigError, match="not free"):
+        check_gpus(spec, num_devices=2, free_threshold_bytes=1 << 30)
+    monkeypatch.setenv("RNB_GPU_FREE_MB", "8192")
+    check_gpus(spec, num_devices=2)                       # 5 GiB < 8 GiB threshold
+    monkeypatch.setenv("RNB_GPU_FREE_MB", "1024")
+    with pytest.raises(ConfigError, match="not free"):
+        check_gpus(spec, num_devices=2)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")        # logical 0 -> physical 1 (free)
+    check_gpus(spec, num_devices=1)
+
+
 @pytest.mark.parametrize("batch,k", [(11, 3), (15, 3), (1, 3), (10, 4), (7, 7)])
 def test_segment_bounds_partition(batch, k):
     bounds = [segment_bounds(batch, k, i) for i in range(k)]

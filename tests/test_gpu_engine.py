@@ -159,3 +159,10 @@ def test_native_libraries_loaded_from_tree():
     paths = native.loaded_paths()
     here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     assert any(p.startswith(here) for p in paths)
+
+
+@pytest.mark.gpu
+def test_amdsmi_vram_query():
+    from rnb_amd.config import gpu_memory_used_bytes
+    used = gpu_memory_used_bytes()
+    assert used is not None and len(used) >= 1 and all(u >= 0 for u in used)

@@ -58,6 +58,11 @@ def test_nopipeline_single_step_bulk(tmp_path):
     header = (logdir / "g-1-group0-0.txt").read_text().splitlines()[0]
     assert header.split() == ["enqueue_filename", "runner0_start", "inference0_start",
                               "inference0_finish", "gpu0"]
+    from rnb_amd.analysis import load_job
+    job = load_job(str(logdir))
+    assert len(job.requests) >= 6 and job.throughput > 0
+    assert job.latency_stats(5)["count"] == res["latency"]["count"]
+    assert list(job.breakdown_ms(0))[-1] == "step 0 (loader/model)"
 
 
 def test_two_stage_host_ring_poisson(tmp_path):
