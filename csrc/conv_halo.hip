@@ -29,6 +29,12 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 
+// Bottleneck experiments (scripts/kernel_exp.py builds variants; 0 = product):
+// 1 no MFMA, 2 no per-tap weight DMA, 3 no per-tap wait/barrier, 4 no DMA at all
+#ifndef HALO_EXP
+#define HALO_EXP 0
+#endif
+
 #define HALO_INVALID 0xFFFFFFF0u
 #define HALO_MAX_PI 8           // patch DMA instructions per wave
 #define HALO_MAX_PX 224         // output pixels per tile (7 waves x 32)
@@ -165,15 +171,15 @@ void conv_halo_kernel(const HaloParams p) {
     for (int b = 0; b < TC; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nchunks = p.Cin >> 6;
-  issue_w(0, 0);
+  if (HALO_EXP != 4) issue_w(0, 0);
   for (int chunk = 0; chunk < nchunks; ++chunk) {
     // the previous chunk's last step ended with a barrier: the patch is free
-    issue_patch(chunk);
+    if (HALO_EXP != 4) issue_patch(chunk);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int tap = 0; tap < 9; ++tap) {
       const int s = chunk * 9 + tap;
-      if (s + 1 < nchunks * 9) issue_w(s + 1, (s + 1) & 1);
+      if (HALO_EXP != 2 && HALO_EXP != 4 && s + 1 < nchunks * 9) issue_w(s + 1, (s + 1) & 1);
       const char* wb = wbase + (s & 1) * WBUF;
       const int dh = tap / 3, dw = tap - dh * 3;
       const int shift = (dh - 1) * W2 + (dw - 1);
@@ -194,12 +200,19 @@ void conv_halo_kernel(const HaloParams p) {
 #pragma unroll
         for (int tp = 0; tp < 2; ++tp)
 #pragma unroll
-          for (int tc = 0; tc < TC; ++tc)
-            acc[tp][tc] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tc], af[tp], acc[tp][tc], 0, 0, 0);
+          for (int tc = 0; tc < TC; ++tc) {
+            if (HALO_EXP == 1) {    // keep the fragment reads alive, drop the MFMA
+              acc[tp][tc][0] += __builtin_bit_cast(float, (int)(wf[tc][0] ^ af[tp][1]));
+            } else {
+              acc[tp][tc] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tc], af[tp], acc[tp][tc], 0, 0, 0);
+            }
+          }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      if (HALO_EXP != 3) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
     }
   }
 

@@ -60,6 +60,12 @@ struct ConvParams {
   uint32_t mG, sG;
 };
 
+// Bottleneck experiments (scripts/kernel_exp.py builds variants; 0 = product):
+// 1 no MFMA, 2 no weight DMA, 3 no per-step wait/barrier (2-stage), 4 no DMA
+#ifndef CONV_EXP
+#define CONV_EXP 0
+#endif
+
 #define INVALID_OFF 0xFFFFFFF0u
 
 static __device__ __forceinline__ uint16_t f2bf(float f) {
@@ -96,8 +102,7 @@ static __device__ __forceinline__ float bf2f(uint32_t u16) {
 // per block), so a chunk is valid iff (rowmask & req) == req. A K chunk past
 // K_total gets req = bit 31, which no row mask has.
 //
-// Double-buffered: the next step's DMA is issued before the current step's
-// MFMAs and retired by vmcnt(0) + barrier at the end of the step.
+// Staging depth (2 or 3 LDS buffers) is a template parameter, see the kernel.
 // Decode GEMM row m into output coordinates; returns false for padding rows.
 static __device__ __forceinline__ bool decode_row(const ConvParams& p, int m, int& n, int& to,
                                                   int& ho, int& wo) {
@@ -123,7 +128,26 @@ static __device__ __forceinline__ bool decode_row(const ConvParams& p, int m, in
   return true;
 }
 
-template <int TP, int TC, int WP, int WC>
+// s_waitcnt with only the vector-memory counter constrained (gfx9 encoding:
+// vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14)
+template <int N>
+static __device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
+}
+
+#define KTAB_MAX 640   // K_pad / 8 entries held in LDS by the 3-stage kernels
+
+// NS = LDS stages. NS == 2: the next step's DMA is issued before the current
+// step's MFMAs and retired by vmcnt(0) + barrier at the end of the step.
+// NS == 3: two steps stay in flight; each step starts with a COUNTED vmcnt
+// (this wave's DMA of step s retired, step s+1 still in flight) and a raw
+// s_barrier (never __syncthreads(), whose fence would drain the in-flight
+// DMA: cdna_hip_programming.md "Pipelining across barriers"), then issues
+// step s+2 into the buffer step s-1 used and computes step s. The K-chunk
+// table is staged into LDS first so no ordinary global load (which hipcc
+// waits for with vmcnt(0)) sits inside the loop.
+template <int TP, int TC, int WP, int WC, int NS>
 __global__ __launch_bounds__(256, 2)
 void conv_igemm_kernel(const ConvParams p) {
   constexpr int P_TILE = WP * TP * 16;
@@ -134,10 +158,12 @@ void conv_igemm_kernel(const ConvParams p) {
   constexpr int W_INSTR = (W_INSTR_TOTAL + 3) / 4;
   constexpr int ACT_BYTES = P_TILE * BK * 2;
   constexpr int BUF_BYTES = (P_TILE + C_TILE) * BK * 2;
+  constexpr int KTAB_BYTES = NS == 3 ? KTAB_MAX * 8 : 0;
   static_assert(WP * WC == 4, "4 waves per block");
   static_assert(C_TILE % 16 == 0 && P_TILE % 32 == 0, "tile shape");
+  static_assert(NS == 2 || NS == 3, "stages");
 
-  __shared__ __attribute__((aligned(16))) char lds[2 * BUF_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[NS * BUF_BYTES + KTAB_BYTES];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -180,6 +206,7 @@ void conv_igemm_kernel(const ConvParams p) {
   const uint32_t wrow_off = ((uint32_t)c0 * (uint32_t)p.K_pad + (uint32_t)kc * 8u) * 2u;
 
   auto issue = [&](int s, int buf, int2 e) {
+    if (CONV_EXP == 4) return;
     char* base = lds + buf * BUF_BYTES;
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) {
@@ -192,7 +219,7 @@ void conv_igemm_kernel(const ConvParams p) {
 #pragma unroll
     for (int j = 0; j < W_INSTR; ++j) {
       const int instr = wave + 4 * j;
-      if (W_INSTR_TOTAL % 4 == 0 || instr < W_INSTR_TOTAL) {
+      if (CONV_EXP != 2 && (W_INSTR_TOTAL % 4 == 0 || instr < W_INSTR_TOTAL)) {
         const uint32_t off = wrow_off + ((uint32_t)(instr * 8 + lrow) * (uint32_t)p.K_pad +
                                          (uint32_t)(s * BK)) * 2u;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -209,22 +236,9 @@ void conv_igemm_kernel(const ConvParams p) {
     for (int b = 0; b < TC; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nsteps = p.K_pad / BK;
-  const int2* ktab = p.ktab + kc;
-  int2 e_next = ktab[0];
-  issue(0, 0, e_next);
-  if (nsteps > 1) e_next = ktab[8];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
   const int frow = lane & 15;
   const int fq = lane >> 4;
-  for (int s = 0; s < nsteps; ++s) {
-    const int cur = s & 1;
-    if (s + 1 < nsteps) {
-      issue(s + 1, cur ^ 1, e_next);
-      if (s + 2 < nsteps) e_next = ktab[(s + 2) * 8];
-    }
-    const char* abase = lds + cur * BUF_BYTES;
+  auto compute = [&](const char* abase) {
     const char* wbase = abase + ACT_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -243,11 +257,66 @@ void conv_igemm_kernel(const ConvParams p) {
 #pragma unroll
       for (int tp = 0; tp < TP; ++tp)
 #pragma unroll
-        for (int tc = 0; tc < TC; ++tc)
-          acc[tp][tc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tc], af[tp], acc[tp][tc], 0, 0, 0);
+        for (int tc = 0; tc < TC; ++tc) {
+          if (CONV_EXP == 1)
+            acc[tp][tc][0] += __builtin_bit_cast(float, (int)(wf[tc][0] ^ af[tp][1]));
+          else
+            acc[tp][tc] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tc], af[tp], acc[tp][tc], 0, 0, 0);
+        }
     }
+  };
+
+  if constexpr (NS == 2) {
+    const int2* ktab = p.ktab + kc;
+    int2 e_next = ktab[0];
+    issue(0, 0, e_next);
+    if (nsteps > 1) e_next = ktab[8];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+      const int cur = s & 1;
+      if (s + 1 < nsteps) {
+        issue(s + 1, cur ^ 1, e_next);
+        if (s + 2 < nsteps) e_next = ktab[(s + 2) * 8];
+      }
+      compute(lds + cur * BUF_BYTES);
+      if (CONV_EXP != 3) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    }
+  } else {
+    // K-chunk table -> LDS (nsteps * 8 entries <= KTAB_MAX, checked on launch)
+    int2* ktab_l = (int2*)(lds + NS * BUF_BYTES);
+    for (int i = tid; i < nsteps * 8; i += 256) ktab_l[i] = p.ktab[i];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // this wave's DMA instructions per step (weights split unevenly over waves)
+    constexpr int W_LAST = W_INSTR_TOTAL % 4 == 0 ? 4 : W_INSTR_TOTAL % 4;
+    constexpr int PER_STEP_HI = A_INSTR + W_INSTR;
+    constexpr int PER_STEP_LO = A_INSTR + W_INSTR - 1;
+    const bool hi = wave < W_LAST;
+    issue(0, 0, ktab_l[kc]);
+    if (nsteps > 1) issue(1, 1, ktab_l[8 + kc]);
+    int cur = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      // retire this wave's DMA of step s (step s+1 may stay in flight)
+      if (s + 1 < nsteps) {
+        if (hi) wait_vmcnt<PER_STEP_HI>(); else wait_vmcnt<PER_STEP_LO>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (s + 2 < nsteps) {
+        const int nb = cur == 0 ? 2 : cur - 1;       // (s + 2) % 3
+        issue(s + 2, nb, ktab_l[(s + 2) * 8 + kc]);
+      }
+      compute(lds + cur * BUF_BYTES);
+      cur = cur == 2 ? 0 : cur + 1;
+    }
   }
 
   // ---- epilogue: bias (+ residual) (+ ReLU) -> bf16, 4 channels per lane ----
@@ -293,11 +362,14 @@ void conv_igemm_kernel(const ConvParams p) {
 // host side: config table + launcher (C ABI, called through ctypes / engine)
 // ---------------------------------------------------------------------------
 struct ConvConfig {
-  int p_tile, c_tile;
+  int p_tile, c_tile, stages;
   void (*kernel)(const ConvParams);
 };
 
-#define CFG(TP, TC, WP, WC) {WP * TP * 16, WC * TC * 16, conv_igemm_kernel<TP, TC, WP, WC>}
+#define CFG(TP, TC, WP, WC) \
+    {WP * TP * 16, WC * TC * 16, 2, conv_igemm_kernel<TP, TC, WP, WC, 2>}
+#define CFG3(TP, TC, WP, WC) \
+    {WP * TP * 16, WC * TC * 16, 3, conv_igemm_kernel<TP, TC, WP, WC, 3>}
 #define TILES(X) \
     X(4, 4, 2, 2),   /* 128 px x 128 ch */ \
     X(4, 4, 4, 1),   /* 256 px x  64 ch */ \
@@ -313,7 +385,17 @@ struct ConvConfig {
     X(4, 3, 4, 1),   /* 256 px x  48 ch */ \
     X(2, 4, 2, 2),   /*  64 px x 128 ch */ \
     X(4, 6, 2, 2)    /* 128 px x 192 ch */
-static const ConvConfig kConfigs[] = {TILES(CFG)};
+// 3-stage variants: two K-steps in flight; LDS 3 x (P+C) x 128 B + 5 KB
+#define TILES3(X) \
+    X(2, 4, 4, 1),   /* 128 px x  64 ch, 77 KB: 2 blocks/CU */ \
+    X(2, 2, 2, 2),   /*  64 px x  64 ch */ \
+    X(4, 2, 1, 4),   /*  64 px x 128 ch */ \
+    X(2, 8, 4, 1),   /* 128 px x 128 ch, 1 block/CU */ \
+    X(4, 4, 2, 2),   /* 128 px x 128 ch, 1 block/CU */ \
+    X(2, 9, 4, 1),   /* 128 px x 144 ch, 1 block/CU */ \
+    X(2, 5, 4, 1),   /* 128 px x  80 ch */ \
+    X(2, 6, 4, 1)    /* 128 px x  96 ch */
+static const ConvConfig kConfigs[] = {TILES(CFG), TILES3(CFG3)};
 static const int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
 extern "C" {
@@ -325,6 +407,10 @@ int rnb_conv_config_info(int id, int* p_tile, int* c_tile) {
   *p_tile = kConfigs[id].p_tile;
   *c_tile = kConfigs[id].c_tile;
   return 0;
+}
+
+int rnb_conv_config_stages(int id) {
+  return (id < 0 || id >= kNumConfigs) ? -1 : kConfigs[id].stages;
 }
 
 int rnb_conv_params_size() { return (int)sizeof(ConvParams); }
@@ -371,6 +457,7 @@ int rnb_conv_launch(const ConvParams* pp, int config_id, hipStream_t stream) {
   if (blocks > 0x7FFFFFFF) return -7;
   if (p.n_ctiles * cfg.c_tile > p.w_rows) return -8;
   if (!p.ktab) return -9;
+  if (cfg.stages == 3 && p.K_pad / 8 > KTAB_MAX) return -11;
   hipLaunchKernelGGL(cfg.kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
 }

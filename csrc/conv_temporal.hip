@@ -1,0 +1,298 @@
+// Register-direct temporal convolution (3x1x1, stride 1, pad (1,0,0)) on CDNA4:
+// the "temporal" half of every stride-1 R(2+1)D SpatioTemporalConv (SURVEY.md
+// §2.4(a) K2/K4/K8/K14 -- ~20 % of R(2+1)D-34's time in the generic kernel).
+//
+// Why a third kernel: the generic implicit-GEMM kernel gathers every input
+// row once per temporal tap through LDS-DMA (3x the input, rows of 64 K
+// elements). Removing its DMA cut its time 2.5-3x while removing its MFMAs
+// changed nothing (scripts/kernel_exp.py), i.e. it is bound by the gather
+// round trips, not by the matrix cores. Here:
+//
+//  * a wave owns 16 output pixels x ALL T output frames x CT*16 output
+//    channels (acc[T][CT] MFMA tiles). It reads each input frame of its 16
+//    pixels exactly once, straight into VGPRs as MFMA B fragments (one 16-B
+//    buffer load per lane = 8 channels of one pixel; out-of-range lanes read
+//    0), and applies every fragment to the <= 3 output frames it feeds
+//    (t_out = t_in - dt + 1), i.e. 3 * CT MFMAs per 16-B load per lane.
+//    The next frame's fragments are in flight while the current frame's
+//    MFMAs run; the next pixel group's first frame is issued before the
+//    epilogue.
+//  * the block's weight slice (CT*16 output channels x all 3 taps x Cin)
+//    is staged ONCE into LDS in MFMA A-fragment order ([tap][chunk][ct]
+//    [lane][16 B], conflict-free ds_read_b128) and blocks are persistent
+//    (grid = a few blocks per CU, waves stride over pixel groups), so the
+//    weights never re-stream and waves run without barriers.
+//
+// GEMM orientation matches the other conv kernels (A = weights 16 cout x 32
+// k, B = activations 32 k x 16 px; v_mfma_f32_16x16x32_bf16): each lane ends
+// with 4 consecutive output channels of one pixel -> bias + residual + ReLU
+// fused epilogue with one 8-byte store.
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+
+#define TEMP_INVALID 0xFFFFFFF0u
+
+struct TemporalParams {
+  const uint16_t* x;     // NDHWC input [N][T][HW][Cin_p]
+  const uint16_t* w;     // [w_rows][K_pad], k = dt * Cin_p + c
+  const float* bias;     // [w_rows]
+  const uint16_t* res;   // residual NDHWC (nullable), channel stride res_stride
+  uint16_t* y;           // output [N][T][HW][y_stride]
+  int N, T, HW, Cin_p;
+  int Cout_p, y_stride, res_stride;
+  int K_pad, relu, w_rows;
+  int ngroups;           // N * ceil(HW / 16) pixel groups
+  int gpc;               // groups per clip = ceil(HW / 16)
+  int n_ctiles;          // Cout tiles of CT*16 channels
+  uint32_t x_bytes;
+  uint32_t mG, sG;       // magic division by gpc
+};
+
+static __device__ __forceinline__ int tdiv(int n, uint32_t m, uint32_t s) {
+  return m ? (int)(__umulhi((uint32_t)n, m) >> s) : n;
+}
+static __device__ __forceinline__ uint16_t tf2bf(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);
+  return __builtin_bit_cast(uint16_t, h);
+}
+static __device__ __forceinline__ float tbf2f(uint32_t u16) { return __uint_as_float(u16 << 16); }
+
+template <int T, int NCH, int CT, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 2)
+void conv_temporal_kernel(const TemporalParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [3][NCH][CT][64][16 B]
+  constexpr int NFRAG = 3 * NCH * CT;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int frow = lane & 15;
+  const int fq = lane >> 4;
+
+  const int ctile = blockIdx.x % p.n_ctiles;
+  const int gblk = blockIdx.x / p.n_ctiles;
+  const int gstride = (gridDim.x / p.n_ctiles) * WAVES;
+  const int c0 = ctile * CT * 16;
+
+  // ---- weights -> LDS in A-fragment order (once per persistent block) ----
+  for (int f = wave; f < NFRAG; f += WAVES) {
+    const int dt = f / (NCH * CT);
+    const int r = f - dt * (NCH * CT);
+    const int ch = r / CT;
+    const int ct = r - ch * CT;
+    const int row = c0 + ct * 16 + frow;
+    const int kk = ch * 32 + fq * 8;
+    i32x4 v = {0, 0, 0, 0};
+    if (kk < p.Cin_p && row < p.w_rows)
+      v = *(const i32x4*)(p.w + (size_t)row * p.K_pad + dt * p.Cin_p + kk);
+    *(i32x4*)(smem + ((size_t)f * 64 + lane) * 16) = v;
+  }
+  float4 bias[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int c = c0 + ct * 16 + fq * 4;
+    bias[ct] = c < p.w_rows ? *(const float4*)(p.bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+  // lane's channel offset inside a 32-channel chunk; chunks past Cin_p read 0
+  const uint32_t frame_bytes = (uint32_t)p.HW * (uint32_t)p.Cin_p * 2u;
+  bool chok[NCH];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) chok[ch] = ch * 32 + fq * 8 < p.Cin_p;
+
+  // byte offset of (group g, frame 0) for this lane, or TEMP_INVALID
+  auto group_base = [&](int g, int& n, int& hw) -> uint32_t {
+    n = tdiv(g, p.mG, p.sG);
+    hw = (g - n * p.gpc) * 16 + frow;
+    if (g >= p.ngroups || hw >= p.HW) return TEMP_INVALID;
+    return ((uint32_t)(n * p.T) * (uint32_t)p.HW + (uint32_t)hw) * (uint32_t)p.Cin_p * 2u +
+           (uint32_t)fq * 16u;
+  };
+  auto load_frame = [&](bf16x8* dst, uint32_t base, int t) {
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const uint32_t off = (base == TEMP_INVALID || !chok[ch])
+                               ? TEMP_INVALID
+                               : base + (uint32_t)t * frame_bytes + (uint32_t)ch * 64u;
+      const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      dst[ch] = __builtin_bit_cast(bf16x8, v);
+    }
+  };
+
+  bf16x8 b[2][NCH];
+  int g = gblk * WAVES + wave;
+  int n, hw;
+  uint32_t base = group_base(g, n, hw);
+  if (g < p.ngroups) load_frame(b[0], base, 0);
+  const char* wl = smem + lane * 16;
+
+  for (; g < p.ngroups; g += gstride) {
+    f32x4 acc[T][CT];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[t][ct] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const int gn = g + gstride;
+    int nn, nhw;
+    const uint32_t nbase = group_base(gn, nn, nhw);
+#pragma unroll
+    for (int ti = 0; ti < T; ++ti) {
+      // opaque zero: keeps the weight-fragment reads inside this frame's
+      // step (otherwise they are hoisted / CSE'd across frames and groups
+      // as loop invariants and 60 fragments x 4 VGPRs spill)
+      int z;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+      const char* wlt = wl + z;
+      if (ti + 1 < T) {
+        load_frame(b[(ti + 1) & 1], base, ti + 1);
+      } else if ((T & 1) == 0 && gn < p.ngroups) {
+        load_frame(b[0], nbase, 0);                  // next group's first frame
+      }
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+#pragma unroll
+        for (int dt = 0; dt < 3; ++dt) {
+          const int to = ti - dt + 1;
+          if (to < 0 || to >= T) continue;
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) {
+            const bf16x8 wf =
+                *(const bf16x8*)(wlt + (size_t)((dt * NCH + ch) * CT + ct) * 1024);
+            acc[to][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, b[ti & 1][ch],
+                                                                  acc[to][ct], 0, 0, 0);
+          }
+        }
+      }
+    }
+
+    // ---- epilogue: bias (+ residual) (+ ReLU) -> bf16, 4 channels per lane ----
+    if (hw < p.HW) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const size_t m = (size_t)(n * p.T + t) * p.HW + hw;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const int c = c0 + ct * 16 + fq * 4;
+          if (c >= p.Cout_p) continue;
+          float v0 = acc[t][ct][0] + bias[ct].x, v1 = acc[t][ct][1] + bias[ct].y;
+          float v2 = acc[t][ct][2] + bias[ct].z, v3 = acc[t][ct][3] + bias[ct].w;
+          if (p.res) {
+            const i32x2 r = *(const i32x2*)(p.res + m * p.res_stride + c);
+            v0 += tbf2f((uint32_t)r[0] & 0xFFFFu);
+            v1 += tbf2f((uint32_t)r[0] >> 16);
+            v2 += tbf2f((uint32_t)r[1] & 0xFFFFu);
+            v3 += tbf2f((uint32_t)r[1] >> 16);
+          }
+          if (p.relu) {
+            v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f);
+            v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+          }
+          i32x2 o;
+          o[0] = (int)((uint32_t)tf2bf(v0) | ((uint32_t)tf2bf(v1) << 16));
+          o[1] = (int)((uint32_t)tf2bf(v2) | ((uint32_t)tf2bf(v3) << 16));
+          *(i32x2*)(p.y + m * p.y_stride + c) = o;
+        }
+      }
+    }
+    if ((T & 1) != 0 && gn < p.ngroups) load_frame(b[0], nbase, 0);
+    base = nbase;
+    n = nn;
+    hw = nhw;
+  }
+}
+
+static void temporal_magic(uint32_t d, uint32_t* m, uint32_t* s) {
+  if (d <= 1) { *m = 0; *s = 0; return; }
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t q = 31 + l;
+  *m = (uint32_t)(((1ull << q) + d - 1) / d);
+  *s = (uint32_t)(q - 32);
+}
+
+struct TemporalVariant {
+  int T, nch, ct, waves;
+  void (*kernel)(const TemporalParams);
+};
+
+#define TV(T, NCH, CT, WV) {T, NCH, CT, WV, conv_temporal_kernel<T, NCH, CT, WV>}
+// (T, 32-channel chunks, 16-channel output tiles per block, waves per block)
+static const TemporalVariant kTemporal[] = {
+    TV(8, 3, 4, 4),    // R(2+1)D stem temporal: 83 (88) -> 64, 8 frames
+    TV(8, 5, 4, 4),    // conv2: 144 -> 64, 8 frames
+    TV(4, 9, 4, 8),    // conv3: 288 -> 128, 4 frames (2 channel tiles)
+    TV(2, 18, 2, 8),   // conv4: 576 -> 256, 2 frames (8 channel tiles)
+};
+static const int kNumTemporal = sizeof(kTemporal) / sizeof(kTemporal[0]);
+
+static int temporal_find(int T, int Cin_p, int Cout_p) {
+  const int nch = (Cin_p + 31) / 32;
+  for (int i = 0; i < kNumTemporal; ++i)
+    if (kTemporal[i].T == T && kTemporal[i].nch == nch) return i;
+  (void)Cout_p;
+  return -1;
+}
+
+static int temporal_lds(const TemporalVariant& v) { return 3 * v.nch * v.ct * 1024; }
+
+extern "C" {
+
+int rnb_temporal_params_size() { return (int)sizeof(TemporalParams); }
+
+// LDS bytes per block for this shape, or -1 if no variant serves it.
+int rnb_temporal_lds_bytes(int T, int Cin_p, int Cout_p) {
+  const int i = temporal_find(T, Cin_p, Cout_p);
+  return i < 0 ? -1 : temporal_lds(kTemporal[i]);
+}
+
+// Persistent grid: blocks_per_cu * num_cus blocks (capped by the work);
+// blocks_per_cu <= 0 picks what LDS allows (2 for 4-wave variants, 1 for 8).
+int rnb_temporal_launch(const TemporalParams* pp, int num_cus, int blocks_per_cu,
+                        hipStream_t stream) {
+  TemporalParams p = *pp;
+  const int vi = temporal_find(p.T, p.Cin_p, p.Cout_p);
+  if (vi < 0) return -1;
+  const TemporalVariant& v = kTemporal[vi];
+  if (p.Cin_p % 8 != 0 || p.Cout_p % 4 != 0 || p.K_pad < 3 * p.Cin_p) return -2;
+  if (p.N <= 0 || p.HW <= 0) return 0;
+  if ((long long)p.N * p.T * p.HW * p.Cin_p * 2 > 0x7FFFFF00LL) return -5;
+  if (p.y_stride < p.Cout_p || (p.res && p.res_stride < p.Cout_p)) return -4;
+  p.gpc = (p.HW + 15) / 16;
+  p.ngroups = p.N * p.gpc;
+  p.n_ctiles = (p.Cout_p + v.ct * 16 - 1) / (v.ct * 16);
+  if (p.n_ctiles * v.ct * 16 > p.w_rows) return -8;
+  p.x_bytes = (uint32_t)((long long)p.N * p.T * p.HW * p.Cin_p * 2);
+  temporal_magic((uint32_t)p.gpc, &p.mG, &p.sG);
+  const int lds = temporal_lds(v);
+  if (lds > 160 * 1024) return -6;
+  static bool attr_set[16] = {false};
+  if (!attr_set[vi]) {
+    hipFuncSetAttribute((const void*)v.kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    attr_set[vi] = true;
+  }
+  if (blocks_per_cu <= 0) {
+    blocks_per_cu = (160 * 1024) / lds;
+    if (blocks_per_cu > 8 / v.waves) blocks_per_cu = 8 / v.waves;
+    if (blocks_per_cu < 1) blocks_per_cu = 1;
+  }
+  if (num_cus <= 0) num_cus = 256;
+  const int gblocks_needed = (p.ngroups + v.waves - 1) / v.waves;
+  int gblocks = (num_cus * blocks_per_cu + p.n_ctiles - 1) / p.n_ctiles;
+  if (gblocks > gblocks_needed) gblocks = gblocks_needed;
+  if (gblocks < 1) gblocks = 1;
+  hipLaunchKernelGGL(v.kernel, dim3((unsigned)(gblocks * p.n_ctiles)), dim3(64 * v.waves), lds,
+                     stream, p);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

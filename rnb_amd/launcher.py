@@ -157,8 +157,13 @@ def run(args) -> dict:
     fin_bar = ctx.Barrier(num_runners + 2)
     counter = ctx.Value("i", 0)
     flag = ctx.Value("i", TerminationFlag.UNSET)
+    # bulk mode: every video (times its segments) plus every producer's exit
+    # markers must fit at once, or a marker burst from a finished replica can
+    # fill a queue another replica still needs (-> spurious FRAME_QUEUE_FULL)
+    from .runner import NUM_EXIT_MARKERS
+    max_segments = max(step.num_segments for step in spec.steps)
     queue_size = args.queue_size if args.mean_interval_ms > 0 \
-        else args.videos + num_runners + 1
+        else args.videos * max_segments + (NUM_EXIT_MARKERS + 1) * (num_runners + 1)
     qt = SharedQueuesAndTensors(spec, ctx.Queue, queue_size, ctx)
     result_queue = ctx.Queue()
     it_kwargs = spec.iterator_kwargs

@@ -93,21 +93,37 @@ class R2P1DEngine:
         self._n += 1
         return "t%d" % self._n
 
-    def _conv(self, conv: torch.nn.Conv3d, bn, relu: bool, name: str) -> ConvLayer:
+    def _conv(self, conv: torch.nn.Conv3d, bn, relu: bool, name: str,
+              src: str, dst: str) -> ConvLayer:
         w, b = fold_bn(conv.weight, conv.bias, bn)
         geom = ConvGeom(cin=conv.in_channels, cout=conv.out_channels,
                         kernel=tuple(conv.kernel_size), stride=tuple(conv.stride),
                         padding=tuple(conv.padding))
-        return ConvLayer(w, b, geom, relu, self.device, name)
+        T, H, W = self._thw[src]
+        self._thw[dst] = geom.out_thw(T, H, W)
+        nominal = geom
+        kt, pt, st = geom.kernel[0], geom.padding[0], geom.stride[0]
+        if T == 1 and kt == 2 * pt + 1 and st == 1 and kt > 1:
+            # a single input frame: only the centre temporal tap ever sees
+            # data (the others read the zero padding), so run the conv as its
+            # centre slice -- e.g. conv5's 3x1x1 convs at 8-frame clips do
+            # 1/3 of the MACs (same result)
+            w = w[:, :, pt:pt + 1].contiguous()
+            geom = ConvGeom(cin=geom.cin, cout=geom.cout, kernel=(1,) + geom.kernel[1:],
+                            stride=geom.stride, padding=(0,) + geom.padding[1:])
+        layer = ConvLayer(w, b, geom, relu, self.device, name)
+        layer.nominal_geom = nominal
+        return layer
 
     def _stconv(self, st: SpatioTemporalConv, src: str, post_bn, relu: bool,
                 res: Optional[str], name: str) -> str:
         mid = self._name()
         self.ops.append(PlanOp("conv", self._conv(st.spatial_conv, st.bn, True,
-                                                  name + ".spatial"), src, mid))
+                                                  name + ".spatial", src, mid), src, mid))
         dst = self._name()
         self.ops.append(PlanOp("conv", self._conv(st.temporal_conv, post_bn, relu,
-                                                  name + ".temporal"), mid, dst, res))
+                                                  name + ".temporal", mid, dst),
+                               mid, dst, res))
         return dst
 
     def _block(self, blk, src: str, name: str) -> str:
@@ -121,6 +137,7 @@ class R2P1DEngine:
 
     def _build(self, body):
         cur = "x"
+        self._thw = {"x": tuple(LAYER_INPUT_CTHW[self.start_idx][1:])}
         for idx in range(self.start_idx, self.end_idx + 1):
             if idx == 1:
                 cur = self._stconv(body.conv1, cur, None, False, None, "conv1")
@@ -153,7 +170,7 @@ class R2P1DEngine:
         c, t, h, w = LAYER_INPUT_CTHW[self.start_idx]
         shapes = {"x": (t, h, w)}
         for op in self.ops:
-            g = op.layer.geom
+            g = getattr(op.layer, "nominal_geom", op.layer.geom)
             T, H, W = shapes[op.src]
             total += g.flops(1, T, H, W)
             shapes[op.dst] = g.out_thw(T, H, W)

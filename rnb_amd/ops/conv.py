@@ -26,7 +26,21 @@ CH_ALIGN = 8        # channel padding of every NDHWC activation
 BK = 64             # K step of the kernel
 W_ROW_SLACK = 256   # extra zero weight rows (>= largest channel tile)
 HALO = 100          # config id of the halo-tiled 1x3x3 stride-1 kernel (conv_halo.hip)
+TEMPORAL = 101      # config id of the register-direct 3x1x1 kernel (conv_temporal.hip)
+SPECIAL_NAMES = {HALO: "halo", TEMPORAL: "temporal"}
 LDS_LIMIT = 160 * 1024
+
+
+_NUM_CUS: Dict[int, int] = {}
+
+
+def num_cus(device) -> int:
+    """Compute units of a GPU (persistent-kernel grid sizing)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    n = _NUM_CUS.get(idx)
+    if n is None:
+        n = _NUM_CUS[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    return n
 
 
 def pad_to(x: int, m: int) -> int:
@@ -111,6 +125,7 @@ class ConvLayer:
         self._ktab: Dict[Tuple[int, int, int], torch.Tensor] = {}
         self.time_major = False   # time-major rows for temporal convs (measured: no gain)
         self.use_halo = True      # allow the halo-tiled kernel for 1x3x3 stride-1 convs
+        self.use_temporal = True  # allow the register-direct kernel for 3x1x1 stride-1 convs
 
     # ------------------------------------------------------------------
     def out_shape(self, x_shape) -> Tuple[int, int, int, int, int]:
@@ -192,6 +207,47 @@ class ConvLayer:
             self._config[key] = ok
         return bool(ok)
 
+    def temporal_eligible(self, x_shape) -> bool:
+        """3x1x1 / stride 1 / pad (1,0,0) with a conv_temporal variant for (T, Cin_p)."""
+        g = self.geom
+        if not (g.kernel == (3, 1, 1) and g.stride == (1, 1, 1) and g.padding == (1, 0, 0)
+                and self.use_temporal):
+            return False
+        from .native import kernels
+        T = x_shape[1]
+        key = ("temporal", T)
+        ok = self._config.get(key)
+        if ok is None:
+            nb = kernels().temporal_lds_bytes(T, g.cin_p, g.cout_p)
+            ok = 0 < nb <= LDS_LIMIT
+            self._config[key] = ok
+        return bool(ok)
+
+    def special_candidates(self, x_shape):
+        """Shape-specialised kernels (config ids >= 100) that can run this input."""
+        out = []
+        if self.halo_eligible(x_shape):
+            out.append(HALO)
+        if self.temporal_eligible(x_shape):
+            out.append(TEMPORAL)
+        return out
+
+    def temporal_params(self, x, y, residual):
+        from .native import TemporalParams
+        g = self.geom
+        N, T, H, W, C = x.shape
+        p = TemporalParams()
+        p.x, p.w, p.bias = x.data_ptr(), self.wmat.data_ptr(), self.bias.data_ptr()
+        p.res = residual.data_ptr() if residual is not None else None
+        p.y = y.data_ptr()
+        p.N, p.T, p.HW, p.Cin_p = N, T, H * W, C
+        p.Cout_p, p.y_stride = g.cout_p, y.shape[-1]
+        p.res_stride = residual.shape[-1] if residual is not None else 0
+        p.K_pad = g.k_pad
+        p.relu = 1 if self.relu else 0
+        p.w_rows = self.wmat.shape[0]
+        return p
+
     def halo_params(self, x, y, residual):
         from .native import HaloParams
         g = self.geom
@@ -226,8 +282,10 @@ class ConvLayer:
     def config_for(self, x_shape) -> int:
         key = tuple(x_shape[:4])
         cid = self._config.get(key)
-        if cid is None and self.halo_eligible(x_shape):
-            cid = self._config[key] = HALO
+        if cid is None:
+            special = self.special_candidates(x_shape)
+            if special:
+                cid = self._config[key] = special[0]
         if cid is None:
             N, T, H, W, _ = x_shape
             To, Ho, Wo = self.geom.out_thw(T, H, W)
@@ -243,9 +301,7 @@ class ConvLayer:
         y = torch.empty(self.out_shape(x.shape), dtype=torch.bfloat16, device=x.device)
         stream = torch.cuda.current_stream(x.device)
         best, best_t = None, None
-        cands = list(range(len(kern.configs)))
-        if self.halo_eligible(x.shape):
-            cands.append(HALO)
+        cands = list(range(len(kern.configs))) + self.special_candidates(x.shape)
         for cid in cands:
             p = self.params(x, y, residual)
             self._launch(p, cid, x, y, residual, stream)    # warm
@@ -266,6 +322,9 @@ class ConvLayer:
         from .native import kernels
         if cid == HALO:
             kernels().halo(self.halo_params(x, y, residual), stream.cuda_stream)
+        elif cid == TEMPORAL:
+            kernels().temporal(self.temporal_params(x, y, residual), num_cus(x.device), 0,
+                               stream.cuda_stream)
         else:
             kernels().conv(p, cid, stream.cuda_stream)
 
@@ -283,8 +342,8 @@ class ConvLayer:
                                  % (self.name, tuple(residual.shape), tuple(y.shape)))
         cid = self.config_for(x.shape) if config is None else config
         stream = torch.cuda.current_stream(x.device)
-        if cid == HALO:
-            kernels().halo(self.halo_params(x, y, residual), stream.cuda_stream)
+        if cid >= HALO:
+            self._launch(None, cid, x, y, residual, stream)
         else:
             kernels().conv(self.params(x, y, residual), cid, stream.cuda_stream)
         return y

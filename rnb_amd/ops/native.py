@@ -128,6 +128,20 @@ class HaloParams(ctypes.Structure):
     ]
 
 
+class TemporalParams(ctypes.Structure):
+    """Mirror of ``struct TemporalParams`` in csrc/conv_temporal.hip."""
+    _fields_ = [
+        ("x", ctypes.c_void_p), ("w", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+        ("res", ctypes.c_void_p), ("y", ctypes.c_void_p),
+        ("N", ctypes.c_int), ("T", ctypes.c_int), ("HW", ctypes.c_int),
+        ("Cin_p", ctypes.c_int), ("Cout_p", ctypes.c_int), ("y_stride", ctypes.c_int),
+        ("res_stride", ctypes.c_int), ("K_pad", ctypes.c_int), ("relu", ctypes.c_int),
+        ("w_rows", ctypes.c_int), ("ngroups", ctypes.c_int), ("gpc", ctypes.c_int),
+        ("n_ctiles", ctypes.c_int), ("x_bytes", ctypes.c_uint32),
+        ("mG", ctypes.c_uint32), ("sG", ctypes.c_uint32),
+    ]
+
+
 class Kernels:
     """Typed wrappers over librnb_kernels.so."""
 
@@ -156,17 +170,25 @@ class Kernels:
         lib.rnb_halo_launch.argtypes = [ctypes.POINTER(HaloParams), ctypes.c_void_p]
         lib.rnb_halo_launch.restype = ctypes.c_int
         lib.rnb_halo_lds_bytes.argtypes = [ctypes.c_int] * 4
+        lib.rnb_temporal_launch.argtypes = [ctypes.POINTER(TemporalParams), ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_void_p]
+        lib.rnb_temporal_launch.restype = ctypes.c_int
+        lib.rnb_temporal_lds_bytes.argtypes = [ctypes.c_int] * 3
+        if lib.rnb_temporal_params_size() != ctypes.sizeof(TemporalParams):
+            raise NativeUnavailable("TemporalParams layout mismatch: rebuild")
         if lib.rnb_halo_params_size() != ctypes.sizeof(HaloParams):
             raise NativeUnavailable("HaloParams layout mismatch: rebuild")
         if lib.rnb_conv_params_size() != ctypes.sizeof(ConvParams):
             raise NativeUnavailable("ConvParams layout mismatch (%d vs %d): rebuild"
                                     % (lib.rnb_conv_params_size(),
                                        ctypes.sizeof(ConvParams)))
-        self.configs = []
+        self.configs = []          # (pixel tile, channel tile) per config id
+        self.stages = []           # LDS staging depth per config id
         for i in range(lib.rnb_conv_num_configs()):
             p, c = ctypes.c_int(), ctypes.c_int()
             lib.rnb_conv_config_info(i, ctypes.byref(p), ctypes.byref(c))
             self.configs.append((p.value, c.value))
+            self.stages.append(lib.rnb_conv_config_stages(i))
 
     def conv(self, params: ConvParams, config_id: int, stream: int) -> None:
         _check(self.lib.rnb_conv_launch(ctypes.byref(params), config_id, stream),
@@ -174,6 +196,14 @@ class Kernels:
 
     def halo(self, params: HaloParams, stream: int) -> None:
         _check(self.lib.rnb_halo_launch(ctypes.byref(params), stream), "conv_halo")
+
+    def temporal(self, params: TemporalParams, num_cus: int, blocks_per_cu: int,
+                 stream: int) -> None:
+        _check(self.lib.rnb_temporal_launch(ctypes.byref(params), num_cus, blocks_per_cu,
+                                            stream), "conv_temporal")
+
+    def temporal_lds_bytes(self, T: int, cin_p: int, cout_p: int) -> int:
+        return self.lib.rnb_temporal_lds_bytes(T, cin_p, cout_p)
 
     def halo_lds_bytes(self, frames: int, H: int, W: int, cin: int) -> int:
         return self.lib.rnb_halo_lds_bytes(frames, H, W, cin)

@@ -19,6 +19,15 @@ from rnb_amd.models.r2p1d.model import build_network  # noqa: E402
 from rnb_amd.models.r2p1d.engine import R2P1DEngine  # noqa: E402
 
 
+def tile_name(cid):
+    from rnb_amd.ops.native import kernels
+    k = kernels()
+    if cid >= len(k.configs):
+        from rnb_amd.ops.conv import SPECIAL_NAMES
+        return SPECIAL_NAMES.get(cid, str(cid))
+    return "%dx%d%s" % (k.configs[cid] + ("s3" if k.stages[cid] == 3 else "",))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--depth", type=int, default=34)
@@ -59,12 +68,11 @@ def main():
         cid = op.layer.config_for(src.shape)
         rows.append({"name": op.layer.name, "M": N * To * Ho * Wo, "N": g.cout,
                      "K": g.cin * g.kernel[0] * g.kernel[1] * g.kernel[2],
-                     "tile": "halo" if cid >= len(cfgs) else "%dx%d" % cfgs[cid], "ms": ms,
+                     "tile": tile_name(cid), "ms": ms,
                      "tflops": flops / ms / 1e9, "gflop": flops / 1e9})
         if args.compare:
             best = {}
-            from rnb_amd.ops.conv import HALO
-            cands = list(range(len(cfgs))) + ([HALO] if op.layer.halo_eligible(src.shape) else [])
+            cands = list(range(len(cfgs))) + op.layer.special_candidates(src.shape)
             for c in cands:
                 s.record()
                 for _ in range(args.reps):
@@ -75,8 +83,7 @@ def main():
                 fam = "best"
                 if fam not in best or t < best[fam][1]:
                     best[fam] = (c, t)
-            rows[-1]["best"] = {k: ("halo" if v[0] >= len(cfgs) else "%dx%d" % cfgs[v[0]], v[1])
-                                for k, v in best.items()}
+            rows[-1]["best"] = {k: (tile_name(v[0]), v[1]) for k, v in best.items()}
         bufs[op.dst] = y
     tot_ms = sum(r["ms"] for r in rows)
     tot_gf = sum(r["gflop"] for r in rows)

@@ -80,8 +80,8 @@ def test_autotune_picks_valid_config():
     hip, _, _ = _engines(1, 5)
     chosen = hip.autotune(2, reps=1)
     from rnb_amd.ops.native import kernels
-    from rnb_amd.ops.conv import HALO
-    assert all(0 <= c < len(kernels().configs) or c == HALO for c in chosen.values())
+    from rnb_amd.ops.conv import SPECIAL_NAMES
+    assert all(0 <= c < len(kernels().configs) or c in SPECIAL_NAMES for c in chosen.values())
 
 
 def _ipc_child(q_in, q_out):

@@ -63,7 +63,7 @@ def test_conv_matches_torch(case):
     assert err <= 1e-2 * scale + 1e-2, (err, scale)
 
 
-@pytest.mark.parametrize("cfg", range(14))
+@pytest.mark.parametrize("cfg", range(24))
 def test_conv_every_tile_config_exact_integers(cfg):
     """Small-integer data is exact in bf16/fp32: any layout bug shows up."""
     from rnb_amd.ops.native import kernels
@@ -75,6 +75,24 @@ def test_conv_every_tile_config_exact_integers(cfg):
     ref = layer.forward_torch(x, out_dtype=torch.bfloat16)
     torch.cuda.synchronize()
     assert torch.equal(y, ref), (y.float() - ref.float()).abs().max().item()
+
+
+@pytest.mark.parametrize("cin,k", [(8, (1, 1, 1)), (128, (1, 1, 1)), (64, (3, 1, 1)),
+                                   (512, (1, 3, 3))])
+def test_conv_three_stage_pipeline_step_counts(cin, k):
+    """1, 2, 3 and 72 K-steps through every 3-stage config (prologue/epilogue of the ring)."""
+    from rnb_amd.ops.native import kernels
+    kern = kernels()
+    cfgs = [i for i, st in enumerate(kern.stages) if st == 3]
+    assert cfgs, "no 3-stage configs built"
+    pad = tuple(x // 2 for x in k)
+    layer = _layer(cin, 72, k, (1, 1, 1), pad, relu=False, integer=True)
+    x = _input(1, (3, 9, 11), layer.geom.cin_p, cin, integer=True)
+    ref = layer.forward_torch(x, out_dtype=torch.bfloat16)
+    for cfg in cfgs:
+        y = layer.forward_hip(x, config=cfg)
+        torch.cuda.synchronize()
+        assert torch.equal(y, ref), (cfg, (y.float() - ref.float()).abs().max().item())
 
 
 def test_conv_residual_relu_epilogue():
@@ -176,6 +194,44 @@ def test_halo_kernel_random_matches_generic():
     b = layer.forward_hip(x, config=2).float()
     torch.cuda.synchronize()
     assert (a - b).abs().max().item() <= 2e-2 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("n,thw,cin,cout,res", [
+    (2, (8, 56, 56), 83, 64, False),    # stem temporal (K2): Cin_p 88, partial chunk
+    (3, (8, 56, 56), 144, 64, True),    # conv2 temporal (K4) + residual
+    (2, (4, 28, 28), 288, 128, True),   # conv3 temporal (K8): 2 channel tiles
+    (3, (2, 14, 14), 576, 256, False),  # conv4 temporal (K14): HW tail (196 = 12.25 x 16)
+    (1, (8, 3, 5), 144, 72, True),      # tiny frames, partial channel tile
+])
+def test_temporal_kernel_exact(n, thw, cin, cout, res):
+    from rnb_amd.ops.conv import TEMPORAL
+    layer = _layer(cin, cout, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=True, integer=True)
+    x = _input(n, thw, layer.geom.cin_p, cin, integer=True)
+    assert layer.temporal_eligible(x.shape)
+    r = None
+    if res:
+        rs = layer.out_shape(x.shape)
+        r = _input(rs[0], rs[1:4], rs[4], cout, integer=True, seed=3)
+    ref = layer.forward_torch(x, residual=r, out_dtype=torch.bfloat16)
+    y = layer.forward_hip(x, residual=r, config=TEMPORAL)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref), (y.float() - ref.float()).abs().max().item()
+
+
+def test_temporal_kernel_random_matches_generic_and_small_grid():
+    from rnb_amd.ops.conv import TEMPORAL
+    from rnb_amd.ops.native import kernels
+    layer = _layer(144, 64, (3, 1, 1), (1, 1, 1), (1, 0, 0))
+    x = _input(4, (8, 56, 56), 144, 144)
+    a = layer.forward_hip(x, config=TEMPORAL).float()
+    b = layer.forward_hip(x, config=8).float()
+    # a 3-block persistent grid: every wave walks many pixel groups
+    y = torch.empty_like(b, dtype=torch.bfloat16)
+    kernels().temporal(layer.temporal_params(x, y, None), 3, 1,
+                       torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert (a - b).abs().max().item() <= 2e-2 * b.abs().max().item()
+    assert torch.equal(y.float(), a)
 
 
 @pytest.mark.parametrize("n", [1, 16, 37])
