@@ -30,10 +30,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 
 // Bottleneck experiments (scripts/kernel_exp.py builds variants; 0 = product):
-// 1 no MFMA, 2 no per-tap weight DMA, 3 no per-tap wait/barrier, 4 no DMA at all
+// 1 no MFMA, 2 no per-tap weight DMA, 3 no per-tap wait/barrier, 4 no DMA at all,
+// 5 no epilogue stores, 6 = 4 + 5
 #ifndef HALO_EXP
 #define HALO_EXP 0
 #endif
+#define HALO_NO_DMA (HALO_EXP == 4 || HALO_EXP == 6)
 
 #define HALO_INVALID 0xFFFFFFF0u
 #define HALO_MAX_PI 8           // patch DMA instructions per wave
@@ -71,8 +73,11 @@ static __device__ __forceinline__ float hbf2f(uint32_t u16) { return __uint_as_f
 // each wave owns 32 output pixels (2 MFMA sub-tiles) x 144 channels. LDS =
 // one patch + 2 weight stages (<= 80 KB), so two blocks share a CU and hide
 // each other's patch prologue.
-template <int TC>
-__global__ __launch_bounds__(448, 2)
+// HP = 16-pixel MFMA sub-tiles per wave (2: up to 7 waves x 32 px; 4: up to
+// 4 waves x 64 px -- fewer LDS reads per MFMA, 13 instead of 11 fragment reads
+// per 36 instead of 18 MFMAs); PI = patch DMA instructions per wave.
+template <int TC, int HP, int PI>
+__global__ __launch_bounds__(HP == 2 ? 448 : 256, 2)
 void conv_halo_kernel(const HaloParams p) {
   constexpr int C_TILE = TC * 16;
   constexpr int W_INSTR_TOTAL = C_TILE / 8;            // weight DMA instructions / step
@@ -102,9 +107,9 @@ void conv_halo_kernel(const HaloParams p) {
   const int kc = (lane & 7) ^ lrow;
   const int n_instr = (p.np + 7) >> 3;
   // patch pixel q <-> image (h0 - 1 + q / W2, q % W2 - 1) of frame f
-  uint32_t poff[HALO_MAX_PI];
+  uint32_t poff[PI];
 #pragma unroll
-  for (int i = 0; i < HALO_MAX_PI; ++i) {
+  for (int i = 0; i < PI; ++i) {
     const int instr = wave + nwaves * i;
     const int q = instr * 8 + lrow;
     uint32_t off = HALO_INVALID;
@@ -120,10 +125,10 @@ void conv_halo_kernel(const HaloParams p) {
 
   const int frow = lane & 15;
   const int fq = lane >> 4;
-  int center[2];
+  int center[HP];
 #pragma unroll
-  for (int tp = 0; tp < 2; ++tp) {
-    const int i = wave * 32 + tp * 16 + frow;          // pixel within the tile
+  for (int tp = 0; tp < HP; ++tp) {
+    const int i = wave * 16 * HP + tp * 16 + frow;     // pixel within the tile
     const int hh = hdiv(min(i, npx - 1), p.mW, p.sW);
     const int ww = min(i, npx - 1) - hh * p.W;
     center[tp] = (hh + 1) * W2 + (ww + 1);
@@ -142,7 +147,7 @@ void conv_halo_kernel(const HaloParams p) {
   auto issue_patch = [&](int chunk) {
     const uint32_t coff = (uint32_t)chunk * 128u;
 #pragma unroll
-    for (int i = 0; i < HALO_MAX_PI; ++i) {
+    for (int i = 0; i < PI; ++i) {
       const int instr = wave + nwaves * i;
       if (instr < n_instr) {
         const uint32_t off = poff[i] == HALO_INVALID ? HALO_INVALID : poff[i] + coff;
@@ -164,41 +169,41 @@ void conv_halo_kernel(const HaloParams p) {
     }
   };
 
-  f32x4 acc[2][TC];
+  f32x4 acc[HP][TC];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < HP; ++a)
 #pragma unroll
     for (int b = 0; b < TC; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nchunks = p.Cin >> 6;
-  if (HALO_EXP != 4) issue_w(0, 0);
+  if (!HALO_NO_DMA) issue_w(0, 0);
   for (int chunk = 0; chunk < nchunks; ++chunk) {
     // the previous chunk's last step ended with a barrier: the patch is free
-    if (HALO_EXP != 4) issue_patch(chunk);
+    if (!HALO_NO_DMA) issue_patch(chunk);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int tap = 0; tap < 9; ++tap) {
       const int s = chunk * 9 + tap;
-      if (HALO_EXP != 2 && HALO_EXP != 4 && s + 1 < nchunks * 9) issue_w(s + 1, (s + 1) & 1);
+      if (HALO_EXP != 2 && !HALO_NO_DMA && s + 1 < nchunks * 9) issue_w(s + 1, (s + 1) & 1);
       const char* wb = wbase + (s & 1) * WBUF;
       const int dh = tap / 3, dw = tap - dh * 3;
       const int shift = (dh - 1) * W2 + (dw - 1);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int ch = kk * 4 + fq;
-        bf16x8 af[2], wf[TC];
+        bf16x8 af[HP], wf[TC];
 #pragma unroll
         for (int tc = 0; tc < TC; ++tc) {
           const int row = tc * 16 + frow;
           wf[tc] = *(const bf16x8*)(wb + row * 128 + ((ch ^ (row & 7)) << 4));
         }
 #pragma unroll
-        for (int tp = 0; tp < 2; ++tp) {
+        for (int tp = 0; tp < HP; ++tp) {
           const int row = center[tp] + shift;
           af[tp] = *(const bf16x8*)(pbuf + row * 128 + ((ch ^ (row & 7)) << 4));
         }
 #pragma unroll
-        for (int tp = 0; tp < 2; ++tp)
+        for (int tp = 0; tp < HP; ++tp)
 #pragma unroll
           for (int tc = 0; tc < TC; ++tc) {
             if (HALO_EXP == 1) {    // keep the fragment reads alive, drop the MFMA
@@ -217,8 +222,8 @@ void conv_halo_kernel(const HaloParams p) {
   }
 
 #pragma unroll
-  for (int tp = 0; tp < 2; ++tp) {
-    const int i = wave * 32 + tp * 16 + frow;
+  for (int tp = 0; tp < HP; ++tp) {
+    const int i = wave * 16 * HP + tp * 16 + frow;
     if (i >= npx) continue;
     const int m = p0 + i;
 #pragma unroll
@@ -242,7 +247,8 @@ void conv_halo_kernel(const HaloParams p) {
       i32x2 o;
       o[0] = (int)((uint32_t)hf2bf(v0) | ((uint32_t)hf2bf(v1) << 16));
       o[1] = (int)((uint32_t)hf2bf(v2) | ((uint32_t)hf2bf(v3) << 16));
-      *(i32x2*)(p.y + (size_t)m * p.y_stride + c) = o;
+      if ((HALO_EXP != 5 && HALO_EXP != 6) || p.relu == 7)
+        *(i32x2*)(p.y + (size_t)m * p.y_stride + c) = o;
     }
   }
 }
@@ -265,17 +271,26 @@ extern "C" {
 
 int rnb_halo_params_size() { return (int)sizeof(HaloParams); }
 
+static int halo_max_pi(int hp) { return hp == 2 ? HALO_MAX_PI : 12; }
+static int halo_waves(int R, int W, int hp) { return (R * W + 16 * hp - 1) / (16 * hp); }
+
 // LDS bytes a launch on this shape requests (-1: shape not supported).
-int rnb_halo_lds_bytes(int frames, int H, int W, int Cin) {
+int rnb_halo_lds_bytes_v(int frames, int H, int W, int Cin, int hp) {
   const int R = halo_rows(H, W);
-  if (R == 0 || Cin % 64 != 0) return -1;
+  if (R == 0 || Cin % 64 != 0 || (hp != 2 && hp != 4)) return -1;
   const int np = (R + 2) * (W + 2);
-  if ((np + 7) / 8 > 7 * HALO_MAX_PI) return -1;
+  if ((np + 7) / 8 > halo_waves(R, W, hp) * halo_max_pi(hp)) return -1;
+  (void)frames;
   return ((np + 7) & ~7) * 128 + 2 * 144 * 128;
 }
 
-int rnb_halo_launch(const HaloParams* pp, hipStream_t stream) {
+int rnb_halo_lds_bytes(int frames, int H, int W, int Cin) {
+  return rnb_halo_lds_bytes_v(frames, H, W, Cin, 2);
+}
+
+int rnb_halo_launch_v(const HaloParams* pp, int hp, hipStream_t stream) {
   HaloParams p = *pp;
+  if (hp != 2 && hp != 4) return -10;
   if (p.Cin % 64 != 0 || p.K_pad != 9 * p.Cin || p.Cout_p % 4 != 0) return -2;
   if (p.M <= 0) return 0;
   if ((long long)p.M * p.Cin * 2 > 0x7FFFFF00LL) return -5;
@@ -283,10 +298,10 @@ int rnb_halo_launch(const HaloParams* pp, hipStream_t stream) {
   if (p.R == 0) return -3;
   p.bands = (p.H + p.R - 1) / p.R;
   p.np = (p.R + 2) * (p.W + 2);
-  const int lds = rnb_halo_lds_bytes(p.frames, p.H, p.W, p.Cin);
+  const int lds = rnb_halo_lds_bytes_v(p.frames, p.H, p.W, p.Cin, hp);
   if (lds < 0 || lds > 160 * 1024) return -6;
-  const int waves = (p.R * p.W + 31) / 32;
-  if ((p.np + 7) / 8 > waves * HALO_MAX_PI) return -4;
+  const int waves = halo_waves(p.R, p.W, hp);
+  if ((p.np + 7) / 8 > waves * halo_max_pi(hp)) return -4;
   p.x_bytes = (uint32_t)((long long)p.M * p.Cin * 2);
   halo_magic((uint32_t)p.bands, &p.mB, &p.sB);
   halo_magic((uint32_t)p.W, &p.mW, &p.sW);
@@ -294,15 +309,21 @@ int rnb_halo_launch(const HaloParams* pp, hipStream_t stream) {
   p.n_ctiles = (p.Cout_p + 143) / 144;
   if (p.n_ctiles * 144 > p.w_rows) return -8;
   if (p.y_stride < p.Cout_p || (p.res && p.res_stride < p.Cout_p)) return -9;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)conv_halo_kernel<9>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
+  void (*kern)(const HaloParams) =
+      hp == 2 ? conv_halo_kernel<9, 2, HALO_MAX_PI> : conv_halo_kernel<9, 4, 12>;
+  static bool attr_set[2] = {false, false};
+  if (!attr_set[hp == 4]) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    attr_set[hp == 4] = true;
   }
-  hipLaunchKernelGGL(conv_halo_kernel<9>, dim3((unsigned)(p.n_ptiles * p.n_ctiles)),
-                     dim3(64 * waves), lds, stream, p);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_ptiles * p.n_ctiles)), dim3(64 * waves), lds,
+                     stream, p);
   return (int)hipGetLastError();
+}
+
+int rnb_halo_launch(const HaloParams* pp, hipStream_t stream) {
+  return rnb_halo_launch_v(pp, 2, stream);
 }
 
 }  // extern "C"

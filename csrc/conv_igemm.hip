@@ -13,7 +13,7 @@
 // (32 k x 16 pixels): with v_mfma_f32_16x16x32_bf16 every lane then holds 4
 // consecutive output channels of one pixel -> one 8-byte store per lane.
 //
-// Tiling: 256 threads = 4 waves arranged WP x WC; each wave owns
+// Tiling: 256 or 512 threads = 4 or 8 waves arranged WP x WC; each wave owns
 // (TP*16 pixels) x (TC*16 channels). BK = 64: an LDS row is 128 B = 8 chunks
 // of 16 B, XOR-swizzled (chunk ^ (row & 7)) so the ds_read_b128 fragment
 // reads are bank-conflict free (cdna_hip_programming.md T2). The K loop is
@@ -61,10 +61,13 @@ struct ConvParams {
 };
 
 // Bottleneck experiments (scripts/kernel_exp.py builds variants; 0 = product):
-// 1 no MFMA, 2 no weight DMA, 3 no per-step wait/barrier (2-stage), 4 no DMA
+// 1 no MFMA, 2 no weight DMA, 3 no per-step wait/barrier (2-stage), 4 no DMA,
+// 5 no epilogue stores, 6 = 4 + 5
 #ifndef CONV_EXP
 #define CONV_EXP 0
 #endif
+#define CONV_NO_DMA (CONV_EXP == 4 || CONV_EXP == 6)
+#define CONV_NO_STORE (CONV_EXP == 5 || CONV_EXP == 6)
 
 #define INVALID_OFF 0xFFFFFFF0u
 
@@ -148,18 +151,20 @@ static __device__ __forceinline__ void wait_vmcnt() {
 // table is staged into LDS first so no ordinary global load (which hipcc
 // waits for with vmcnt(0)) sits inside the loop.
 template <int TP, int TC, int WP, int WC, int NS>
-__global__ __launch_bounds__(256, 2)
+__global__ __launch_bounds__(64 * WP * WC, 2)
 void conv_igemm_kernel(const ConvParams p) {
   constexpr int P_TILE = WP * TP * 16;
   constexpr int C_TILE = WC * TC * 16;
   constexpr int BK = 64;
-  constexpr int A_INSTR = P_TILE / 32;            // act DMA instructions per wave
+  constexpr int NW = WP * WC;                     // waves per block
+  constexpr int A_INSTR = P_TILE / (8 * NW);      // act DMA instructions per wave
   constexpr int W_INSTR_TOTAL = C_TILE / 8;       // weight DMA instructions per block
-  constexpr int W_INSTR = (W_INSTR_TOTAL + 3) / 4;
+  constexpr int W_INSTR = (W_INSTR_TOTAL + NW - 1) / NW;
   constexpr int ACT_BYTES = P_TILE * BK * 2;
   constexpr int BUF_BYTES = (P_TILE + C_TILE) * BK * 2;
   constexpr int KTAB_BYTES = NS == 3 ? KTAB_MAX * 8 : 0;
-  static_assert(WP * WC == 4, "4 waves per block");
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves per block");
+  static_assert(P_TILE % (8 * NW) == 0, "activation DMA split");
   static_assert(C_TILE % 16 == 0 && P_TILE % 32 == 0, "tile shape");
   static_assert(NS == 2 || NS == 3, "stages");
 
@@ -206,7 +211,7 @@ void conv_igemm_kernel(const ConvParams p) {
   const uint32_t wrow_off = ((uint32_t)c0 * (uint32_t)p.K_pad + (uint32_t)kc * 8u) * 2u;
 
   auto issue = [&](int s, int buf, int2 e) {
-    if (CONV_EXP == 4) return;
+    if (CONV_NO_DMA) return;
     char* base = lds + buf * BUF_BYTES;
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) {
@@ -218,8 +223,8 @@ void conv_igemm_kernel(const ConvParams p) {
     }
 #pragma unroll
     for (int j = 0; j < W_INSTR; ++j) {
-      const int instr = wave + 4 * j;
-      if (CONV_EXP != 2 && (W_INSTR_TOTAL % 4 == 0 || instr < W_INSTR_TOTAL)) {
+      const int instr = wave + NW * j;
+      if (CONV_EXP != 2 && (W_INSTR_TOTAL % NW == 0 || instr < W_INSTR_TOTAL)) {
         const uint32_t off = wrow_off + ((uint32_t)(instr * 8 + lrow) * (uint32_t)p.K_pad +
                                          (uint32_t)(s * BK)) * 2u;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -289,11 +294,11 @@ void conv_igemm_kernel(const ConvParams p) {
   } else {
     // K-chunk table -> LDS (nsteps * 8 entries <= KTAB_MAX, checked on launch)
     int2* ktab_l = (int2*)(lds + NS * BUF_BYTES);
-    for (int i = tid; i < nsteps * 8; i += 256) ktab_l[i] = p.ktab[i];
+    for (int i = tid; i < nsteps * 8; i += 64 * NW) ktab_l[i] = p.ktab[i];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // this wave's DMA instructions per step (weights split unevenly over waves)
-    constexpr int W_LAST = W_INSTR_TOTAL % 4 == 0 ? 4 : W_INSTR_TOTAL % 4;
+    constexpr int W_LAST = W_INSTR_TOTAL % NW == 0 ? NW : W_INSTR_TOTAL % NW;
     constexpr int PER_STEP_HI = A_INSTR + W_INSTR;
     constexpr int PER_STEP_LO = A_INSTR + W_INSTR - 1;
     const bool hi = wave < W_LAST;
@@ -353,7 +358,7 @@ void conv_igemm_kernel(const ConvParams p) {
       i32x2 o;
       o[0] = (int)((uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16));
       o[1] = (int)((uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16));
-      *(i32x2*)(p.y + (size_t)m * p.y_stride + c) = o;
+      if (!CONV_NO_STORE || p.relu == 7) *(i32x2*)(p.y + (size_t)m * p.y_stride + c) = o;
     }
   }
 }
@@ -362,14 +367,14 @@ void conv_igemm_kernel(const ConvParams p) {
 // host side: config table + launcher (C ABI, called through ctypes / engine)
 // ---------------------------------------------------------------------------
 struct ConvConfig {
-  int p_tile, c_tile, stages;
+  int p_tile, c_tile, stages, threads;
   void (*kernel)(const ConvParams);
 };
 
 #define CFG(TP, TC, WP, WC) \
-    {WP * TP * 16, WC * TC * 16, 2, conv_igemm_kernel<TP, TC, WP, WC, 2>}
+    {WP * TP * 16, WC * TC * 16, 2, 64 * WP * WC, conv_igemm_kernel<TP, TC, WP, WC, 2>}
 #define CFG3(TP, TC, WP, WC) \
-    {WP * TP * 16, WC * TC * 16, 3, conv_igemm_kernel<TP, TC, WP, WC, 3>}
+    {WP * TP * 16, WC * TC * 16, 3, 64 * WP * WC, conv_igemm_kernel<TP, TC, WP, WC, 3>}
 #define TILES(X) \
     X(4, 4, 2, 2),   /* 128 px x 128 ch */ \
     X(4, 4, 4, 1),   /* 256 px x  64 ch */ \
@@ -394,8 +399,19 @@ struct ConvConfig {
     X(4, 4, 2, 2),   /* 128 px x 128 ch, 1 block/CU */ \
     X(2, 9, 4, 1),   /* 128 px x 144 ch, 1 block/CU */ \
     X(2, 5, 4, 1),   /* 128 px x  80 ch */ \
-    X(2, 6, 4, 1)    /* 128 px x  96 ch */
-static const ConvConfig kConfigs[] = {TILES(CFG), TILES3(CFG3)};
+    X(2, 6, 4, 1),   /* 128 px x  96 ch */ \
+    /* 8 waves (2 per SIMD at 1 block/CU) sharing one 3-stage ring */ \
+    X(2, 9, 8, 1),   /* 256 px x 144 ch, 159 KB */ \
+    X(2, 8, 8, 1),   /* 256 px x 128 ch, 152 KB */ \
+    X(2, 6, 8, 1),   /* 256 px x  96 ch */ \
+    X(2, 4, 8, 1),   /* 256 px x  64 ch */ \
+    X(4, 4, 4, 2),   /* 256 px x 128 ch, 64x64 per wave */ \
+    X(2, 4, 4, 2)    /* 128 px x 128 ch, 32x64 per wave */
+// 8-wave 2-stage variants
+#define TILES8(X) \
+    X(2, 9, 8, 1),   /* 256 px x 144 ch, 102 KB */ \
+    X(2, 4, 8, 1)    /* 256 px x  64 ch */
+static const ConvConfig kConfigs[] = {TILES(CFG), TILES3(CFG3), TILES8(CFG)};
 static const int kNumConfigs = sizeof(kConfigs) / sizeof(kConfigs[0]);
 
 extern "C" {
@@ -458,7 +474,7 @@ int rnb_conv_launch(const ConvParams* pp, int config_id, hipStream_t stream) {
   if (p.n_ctiles * cfg.c_tile > p.w_rows) return -8;
   if (!p.ktab) return -9;
   if (cfg.stages == 3 && p.K_pad / 8 > KTAB_MAX) return -11;
-  hipLaunchKernelGGL(cfg.kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL(cfg.kernel, dim3((unsigned)blocks), dim3(cfg.threads), 0, stream, p);
   return (int)hipGetLastError();
 }
 

@@ -36,6 +36,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 
+// Bottleneck experiments (scripts/kernel_exp.py; 0 = product): 1 no MFMA,
+// 4 no activation traffic (all loads out of range), 5 no stores, 6 = 4 + 5
+#ifndef TEMP_EXP
+#define TEMP_EXP 0
+#endif
+
 #define TEMP_INVALID 0xFFFFFFF0u
 
 struct TemporalParams {
@@ -119,7 +125,7 @@ void conv_temporal_kernel(const TemporalParams p) {
   auto load_frame = [&](bf16x8* dst, uint32_t base, int t) {
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
-      const uint32_t off = (base == TEMP_INVALID || !chok[ch])
+      const uint32_t off = (TEMP_EXP == 4 || TEMP_EXP == 6 || base == TEMP_INVALID || !chok[ch])
                                ? TEMP_INVALID
                                : base + (uint32_t)t * frame_bytes + (uint32_t)ch * 64u;
       const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
@@ -167,31 +173,44 @@ void conv_temporal_kernel(const TemporalParams p) {
           for (int ct = 0; ct < CT; ++ct) {
             const bf16x8 wf =
                 *(const bf16x8*)(wlt + (size_t)((dt * NCH + ch) * CT + ct) * 1024);
-            acc[to][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, b[ti & 1][ch],
-                                                                  acc[to][ct], 0, 0, 0);
+            if (TEMP_EXP == 1)
+              acc[to][ct][0] += __builtin_bit_cast(float, (int)(wf[0] ^ b[ti & 1][ch][1]));
+            else
+              acc[to][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, b[ti & 1][ch],
+                                                                    acc[to][ct], 0, 0, 0);
           }
         }
       }
     }
 
-    // ---- epilogue: bias (+ residual) (+ ReLU) -> bf16, 4 channels per lane ----
+    // ---- epilogue: bias (+ residual) (+ ReLU) -> bf16, 4 channels per lane;
+    // the residual of frame t+1 is in flight while frame t is written ----
     if (hw < p.HW) {
+      const bool has_res = p.res != nullptr;
+      i32x2 rb[2][CT];
+      auto load_res = [&](i32x2* dst, int t) {
+        const size_t m = (size_t)(n * p.T + t) * p.HW + hw;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const int c = c0 + ct * 16 + fq * 4;
+          dst[ct] = (has_res && c < p.Cout_p) ? *(const i32x2*)(p.res + m * p.res_stride + c)
+                                               : (i32x2){0, 0};
+        }
+      };
+      load_res(rb[0], 0);
 #pragma unroll
       for (int t = 0; t < T; ++t) {
+        if (t + 1 < T) load_res(rb[(t + 1) & 1], t + 1);
         const size_t m = (size_t)(n * p.T + t) * p.HW + hw;
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
           const int c = c0 + ct * 16 + fq * 4;
           if (c >= p.Cout_p) continue;
-          float v0 = acc[t][ct][0] + bias[ct].x, v1 = acc[t][ct][1] + bias[ct].y;
-          float v2 = acc[t][ct][2] + bias[ct].z, v3 = acc[t][ct][3] + bias[ct].w;
-          if (p.res) {
-            const i32x2 r = *(const i32x2*)(p.res + m * p.res_stride + c);
-            v0 += tbf2f((uint32_t)r[0] & 0xFFFFu);
-            v1 += tbf2f((uint32_t)r[0] >> 16);
-            v2 += tbf2f((uint32_t)r[1] & 0xFFFFu);
-            v3 += tbf2f((uint32_t)r[1] >> 16);
-          }
+          const i32x2 r = rb[t & 1][ct];
+          float v0 = acc[t][ct][0] + bias[ct].x + tbf2f((uint32_t)r[0] & 0xFFFFu);
+          float v1 = acc[t][ct][1] + bias[ct].y + tbf2f((uint32_t)r[0] >> 16);
+          float v2 = acc[t][ct][2] + bias[ct].z + tbf2f((uint32_t)r[1] & 0xFFFFu);
+          float v3 = acc[t][ct][3] + bias[ct].w + tbf2f((uint32_t)r[1] >> 16);
           if (p.relu) {
             v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f);
             v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
@@ -199,7 +218,8 @@ void conv_temporal_kernel(const TemporalParams p) {
           i32x2 o;
           o[0] = (int)((uint32_t)tf2bf(v0) | ((uint32_t)tf2bf(v1) << 16));
           o[1] = (int)((uint32_t)tf2bf(v2) | ((uint32_t)tf2bf(v3) << 16));
-          *(i32x2*)(p.y + m * p.y_stride + c) = o;
+          if ((TEMP_EXP != 5 && TEMP_EXP != 6) || p.relu == 7)
+            *(i32x2*)(p.y + m * p.y_stride + c) = o;
         }
       }
     }

@@ -27,7 +27,8 @@ BK = 64             # K step of the kernel
 W_ROW_SLACK = 256   # extra zero weight rows (>= largest channel tile)
 HALO = 100          # config id of the halo-tiled 1x3x3 stride-1 kernel (conv_halo.hip)
 TEMPORAL = 101      # config id of the register-direct 3x1x1 kernel (conv_temporal.hip)
-SPECIAL_NAMES = {HALO: "halo", TEMPORAL: "temporal"}
+HALO4 = 102         # halo kernel with 64-pixel waves (4 MFMA pixel sub-tiles per wave)
+SPECIAL_NAMES = {HALO: "halo", TEMPORAL: "temporal", HALO4: "halo4"}
 LDS_LIMIT = 160 * 1024
 
 
@@ -228,6 +229,10 @@ class ConvLayer:
         out = []
         if self.halo_eligible(x_shape):
             out.append(HALO)
+            from .native import kernels
+            N, T, H, W, _ = x_shape
+            if 0 < kernels().halo_lds_bytes(N * T, H, W, self.geom.cin_p, 4) <= LDS_LIMIT:
+                out.append(HALO4)
         if self.temporal_eligible(x_shape):
             out.append(TEMPORAL)
         return out
@@ -320,8 +325,9 @@ class ConvLayer:
 
     def _launch(self, p, cid, x, y, residual, stream):
         from .native import kernels
-        if cid == HALO:
-            kernels().halo(self.halo_params(x, y, residual), stream.cuda_stream)
+        if cid in (HALO, HALO4):
+            kernels().halo(self.halo_params(x, y, residual), stream.cuda_stream,
+                           hp=4 if cid == HALO4 else 2)
         elif cid == TEMPORAL:
             kernels().temporal(self.temporal_params(x, y, residual), num_cus(x.device), 0,
                                stream.cuda_stream)

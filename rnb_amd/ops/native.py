@@ -167,9 +167,10 @@ class Kernels:
         lib.rnb_video_reduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_void_p]
-        lib.rnb_halo_launch.argtypes = [ctypes.POINTER(HaloParams), ctypes.c_void_p]
-        lib.rnb_halo_launch.restype = ctypes.c_int
-        lib.rnb_halo_lds_bytes.argtypes = [ctypes.c_int] * 4
+        lib.rnb_halo_launch_v.argtypes = [ctypes.POINTER(HaloParams), ctypes.c_int,
+                                          ctypes.c_void_p]
+        lib.rnb_halo_launch_v.restype = ctypes.c_int
+        lib.rnb_halo_lds_bytes_v.argtypes = [ctypes.c_int] * 5
         lib.rnb_temporal_launch.argtypes = [ctypes.POINTER(TemporalParams), ctypes.c_int,
                                             ctypes.c_int, ctypes.c_void_p]
         lib.rnb_temporal_launch.restype = ctypes.c_int
@@ -194,8 +195,9 @@ class Kernels:
         _check(self.lib.rnb_conv_launch(ctypes.byref(params), config_id, stream),
                "conv (config %d)" % config_id)
 
-    def halo(self, params: HaloParams, stream: int) -> None:
-        _check(self.lib.rnb_halo_launch(ctypes.byref(params), stream), "conv_halo")
+    def halo(self, params: HaloParams, stream: int, hp: int = 2) -> None:
+        """hp: 16-pixel MFMA sub-tiles per wave (2 or 4)."""
+        _check(self.lib.rnb_halo_launch_v(ctypes.byref(params), hp, stream), "conv_halo")
 
     def temporal(self, params: TemporalParams, num_cus: int, blocks_per_cu: int,
                  stream: int) -> None:
@@ -205,8 +207,8 @@ class Kernels:
     def temporal_lds_bytes(self, T: int, cin_p: int, cout_p: int) -> int:
         return self.lib.rnb_temporal_lds_bytes(T, cin_p, cout_p)
 
-    def halo_lds_bytes(self, frames: int, H: int, W: int, cin: int) -> int:
-        return self.lib.rnb_halo_lds_bytes(frames, H, W, cin)
+    def halo_lds_bytes(self, frames: int, H: int, W: int, cin: int, hp: int = 2) -> int:
+        return self.lib.rnb_halo_lds_bytes_v(frames, H, W, cin, hp)
 
     def clipgen_u8(self, out_ptr, vids_ptr, starts_ptr, nclips, F, H, W, stream):
         _check(self.lib.rnb_clipgen_u8(out_ptr, vids_ptr, starts_ptr, nclips, F, H, W,

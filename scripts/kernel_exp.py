@@ -19,7 +19,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 EXP_DIR = os.path.join(ROOT, "rnb_amd", "_native", "exp")
-VARIANTS = {0: "product", 1: "no-mfma", 2: "no-wdma", 3: "no-sync", 4: "no-dma"}
+VARIANTS = {0: "product", 1: "no-mfma", 2: "no-wdma", 3: "no-sync", 4: "no-dma",
+            5: "no-store", 6: "mfma-only"}
 
 
 def build():
@@ -28,9 +29,10 @@ def build():
     for v in VARIANTS:
         out = os.path.join(EXP_DIR, "libexp%d.so" % v)
         cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-DHALO_EXP=%d" % v, "-DCONV_EXP=%d" % v,
+               "-DHALO_EXP=%d" % v, "-DCONV_EXP=%d" % v, "-DTEMP_EXP=%d" % v,
                os.path.join(ROOT, "csrc", "conv_igemm.hip"),
                os.path.join(ROOT, "csrc", "conv_halo.hip"),
+               os.path.join(ROOT, "csrc", "conv_temporal.hip"),
                os.path.join(ROOT, "csrc", "video_ops.hip"), "-o", out]
         procs.append(subprocess.Popen(cmd))
     for p in procs:
@@ -43,14 +45,17 @@ def run(args):
     import torch
     from rnb_amd.models.r2p1d.model import build_network
     from rnb_amd.models.r2p1d.engine import R2P1DEngine
-    from rnb_amd.ops.native import ConvParams, HaloParams
-    from rnb_amd.ops.conv import HALO
+    from rnb_amd.ops.native import ConvParams, HaloParams, TemporalParams
+    from rnb_amd.ops.conv import HALO, HALO4, TEMPORAL, num_cus
     libs = {}
     for v in VARIANTS:
         lib = ctypes.CDLL(os.path.join(EXP_DIR, "libexp%d.so" % v))
         lib.rnb_conv_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
                                         ctypes.c_void_p]
-        lib.rnb_halo_launch.argtypes = [ctypes.POINTER(HaloParams), ctypes.c_void_p]
+        lib.rnb_halo_launch_v.argtypes = [ctypes.POINTER(HaloParams), ctypes.c_int,
+                                          ctypes.c_void_p]
+        lib.rnb_temporal_launch.argtypes = [ctypes.POINTER(TemporalParams), ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_void_p]
         libs[v] = lib
     dev = torch.device("cuda:0")
     eng = R2P1DEngine(build_network(1, 5, depth=args.depth), dev, backend="hip")
@@ -65,13 +70,20 @@ def run(args):
         res = bufs[op.res] if op.res is not None else None
         y = op.layer.forward_hip(src, res)
         if op.layer.name in want:
-            cfgs = [op.layer.autotune(src, res)] + [int(c) for c in args.configs.split(",") if c]
+            cfgs = [op.layer.autotune(src, res)] + op.layer.special_candidates(src.shape) \
+                + [int(c) for c in args.configs.split(",") if c]
             for cfg in cfgs:
                 times = []
                 for v, lib in libs.items():
-                    if cfg == HALO:
+                    if cfg in (HALO, HALO4):
                         p = op.layer.halo_params(src, y, res)
-                        launch = lambda: lib.rnb_halo_launch(ctypes.byref(p), stream.cuda_stream)
+                        hp = 4 if cfg == HALO4 else 2
+                        launch = lambda: lib.rnb_halo_launch_v(ctypes.byref(p), hp,
+                                                               stream.cuda_stream)
+                    elif cfg == TEMPORAL:
+                        p = op.layer.temporal_params(src, y, res)
+                        launch = lambda: lib.rnb_temporal_launch(
+                            ctypes.byref(p), num_cus(dev), 0, stream.cuda_stream)
                     else:
                         p = op.layer.params(src, y, res)
                         launch = lambda: lib.rnb_conv_launch(ctypes.byref(p), cfg,
@@ -87,7 +99,8 @@ def run(args):
                     e.record()
                     e.synchronize()
                     times.append(s.elapsed_time(e) / args.reps * 1e3)
-                print("%-32s %-8s " % (op.layer.name[-32:], "halo" if cfg == HALO else cfg)
+                print("%-32s %-8s " % (op.layer.name[-32:], {HALO: "halo", HALO4: "halo4", TEMPORAL: "temp"}
+                                       .get(cfg, cfg))
                       + " ".join("%7.1fus" % t for t in times), flush=True)
         bufs[op.dst] = y
 

@@ -63,7 +63,7 @@ def test_conv_matches_torch(case):
     assert err <= 1e-2 * scale + 1e-2, (err, scale)
 
 
-@pytest.mark.parametrize("cfg", range(24))
+@pytest.mark.parametrize("cfg", range(36))
 def test_conv_every_tile_config_exact_integers(cfg):
     """Small-integer data is exact in bf16/fp32: any layout bug shows up."""
     from rnb_amd.ops.native import kernels
@@ -174,16 +174,19 @@ def test_time_major_rows_exact(thw, cin, cout, stride):
     (1, (1, 9, 40), 192, 144),      # 3 chunks, single frame, M tail
 ])
 def test_halo_kernel_exact(n, thw, cin, cout):
-    from rnb_amd.ops.conv import HALO
+    from rnb_amd.ops.conv import HALO, HALO4
     layer = _layer(cin, cout, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=True, integer=True)
     x = _input(n, thw, cin, cin, integer=True)
     assert layer.halo_eligible(x.shape)
     res_shape = layer.out_shape(x.shape)
     res = _input(res_shape[0], res_shape[1:4], res_shape[4], cout, integer=True, seed=3)
     ref = layer.forward_torch(x, residual=res, out_dtype=torch.bfloat16)
-    y = layer.forward_hip(x, residual=res, config=HALO)
-    torch.cuda.synchronize()
-    assert torch.equal(y, ref), (y.float() - ref.float()).abs().max().item()
+    variants = [c for c in layer.special_candidates(x.shape) if c in (HALO, HALO4)]
+    assert HALO in variants
+    for cid in variants:
+        y = layer.forward_hip(x, residual=res, config=cid)
+        torch.cuda.synchronize()
+        assert torch.equal(y, ref), (cid, (y.float() - ref.float()).abs().max().item())
 
 
 def test_halo_kernel_random_matches_generic():
