@@ -25,6 +25,8 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+#include "conv_epilogue.h"
+
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
@@ -61,11 +63,6 @@ struct HaloParams {
 static __device__ __forceinline__ int hdiv(int n, uint32_t m, uint32_t s) {
   return m ? (int)(__umulhi((uint32_t)n, m) >> s) : n;
 }
-static __device__ __forceinline__ uint16_t hf2bf(float f) {
-  __hip_bfloat16 h = __float2bfloat16(f);
-  return __builtin_bit_cast(uint16_t, h);
-}
-static __device__ __forceinline__ float hbf2f(uint32_t u16) { return __uint_as_float(u16 << 16); }
 
 // One block = one tile of R full image rows of one frame (row-aligned, so the
 // patch is a fixed (R+2) x (W+2) box whose border rows/columns are the conv
@@ -221,35 +218,14 @@ void conv_halo_kernel(const HaloParams p) {
     }
   }
 
+  const int npairs = p.Cout_p >> 5;
 #pragma unroll
   for (int tp = 0; tp < HP; ++tp) {
     const int i = wave * 16 * HP + tp * 16 + frow;
     if (i >= npx) continue;
-    const int m = p0 + i;
-#pragma unroll
-    for (int tc = 0; tc < TC; ++tc) {
-      const int c = c0 + tc * 16 + fq * 4;
-      if (c >= p.Cout_p) continue;
-      const float4 b4 = *(const float4*)(p.bias + c);
-      float v0 = acc[tp][tc][0] + b4.x, v1 = acc[tp][tc][1] + b4.y;
-      float v2 = acc[tp][tc][2] + b4.z, v3 = acc[tp][tc][3] + b4.w;
-      if (p.res) {
-        const i32x2 r = *(const i32x2*)(p.res + (size_t)m * p.res_stride + c);
-        v0 += hbf2f((uint32_t)r[0] & 0xFFFFu);
-        v1 += hbf2f((uint32_t)r[0] >> 16);
-        v2 += hbf2f((uint32_t)r[1] & 0xFFFFu);
-        v3 += hbf2f((uint32_t)r[1] >> 16);
-      }
-      if (p.relu) {
-        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f);
-        v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-      }
-      i32x2 o;
-      o[0] = (int)((uint32_t)hf2bf(v0) | ((uint32_t)hf2bf(v1) << 16));
-      o[1] = (int)((uint32_t)hf2bf(v2) | ((uint32_t)hf2bf(v3) << 16));
-      if ((HALO_EXP != 5 && HALO_EXP != 6) || p.relu == 7)
-        *(i32x2*)(p.y + (size_t)m * p.y_stride + c) = o;
-    }
+    ep_row<TC>(p.y, p.y_stride, p.res, p.res_stride, p.bias, (size_t)(p0 + i), c0 >> 4, fq,
+               npairs, p.Cout_p, p.relu != 0, acc[tp],
+               (HALO_EXP != 5 && HALO_EXP != 6) || p.relu == 7);
   }
 }
 

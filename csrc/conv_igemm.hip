@@ -24,6 +24,8 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+#include "conv_epilogue.h"
+
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -71,10 +73,6 @@ struct ConvParams {
 
 #define INVALID_OFF 0xFFFFFFF0u
 
-static __device__ __forceinline__ uint16_t f2bf(float f) {
-  __hip_bfloat16 h = __float2bfloat16(f);
-  return __builtin_bit_cast(uint16_t, h);
-}
 // n / d for 0 <= n < 2^31 with a host-computed (m, s); m == 0 encodes d == 1
 static __device__ __forceinline__ int fast_div(int n, uint32_t m, uint32_t s) {
   return m ? (int)(__umulhi((uint32_t)n, m) >> s) : n;
@@ -84,9 +82,6 @@ static __device__ __forceinline__ int range_mask(int o, int K, int S) {
   const int lo = max(0, -o);
   const int hi = min(K, S - o);
   return hi > lo ? (int)(((1u << hi) - 1u) ^ ((1u << lo) - 1u)) : 0;
-}
-static __device__ __forceinline__ float bf2f(uint32_t u16) {
-  return __uint_as_float(u16 << 16);
 }
 
 // ---------------------------------------------------------------------------
@@ -324,7 +319,8 @@ void conv_igemm_kernel(const ConvParams p) {
     }
   }
 
-  // ---- epilogue: bias (+ residual) (+ ReLU) -> bf16, 4 channels per lane ----
+  // ---- epilogue: bias (+ residual) (+ ReLU) -> bf16 (conv_epilogue.h) ----
+  const int npairs = p.Cout_p >> 5;
 #pragma unroll
   for (int tp = 0; tp < TP; ++tp) {
     int m = p0 + wp * TP * 16 + tp * 16 + frow;
@@ -335,31 +331,8 @@ void conv_igemm_kernel(const ConvParams p) {
     } else if (m >= p.M) {
       continue;
     }
-#pragma unroll
-    for (int tc = 0; tc < TC; ++tc) {
-      const int c = c0 + wc * TC * 16 + tc * 16 + fq * 4;
-      if (c >= p.Cout_p) continue;
-      const float4 b4 = *(const float4*)(p.bias + c);
-      float v0 = acc[tp][tc][0] + b4.x;
-      float v1 = acc[tp][tc][1] + b4.y;
-      float v2 = acc[tp][tc][2] + b4.z;
-      float v3 = acc[tp][tc][3] + b4.w;
-      if (p.res) {
-        const i32x2 r = *(const i32x2*)(p.res + (size_t)m * p.res_stride + c);
-        v0 += bf2f((uint32_t)r[0] & 0xFFFFu);
-        v1 += bf2f((uint32_t)r[0] >> 16);
-        v2 += bf2f((uint32_t)r[1] & 0xFFFFu);
-        v3 += bf2f((uint32_t)r[1] >> 16);
-      }
-      if (p.relu) {
-        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f);
-        v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-      }
-      i32x2 o;
-      o[0] = (int)((uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16));
-      o[1] = (int)((uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16));
-      if (!CONV_NO_STORE || p.relu == 7) *(i32x2*)(p.y + (size_t)m * p.y_stride + c) = o;
-    }
+    ep_row<TC>(p.y, p.y_stride, p.res, p.res_stride, p.bias, (size_t)m, (c0 >> 4) + wc * TC,
+               fq, npairs, p.Cout_p, p.relu != 0, acc[tp], !CONV_NO_STORE || p.relu == 7);
   }
 }
 

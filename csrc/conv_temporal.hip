@@ -31,6 +31,8 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+#include "conv_epilogue.h"
+
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -63,11 +65,6 @@ struct TemporalParams {
 static __device__ __forceinline__ int tdiv(int n, uint32_t m, uint32_t s) {
   return m ? (int)(__umulhi((uint32_t)n, m) >> s) : n;
 }
-static __device__ __forceinline__ uint16_t tf2bf(float f) {
-  __hip_bfloat16 h = __float2bfloat16(f);
-  return __builtin_bit_cast(uint16_t, h);
-}
-static __device__ __forceinline__ float tbf2f(uint32_t u16) { return __uint_as_float(u16 << 16); }
 
 template <int T, int NCH, int CT, int WAVES>
 __global__ __launch_bounds__(WAVES * 64, 2)
@@ -84,6 +81,8 @@ void conv_temporal_kernel(const TemporalParams p) {
   const int gblk = blockIdx.x / p.n_ctiles;
   const int gstride = (gridDim.x / p.n_ctiles) * WAVES;
   const int c0 = ctile * CT * 16;
+  const int npairs = p.Cout_p >> 5;
+  static_assert(CT % 2 == 0, "channel tiles come in pairs");
 
   // ---- weights -> LDS in A-fragment order (once per persistent block) ----
   for (int f = wave; f < NFRAG; f += WAVES) {
@@ -97,12 +96,6 @@ void conv_temporal_kernel(const TemporalParams p) {
     if (kk < p.Cin_p && row < p.w_rows)
       v = *(const i32x4*)(p.w + (size_t)row * p.K_pad + dt * p.Cin_p + kk);
     *(i32x4*)(smem + ((size_t)f * 64 + lane) * 16) = v;
-  }
-  float4 bias[CT];
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) {
-    const int c = c0 + ct * 16 + fq * 4;
-    bias[ct] = c < p.w_rows ? *(const float4*)(p.bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
 
@@ -183,43 +176,47 @@ void conv_temporal_kernel(const TemporalParams p) {
       }
     }
 
-    // ---- epilogue: bias (+ residual) (+ ReLU) -> bf16, 4 channels per lane;
-    // the residual of frame t+1 is in flight while frame t is written ----
+    // ---- epilogue: bias (+ residual) (+ ReLU) -> bf16 (conv_epilogue.h
+    // channel pairs: CT is even and tiles start even, so a pair never
+    // straddles waves); the residual of frame t+1 is in flight while frame
+    // t is written ----
     if (hw < p.HW) {
-      const bool has_res = p.res != nullptr;
-      i32x2 rb[2][CT];
-      auto load_res = [&](i32x2* dst, int t) {
+      const int gt0 = c0 >> 4;
+      ep_i32x4 rb[2][CT / 2];
+      auto load_res = [&](ep_i32x4* dst, int t) {
         const size_t m = (size_t)(n * p.T + t) * p.HW + hw;
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-          const int c = c0 + ct * 16 + fq * 4;
-          dst[ct] = (has_res && c < p.Cout_p) ? *(const i32x2*)(p.res + m * p.res_stride + c)
-                                               : (i32x2){0, 0};
+        for (int k = 0; k < CT / 2; ++k) {
+          const int gt = gt0 + 2 * k;
+          if ((gt >> 1) < npairs) {
+            dst[k] = ep_load_res8(p.res, p.res_stride, m, gt, fq);
+          } else {
+            const ep_i32x2 lo = ep_load_res4(p.res, p.res_stride, m, gt, fq, npairs, p.Cout_p);
+            const ep_i32x2 hi =
+                ep_load_res4(p.res, p.res_stride, m, gt + 1, fq, npairs, p.Cout_p);
+            dst[k] = (ep_i32x4){lo[0], lo[1], hi[0], hi[1]};
+          }
         }
       };
+      const bool do_store = (TEMP_EXP != 5 && TEMP_EXP != 6) || p.relu == 7;
       load_res(rb[0], 0);
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         if (t + 1 < T) load_res(rb[(t + 1) & 1], t + 1);
         const size_t m = (size_t)(n * p.T + t) * p.HW + hw;
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-          const int c = c0 + ct * 16 + fq * 4;
-          if (c >= p.Cout_p) continue;
-          const i32x2 r = rb[t & 1][ct];
-          float v0 = acc[t][ct][0] + bias[ct].x + tbf2f((uint32_t)r[0] & 0xFFFFu);
-          float v1 = acc[t][ct][1] + bias[ct].y + tbf2f((uint32_t)r[0] >> 16);
-          float v2 = acc[t][ct][2] + bias[ct].z + tbf2f((uint32_t)r[1] & 0xFFFFu);
-          float v3 = acc[t][ct][3] + bias[ct].w + tbf2f((uint32_t)r[1] >> 16);
-          if (p.relu) {
-            v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f);
-            v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+        for (int k = 0; k < CT / 2; ++k) {
+          const int gt = gt0 + 2 * k;
+          const ep_i32x4 r = rb[t & 1][k];
+          if ((gt >> 1) < npairs) {
+            ep_store8r(p.y, p.y_stride, p.bias, m, gt, fq, p.relu != 0, acc[t][2 * k],
+                       acc[t][2 * k + 1], r, do_store);
+          } else {
+            ep_store4r(p.y, p.y_stride, p.bias, m, gt, fq, npairs, p.Cout_p, p.relu != 0,
+                       acc[t][2 * k], (ep_i32x2){r[0], r[1]}, do_store);
+            ep_store4r(p.y, p.y_stride, p.bias, m, gt + 1, fq, npairs, p.Cout_p, p.relu != 0,
+                       acc[t][2 * k + 1], (ep_i32x2){r[2], r[3]}, do_store);
           }
-          i32x2 o;
-          o[0] = (int)((uint32_t)tf2bf(v0) | ((uint32_t)tf2bf(v1) << 16));
-          o[1] = (int)((uint32_t)tf2bf(v2) | ((uint32_t)tf2bf(v3) << 16));
-          if ((TEMP_EXP != 5 && TEMP_EXP != 6) || p.relu == 7)
-            *(i32x2*)(p.y + m * p.y_stride + c) = o;
         }
       }
     }

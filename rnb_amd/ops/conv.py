@@ -44,6 +44,21 @@ def num_cus(device) -> int:
     return n
 
 
+def pair_permutation(cout_p: int) -> torch.Tensor:
+    """Physical weight row -> output channel (csrc/conv_epilogue.h).
+
+    Inside every full 32-channel group g, physical row 32g + 16b + i (tile b
+    of the MFMA tile pair, row i of the tile) computes channel
+    32g + 8(i // 4) + 4b + i % 4, so the lane that holds rows 4q..4q+3 of both
+    tiles owns 8 consecutive channels and stores them with one 16-byte write.
+    Rows past the last full group keep their own channel.
+    """
+    r = torch.arange(cout_p)
+    g, b, i = r // 32, (r % 32) // 16, r % 16
+    paired = 32 * g + 8 * (i // 4) + 4 * b + i % 4
+    return torch.where(g < cout_p // 32, paired, r)
+
+
 def pad_to(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
@@ -115,9 +130,13 @@ class ConvLayer:
         w[..., :geom.cin] = weight.detach().float().permute(0, 2, 3, 4, 1)
         wmat = torch.zeros(cout_p + W_ROW_SLACK, geom.k_pad, dtype=torch.float32)
         wmat[:geom.cout, :geom.k_total] = w.reshape(geom.cout, -1)
-        self.wmat = wmat.to(torch.bfloat16).to(device).contiguous()
         b = torch.zeros(cout_p + W_ROW_SLACK, dtype=torch.float32)
         b[:geom.cout] = bias.detach().float()
+        # rows in the kernels' paired-store order (conv_epilogue.h)
+        perm = pair_permutation(cout_p)
+        wmat[:cout_p] = wmat[:cout_p][perm].clone()
+        b[:cout_p] = b[:cout_p][perm].clone()
+        self.wmat = wmat.to(torch.bfloat16).to(device).contiguous()
         self.bias = b.to(device).contiguous()
         # the bf16-rounded weight in conv layout, for the torch path
         self.w_ref = (weight.detach().to(torch.bfloat16).float().to(device))
