@@ -6,7 +6,7 @@ forward through the HIP engine.
 """
 from rnb_amd.profiling import tracer
 
-tracer.initialize()     # roctracer must register before the HIP runtime starts
+tracer.initialize()     # the rocprofiler-sdk tool must register before the HIP runtime starts
 import torch  # noqa: E402
 
 
