@@ -33,6 +33,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
+from ...ops.bn import BatchNormBatch
 from ...ops.conv import ConvGeom, ConvLayer, fold_bn, pad_to, CH_ALIGN
 from ...ops.video import Head, IN_CHANNELS_P, ndhwc_to_ncdhw, ncdhw_to_ndhwc
 from .network import (LAYER_CHANNELS, LAYER_INPUT_CTHW, LAYER_OUTPUT_CTHW,
@@ -55,10 +56,13 @@ def boundary_shape(layer_idx: int, n: int) -> Tuple[int, ...]:
 
 
 class PlanOp:
-    __slots__ = ("kind", "layer", "src", "dst", "res")
+    """One conv of the plan; ``bn`` is set in bn_mode='batch' (BatchNorm with
+    batch statistics applied after the unfolded conv, then residual + ReLU)."""
+    __slots__ = ("kind", "layer", "src", "dst", "res", "bn", "bn_relu")
 
-    def __init__(self, kind, layer, src, dst, res=None):
+    def __init__(self, kind, layer, src, dst, res=None, bn=None, bn_relu=False):
         self.kind, self.layer, self.src, self.dst, self.res = kind, layer, src, dst, res
+        self.bn, self.bn_relu = bn, bn_relu
 
 
 class R2P1DEngine:
@@ -68,9 +72,6 @@ class R2P1DEngine:
             raise ValueError("unknown backend %r" % backend)
         if bn_mode not in ("eval", "batch"):
             raise ValueError("bn_mode must be 'eval' or 'batch'")
-        if bn_mode == "batch" and backend != "module":
-            raise ValueError("bn_mode='batch' (reference training-mode BN) needs "
-                             "backend='module'")
         self.net = net
         self.device = device
         self.backend = backend
@@ -118,13 +119,21 @@ class R2P1DEngine:
     def _stconv(self, st: SpatioTemporalConv, src: str, post_bn, relu: bool,
                 res: Optional[str], name: str) -> str:
         mid = self._name()
-        self.ops.append(PlanOp("conv", self._conv(st.spatial_conv, st.bn, True,
-                                                  name + ".spatial", src, mid), src, mid))
+        self._append(st.spatial_conv, st.bn, True, None, name + ".spatial", src, mid)
         dst = self._name()
-        self.ops.append(PlanOp("conv", self._conv(st.temporal_conv, post_bn, relu,
-                                                  name + ".temporal", mid, dst),
-                               mid, dst, res))
+        self._append(st.temporal_conv, post_bn, relu, res, name + ".temporal", mid, dst)
         return dst
+
+    def _append(self, conv, bn, relu: bool, res: Optional[str], name: str, src: str, dst: str):
+        if self.bn_mode == "batch" and bn is not None:
+            # reference numerics: conv (unfolded) -> BN with batch statistics
+            # -> (+ residual) -> ReLU
+            layer = self._conv(conv, None, False, name, src, dst)
+            bnop = BatchNormBatch(bn, layer.geom.cout_p, self.device)
+            self.ops.append(PlanOp("conv", layer, src, dst, res, bn=bnop, bn_relu=relu))
+        else:
+            self.ops.append(PlanOp("conv", self._conv(conv, bn, relu, name, src, dst),
+                                   src, dst, res))
 
     def _block(self, blk, src: str, name: str) -> str:
         if blk.downsample:
@@ -199,7 +208,14 @@ class R2P1DEngine:
         for op in self.ops:
             src = bufs[op.src]
             res = bufs[op.res] if op.res is not None else None
-            if hip:
+            if op.bn is not None:
+                if hip:
+                    y = op.layer.forward_hip(src, None)
+                    y = op.bn.forward_hip(y, res, op.bn_relu, out=y)
+                else:
+                    y = op.layer.forward_torch(src, None)
+                    y = op.bn.forward_torch(y, res, op.bn_relu)
+            elif hip:
                 y = op.layer.forward_hip(src, res)
             else:
                 y = op.layer.forward_torch(src, res)
@@ -223,6 +239,8 @@ class R2P1DEngine:
         for op in self.ops:
             src = bufs[op.src]
             res = bufs[op.res] if op.res is not None else None
+            if op.bn is not None:
+                res = None               # the residual is added after the BN
             chosen[op.layer.name] = op.layer.autotune(src, res, reps)
             bufs[op.dst] = op.layer.forward_hip(src, res)
         torch.cuda.synchronize(self.device)
@@ -236,6 +254,9 @@ class GraphedEngine:
                  buckets: Sequence[int] = DEFAULT_BUCKETS, autotune: bool = True,
                  warmup: int = 2):
         assert engine.backend == "hip"
+        if engine.bn_mode != "eval":
+            # bucket padding rows would enter the batch statistics
+            raise ValueError("HIP graphs need bn_mode='eval'; run bn_mode='batch' eagerly")
         self.engine = engine
         self.device = engine.device
         self.buckets = sorted({b for b in buckets if b < max_clips} | {max_clips})

@@ -75,11 +75,10 @@ def build_engine(device: torch.device, start_index=1, end_index=5, num_classes=4
                  autotune=True):
     net = build_network(start_index, end_index, num_classes, layer_sizes, depth, seed,
                         ckpt_path)
-    if bn_mode == "batch":
-        backend = "module"
     backend = _resolve_backend(backend, device)
     eng = R2P1DEngine(net, device, backend=backend, bn_mode=bn_mode)
-    if backend == "hip" and use_graphs:
+    # batch-statistics BN runs eagerly: bucket graphs pad the clip batch
+    if backend == "hip" and use_graphs and bn_mode == "eval":
         return GraphedEngine(eng, max_clips, autotune=autotune)
     return eng
 

@@ -164,6 +164,16 @@ class Kernels:
         lib.rnb_head.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        lib.rnb_bn_scratch_floats.argtypes = [ctypes.c_int, ctypes.c_int]
+        lib.rnb_bn_scratch_floats.restype = ctypes.c_longlong
+        lib.rnb_bn_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p]
+        lib.rnb_bn_apply.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_float, ctypes.c_int,
+                                     ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         lib.rnb_video_reduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_void_p]
@@ -209,6 +219,19 @@ class Kernels:
 
     def halo_lds_bytes(self, frames: int, H: int, W: int, cin: int, hp: int = 2) -> int:
         return self.lib.rnb_halo_lds_bytes_v(frames, H, W, cin, hp)
+
+    def bn_scratch_floats(self, M: int, C: int) -> int:
+        return self.lib.rnb_bn_scratch_floats(M, C)
+
+    def bn_stats(self, y_ptr, M, C, stride, scratch_ptr, mean_ptr, var_ptr, stream):
+        _check(self.lib.rnb_bn_stats(y_ptr, M, C, stride, scratch_ptr, mean_ptr, var_ptr,
+                                     stream), "bn_stats")
+
+    def bn_apply(self, y_ptr, z_ptr, res_ptr, mean_ptr, var_ptr, gamma_ptr, beta_ptr, eps,
+                 relu, M, C, y_stride, z_stride, res_stride, stream):
+        _check(self.lib.rnb_bn_apply(y_ptr, z_ptr, res_ptr, mean_ptr, var_ptr, gamma_ptr,
+                                     beta_ptr, eps, relu, M, C, y_stride, z_stride, res_stride,
+                                     stream), "bn_apply")
 
     def clipgen_u8(self, out_ptr, vids_ptr, starts_ptr, nclips, F, H, W, stream):
         _check(self.lib.rnb_clipgen_u8(out_ptr, vids_ptr, starts_ptr, nclips, F, H, W,

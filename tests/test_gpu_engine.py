@@ -166,3 +166,30 @@ def test_amdsmi_vram_query():
     from rnb_amd.config import gpu_memory_used_bytes
     used = gpu_memory_used_bytes()
     assert used is not None and len(used) >= 1 and all(u >= 0 for u in used)
+
+
+def test_batch_bn_mode_hip_matches_torch_and_module():
+    """Reference training-mode BN numerics on the HIP kernels (eager, no graphs)."""
+    from rnb_amd.models.r2p1d.model import build_network, build_engine
+    from rnb_amd.models.r2p1d.engine import R2P1DEngine
+    x = torch.randn(3, 3, 8, 112, 112, generator=torch.Generator().manual_seed(2)).to(DEV)
+    mk = lambda b: R2P1DEngine(build_network(1, 5, depth=18, seed=4), DEV, backend=b,
+                               bn_mode="batch")
+    hip, tor, mod = mk("hip"), mk("torch"), mk("module")
+    from rnb_amd.ops.video import ncdhw_to_ndhwc
+    xb = ncdhw_to_ndhwc(x, 8)
+    with torch.no_grad():
+        a = hip.forward(xb).float()
+        b = tor.forward(xb).float()
+        m = mod.forward(x).float()
+    torch.cuda.synchronize()
+    scale = m.abs().max().item()
+    e_hip, e_tor = (a - m).abs().max().item(), (b - m).abs().max().item()
+    print("batch-BN max err vs fp32 module: hip %.4f torch-plan %.4f (scale %.3f)"
+          % (e_hip, e_tor, scale))
+    # both bf16 plans drift from the fp32 module by the same order (batch
+    # statistics renormalise every layer, so bf16 rounding does not cancel)
+    assert e_hip <= max(2.0 * e_tor, 3e-2 * scale)
+    assert e_hip <= 8e-2 * scale
+    eng = build_engine(DEV, depth=18, bn_mode="batch", backend="hip")
+    assert isinstance(eng, R2P1DEngine) and eng.bn_mode == "batch"

@@ -253,3 +253,28 @@ def test_clipgen_partial_and_many_clips():
     g = vops.clipgen_u8(vids.to(DEV), starts.to(DEV), 8, 112, 112)
     torch.cuda.synchronize()
     assert torch.equal(g.cpu(), vops.clipgen_u8(vids, starts, 8, 112, 112))
+
+
+@pytest.mark.parametrize("shape,c,res,relu", [((2, 8, 56, 56, 144), 144, False, True),
+                                             ((3, 4, 28, 28, 128), 128, True, True),
+                                             ((1, 8, 56, 56, 88), 83, False, False),
+                                             ((5, 1, 7, 7, 512), 512, True, False)])
+def test_batchnorm_batch_stats_kernel(shape, c, res, relu):
+    from rnb_amd.ops.bn import BatchNormBatch
+    bn = torch.nn.BatchNorm3d(c)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    op_h = BatchNormBatch(bn, shape[-1], DEV)
+    op_t = BatchNormBatch(bn, shape[-1], DEV)
+    y = (torch.randn(shape) * 2 + 0.7)
+    y[..., c:] = 0
+    y = y.to(torch.bfloat16).to(DEV)
+    r = torch.randn(shape).to(torch.bfloat16).to(DEV) if res else None
+    ref = op_t.forward_torch(y, r, relu, out_dtype=torch.float32)
+    out = op_h.forward_hip(y, r, relu)
+    torch.cuda.synchronize()
+    assert torch.allclose(op_h.mean[:c], op_t.mean[:c], atol=1e-4, rtol=1e-4)
+    assert torch.allclose(op_h.var[:c], op_t.var[:c], atol=1e-3, rtol=1e-3)
+    assert (out.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+    assert torch.allclose(op_h.running_var, op_t.running_var, rtol=1e-3, atol=1e-4)

@@ -84,12 +84,28 @@ def test_layer_split_composes_to_whole():
     assert torch.allclose(b(mid), whole(x), atol=1e-3, rtol=1e-3)
 
 
-def test_batch_mode_bn_only_on_module_backend():
-    net = build_network(1, 5, depth=10)
-    with pytest.raises(ValueError):
-        R2P1DEngine(net, CPU, backend="torch", bn_mode="batch")
-    eng = R2P1DEngine(net, CPU, backend="module", bn_mode="batch")
-    assert eng.module.training
+def test_batch_mode_bn_plan_matches_module():
+    """Reference training-mode BN (batch statistics) through the kernel plan."""
+    x = torch.randn(3, 3, 8, 112, 112, generator=torch.Generator().manual_seed(5))
+    mod = R2P1DEngine(build_network(1, 5, depth=10, seed=1), CPU, backend="module",
+                      bn_mode="batch")
+    assert mod.module.training
+    tor = R2P1DEngine(build_network(1, 5, depth=10, seed=1), CPU, backend="torch",
+                      bn_mode="batch")
+    n_bn = sum(isinstance(m, torch.nn.BatchNorm3d) for m in mod.module.modules())
+    assert sum(op.bn is not None for op in tor.ops) == n_bn == 23
+    with torch.no_grad():
+        a = mod.forward(x)
+        b = tor.forward(ncdhw_to_ndhwc(x, 8)).float()
+    assert (a - b).abs().max().item() <= 3e-2 * a.abs().max().item()
+    # batch statistics differ from eval (folded running stats): a different model
+    ev = R2P1DEngine(build_network(1, 5, depth=10, seed=1), CPU, backend="torch")
+    assert (ev.forward(ncdhw_to_ndhwc(x, 8)).float() - b).abs().max().item() > 1e-2
+    # running statistics updated like nn.BatchNorm3d in train mode
+    first = tor.ops[0].bn
+    ref_bn = [m for m in mod.module.modules() if isinstance(m, torch.nn.BatchNorm3d)][0]
+    assert torch.allclose(first.running_mean, ref_bn.running_mean.float(), atol=2e-3)
+    assert torch.allclose(first.running_var, ref_bn.running_var.float(), rtol=2e-2, atol=2e-3)
 
 
 def test_runner_accepts_reference_layout_and_empty_batch():
