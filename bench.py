@@ -89,10 +89,19 @@ def main(argv=None) -> int:
             print("bench.py: --gpus %d needs torch.distributed.run with %d processes"
                   % (args.gpus, args.gpus), file=sys.stderr)
             return 2
-    device = torch.device("cuda:%d" % local_rank)
+    # RNB_BENCH_BACKEND=gloo + RNB_BENCH_SHARE_GPU=1 rehearse the multi-rank
+    # path on a single GPU (every rank on cuda:0, host-side reductions); the
+    # real run is one rank per GPU over RCCL ("nccl")
+    backend = os.environ.get("RNB_BENCH_BACKEND", "nccl")
+    dev_idx = 0 if os.environ.get("RNB_BENCH_SHARE_GPU") == "1" else local_rank
+    device = torch.device("cuda:%d" % dev_idx)
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+    red_dev = device if backend == "nccl" else torch.device("cpu")
 
     from rnb_amd.models.r2p1d.fused import FusedR2P1D
     from rnb_amd.timecard import percentile_stats
@@ -185,10 +194,10 @@ def main(argv=None) -> int:
     clips = sum(len(st) for sb in step_batches[args.warmup:] for b in sb for _, st in b)
     stats = percentile_stats(np.asarray(lat_ms) / 1e3)
     if world > 1:
-        t = torch.tensor([elapsed, stats["p50_ms"], stats["p99_ms"]], device=device)
+        t = torch.tensor([elapsed, stats["p50_ms"], stats["p99_ms"]], device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, p50, p99 = t.tolist()
-        c = torch.tensor([float(clips), float(preds)], device=device)
+        c = torch.tensor([float(clips), float(preds)], device=red_dev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         clips_all, preds_all = c.tolist()
     else:
