@@ -82,6 +82,32 @@ class PipelineSpec:
         used = self.gpus_used()
         return max(used) if used else -1
 
+    def on_cpu(self) -> "PipelineSpec":
+        """Copy with every GPU replica placed on the CPU (same topology).
+
+        Groups, replica counts, queue wiring, segments and selectors are
+        unchanged, so a multi-GPU configuration can be exercised end to end on
+        a machine without GPUs (multi-GPU topologies without
+        GPUs). Transports fall back to host shared-memory rings.
+        """
+        import copy
+        spec = copy.deepcopy(self)
+        for s in spec.steps:
+            for g in s.groups:
+                g.gpus = [CPU_DEVICE for _ in g.gpus]
+                g.transport = "auto"
+        return spec
+
+    def override_kwargs(self, overrides: Dict[str, Any]) -> "PipelineSpec":
+        """Copy with ``overrides`` set in every step's and group's model kwargs."""
+        import copy
+        spec = copy.deepcopy(self)
+        for s in spec.steps:
+            s.kwargs.update(overrides)
+            for g in s.groups:
+                g.kwargs.update(overrides)
+        return spec
+
     def remap_gpus(self, mapping: Dict[int, int]) -> "PipelineSpec":
         """Return a copy with logical GPU ids replaced through ``mapping``."""
         import copy

@@ -51,7 +51,26 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--json-out", type=str, default=None,
                    help="Write the run's metrics as JSON to this path")
     p.add_argument("--log-root", type=str, default=None, help="Log directory root")
+    p.add_argument("--cpu-only", action="store_true",
+                   help="Place every replica on the CPU, keeping the topology (no GPU needed)")
+    p.add_argument("--set", dest="overrides", action="append", default=[],
+                   metavar="KEY=JSON",
+                   help="Override a model kwarg in every step, e.g. --set depth=18")
     return p
+
+
+def _parse_overrides(items):
+    from .config import ConfigError
+    out = {}
+    for item in items:
+        if "=" not in item:
+            raise ConfigError("--set expects KEY=VALUE, got %r" % item)
+        k, v = item.split("=", 1)
+        try:
+            out[k] = json.loads(v)
+        except json.JSONDecodeError:
+            out[k] = v
+    return out
 
 
 def _apply_batch_default(spec, batch_size: int) -> None:
@@ -145,6 +164,10 @@ def run(args) -> dict:
     if args.log_root:
         os.environ[LOG_ROOT_ENV] = args.log_root
     spec = load_pipeline(args.config_file_path)
+    if args.cpu_only:
+        spec = spec.on_cpu()
+    if args.overrides:
+        spec = spec.override_kwargs(_parse_overrides(args.overrides))
     check_gpus(spec)
     _apply_batch_default(spec, args.batch_size)
 

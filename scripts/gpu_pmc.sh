@@ -9,13 +9,18 @@ LAYER=${LAYER:-conv2.blocks.0.conv1.spatial}
 CFG=${CFG:-2}
 timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1 || true
 i=0
+OUT=${OUT:-gpurun_out/pmc}
+mkdir -p $OUT
 for set in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
            "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU" \
-           "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum" \
+           "SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE" \
+           "SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL" \
+           "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" \
            "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE" ; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/pmc/p$i -o run -- python scripts/conv_bench.py --layer $LAYER --config $CFG --reps 5 > gpurun_out/pmc/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/p$i -o run -- python scripts/conv_bench.py --layer $LAYER --config $CFG --reps 5 > $OUT/p$i.log 2>&1
   rc=$?
   echo "pass $i rc=$rc"
-  if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/p$i.log; [ $rc -eq 1 ] || exit $rc; fi
+  if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; [ $rc -eq 1 ] || exit $rc; fi
 done
+python scripts/pmc_summary.py $OUT

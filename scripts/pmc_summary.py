@@ -26,3 +26,9 @@ if "SQ_WAVE_CYCLES" in vals:
     for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
         if k in vals:
             print("%s / WAVE_CYCLES = %.2f" % (k, vals[k] / w))
+if "SQ_VALU_MFMA_BUSY_CYCLES" in vals and "GRBM_GUI_ACTIVE" in vals:
+    # busy cycles are summed over SIMDs; 256 CUs x 4 SIMDs
+    print("MFMA busy / (GUI_ACTIVE x 1024 SIMDs) = %.2f"
+          % (vals["SQ_VALU_MFMA_BUSY_CYCLES"] / (vals["GRBM_GUI_ACTIVE"] * 1024.0)))
+if "SQ_WAIT_INST_LDS" in vals and "SQ_WAVE_CYCLES" in vals:
+    print("SQ_WAIT_INST_LDS / WAVE_CYCLES = %.2f" % (vals["SQ_WAIT_INST_LDS"] / vals["SQ_WAVE_CYCLES"]))

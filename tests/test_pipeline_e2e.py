@@ -148,3 +148,22 @@ def test_malformed_config_clean_error(tmp_path):
         {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [-1], "in_queue": 3}]}]}
     proc, res, _ = run_cfg(tmp_path, cfg, "-v", "2")
     assert proc.returncode == 2 and "do not match" in proc.stdout
+
+
+SHIPPED_MULTI_GPU = ["r2p1d-aggressive.json", "r2p1d-aggressive-global.json",
+                     "r2p1d-aggressive-four-groups.json", "r2p1d-segment-4gpu.json",
+                     "rnb.json", "baseline.json", "r2p1d-two-stage.json",
+                     "r2p1d-layer-split.json"]
+
+
+@pytest.mark.parametrize("name", SHIPPED_MULTI_GPU)
+def test_shipped_multi_gpu_topology_on_cpu(tmp_path, name):
+    """Every shipped multi-GPU topology runs end to end with replicas on the CPU."""
+    cfg = json.loads(open(os.path.join(ROOT, "configs", name)).read())
+    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "8", "-mi", "0", "--cpu-only",
+                           "--set", "depth=10", "--set", "num_clips_population=[1,3]",
+                           "--set", "num_clips_weights=[2,1]", "--set", "warmup=0",
+                           timeout=400)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert res["termination_flag"] == "TARGET_NUM_VIDEOS_REACHED"
+    assert res["videos_done"] >= 8
