@@ -166,11 +166,13 @@ void conv_halo_kernel(const HaloParams p) {
     }
   };
 
-  f32x4 acc[HP][TC];
+  f32x4 acc[HP][TC];                               // starts at the (folded) bias
 #pragma unroll
-  for (int a = 0; a < HP; ++a)
+  for (int b = 0; b < TC; ++b) {
+    const f32x4 b4 = ep_bias4(p.bias, (c0 >> 4) + b, fq);
 #pragma unroll
-    for (int b = 0; b < TC; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int a = 0; a < HP; ++a) acc[a][b] = b4;
+  }
 
   const int nchunks = p.Cin >> 6;
   if (!HALO_NO_DMA) issue_w(0, 0);
@@ -218,13 +220,11 @@ void conv_halo_kernel(const HaloParams p) {
     }
   }
 
-  const int npairs = p.Cout_p >> 5;
+  const EpCtx e = ep_make(p.y, p.y_stride, p.res, p.res_stride, p.M, p.Cout_p, p.relu != 0);
 #pragma unroll
   for (int tp = 0; tp < HP; ++tp) {
     const int i = wave * 16 * HP + tp * 16 + frow;
-    if (i >= npx) continue;
-    ep_row<TC>(p.y, p.y_stride, p.res, p.res_stride, p.bias, (size_t)(p0 + i), c0 >> 4, fq,
-               npairs, p.Cout_p, p.relu != 0, acc[tp],
+    ep_row<TC>(e, i < npx, (long long)(p0 + i), c0 >> 4, fq, acc[tp],
                (HALO_EXP != 5 && HALO_EXP != 6) || p.relu == 7);
   }
 }
@@ -285,6 +285,8 @@ int rnb_halo_launch_v(const HaloParams* pp, int hp, hipStream_t stream) {
   p.n_ctiles = (p.Cout_p + 143) / 144;
   if (p.n_ctiles * 144 > p.w_rows) return -8;
   if (p.y_stride < p.Cout_p || (p.res && p.res_stride < p.Cout_p)) return -9;
+  if ((long long)p.M * p.y_stride * 2 > 0xFFFFFF00LL ||
+      (long long)p.M * (p.res ? p.res_stride : 0) * 2 > 0xFFFFFF00LL) return -11;
   void (*kern)(const HaloParams) =
       hp == 2 ? conv_halo_kernel<9, 2, HALO_MAX_PI> : conv_halo_kernel<9, 4, 12>;
   static bool attr_set[2] = {false, false};

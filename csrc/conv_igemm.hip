@@ -229,15 +229,18 @@ void conv_igemm_kernel(const ConvParams p) {
     }
   };
 
-  f32x4 acc[TP][TC];
-#pragma unroll
-  for (int a = 0; a < TP; ++a)
-#pragma unroll
-    for (int b = 0; b < TC; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int nsteps = p.K_pad / BK;
   const int frow = lane & 15;
   const int fq = lane >> 4;
+  const int gt0 = (c0 >> 4) + wc * TC;             // first physical 16-row tile of the wave
+  f32x4 acc[TP][TC];                               // starts at the (folded) bias
+#pragma unroll
+  for (int b = 0; b < TC; ++b) {
+    const f32x4 b4 = ep_bias4(p.bias, gt0 + b, fq);
+#pragma unroll
+    for (int a = 0; a < TP; ++a) acc[a][b] = b4;
+  }
+
+  const int nsteps = p.K_pad / BK;
   auto compute = [&](const char* abase) {
     const char* wbase = abase + ACT_BYTES;
 #pragma unroll
@@ -319,20 +322,19 @@ void conv_igemm_kernel(const ConvParams p) {
     }
   }
 
-  // ---- epilogue: bias (+ residual) (+ ReLU) -> bf16 (conv_epilogue.h) ----
-  const int npairs = p.Cout_p >> 5;
+  // ---- epilogue: (+ residual) (+ ReLU) -> bf16 (conv_epilogue.h) ----
+  const EpCtx e = ep_make(p.y, p.y_stride, p.res, p.res_stride,
+                          (long long)p.N * p.To * p.Ho * p.Wo, p.Cout_p, p.relu != 0);
 #pragma unroll
   for (int tp = 0; tp < TP; ++tp) {
     int m = p0 + wp * TP * 16 + tp * 16 + frow;
+    bool ok = m < p.M;
     if (p.row_mode == 1) {            // GEMM row -> output pixel index
       int n, to, ho, wo;
-      if (!decode_row(p, m, n, to, ho, wo)) continue;
-      m = ((n * p.To + to) * p.Ho + ho) * p.Wo + wo;
-    } else if (m >= p.M) {
-      continue;
+      ok = decode_row(p, m, n, to, ho, wo);
+      m = ok ? ((n * p.To + to) * p.Ho + ho) * p.Wo + wo : 0;
     }
-    ep_row<TC>(p.y, p.y_stride, p.res, p.res_stride, p.bias, (size_t)m, (c0 >> 4) + wc * TC,
-               fq, npairs, p.Cout_p, p.relu != 0, acc[tp], !CONV_NO_STORE || p.relu == 7);
+    ep_row<TC>(e, ok, m, gt0, fq, acc[tp], !CONV_NO_STORE || p.relu == 7);
   }
 }
 
@@ -426,6 +428,7 @@ int rnb_conv_launch(const ConvParams* pp, int config_id, hipStream_t stream) {
   if (p.K_total > p.K_pad) return -3;
   if (p.M <= 0) return 0;
   if (p.y_stride < p.Cout_p || (p.res && p.res_stride < p.Cout_p)) return -4;
+  if ((long long)p.N * p.To * p.Ho * p.Wo * (p.res ? p.res_stride : 0) >= (1LL << 31)) return -6;
   if ((long long)p.N * p.T * p.H * p.W * p.Cin_p * 2 > 0x7FFFFF00LL) return -5;
   if ((long long)p.M * p.y_stride >= (1LL << 31)) return -6;
   p.x_bytes = (uint32_t)((long long)p.N * p.T * p.H * p.W * p.Cin_p * 2);

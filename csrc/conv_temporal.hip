@@ -83,6 +83,8 @@ void conv_temporal_kernel(const TemporalParams p) {
   const int c0 = ctile * CT * 16;
   const int npairs = p.Cout_p >> 5;
   static_assert(CT % 2 == 0, "channel tiles come in pairs");
+  const EpCtx e = ep_make(p.y, p.y_stride, p.res, p.res_stride,
+                          (long long)p.N * p.T * p.HW, p.Cout_p, p.relu != 0);
 
   // ---- weights -> LDS in A-fragment order (once per persistent block) ----
   for (int f = wave; f < NFRAG; f += WAVES) {
@@ -134,11 +136,13 @@ void conv_temporal_kernel(const TemporalParams p) {
   const char* wl = smem + lane * 16;
 
   for (; g < p.ngroups; g += gstride) {
-    f32x4 acc[T][CT];
+    f32x4 acc[T][CT];                              // starts at the (folded) bias
 #pragma unroll
-    for (int t = 0; t < T; ++t)
+    for (int ct = 0; ct < CT; ++ct) {
+      const f32x4 b4 = ep_bias4(p.bias, (c0 >> 4) + ct, fq);
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) acc[t][ct] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < T; ++t) acc[t][ct] = b4;
+    }
 
     const int gn = g + gstride;
     int nn, nhw;
@@ -176,46 +180,54 @@ void conv_temporal_kernel(const TemporalParams p) {
       }
     }
 
-    // ---- epilogue: bias (+ residual) (+ ReLU) -> bf16 (conv_epilogue.h
-    // channel pairs: CT is even and tiles start even, so a pair never
-    // straddles waves); the residual of frame t+1 is in flight while frame
-    // t is written ----
-    if (hw < p.HW) {
+    // ---- epilogue: (+ residual) (+ ReLU) -> bf16 (conv_epilogue.h channel
+    // pairs: CT is even and tiles start even, so a pair never straddles
+    // waves); the residual of frame t+1 is in flight while frame t is
+    // written; padding pixels (hw >= HW) read 0 and drop their stores ----
+    {
+      const bool ok = hw < p.HW;
       const int gt0 = c0 >> 4;
+      const bool do_store = (TEMP_EXP != 5 && TEMP_EXP != 6) || p.relu == 7;
       ep_i32x4 rb[2][CT / 2];
+      auto chan = [&](int gt) { return ep_channel(gt, fq, npairs); };
       auto load_res = [&](ep_i32x4* dst, int t) {
-        const size_t m = (size_t)(n * p.T + t) * p.HW + hw;
+        const long long m = (long long)(n * p.T + t) * p.HW + hw;
 #pragma unroll
         for (int k = 0; k < CT / 2; ++k) {
           const int gt = gt0 + 2 * k;
-          if ((gt >> 1) < npairs) {
-            dst[k] = ep_load_res8(p.res, p.res_stride, m, gt, fq);
+          if (!e.has_res) {
+            dst[k] = (ep_i32x4){0, 0, 0, 0};
+          } else if ((gt >> 1) < npairs) {
+            dst[k] = __builtin_amdgcn_raw_buffer_load_b128(
+                e.res, ep_off(ok, m, e.res_stride, chan(gt)), 0, 0);
           } else {
-            const ep_i32x2 lo = ep_load_res4(p.res, p.res_stride, m, gt, fq, npairs, p.Cout_p);
-            const ep_i32x2 hi =
-                ep_load_res4(p.res, p.res_stride, m, gt + 1, fq, npairs, p.Cout_p);
+            const int c0_ = chan(gt), c1_ = chan(gt + 1);
+            const ep_i32x2 lo = __builtin_amdgcn_raw_buffer_load_b64(
+                e.res, ep_off(ok && c0_ < p.Cout_p, m, e.res_stride, c0_), 0, 0);
+            const ep_i32x2 hi = __builtin_amdgcn_raw_buffer_load_b64(
+                e.res, ep_off(ok && c1_ < p.Cout_p, m, e.res_stride, c1_), 0, 0);
             dst[k] = (ep_i32x4){lo[0], lo[1], hi[0], hi[1]};
           }
         }
       };
-      const bool do_store = (TEMP_EXP != 5 && TEMP_EXP != 6) || p.relu == 7;
       load_res(rb[0], 0);
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         if (t + 1 < T) load_res(rb[(t + 1) & 1], t + 1);
-        const size_t m = (size_t)(n * p.T + t) * p.HW + hw;
+        const long long m = (long long)(n * p.T + t) * p.HW + hw;
 #pragma unroll
         for (int k = 0; k < CT / 2; ++k) {
           const int gt = gt0 + 2 * k;
           const ep_i32x4 r = rb[t & 1][k];
           if ((gt >> 1) < npairs) {
-            ep_store8r(p.y, p.y_stride, p.bias, m, gt, fq, p.relu != 0, acc[t][2 * k],
-                       acc[t][2 * k + 1], r, do_store);
+            ep_out8(e, ep_off(ok, m, e.y_stride, chan(gt)), acc[t][2 * k], acc[t][2 * k + 1],
+                    r, do_store);
           } else {
-            ep_store4r(p.y, p.y_stride, p.bias, m, gt, fq, npairs, p.Cout_p, p.relu != 0,
-                       acc[t][2 * k], (ep_i32x2){r[0], r[1]}, do_store);
-            ep_store4r(p.y, p.y_stride, p.bias, m, gt + 1, fq, npairs, p.Cout_p, p.relu != 0,
-                       acc[t][2 * k + 1], (ep_i32x2){r[2], r[3]}, do_store);
+            const int c0_ = chan(gt), c1_ = chan(gt + 1);
+            ep_out4(e, ep_off(ok && c0_ < p.Cout_p, m, e.y_stride, c0_), acc[t][2 * k],
+                    (ep_i32x2){r[0], r[1]}, do_store);
+            ep_out4(e, ep_off(ok && c1_ < p.Cout_p, m, e.y_stride, c1_), acc[t][2 * k + 1],
+                    (ep_i32x2){r[2], r[3]}, do_store);
           }
         }
       }
@@ -283,6 +295,8 @@ int rnb_temporal_launch(const TemporalParams* pp, int num_cus, int blocks_per_cu
   if (p.N <= 0 || p.HW <= 0) return 0;
   if ((long long)p.N * p.T * p.HW * p.Cin_p * 2 > 0x7FFFFF00LL) return -5;
   if (p.y_stride < p.Cout_p || (p.res && p.res_stride < p.Cout_p)) return -4;
+  if ((long long)p.N * p.T * p.HW * p.y_stride * 2 > 0xFFFFFF00LL ||
+      (long long)p.N * p.T * p.HW * (p.res ? p.res_stride : 0) * 2 > 0xFFFFFF00LL) return -7;
   p.gpc = (p.HW + 15) / 16;
   p.ngroups = p.N * p.gpc;
   p.n_ctiles = (p.Cout_p + v.ct * 16 - 1) / (v.ct * 16);

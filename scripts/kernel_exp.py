@@ -5,7 +5,8 @@
 
 Variant n of librnb_kernels is built with -DHALO_EXP=n -DCONV_EXP=n
 (csrc/conv_halo.hip / conv_igemm.hip): 1 no MFMA, 2 no weight DMA, 3 no
-per-step wait + barrier, 4 no DMA at all. Results of variants 1-4 are
+per-step wait + barrier, 4 no DMA at all, 5 no stores, 6 = 4 + 5. Results of
+variants 1-6 are
 garbage by design; only their time matters. Variants are loaded with
 ctypes under distinct paths (RTLD_LOCAL), sharing the product ConvLayer
 parameter setup.
