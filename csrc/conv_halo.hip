@@ -33,15 +33,15 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 
 // Bottleneck experiments (scripts/kernel_exp.py builds variants; 0 = product):
 // 1 no MFMA, 2 no per-tap weight DMA, 3 no per-tap wait/barrier, 4 no DMA at all,
-// 5 no epilogue stores, 6 = 4 + 5
+// 5 no epilogue stores, 6 = 4 + 5, 8 = 6 with fragments read from LDS once
 #ifndef HALO_EXP
 #define HALO_EXP 0
 #endif
-#define HALO_NO_DMA (HALO_EXP == 4 || HALO_EXP == 6)
+#define HALO_NO_DMA (HALO_EXP == 4 || HALO_EXP == 6 || HALO_EXP == 8)
 
 #define HALO_INVALID 0xFFFFFFF0u
 #define HALO_MAX_PI 8           // patch DMA instructions per wave
-#define HALO_MAX_PX 224         // output pixels per tile (7 waves x 32)
+
 
 struct HaloParams {
   const uint16_t* x;   // NDHWC input, Cin channels (multiple of 64)
@@ -73,8 +73,8 @@ static __device__ __forceinline__ int hdiv(int n, uint32_t m, uint32_t s) {
 // HP = 16-pixel MFMA sub-tiles per wave (2: up to 7 waves x 32 px; 4: up to
 // 4 waves x 64 px -- fewer LDS reads per MFMA, 13 instead of 11 fragment reads
 // per 36 instead of 18 MFMAs); PI = patch DMA instructions per wave.
-template <int TC, int HP, int PI>
-__global__ __launch_bounds__(HP == 2 ? 448 : 256, 2)
+template <int TC, int HP, int PI, int MAXT>
+__global__ __launch_bounds__(MAXT, 2)
 void conv_halo_kernel(const HaloParams p) {
   constexpr int C_TILE = TC * 16;
   constexpr int W_INSTR_TOTAL = C_TILE / 8;            // weight DMA instructions / step
@@ -174,6 +174,15 @@ void conv_halo_kernel(const HaloParams p) {
     for (int a = 0; a < HP; ++a) acc[a][b] = b4;
   }
 
+  bf16x8 wkeep[HALO_EXP == 8 ? TC : 1], akeep[HALO_EXP == 8 ? HP : 1];
+  if (HALO_EXP == 8) {
+#pragma unroll
+    for (int i = 0; i < (HALO_EXP == 8 ? TC : 1); ++i)
+      wkeep[i] = *(const bf16x8*)(smem + ((i * 16 + frow) * 128) + fq * 16);
+#pragma unroll
+    for (int i = 0; i < (HALO_EXP == 8 ? HP : 1); ++i)
+      akeep[i] = *(const bf16x8*)(smem + 8192 + ((i * 16 + frow) * 128) + fq * 16);
+  }
   const int nchunks = p.Cin >> 6;
   if (!HALO_NO_DMA) issue_w(0, 0);
   for (int chunk = 0; chunk < nchunks; ++chunk) {
@@ -191,15 +200,22 @@ void conv_halo_kernel(const HaloParams p) {
       for (int kk = 0; kk < 2; ++kk) {
         const int ch = kk * 4 + fq;
         bf16x8 af[HP], wf[TC];
+        if (HALO_EXP == 8) {        // MFMA + barriers only: operands stay in registers
 #pragma unroll
-        for (int tc = 0; tc < TC; ++tc) {
-          const int row = tc * 16 + frow;
-          wf[tc] = *(const bf16x8*)(wb + row * 128 + ((ch ^ (row & 7)) << 4));
-        }
+          for (int tc = 0; tc < TC; ++tc) wf[tc] = wkeep[tc];
 #pragma unroll
-        for (int tp = 0; tp < HP; ++tp) {
-          const int row = center[tp] + shift;
-          af[tp] = *(const bf16x8*)(pbuf + row * 128 + ((ch ^ (row & 7)) << 4));
+          for (int tp = 0; tp < HP; ++tp) af[tp] = akeep[tp];
+        } else {
+#pragma unroll
+          for (int tc = 0; tc < TC; ++tc) {
+            const int row = tc * 16 + frow;
+            wf[tc] = *(const bf16x8*)(wb + row * 128 + ((ch ^ (row & 7)) << 4));
+          }
+#pragma unroll
+          for (int tp = 0; tp < HP; ++tp) {
+            const int row = center[tp] + shift;
+            af[tp] = *(const bf16x8*)(pbuf + row * 128 + ((ch ^ (row & 7)) << 4));
+          }
         }
 #pragma unroll
         for (int tp = 0; tp < HP; ++tp)
@@ -225,7 +241,7 @@ void conv_halo_kernel(const HaloParams p) {
   for (int tp = 0; tp < HP; ++tp) {
     const int i = wave * 16 * HP + tp * 16 + frow;
     ep_row<TC>(e, i < npx, (long long)(p0 + i), c0 >> 4, fq, acc[tp],
-               (HALO_EXP != 5 && HALO_EXP != 6) || p.relu == 7);
+               (HALO_EXP != 5 && HALO_EXP != 6 && HALO_EXP != 8) || p.relu == 7);
   }
 }
 
@@ -238,24 +254,42 @@ static void halo_magic(uint32_t d, uint32_t* m, uint32_t* s) {
   *s = (uint32_t)(p - 32);
 }
 
-static int halo_rows(int H, int W) {
-  int R = HALO_MAX_PX / W;
+// Variants: pixel sub-tiles per wave, pixels per tile, patch DMA
+// instructions per wave, kernel. v = 2: 7 waves x 32 px (2 blocks/CU);
+// v = 4: 4 waves x 64 px (2 blocks/CU, 12.5 % idle slots at W = 56);
+// v = 5: 7 waves x 64 px over 448-pixel tiles (1 block/CU, no idle slots at
+// W = 56, 1.25x instead of 1.5x patch overfetch, half the weight traffic).
+struct HaloVariant {
+  int hp, max_px, pi;
+  void (*kernel)(const HaloParams);
+};
+static const HaloVariant kHalo[] = {
+    {2, 224, HALO_MAX_PI, conv_halo_kernel<9, 2, HALO_MAX_PI, 448>},
+    {4, 224, 12, conv_halo_kernel<9, 4, 12, 256>},
+    {4, 448, 12, conv_halo_kernel<9, 4, 12, 448>},
+};
+static const HaloVariant* halo_variant(int v) {
+  return v == 2 ? &kHalo[0] : v == 4 ? &kHalo[1] : v == 5 ? &kHalo[2] : nullptr;
+}
+
+static int halo_rows(int H, int W, int max_px) {
+  int R = max_px / W;
   return R < 1 ? 0 : (R > H ? H : R);
 }
+static int halo_waves(int R, int W, int hp) { return (R * W + 16 * hp - 1) / (16 * hp); }
 
 extern "C" {
 
 int rnb_halo_params_size() { return (int)sizeof(HaloParams); }
 
-static int halo_max_pi(int hp) { return hp == 2 ? HALO_MAX_PI : 12; }
-static int halo_waves(int R, int W, int hp) { return (R * W + 16 * hp - 1) / (16 * hp); }
-
-// LDS bytes a launch on this shape requests (-1: shape not supported).
-int rnb_halo_lds_bytes_v(int frames, int H, int W, int Cin, int hp) {
-  const int R = halo_rows(H, W);
-  if (R == 0 || Cin % 64 != 0 || (hp != 2 && hp != 4)) return -1;
+// LDS bytes a launch of variant v on this shape requests (-1: not supported).
+int rnb_halo_lds_bytes_v(int frames, int H, int W, int Cin, int v) {
+  const HaloVariant* hv = halo_variant(v);
+  if (!hv) return -1;
+  const int R = halo_rows(H, W, hv->max_px);
+  if (R == 0 || Cin % 64 != 0) return -1;
   const int np = (R + 2) * (W + 2);
-  if ((np + 7) / 8 > halo_waves(R, W, hp) * halo_max_pi(hp)) return -1;
+  if ((np + 7) / 8 > halo_waves(R, W, hv->hp) * hv->pi) return -1;
   (void)frames;
   return ((np + 7) & ~7) * 128 + 2 * 144 * 128;
 }
@@ -264,20 +298,21 @@ int rnb_halo_lds_bytes(int frames, int H, int W, int Cin) {
   return rnb_halo_lds_bytes_v(frames, H, W, Cin, 2);
 }
 
-int rnb_halo_launch_v(const HaloParams* pp, int hp, hipStream_t stream) {
+int rnb_halo_launch_v(const HaloParams* pp, int v, hipStream_t stream) {
   HaloParams p = *pp;
-  if (hp != 2 && hp != 4) return -10;
+  const HaloVariant* hv = halo_variant(v);
+  if (!hv) return -10;
   if (p.Cin % 64 != 0 || p.K_pad != 9 * p.Cin || p.Cout_p % 4 != 0) return -2;
   if (p.M <= 0) return 0;
   if ((long long)p.M * p.Cin * 2 > 0x7FFFFF00LL) return -5;
-  p.R = halo_rows(p.H, p.W);
+  p.R = halo_rows(p.H, p.W, hv->max_px);
   if (p.R == 0) return -3;
   p.bands = (p.H + p.R - 1) / p.R;
   p.np = (p.R + 2) * (p.W + 2);
-  const int lds = rnb_halo_lds_bytes_v(p.frames, p.H, p.W, p.Cin, hp);
+  const int lds = rnb_halo_lds_bytes_v(p.frames, p.H, p.W, p.Cin, v);
   if (lds < 0 || lds > 160 * 1024) return -6;
-  const int waves = halo_waves(p.R, p.W, hp);
-  if ((p.np + 7) / 8 > waves * halo_max_pi(hp)) return -4;
+  const int waves = halo_waves(p.R, p.W, hv->hp);
+  if ((p.np + 7) / 8 > waves * hv->pi) return -4;
   p.x_bytes = (uint32_t)((long long)p.M * p.Cin * 2);
   halo_magic((uint32_t)p.bands, &p.mB, &p.sB);
   halo_magic((uint32_t)p.W, &p.mW, &p.sW);
@@ -287,16 +322,15 @@ int rnb_halo_launch_v(const HaloParams* pp, int hp, hipStream_t stream) {
   if (p.y_stride < p.Cout_p || (p.res && p.res_stride < p.Cout_p)) return -9;
   if ((long long)p.M * p.y_stride * 2 > 0xFFFFFF00LL ||
       (long long)p.M * (p.res ? p.res_stride : 0) * 2 > 0xFFFFFF00LL) return -11;
-  void (*kern)(const HaloParams) =
-      hp == 2 ? conv_halo_kernel<9, 2, HALO_MAX_PI> : conv_halo_kernel<9, 4, 12>;
-  static bool attr_set[2] = {false, false};
-  if (!attr_set[hp == 4]) {
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+  static bool attr_set[3] = {false, false, false};
+  const int vi = (int)(hv - kHalo);
+  if (!attr_set[vi]) {
+    hipFuncSetAttribute((const void*)hv->kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                         160 * 1024);
-    attr_set[hp == 4] = true;
+    attr_set[vi] = true;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)(p.n_ptiles * p.n_ctiles)), dim3(64 * waves), lds,
-                     stream, p);
+  hipLaunchKernelGGL(hv->kernel, dim3((unsigned)(p.n_ptiles * p.n_ctiles)), dim3(64 * waves),
+                     lds, stream, p);
   return (int)hipGetLastError();
 }
 

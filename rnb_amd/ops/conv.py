@@ -28,7 +28,9 @@ W_ROW_SLACK = 256   # extra zero weight rows (>= largest channel tile)
 HALO = 100          # config id of the halo-tiled 1x3x3 stride-1 kernel (conv_halo.hip)
 TEMPORAL = 101      # config id of the register-direct 3x1x1 kernel (conv_temporal.hip)
 HALO4 = 102         # halo kernel with 64-pixel waves (4 MFMA pixel sub-tiles per wave)
-SPECIAL_NAMES = {HALO: "halo", TEMPORAL: "temporal", HALO4: "halo4"}
+HALO4B = 103        # 64-pixel waves over 448-pixel tiles (7 waves, 1 block per CU)
+SPECIAL_NAMES = {HALO: "halo", TEMPORAL: "temporal", HALO4: "halo4", HALO4B: "halo4b"}
+HALO_VARIANT = {HALO: 2, HALO4: 4, HALO4B: 5}     # variant id of rnb_halo_launch_v
 LDS_LIMIT = 160 * 1024
 
 
@@ -250,8 +252,10 @@ class ConvLayer:
             out.append(HALO)
             from .native import kernels
             N, T, H, W, _ = x_shape
-            if 0 < kernels().halo_lds_bytes(N * T, H, W, self.geom.cin_p, 4) <= LDS_LIMIT:
-                out.append(HALO4)
+            for cid in (HALO4, HALO4B):
+                v = HALO_VARIANT[cid]
+                if 0 < kernels().halo_lds_bytes(N * T, H, W, self.geom.cin_p, v) <= LDS_LIMIT:
+                    out.append(cid)
         if self.temporal_eligible(x_shape):
             out.append(TEMPORAL)
         return out
@@ -344,9 +348,9 @@ class ConvLayer:
 
     def _launch(self, p, cid, x, y, residual, stream):
         from .native import kernels
-        if cid in (HALO, HALO4):
+        if cid in HALO_VARIANT:
             kernels().halo(self.halo_params(x, y, residual), stream.cuda_stream,
-                           hp=4 if cid == HALO4 else 2)
+                           variant=HALO_VARIANT[cid])
         elif cid == TEMPORAL:
             kernels().temporal(self.temporal_params(x, y, residual), num_cus(x.device), 0,
                                stream.cuda_stream)

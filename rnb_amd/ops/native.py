@@ -205,9 +205,10 @@ class Kernels:
         _check(self.lib.rnb_conv_launch(ctypes.byref(params), config_id, stream),
                "conv (config %d)" % config_id)
 
-    def halo(self, params: HaloParams, stream: int, hp: int = 2) -> None:
-        """hp: 16-pixel MFMA sub-tiles per wave (2 or 4)."""
-        _check(self.lib.rnb_halo_launch_v(ctypes.byref(params), hp, stream), "conv_halo")
+    def halo(self, params: HaloParams, stream: int, variant: int = 2) -> None:
+        """variant (csrc/conv_halo.hip kHalo): 2 = 32-pixel waves, 4 = 64-pixel
+        waves, 5 = 64-pixel waves over 448-pixel tiles."""
+        _check(self.lib.rnb_halo_launch_v(ctypes.byref(params), variant, stream), "conv_halo")
 
     def temporal(self, params: TemporalParams, num_cus: int, blocks_per_cu: int,
                  stream: int) -> None:
@@ -217,8 +218,8 @@ class Kernels:
     def temporal_lds_bytes(self, T: int, cin_p: int, cout_p: int) -> int:
         return self.lib.rnb_temporal_lds_bytes(T, cin_p, cout_p)
 
-    def halo_lds_bytes(self, frames: int, H: int, W: int, cin: int, hp: int = 2) -> int:
-        return self.lib.rnb_halo_lds_bytes_v(frames, H, W, cin, hp)
+    def halo_lds_bytes(self, frames: int, H: int, W: int, cin: int, variant: int = 2) -> int:
+        return self.lib.rnb_halo_lds_bytes_v(frames, H, W, cin, variant)
 
     def bn_scratch_floats(self, M: int, C: int) -> int:
         return self.lib.rnb_bn_scratch_floats(M, C)

@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 EXP_DIR = os.path.join(ROOT, "rnb_amd", "_native", "exp")
 VARIANTS = {0: "product", 1: "no-mfma", 2: "no-wdma", 3: "no-sync", 4: "no-dma",
-            5: "no-store", 6: "mfma-only"}
+            5: "no-store", 6: "mfma-only", 8: "mfma+sync"}
 
 
 def build():
@@ -47,7 +47,7 @@ def run(args):
     from rnb_amd.models.r2p1d.model import build_network
     from rnb_amd.models.r2p1d.engine import R2P1DEngine
     from rnb_amd.ops.native import ConvParams, HaloParams, TemporalParams
-    from rnb_amd.ops.conv import HALO, HALO4, TEMPORAL, num_cus
+    from rnb_amd.ops.conv import HALO_VARIANT, SPECIAL_NAMES, TEMPORAL, num_cus
     libs = {}
     for v in VARIANTS:
         lib = ctypes.CDLL(os.path.join(EXP_DIR, "libexp%d.so" % v))
@@ -76,10 +76,10 @@ def run(args):
             for cfg in cfgs:
                 times = []
                 for v, lib in libs.items():
-                    if cfg in (HALO, HALO4):
+                    if cfg in HALO_VARIANT:
                         p = op.layer.halo_params(src, y, res)
-                        hp = 4 if cfg == HALO4 else 2
-                        launch = lambda: lib.rnb_halo_launch_v(ctypes.byref(p), hp,
+                        hv = HALO_VARIANT[cfg]
+                        launch = lambda: lib.rnb_halo_launch_v(ctypes.byref(p), hv,
                                                                stream.cuda_stream)
                     elif cfg == TEMPORAL:
                         p = op.layer.temporal_params(src, y, res)
@@ -100,8 +100,7 @@ def run(args):
                     e.record()
                     e.synchronize()
                     times.append(s.elapsed_time(e) / args.reps * 1e3)
-                print("%-32s %-8s " % (op.layer.name[-32:], {HALO: "halo", HALO4: "halo4", TEMPORAL: "temp"}
-                                       .get(cfg, cfg))
+                print("%-32s %-8s " % (op.layer.name[-32:], SPECIAL_NAMES.get(cfg, cfg))
                       + " ".join("%7.1fus" % t for t in times), flush=True)
         bufs[op.dst] = y
 

@@ -174,14 +174,14 @@ def test_time_major_rows_exact(thw, cin, cout, stride):
     (1, (1, 9, 40), 192, 144),      # 3 chunks, single frame, M tail
 ])
 def test_halo_kernel_exact(n, thw, cin, cout):
-    from rnb_amd.ops.conv import HALO, HALO4
+    from rnb_amd.ops.conv import HALO, HALO_VARIANT
     layer = _layer(cin, cout, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=True, integer=True)
     x = _input(n, thw, cin, cin, integer=True)
     assert layer.halo_eligible(x.shape)
     res_shape = layer.out_shape(x.shape)
     res = _input(res_shape[0], res_shape[1:4], res_shape[4], cout, integer=True, seed=3)
     ref = layer.forward_torch(x, residual=res, out_dtype=torch.bfloat16)
-    variants = [c for c in layer.special_candidates(x.shape) if c in (HALO, HALO4)]
+    variants = [c for c in layer.special_candidates(x.shape) if c in HALO_VARIANT]
     assert HALO in variants
     for cid in variants:
         y = layer.forward_hip(x, residual=res, config=cid)
