@@ -66,7 +66,7 @@ static __device__ __forceinline__ int tdiv(int n, uint32_t m, uint32_t s) {
   return m ? (int)(__umulhi((uint32_t)n, m) >> s) : n;
 }
 
-template <int T, int NCH, int CT, int WAVES>
+template <int T, int NCH, int CT, int WAVES, int FP>
 __global__ __launch_bounds__(WAVES * 64, 2)
 void conv_temporal_kernel(const TemporalParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [3][NCH][CT][64][16 B]
@@ -127,12 +127,19 @@ void conv_temporal_kernel(const TemporalParams p) {
       dst[ch] = __builtin_bit_cast(bf16x8, v);
     }
   };
+  // FP frames per step: each weight fragment read from LDS feeds FP MFMAs
+  constexpr int NS = T / FP;
+  static_assert(T % FP == 0, "frames per step");
+  auto load_step = [&](bf16x8 (*dst)[NCH], uint32_t base, int t0) {
+#pragma unroll
+    for (int j = 0; j < FP; ++j) load_frame(dst[j], base, t0 + j);
+  };
 
-  bf16x8 b[2][NCH];
+  bf16x8 b[2][FP][NCH];
   int g = gblk * WAVES + wave;
   int n, hw;
   uint32_t base = group_base(g, n, hw);
-  if (g < p.ngroups) load_frame(b[0], base, 0);
+  if (g < p.ngroups) load_step(b[0], base, 0);
   const char* wl = smem + lane * 16;
 
   for (; g < p.ngroups; g += gstride) {
@@ -148,33 +155,43 @@ void conv_temporal_kernel(const TemporalParams p) {
     int nn, nhw;
     const uint32_t nbase = group_base(gn, nn, nhw);
 #pragma unroll
-    for (int ti = 0; ti < T; ++ti) {
-      // opaque zero: keeps the weight-fragment reads inside this frame's
-      // step (otherwise they are hoisted / CSE'd across frames and groups
-      // as loop invariants and 60 fragments x 4 VGPRs spill)
+    for (int si = 0; si < NS; ++si) {
+      // opaque zero: keeps the weight-fragment reads inside this step
+      // (otherwise they are hoisted / CSE'd across steps and groups as loop
+      // invariants and 60 fragments x 4 VGPRs spill)
       int z;
       asm volatile("v_mov_b32 %0, 0" : "=v"(z));
       const char* wlt = wl + z;
-      if (ti + 1 < T) {
-        load_frame(b[(ti + 1) & 1], base, ti + 1);
-      } else if ((T & 1) == 0 && gn < p.ngroups) {
-        load_frame(b[0], nbase, 0);                  // next group's first frame
+      if (si + 1 < NS) {
+        load_step(b[(si + 1) & 1], base, (si + 1) * FP);
+      } else if ((NS & 1) == 0 && gn < p.ngroups) {
+        load_step(b[0], nbase, 0);                   // next group's first frames
       }
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
 #pragma unroll
         for (int dt = 0; dt < 3; ++dt) {
-          const int to = ti - dt + 1;
-          if (to < 0 || to >= T) continue;
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct) {
+            bool any = false;
+#pragma unroll
+            for (int j = 0; j < FP; ++j) {
+              const int to = si * FP + j - dt + 1;
+              any |= (to >= 0 && to < T);
+            }
+            if (!any) continue;
             const bf16x8 wf =
                 *(const bf16x8*)(wlt + (size_t)((dt * NCH + ch) * CT + ct) * 1024);
-            if (TEMP_EXP == 1)
-              acc[to][ct][0] += __builtin_bit_cast(float, (int)(wf[0] ^ b[ti & 1][ch][1]));
-            else
-              acc[to][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, b[ti & 1][ch],
-                                                                    acc[to][ct], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < FP; ++j) {
+              const int to = si * FP + j - dt + 1;
+              if (to < 0 || to >= T) continue;
+              if (TEMP_EXP == 1)
+                acc[to][ct][0] += __builtin_bit_cast(float, (int)(wf[0] ^ b[si & 1][j][ch][1]));
+              else
+                acc[to][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, b[si & 1][j][ch],
+                                                                      acc[to][ct], 0, 0, 0);
+            }
           }
         }
       }
@@ -232,7 +249,7 @@ void conv_temporal_kernel(const TemporalParams p) {
         }
       }
     }
-    if ((T & 1) != 0 && gn < p.ngroups) load_frame(b[0], nbase, 0);
+    if ((NS & 1) != 0 && gn < p.ngroups) load_step(b[0], nbase, 0);
     base = nbase;
     n = nn;
     hw = nhw;
@@ -253,13 +270,14 @@ struct TemporalVariant {
   void (*kernel)(const TemporalParams);
 };
 
-#define TV(T, NCH, CT, WV) {T, NCH, CT, WV, conv_temporal_kernel<T, NCH, CT, WV>}
-// (T, 32-channel chunks, 16-channel output tiles per block, waves per block)
+#define TV(T, NCH, CT, WV, FP) {T, NCH, CT, WV, conv_temporal_kernel<T, NCH, CT, WV, FP>}
+// (T, 32-channel chunks, 16-channel output tiles per block, waves per block,
+//  frames per step)
 static const TemporalVariant kTemporal[] = {
-    TV(8, 3, 4, 4),    // R(2+1)D stem temporal: 83 (88) -> 64, 8 frames
-    TV(8, 5, 4, 4),    // conv2: 144 -> 64, 8 frames
-    TV(4, 9, 4, 8),    // conv3: 288 -> 128, 4 frames (2 channel tiles)
-    TV(2, 18, 2, 8),   // conv4: 576 -> 256, 2 frames (8 channel tiles)
+    TV(8, 3, 4, 4, 2),    // R(2+1)D stem temporal: 83 (88) -> 64, 8 frames
+    TV(8, 5, 4, 4, 2),    // conv2: 144 -> 64, 8 frames
+    TV(4, 9, 4, 8, 2),    // conv3: 288 -> 128, 4 frames (2 channel tiles)
+    TV(2, 18, 2, 8, 2),   // conv4: 576 -> 256, 2 frames (8 channel tiles)
 };
 static const int kNumTemporal = sizeof(kTemporal) / sizeof(kTemporal[0]);
 
