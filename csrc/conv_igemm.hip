@@ -270,18 +270,41 @@ void conv_igemm_kernel(const ConvParams p) {
     }
   };
 
+  // K-step range. For a (KT x 1 x 1) conv whose tile lies inside one clip,
+  // a temporal tap that reads only padding for every row of the tile adds
+  // zeros: its K-steps (k = dt * Cin_p + c) are skipped, e.g. a third of the
+  // MACs of the tiles in a clip's first / last frame, all tiles at T = 2.
+  int s_begin = 0, s_end = nsteps;
+  if (p.KH == 1 && p.KW == 1 && p.KT > 1 && p.row_mode == 0) {
+    int n0, t0, n1, t1, hh, ww;
+    decode_row(p, p0, n0, t0, hh, ww);
+    decode_row(p, min(p0 + P_TILE, p.M) - 1, n1, t1, hh, ww);
+    n0 = __builtin_amdgcn_readfirstlane(n0);
+    n1 = __builtin_amdgcn_readfirstlane(n1);
+    t0 = __builtin_amdgcn_readfirstlane(t0);
+    t1 = __builtin_amdgcn_readfirstlane(t1);
+    if (n0 == n1) {
+      const int dt_lo = max(0, p.PT - t1 * p.ST);
+      const int dt_hi = min(p.KT - 1, p.T - 1 + p.PT - t0 * p.ST);
+      if (dt_hi >= dt_lo) {
+        s_begin = (dt_lo * p.Cin_p) / BK;
+        s_end = min(nsteps, ((dt_hi + 1) * p.Cin_p + BK - 1) / BK);
+      }
+    }
+  }
+
   if constexpr (NS == 2) {
     const int2* ktab = p.ktab + kc;
-    int2 e_next = ktab[0];
-    issue(0, 0, e_next);
-    if (nsteps > 1) e_next = ktab[8];
+    int2 e_next = ktab[s_begin * 8];
+    issue(s_begin, 0, e_next);
+    if (s_begin + 1 < s_end) e_next = ktab[(s_begin + 1) * 8];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int s = 0; s < nsteps; ++s) {
-      const int cur = s & 1;
-      if (s + 1 < nsteps) {
+    for (int s = s_begin; s < s_end; ++s) {
+      const int cur = (s - s_begin) & 1;
+      if (s + 1 < s_end) {
         issue(s + 1, cur ^ 1, e_next);
-        if (s + 2 < nsteps) e_next = ktab[(s + 2) * 8];
+        if (s + 2 < s_end) e_next = ktab[(s + 2) * 8];
       }
       compute(lds + cur * BUF_BYTES);
       if (CONV_EXP != 3) {
@@ -300,12 +323,12 @@ void conv_igemm_kernel(const ConvParams p) {
     constexpr int PER_STEP_HI = A_INSTR + W_INSTR;
     constexpr int PER_STEP_LO = A_INSTR + W_INSTR - 1;
     const bool hi = wave < W_LAST;
-    issue(0, 0, ktab_l[kc]);
-    if (nsteps > 1) issue(1, 1, ktab_l[8 + kc]);
+    issue(s_begin, 0, ktab_l[s_begin * 8 + kc]);
+    if (s_begin + 1 < s_end) issue(s_begin + 1, 1, ktab_l[(s_begin + 1) * 8 + kc]);
     int cur = 0;
-    for (int s = 0; s < nsteps; ++s) {
+    for (int s = s_begin; s < s_end; ++s) {
       // retire this wave's DMA of step s (step s+1 may stay in flight)
-      if (s + 1 < nsteps) {
+      if (s + 1 < s_end) {
         if (hi) wait_vmcnt<PER_STEP_HI>(); else wait_vmcnt<PER_STEP_LO>();
       } else {
         wait_vmcnt<0>();
@@ -313,8 +336,8 @@ void conv_igemm_kernel(const ConvParams p) {
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (s + 2 < nsteps) {
-        const int nb = cur == 0 ? 2 : cur - 1;       // (s + 2) % 3
+      if (s + 2 < s_end) {
+        const int nb = cur == 0 ? 2 : cur - 1;       // (s + 2 - s_begin) % 3
         issue(s + 2, nb, ktab_l[(s + 2) * 8 + kc]);
       }
       compute(lds + cur * BUF_BYTES);

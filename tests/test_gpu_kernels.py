@@ -278,3 +278,17 @@ def test_batchnorm_batch_stats_kernel(shape, c, res, relu):
     assert torch.allclose(op_h.var[:c], op_t.var[:c], atol=1e-3, rtol=1e-3)
     assert (out.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
     assert torch.allclose(op_h.running_var, op_t.running_var, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("thw,cin,stride", [((2, 14, 14), 96, 1), ((4, 7, 9), 72, 1),
+                                            ((8, 5, 6), 64, 2), ((3, 11, 13), 40, 1)])
+def test_temporal_tap_skipping_every_config(thw, cin, stride):
+    """Tiles inside one clip skip K-steps of temporal taps that only read padding."""
+    from rnb_amd.ops.native import kernels
+    layer = _layer(cin, 48, (3, 1, 1), (stride, 1, 1), (1, 0, 0), relu=False, integer=True)
+    x = _input(3, thw, layer.geom.cin_p, cin, integer=True)
+    ref = layer.forward_torch(x, out_dtype=torch.bfloat16)
+    for cfg in range(len(kernels().configs)):
+        y = layer.forward_hip(x, config=cfg)
+        torch.cuda.synchronize()
+        assert torch.equal(y, ref), (cfg, (y.float() - ref.float()).abs().max().item())
