@@ -51,9 +51,10 @@ class TerminationFlag:
 
 
 # (group_idx, instance_idx, tensor_idx) like control.py:209; ``ring`` carries
-# the producer ring's import descriptor (HIP IPC handles) for GPU transports.
-Signal = namedtuple("Signal", ["group_idx", "instance_idx", "tensor_idx", "ring"],
-                    defaults=(None,))
+# the producer ring's import descriptor (HIP IPC handles) for GPU transports;
+# ``gen`` the slot's generation stamp when race checking is on (transport.py).
+Signal = namedtuple("Signal", ["group_idx", "instance_idx", "tensor_idx", "ring", "gen"],
+                    defaults=(None, None))
 
 
 def segment_bounds(batch: int, num_segments: int, segment_idx: int) -> Tuple[int, int]:

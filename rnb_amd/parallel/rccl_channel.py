@@ -141,7 +141,7 @@ class RcclRing(RingBase):
         if self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()
         self._set_valid(idx, rows)
-        self.events[idx].clear()
+        return self._publish(idx)
 
     def descriptor(self):
         return self.producer_rank
@@ -170,6 +170,15 @@ class RcclRing(RingBase):
     def release(self, idx):
         # the producer frees the slot once its send has completed
         pass
+
+    def verify(self, idx, gen, when="after pull"):
+        # the slot is released by the sender thread as soon as the send
+        # completes, i.e. possibly before the receiver returns: only the
+        # generation can be checked before the claim
+        if gen is not None and when == "before pull" and self.gen[idx] != gen:
+            from .transport import RingRaceError
+            raise RingRaceError("rccl ring %s slot %d: expected generation %d, found %d"
+                                % (self.name, idx, gen, self.gen[idx]))
 
 
 class _nullctx:

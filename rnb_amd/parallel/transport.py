@@ -23,6 +23,15 @@ Backends (chosen per edge by ``make_ring``):
 
 The RCCL send/recv channel for static 1:1 edges lives in
 ``parallel/rccl_channel.py``.
+
+Race detection (the reference has none). With
+``RNB_CHECK_RINGS=1`` every slot carries a generation stamp in shared memory.
+The producer bumps it when it publishes the slot and sends it in the
+``Signal``. The consumer verifies it around its pull (``verify``): the slot
+must still be marked full and carry the same generation after the copy.
+A slot overwritten before the consumer finished reading raises
+``RingRaceError``. One example is the reference's release-before-copy bug,
+which the ``early_release`` fault injection reproduces.
 """
 from __future__ import annotations
 
@@ -33,6 +42,11 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 SLOT_WAIT_POLL_S = 0.05
+CHECK_ENV = "RNB_CHECK_RINGS"
+
+
+class RingRaceError(RuntimeError):
+    """A slot was overwritten or released while its consumer was reading it."""
 
 
 def _nbytes(shape, dtype) -> int:
@@ -62,6 +76,9 @@ class RingBase:
         for e in self.events:
             e.set()
         self.valid = ctx.Array("i", self.num_slots * len(self.shapes), lock=False)
+        # generation stamp per slot (race detection, RNB_CHECK_RINGS=1)
+        self.gen = ctx.Array("q", self.num_slots, lock=False)
+        self.check = os.environ.get(CHECK_ENV) == "1"
 
     def __len__(self) -> int:
         return self.num_slots
@@ -78,8 +95,16 @@ class RingBase:
                 return False
         return True
 
-    def write(self, idx: int, tensors: Sequence[torch.Tensor]) -> None:
+    def write(self, idx: int, tensors: Sequence[torch.Tensor]) -> int:
+        """Fill slot ``idx`` and publish it; returns its new generation."""
         raise NotImplementedError
+
+    def _publish(self, idx: int) -> int:
+        """Mark slot ``idx`` full (after its data is complete)."""
+        self.gen[idx] += 1
+        g = self.gen[idx]
+        self.events[idx].clear()
+        return g
 
     def descriptor(self):
         return None
@@ -94,6 +119,17 @@ class RingBase:
     def read_into(self, idx: int, placeholders: Sequence[torch.Tensor],
                   descriptor=None) -> List[torch.Tensor]:
         raise NotImplementedError
+
+    def verify(self, idx: int, gen: Optional[int], when: str = "after pull") -> None:
+        """Race check: slot ``idx`` must still hold generation ``gen``, unreleased."""
+        if gen is None:
+            return
+        cur = self.gen[idx]
+        if cur != gen or self.events[idx].is_set():
+            raise RingRaceError(
+                "ring %s slot %d %s: expected generation %d, found %d (%s)"
+                % (self.name, idx, when, gen, cur,
+                   "released" if self.events[idx].is_set() else "overwritten"))
 
     def release(self, idx: int) -> None:
         self.events[idx].set()
@@ -134,7 +170,7 @@ class HostRing(RingBase):
                 dst[:b].copy_(src)     # D2H copies are synchronous here
             rows.append(b)
         self._set_valid(idx, rows)
-        self.events[idx].clear()
+        return self._publish(idx)
 
     def read_into(self, idx, placeholders, descriptor=None):
         out = []
@@ -203,7 +239,7 @@ class IpcRing(RingBase):
             rows.append(b)
         stream.synchronize()       # push completes before the slot is marked full
         self._set_valid(idx, rows)
-        self.events[idx].clear()
+        return self._publish(idx)
 
     def _open(self, desc):
         from ..ops import native

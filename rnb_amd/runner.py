@@ -191,9 +191,10 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                     slot = state["out_counter"] % len(shared_output_ring)
                     if not shared_output_ring.wait_free(slot, aborted):
                         return False
-                    shared_output_ring.write(slot, seg_tensors)
+                    gen = shared_output_ring.write(slot, seg_tensors)
                     signal_out = Signal(group_idx, instance_idx, slot,
-                                        shared_output_ring.descriptor())
+                                        shared_output_ring.descriptor(),
+                                        gen if shared_output_ring.check else None)
                     state["out_counter"] = (state["out_counter"] + 1) % len(shared_output_ring)
                 tc = time_card.fork(seg) if num_segments > 1 else time_card
                 msgs.append((signal_out, non_tensor_outputs, tc))
@@ -238,7 +239,20 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 ring = shared_input_rings[signal.group_idx][signal.instance_idx]
                 if ring.is_free(signal.tensor_idx) and aborted():
                     break
+                ring.verify(signal.tensor_idx, signal.gen, "before pull")
+                if fault == "early_release":
+                    # test hook: the reference's bug (slot released before the
+                    # pull completes, runner.py:112-117) -> the race checker
+                    # must catch the producer's overwrite
+                    ring.release(signal.tensor_idx)
+                    time.sleep(0.3)
                 tensor_inputs = ring.read_into(signal.tensor_idx, placeholders, signal.ring)
+                if fault != "early_release":
+                    ring.verify(signal.tensor_idx, signal.gen, "after pull")
+                elif signal.gen is not None and ring.gen[signal.tensor_idx] != signal.gen:
+                    from .parallel.transport import RingRaceError
+                    raise RingRaceError("ring %s slot %d overwritten during the pull"
+                                        % (ring.name, signal.tensor_idx))
                 ring.release(signal.tensor_idx)
             else:
                 tensor_inputs = None

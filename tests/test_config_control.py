@@ -168,7 +168,8 @@ def test_segmented_shapes():
 def test_termination_flag_values_match_reference():
     assert (TerminationFlag.UNSET, TerminationFlag.TARGET_NUM_VIDEOS_REACHED,
             TerminationFlag.FILENAME_QUEUE_FULL, TerminationFlag.FRAME_QUEUE_FULL) == (-1, 0, 1, 2)
-    assert Signal(1, 2, 3) == (1, 2, 3, None)
+    assert Signal(1, 2, 3) == (1, 2, 3, None, None)
+    assert Signal(1, 2, 3)[:3] == (1, 2, 3)          # reference control.py:209 triple
 
 
 def test_shared_queues_and_rings_wiring_rnb():

@@ -167,3 +167,27 @@ def test_shipped_multi_gpu_topology_on_cpu(tmp_path, name):
     assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
     assert res["termination_flag"] == "TARGET_NUM_VIDEOS_REACHED"
     assert res["videos_done"] >= 8
+
+
+def _two_stage(slots):
+    return {"video_path_iterator": IT, "defaults": SMALL, "pipeline": [
+        {"model": M + "R2P1DLoader", "queue_groups": [{"gpus": [-1], "out_queues": [0]}],
+         "num_shared_tensors": slots, "num_segments": 1},
+        {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [-1], "in_queue": 0}]}]}
+
+
+def test_ring_race_checker_clean_run(tmp_path):
+    """RNB_CHECK_RINGS=1 stamps and verifies every slot; a correct run stays clean."""
+    proc, res, _ = run_cfg(tmp_path, _two_stage(2), "-v", "8", "-mi", "0",
+                           env={"RNB_CHECK_RINGS": "1"})
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert res["ok"] and "RingRaceError" not in proc.stderr
+
+
+def test_ring_race_checker_catches_early_release(tmp_path):
+    """The reference's release-before-copy bug is detected, not silently wrong."""
+    proc, res, _ = run_cfg(tmp_path, _two_stage(1), "-v", "8", "-mi", "0",
+                           env={"RNB_CHECK_RINGS": "1", "RNB_FAULT_INJECT": "early_release"})
+    assert proc.returncode != 0
+    assert "RingRaceError" in proc.stdout + proc.stderr
+    assert res is not None and res["termination_flag"] == "CHILD_FAILED"
