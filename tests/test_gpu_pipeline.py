@@ -30,7 +30,9 @@ def test_segment_pipeline_gpu_to_cpu_aggregator(tmp_path):
          "max_clips": 5, "num_shared_tensors": 4},
         {"model": M + "R2P1DAggregator", "queue_groups": [{"gpus": [-1], "in_queue": 0}],
          "aggregate": 3}]}
-    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "30", "-mi", "0", timeout=600)
+    # race checker on: every IPC slot pull is verified against its generation
+    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "30", "-mi", "0", timeout=600,
+                           env={"RNB_CHECK_RINGS": "1"})
     assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
     assert res["ok"]
 
