@@ -7,8 +7,10 @@
 //  * rnb_preprocess      uint8 NFHWC3 -> normalised bf16 NDHWC8 (channels 3..7
 //                        zero), the fused form of the reference's
 //                        .float().permute() + slot copy.
-//  * rnb_head            AdaptiveAvgPool3d(1) + Linear(512 -> classes) fused
-//                        into one kernel, 16 clips per block.
+//  * rnb_head            AdaptiveAvgPool3d(1) + Linear(512 -> classes): a
+//                        pooling kernel (one thread per clip x channel pair)
+//                        and a linear kernel (16 clips x 64 classes per block)
+//                        (SURVEY.md K28).
 //  * rnb_video_reduce    per-video sum of clip logits + argmax, the GPU form
 //                        of R2P1DAggregator's reduction.
 #include <hip/hip_runtime.h>
@@ -74,67 +76,127 @@ static __device__ __forceinline__ uint32_t f2bf_bits(float f) {
   return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
 }
 
-// one thread per pixel: 3 bytes in, 8 bf16 (16 B) out
+// one thread per 4 pixels: 12 bytes in (three aligned dword loads), 4 x 16 B
+// out (8 bf16 per pixel, channels 3..7 zero); a tail thread goes per pixel
 __global__ void preprocess_kernel(const uint8_t* __restrict__ in, uint16_t* __restrict__ out,
                                   long long npix, NormParams np) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= npix) return;
-  const uint8_t* px = in + i * 3;
-  uint32_t r = f2bf_bits(px[0] * np.scale[0] + np.shift[0]);
-  uint32_t g = f2bf_bits(px[1] * np.scale[1] + np.shift[1]);
-  uint32_t b = f2bf_bits(px[2] * np.scale[2] + np.shift[2]);
-  *(uint4*)(out + i * 8) = make_uint4(r | (g << 16), b, 0u, 0u);
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long i0 = q * 4;
+  if (i0 >= npix) return;
+  auto emit = [&](long long i, uint32_t r8, uint32_t g8, uint32_t b8) {
+    const uint32_t r = f2bf_bits((float)r8 * np.scale[0] + np.shift[0]);
+    const uint32_t g = f2bf_bits((float)g8 * np.scale[1] + np.shift[1]);
+    const uint32_t b = f2bf_bits((float)b8 * np.scale[2] + np.shift[2]);
+    *(uint4*)(out + i * 8) = make_uint4(r | (g << 16), b, 0u, 0u);
+  };
+  if (i0 + 4 <= npix) {
+    const uint32_t* w = (const uint32_t*)(in + i0 * 3);   // 12-byte aligned groups
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    emit(i0 + 0, w0 & 255u, (w0 >> 8) & 255u, (w0 >> 16) & 255u);
+    emit(i0 + 1, w0 >> 24, w1 & 255u, (w1 >> 8) & 255u);
+    emit(i0 + 2, (w1 >> 16) & 255u, w1 >> 24, w2 & 255u);
+    emit(i0 + 3, (w2 >> 8) & 255u, (w2 >> 16) & 255u, w2 >> 24);
+  } else {
+    for (long long i = i0; i < npix; ++i) {
+      const uint8_t* px = in + i * 3;
+      emit(i, px[0], px[1], px[2]);
+    }
+  }
 }
 
-// x: [N][S][Cs] bf16 (NDHWC, S = T*H*W), wt: [C][ncls] f32 (TRANSPOSED linear
-// weight), out: [N][ncls] f32. Grid = (ceil(ncls / 64), ceil(N / 16)): a block
-// pools its 16 clips into LDS, then lane l of every wave computes class
-// 64 * blockIdx.x + l for 4 of the clips, reading wt[c][class] coalesced (each
-// wave one 256-B row segment per c) and the pooled features as LDS broadcasts.
+// Head, part 1: average pool. x: [N][S][Cs] bf16 (NDHWC, S = T*H*W) ->
+// pooled [N][C] f32. One thread per (clip, channel pair); the S-loop is
+// unrolled so 7 loads are in flight per thread (a pooled sum is a chain of
+// dependent adds, but its loads are independent).
+__global__ __launch_bounds__(256) void head_pool_kernel(const uint16_t* __restrict__ x,
+                                                        float* __restrict__ pooled, int N,
+                                                        int S, int C, int Cs) {
+  const int cp = C / 2;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)N * cp) return;
+  const int n = (int)(i / cp);
+  const int c = (int)(i - (long long)n * cp) * 2;
+  const uint16_t* xc = x + (size_t)n * S * Cs + c;
+  float s0 = 0.f, s1 = 0.f;
+  int s = 0;
+  for (; s + 7 <= S; s += 7) {
+    uint32_t v[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) v[j] = *(const uint32_t*)(xc + (size_t)(s + j) * Cs);
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      s0 += __uint_as_float(v[j] << 16);
+      s1 += __uint_as_float(v[j] & 0xFFFF0000u);
+    }
+  }
+  for (; s < S; ++s) {
+    const uint32_t v = *(const uint32_t*)(xc + (size_t)s * Cs);
+    s0 += __uint_as_float(v << 16);
+    s1 += __uint_as_float(v & 0xFFFF0000u);
+  }
+  const float inv = 1.0f / (float)S;
+  *(float2*)(pooled + (size_t)n * C + c) = make_float2(s0 * inv, s1 * inv);
+}
+
+// Head, part 2: linear. pooled [N][C] f32, wt: [C][ncls] f32 (TRANSPOSED linear
+// weight), out: [N][ncls] f32. Grid = (ceil(ncls / 64), ceil(N / 16)); a
+// block stages its 16 clips' pooled rows in LDS. The C reduction is split
+// over the 4 waves (a quarter of C each, 16 weight loads in flight per lane)
+// so the dependent-load chain is C/64 deep instead of C; lane l computes class
+// 64 * blockIdx.x + l for all 16 clips and the 4 partial sums meet in LDS.
 #define HEAD_CLIPS 16
 #define HEAD_CLS 64
-__global__ __launch_bounds__(256) void head_kernel(const uint16_t* __restrict__ x,
-                                                   const float* __restrict__ wt,
-                                                   const float* __restrict__ bias,
-                                                   float* __restrict__ out, int N, int S,
-                                                   int C, int Cs, int ncls) {
-  extern __shared__ float pooled[];                  // [HEAD_CLIPS][C]
+__global__ __launch_bounds__(256) void head_linear_kernel(const float* __restrict__ pooled_g,
+                                                          const float* __restrict__ wt,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ out, int N,
+                                                          int C, int ncls) {
+  extern __shared__ float smem_f[];                  // pooled [16][C] | partial [4][16][64]
+  float* pooled = smem_f;
+  float* partial = smem_f + HEAD_CLIPS * C;
   const int n0 = blockIdx.y * HEAD_CLIPS;
   const int nb = min(HEAD_CLIPS, N - n0);
-  const float inv = 1.0f / (float)S;
-  for (int idx = threadIdx.x; idx < HEAD_CLIPS * (C / 2); idx += blockDim.x) {
-    const int j = idx / (C / 2);
-    const int c = (idx - j * (C / 2)) * 2;
-    float s0 = 0.f, s1 = 0.f;
-    if (j < nb) {
-      const uint16_t* xc = x + (size_t)(n0 + j) * S * Cs + c;
-      for (int s = 0; s < S; ++s) {
-        const uint32_t v = *(const uint32_t*)(xc + (size_t)s * Cs);
-        s0 += __uint_as_float(v << 16);
-        s1 += __uint_as_float(v & 0xFFFF0000u);
-      }
-    }
-    pooled[j * C + c] = s0 * inv;
-    pooled[j * C + c + 1] = s1 * inv;
+  for (int idx = threadIdx.x; idx < HEAD_CLIPS * C / 4; idx += blockDim.x) {
+    const int j = idx / (C / 4);
+    const float4 v = j < nb ? *(const float4*)(pooled_g + (size_t)(n0 + j) * C +
+                                                (idx - j * (C / 4)) * 4)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+    *(float4*)(pooled + idx * 4) = v;
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;                 // clips 4*wave .. 4*wave+3
+  const int wave = threadIdx.x >> 6;
   const int o = blockIdx.x * HEAD_CLS + lane;
-  if (o >= ncls) return;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  const float* pj = pooled + (wave * 4) * C;
-#pragma unroll 8
-  for (int c = 0; c < C; ++c) {
-    const float w = wt[(size_t)c * ncls + o];
+  const int oc = min(o, ncls - 1);                   // clamped: every lane joins the reduce
+  const int cq = C / 4;
+  const int c0 = wave * cq;
+  float acc[HEAD_CLIPS];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] += w * pj[j * C + c];
+  for (int j = 0; j < HEAD_CLIPS; ++j) acc[j] = 0.f;
+  for (int c = c0; c < c0 + cq; c += 16) {
+    float w[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) w[u] = c + u < c0 + cq ? wt[(size_t)(c + u) * ncls + oc] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (c + u >= c0 + cq) break;
+#pragma unroll
+      for (int j = 0; j < HEAD_CLIPS; ++j) acc[j] += w[u] * pooled[j * C + c + u];
+    }
   }
-  const float b = bias[o];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int clip = wave * 4 + j;
-    if (clip < nb) out[(size_t)(n0 + clip) * ncls + o] = acc[j] + b;
+  for (int j = 0; j < HEAD_CLIPS; ++j) partial[(wave * HEAD_CLIPS + j) * HEAD_CLS + lane] = acc[j];
+  __syncthreads();
+  // 256 threads finish 16 clips x 64 classes: 4 outputs each
+  for (int q = threadIdx.x; q < HEAD_CLIPS * HEAD_CLS; q += 256) {
+    const int j = q / HEAD_CLS, l = q - j * HEAD_CLS;
+    const int oo = blockIdx.x * HEAD_CLS + l;
+    if (j < nb && oo < ncls) {
+      float v = bias[oo];
+#pragma unroll
+      for (int w4 = 0; w4 < 4; ++w4) v += partial[(w4 * HEAD_CLIPS + j) * HEAD_CLS + l];
+      out[(size_t)(n0 + j) * ncls + oo] = v;
+    }
   }
 }
 
@@ -195,22 +257,27 @@ int rnb_preprocess(const void* in, void* out, long long npix, const float* mean,
     np.scale[c] = 1.0f / (255.0f * stdv[c]);
     np.shift[c] = -mean[c] / stdv[c];
   }
+  if (((uintptr_t)in & 3u) != 0) return -2;         // dword loads of 4-pixel groups
   const int block = 256;
-  const long long grid = (npix + block - 1) / block;
+  const long long grid = ((npix + 3) / 4 + block - 1) / block;
   hipLaunchKernelGGL(preprocess_kernel, dim3((unsigned)grid), dim3(block), 0, stream,
                      (const uint8_t*)in, (uint16_t*)out, npix, np);
   return (int)hipGetLastError();
 }
 
-// w: TRANSPOSED linear weight [C][ncls]
-int rnb_head(const void* x, const float* w, const float* b, float* out, int N, int S, int C,
-             int Cs, int ncls, hipStream_t stream) {
+// w: TRANSPOSED linear weight [C][ncls]; pooled: [N][C] f32 scratch
+int rnb_head(const void* x, const float* w, const float* b, float* out, float* pooled, int N,
+             int S, int C, int Cs, int ncls, hipStream_t stream) {
   if (N <= 0) return 0;
-  if (C % 2 != 0 || Cs % 2 != 0 || Cs < C) return -2;
-  if ((size_t)HEAD_CLIPS * C * sizeof(float) > 64 * 1024) return -3;
+  if (C % 4 != 0 || Cs % 2 != 0 || Cs < C || !pooled) return -2;
+  const size_t lds = ((size_t)HEAD_CLIPS * C + 4 * HEAD_CLIPS * HEAD_CLS) * sizeof(float);
+  if (lds > 64 * 1024 || C % 16 != 0) return -3;
+  const long long threads = (long long)N * (C / 2);
+  hipLaunchKernelGGL(head_pool_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     stream, (const uint16_t*)x, pooled, N, S, C, Cs);
   const dim3 grid((ncls + HEAD_CLS - 1) / HEAD_CLS, (N + HEAD_CLIPS - 1) / HEAD_CLIPS);
-  hipLaunchKernelGGL(head_kernel, grid, dim3(256), HEAD_CLIPS * C * sizeof(float), stream,
-                     (const uint16_t*)x, w, b, out, N, S, C, Cs, ncls);
+  hipLaunchKernelGGL(head_linear_kernel, grid, dim3(256), lds, stream, pooled, w, b, out, N, C,
+                     ncls);
   return (int)hipGetLastError();
 }
 

@@ -162,8 +162,8 @@ class Kernels:
                                        ctypes.POINTER(ctypes.c_float),
                                        ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
         lib.rnb_head.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                 ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                 ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         lib.rnb_bn_scratch_floats.argtypes = [ctypes.c_int, ctypes.c_int]
         lib.rnb_bn_scratch_floats.restype = ctypes.c_longlong
         lib.rnb_bn_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -243,9 +243,9 @@ class Kernels:
         s = (ctypes.c_float * 3)(*std)
         _check(self.lib.rnb_preprocess(in_ptr, out_ptr, npix, m, s, stream), "preprocess")
 
-    def head(self, x_ptr, w_ptr, b_ptr, out_ptr, N, S, C, Cs, ncls, stream):
-        _check(self.lib.rnb_head(x_ptr, w_ptr, b_ptr, out_ptr, N, S, C, Cs, ncls, stream),
-               "head")
+    def head(self, x_ptr, w_ptr, b_ptr, out_ptr, pooled_ptr, N, S, C, Cs, ncls, stream):
+        _check(self.lib.rnb_head(x_ptr, w_ptr, b_ptr, out_ptr, pooled_ptr, N, S, C, Cs, ncls,
+                                 stream), "head")
 
     def video_reduce(self, logits_ptr, offsets_ptr, sums_ptr, argmax_ptr, nvid, ncls,
                      stream):

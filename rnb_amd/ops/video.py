@@ -106,9 +106,10 @@ class Head:
             from .native import kernels
             if out is None:
                 out = torch.empty((N, self.num_classes), dtype=torch.float32, device=x.device)
+            pooled = torch.empty((N, self.channels), dtype=torch.float32, device=x.device)
             kernels().head(x.data_ptr(), self.weight_t.data_ptr(), self.bias.data_ptr(),
-                           out.data_ptr(), N, T * H * W, self.channels, Cs, self.num_classes,
-                           torch.cuda.current_stream(x.device).cuda_stream)
+                           out.data_ptr(), pooled.data_ptr(), N, T * H * W, self.channels, Cs,
+                           self.num_classes, torch.cuda.current_stream(x.device).cuda_stream)
             return out
         return self.forward_torch(x)
 

@@ -149,6 +149,15 @@ def test_clipgen_and_preprocess_bit_exact():
     assert torch.equal(pg.cpu().float(), pc.float())
 
 
+@pytest.mark.parametrize("shape", [(1, 1, 3, 5, 3), (2, 3, 7, 9, 3), (1, 2, 4, 4, 3)])
+def test_preprocess_pixel_tails(shape):
+    """4-pixel vector path + per-pixel tail (pixel counts not divisible by 4)."""
+    u8 = torch.randint(0, 256, shape, dtype=torch.uint8, generator=torch.Generator().manual_seed(1))
+    pg = vops.preprocess(u8.to(DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(pg.cpu().float(), vops.preprocess(u8).float())
+
+
 @pytest.mark.parametrize("thw,cin,cout,stride", [((8, 14, 14), 144, 64, 1), ((4, 7, 7), 288, 128, 2),
                                                  ((2, 5, 3), 64, 96, 1)])
 def test_time_major_rows_exact(thw, cin, cout, stride):
