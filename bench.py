@@ -133,6 +133,11 @@ def main(argv=None) -> int:
     t_prep = time.time()
     eng.prepare([sum(len(s) for _, s in b) for b in batches])
     prep_s = time.time() - t_prep
+    # one pinned result buffer per batch: every prediction is read back after
+    # the timed loop without racing the staging-ring reuse
+    result_bufs = [[torch.full((len(b),), -1, dtype=torch.int32).pin_memory() for b in sb]
+                   for sb in step_batches]
+
     def run_step(step):
         start = torch.cuda.Event(enable_timing=True)
         start.record(torch.cuda.current_stream(device))
@@ -142,7 +147,8 @@ def main(argv=None) -> int:
         bs = step_batches[step]
         for i, b in enumerate(bs):
             rep = eng.replicas[i % len(eng.replicas)]
-            ev_done, out, nvid = rep.submit([(vid, st) for vid, st in b])
+            ev_done, out, nvid = rep.submit([(vid, st) for vid, st in b],
+                                            out=result_bufs[step][i])
             tev = torch.cuda.Event(enable_timing=True)
             tev.record(rep.stream)
             pending.append((tev, out, nvid))

@@ -102,12 +102,16 @@ class Replica:
         logits = self.engine.forward(bg.frames)
         vops.video_reduce(logits, bg.offsets, sums=bg.sums)
 
-    def submit(self, videos: Sequence[Tuple[int, Sequence[int]]]):
+    def submit(self, videos: Sequence[Tuple[int, Sequence[int]]],
+               out: Optional[torch.Tensor] = None):
         """Queue one batch of videos on this replica's stream.
 
         ``videos`` = [(video id, [clip start frames])]. Returns
-        (done event, pinned int32 argmax tensor view, #videos); the argmax
-        view is valid once the event has completed.
+        (done event, int32 argmax per video, #videos), valid once the event
+        has completed. The argmax lands in ``out`` (a pinned host int32
+        tensor of >= #videos entries) when given; otherwise in this
+        replica's staging ring, whose slots are reused ``pinned_ring``
+        submissions later -- read it before then.
         """
         nvid = len(videos)
         if nvid == 0 or nvid > self.max_videos:
@@ -134,9 +138,10 @@ class Replica:
             bg.meta.view(-1).copy_(host[:2 * b], non_blocking=True)
             bg.offsets.copy_(host[2 * b:2 * b + self.max_videos + 1], non_blocking=True)
             bg.graph.replay()
-            out_host[:nvid].copy_(bg.argmax[:nvid], non_blocking=True)
+            dst = out if out is not None else out_host
+            dst[:nvid].copy_(bg.argmax[:nvid], non_blocking=True)
             ev.record(self.stream)
-        return ev, out_host[:nvid], nvid
+        return ev, dst[:nvid], nvid
 
 
 class FusedR2P1D:
