@@ -26,6 +26,7 @@
 #include <stdint.h>
 
 #include "conv_epilogue.h"
+#include "conv_halo.h"
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -41,24 +42,6 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 
 #define HALO_INVALID 0xFFFFFFF0u
 #define HALO_MAX_PI 8           // patch DMA instructions per wave
-
-
-struct HaloParams {
-  const uint16_t* x;   // NDHWC input, Cin channels (multiple of 64)
-  const uint16_t* w;   // [w_rows][K_pad], k = tap * Cin + c, tap = dh * 3 + dw
-  const float* bias;
-  const uint16_t* res;
-  uint16_t* y;
-  int frames, H, W, Cin;
-  int Cout_p, y_stride, res_stride;
-  int K_pad, M, relu, w_rows;
-  int n_ptiles, n_ctiles;
-  int R;               // image rows per tile (R * W <= 224)
-  int bands;           // ceil(H / R) tiles per frame
-  int np;              // patch pixels = (R + 2) * (W + 2)
-  uint32_t x_bytes;
-  uint32_t mB, sB, mW, sW;   // magic division by bands, W
-};
 
 static __device__ __forceinline__ int hdiv(int n, uint32_t m, uint32_t s) {
   return m ? (int)(__umulhi((uint32_t)n, m) >> s) : n;
@@ -284,6 +267,7 @@ int rnb_halo_params_size() { return (int)sizeof(HaloParams); }
 
 // LDS bytes a launch of variant v on this shape requests (-1: not supported).
 int rnb_halo_lds_bytes_v(int frames, int H, int W, int Cin, int v) {
+  if (v == 6) return rnb_halo_ws_lds_bytes(frames, H, W, Cin);
   const HaloVariant* hv = halo_variant(v);
   if (!hv) return -1;
   const int R = halo_rows(H, W, hv->max_px);
@@ -299,6 +283,7 @@ int rnb_halo_lds_bytes(int frames, int H, int W, int Cin) {
 }
 
 int rnb_halo_launch_v(const HaloParams* pp, int v, hipStream_t stream) {
+  if (v == 6) return rnb_halo_ws_launch(pp, stream);
   HaloParams p = *pp;
   const HaloVariant* hv = halo_variant(v);
   if (!hv) return -10;

@@ -29,8 +29,10 @@ HALO = 100          # config id of the halo-tiled 1x3x3 stride-1 kernel (conv_ha
 TEMPORAL = 101      # config id of the register-direct 3x1x1 kernel (conv_temporal.hip)
 HALO4 = 102         # halo kernel with 64-pixel waves (4 MFMA pixel sub-tiles per wave)
 HALO4B = 103        # 64-pixel waves over 448-pixel tiles (7 waves, 1 block per CU)
-SPECIAL_NAMES = {HALO: "halo", TEMPORAL: "temporal", HALO4: "halo4", HALO4B: "halo4b"}
-HALO_VARIANT = {HALO: 2, HALO4: 4, HALO4B: 5}     # variant id of rnb_halo_launch_v
+HALOWS = 104        # weight-stationary halo kernel (conv_halo_ws.hip: Cin 64, Cout 128..144)
+SPECIAL_NAMES = {HALO: "halo", TEMPORAL: "temporal", HALO4: "halo4", HALO4B: "halo4b",
+                 HALOWS: "halows"}
+HALO_VARIANT = {HALO: 2, HALO4: 4, HALO4B: 5, HALOWS: 6}   # variant of rnb_halo_launch_v
 LDS_LIMIT = 160 * 1024
 
 
@@ -148,6 +150,7 @@ class ConvLayer:
         self.time_major = False   # time-major rows for temporal convs (measured: no gain)
         self.use_halo = True      # allow the halo-tiled kernel for 1x3x3 stride-1 convs
         self.use_temporal = True  # allow the register-direct kernel for 3x1x1 stride-1 convs
+        self.use_halo_ws = True   # allow the weight-stationary halo kernel (conv2 spatial)
 
     # ------------------------------------------------------------------
     def out_shape(self, x_shape) -> Tuple[int, int, int, int, int]:
@@ -245,9 +248,24 @@ class ConvLayer:
             self._config[key] = ok
         return bool(ok)
 
+    def halo_ws_eligible(self, x_shape) -> bool:
+        """The weight-stationary halo kernel holds all 128..144 output channels
+        of a 64-channel input on chip (conv2's spatial convs)."""
+        g = self.geom
+        if not (self.halo_eligible(x_shape) and g.cin_p == 64 and 128 <= g.cout_p <= 144
+                and self.use_halo_ws):
+            return False
+        from .native import kernels
+        N, T, H, W, _ = x_shape
+        nb = kernels().halo_lds_bytes(N * T, H, W, g.cin_p, HALO_VARIANT[HALOWS])
+        return 0 < nb <= LDS_LIMIT
+
     def special_candidates(self, x_shape):
-        """Shape-specialised kernels (config ids >= 100) that can run this input."""
+        """Shape-specialised kernels (config ids >= 100) that can run this input.
+        The first entry is the default when the layer is not autotuned."""
         out = []
+        if self.halo_ws_eligible(x_shape):
+            out.append(HALOWS)
         if self.halo_eligible(x_shape):
             out.append(HALO)
             from .native import kernels

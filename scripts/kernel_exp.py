@@ -31,6 +31,7 @@ def build():
         out = os.path.join(EXP_DIR, "libexp%d.so" % v)
         cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-DHALO_EXP=%d" % v, "-DCONV_EXP=%d" % v, "-DTEMP_EXP=%d" % v,
+               "-DWS_EXP=%d" % v, os.path.join(ROOT, "csrc", "conv_halo_ws.hip"),
                os.path.join(ROOT, "csrc", "conv_igemm.hip"),
                os.path.join(ROOT, "csrc", "conv_halo.hip"),
                os.path.join(ROOT, "csrc", "conv_temporal.hip"),

@@ -181,6 +181,9 @@ def test_time_major_rows_exact(thw, cin, cout, stride):
     (3, (2, 14, 14), 256, 576),     # conv4 spatial (K13): tiles span 2-3 frames
     (1, (3, 5, 7), 64, 96),         # tiny frames, partial channel tile
     (1, (1, 9, 40), 192, 144),      # 3 chunks, single frame, M tail
+    (6, (8, 56, 56), 64, 144),      # conv2 spatial, >2 tiles per persistent halows block
+    (2, (3, 9, 20), 64, 136),       # halows: partial ninth tile, partial last band
+    (1, (2, 7, 12), 64, 128),       # halows without the LDS-resident ninth tile
 ])
 def test_halo_kernel_exact(n, thw, cin, cout):
     from rnb_amd.ops.conv import HALO, HALO_VARIANT
@@ -192,6 +195,9 @@ def test_halo_kernel_exact(n, thw, cin, cout):
     ref = layer.forward_torch(x, residual=res, out_dtype=torch.bfloat16)
     variants = [c for c in layer.special_candidates(x.shape) if c in HALO_VARIANT]
     assert HALO in variants
+    if cin == 64 and 128 <= cout <= 144:
+        from rnb_amd.ops.conv import HALOWS
+        assert variants[0] == HALOWS
     for cid in variants:
         y = layer.forward_hip(x, residual=res, config=cid)
         torch.cuda.synchronize()
