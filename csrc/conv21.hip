@@ -1,0 +1,382 @@
+// Fused (2+1)D convolution: one R(2+1)D SpatioTemporalConv of the conv2
+// stage -- spatial 1x3x3 (64 -> 144, folded BN, ReLU) followed by temporal
+// 3x1x1 (144 -> 64, folded BN, + residual, ReLU) -- in ONE kernel, with the
+// 144-channel intermediate never leaving the CU (SURVEY.md §2.4(a) K3 + K4,
+// 14 of R(2+1)D-34's 72 convs, ~52 % of its conv time when run as two kernels).
+//
+// Why: run separately, the spatial conv writes and the temporal conv re-reads
+// a 144-channel bf16 intermediate -- 925 MB each way per 128 clips, more
+// than the input, output and residual together -- and both kernels sat at
+// roughly 2x their MFMA roofline (profiles/NOTES.md). Here:
+//
+//  * a persistent block (4 waves, one per SIMD, up to 512 VGPRs each) owns a
+//    "column" unit: 2 image rows x W (<= 56) pixels of one clip, all T frames;
+//  * step t: (S) every wave computes its 32 intermediate channels (+ the
+//    ninth 16-channel tile for a quarter of the pixel chunks) of frame t
+//    from a DMA'd (2+2) x 64-pixel input patch, exactly like
+//    conv_halo_ws.hip (all spatial weights stationary in VGPRs, ds_read
+//    immediates, no address VALU in the K loop), and writes ReLU(bf16) into
+//    slot t % 3 of an LDS ring of intermediate frames; (T) output frame t-1
+//    is the temporal GEMM over ring slots t-2, t-1, t (K = 3 x 160, the 16
+//    pad channels are zero): each wave owns one 32-channel output pair
+//    (temporal weights stationary in VGPRs) for half of the pixel chunks,
+//    B fragments straight from the ring, epilogue = bias + residual + ReLU
+//    with 16-byte paired stores (conv_epilogue.h);
+//  * the next frame's patch DMA runs under the temporal phase; two barriers
+//    per frame, none inside a K loop;
+//  * ring layout [20 channel planes of 8][pixel][16 B]: conflict-free
+//    ds_read_b128 B fragments and conflict-free ds_write_b128 from the
+//    spatial epilogue (a lane holds 8 consecutive channels of one pixel).
+//
+// Weights: the spatial matrix is the ConvLayer GEMM matrix of the spatial
+// conv (rows pair-permuted, k = tap * 64 + c); the temporal matrix is the
+// temporal ConvLayer's rows (pair-permuted) repacked to k = dt * 160 + c.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "conv_epilogue.h"
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2v __attribute__((ext_vector_type(2)));
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+
+#define C21_INVALID 0xFFFFFFF0u
+#define C21_NS 18                  // spatial K-steps: 9 taps x 64 channels / 32
+#define C21_KT 15                  // temporal K-steps: 3 dt x 160 / 32
+#define C21_PITCH 64               // patch row pitch (pixels)
+#define C21_ROWS 2                 // image rows per unit
+#define C21_PATCH ((C21_ROWS + 2) * C21_PITCH * 128)         // 32 KB
+#define C21_PI ((C21_ROWS + 2) * C21_PITCH / 8 / 4)           // DMA pieces per wave
+#define C21_MAXW 56        // image width limit: 2 rows of 56 px = one 1792-B plane
+#define C21_PLANE (2 * C21_MAXW * 16)  // one 8-channel plane (= 0 mod 256 B: conflict-free)
+#define C21_SLOT (20 * C21_PLANE)                              // 160 channels
+#define C21_W8 (C21_NS * 1024)                                 // ninth spatial tile
+#define C21_LDS (C21_PATCH + 3 * C21_SLOT + 1024 + C21_W8)
+
+struct Conv21Params {
+  const uint16_t* x;     // NDHWC [N][T][H][W][64]
+  const uint16_t* ws;    // spatial [>= 144 rows][ks_pad], k = tap * 64 + c
+  const float* bs;       // spatial bias [144] (row order of ws)
+  const uint16_t* wt;    // temporal [64 rows][480], k = dt * 160 + c
+  const float* bt;       // temporal bias [64] (row order of wt)
+  const uint16_t* res;   // residual NDHWC (nullable)
+  uint16_t* y;           // output NDHWC, channel stride y_stride
+  int N, T, H, W;
+  int ks_pad, y_stride, res_stride, relu;
+  int n_units, bands;    // bands = ceil(H / 2)
+  uint32_t x_bytes;
+  uint32_t mB, sB, mW, sW;
+};
+
+static __device__ __forceinline__ int c21div(int n, uint32_t m, uint32_t s) {
+  return m ? (int)(__umulhi((uint32_t)n, m) >> s) : n;
+}
+
+__global__ __launch_bounds__(256, 1)
+void conv21_kernel(const Conv21Params p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int frow = lane & 15;
+  const int fq = lane >> 4;
+  const int pp = wave & 1;                   // temporal output pair of this wave
+  const int half = wave >> 1;                // temporal pixel chunks c = half, half + 2, ..
+  char* ring = smem + C21_PATCH;
+  char* w8 = smem + C21_PATCH + 3 * C21_SLOT + 1024;   // [18 steps][64 lanes][16 B]
+
+  // ---- prologue: stationary weights, biases, zero pad planes ----
+  bf16x8 wv[2][C21_NS], wtv[2][C21_KT];
+  {
+    const uint16_t* wr = p.ws + (size_t)(32 * wave + frow) * p.ks_pad + 8 * fq;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < C21_NS; ++s)
+        wv[t][s] = *(const bf16x8*)(wr + (size_t)16 * t * p.ks_pad + 32 * s);
+    const uint16_t* w8g = p.ws + (size_t)(128 + frow) * p.ks_pad + 8 * fq;
+    for (int s = wave; s < C21_NS; s += 4)
+      *(bf16x8*)(w8 + (s * 64 + lane) * 16) = *(const bf16x8*)(w8g + 32 * s);
+    const uint16_t* wt = p.wt + (size_t)(32 * pp + frow) * 480 + 8 * fq;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int s = 0; s < C21_KT; ++s)
+        wtv[b][s] = *(const bf16x8*)(wt + (size_t)16 * b * 480 + 32 * s);
+  }
+  // biases (the initial accumulators) stay in registers
+  const f32x4 bs0 = *(const f32x4*)(p.bs + 32 * wave + 4 * fq);
+  const f32x4 bs1 = *(const f32x4*)(p.bs + 32 * wave + 16 + 4 * fq);
+  const f32x4 bs8 = *(const f32x4*)(p.bs + 128 + 4 * fq);
+  const f32x4 bt0 = *(const f32x4*)(p.bt + 32 * pp + 4 * fq);
+  const f32x4 bt1 = *(const f32x4*)(p.bt + 32 * pp + 16 + 4 * fq);
+  for (int i = tid; i < 3 * 2 * C21_PLANE / 16; i += 256) {     // planes 18, 19 of each slot
+    const int slot = i / (2 * C21_PLANE / 16), r = i - slot * (2 * C21_PLANE / 16);
+    *(i32x4v*)(ring + slot * C21_SLOT + 18 * C21_PLANE + r * 16) = (i32x4v){0, 0, 0, 0};
+  }
+
+  // ---- this block's units: XCD-grouped contiguous range ----
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int u_begin = (int)((long long)wgid * p.n_units / nwg);
+  const int u_end = (int)((long long)(wgid + 1) * p.n_units / nwg);
+
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+  const EpCtx e = ep_make(p.y, p.y_stride, p.res, p.res_stride,
+                          (long long)p.N * p.T * p.H * p.W, 64, p.relu != 0);
+  const int lrow = lane >> 3;
+  const int kc = (lane & 7) ^ lrow;          // swizzle on the DMA source side
+
+  // patch pixel q = pr * 64 + pc <-> image (h0 - 1 + pr, pc - 1) of frame t
+  auto issue_patch = [&](int unit, int t) {
+    const int n = c21div(unit, p.mB, p.sB);
+    const int h0 = (unit - n * p.bands) * C21_ROWS;
+    const int fbase = (n * p.T + t) * p.H;
+#pragma unroll
+    for (int i = 0; i < C21_PI; ++i) {
+      const int instr = wave + 4 * i;
+      const int q = instr * 8 + lrow;
+      const int h = h0 - 1 + q / C21_PITCH, wc = q % C21_PITCH - 1;
+      const uint32_t off = ((unsigned)h < (unsigned)p.H && (unsigned)wc < (unsigned)p.W)
+                               ? (uint32_t)((((fbase + h) * p.W + wc) * 64 + kc * 8) * 2)
+                               : C21_INVALID;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xr, (__attribute__((address_space(3))) void*)(smem + instr * 1024), 16, off, 0, 0,
+          0);
+    }
+  };
+
+  if (u_begin < u_end) issue_patch(u_begin, 0);
+  int nvm = 0;                               // vector-memory ops issued after the last DMA
+  for (int unit = u_begin; unit < u_end; ++unit) {
+    const int n = c21div(unit, p.mB, p.sB);
+    const int h0 = (unit - n * p.bands) * C21_ROWS;
+    const int npx = min(C21_ROWS, p.H - h0) * p.W;
+    const int nch = (npx + 15) >> 4;
+
+    // this wave's temporal chunks: c = half + 2 k, k < nmine (<= 4: W <= 56)
+    const int nmine = (nch - half + 1) >> 1;
+    for (int t = 0; t <= p.T; ++t) {
+      // residual of output frame t - 1, loaded now so that its latency hides
+      // under the spatial phase (16 B per lane and chunk: channels 32 pp + 8 fq)
+      ep_i32x4 rres[4];
+      const long long m0 = ((long long)(n * p.T + max(t - 1, 0)) * p.H + h0) * p.W;
+      if (t >= 1) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int i = (half + 2 * k) * 16 + frow;
+          rres[k] = e.has_res ? __builtin_amdgcn_raw_buffer_load_b128(
+                                    e.res, ep_off(k < nmine && i < npx, m0 + i, e.res_stride,
+                                                  32 * pp + 8 * fq), 0, 0)
+                              : (ep_i32x4){0, 0, 0, 0};
+        }
+      }
+      if (t < p.T) {
+        // ---------------- (S) spatial conv of frame t -> ring slot t % 3 ----
+        // this wave's DMA pieces are older than its nvm newest vm ops
+        if (nvm >= 4)
+          asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else if (nvm >= 2)
+          asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        nvm = 0;
+        char* slot = ring + (t % 3) * C21_SLOT;
+        // LDS offset of this lane's B-fragment row for tap (dh, dw), K half
+        // kh: patch row q = (hh + dh) * 64 + ww + dw holds channel chunk
+        // ch = 4 kh + fq at ((ch ^ (q & 7)) << 4); the pitch is a multiple of
+        // 8, so one base per (dw, kh) and dh * 8 KB as the ds_read immediate
+        auto chunk_base = [&](int c, uint32_t (*bs)[2]) {
+          const int i = min(c * 16 + frow, npx - 1);
+          const int hh = c21div(i, p.mW, p.sW);
+          const int q0 = hh * C21_PITCH + (i - hh * p.W);
+#pragma unroll
+          for (int dw = 0; dw < 3; ++dw) {
+            const uint32_t rel =
+                (uint32_t)(q0 + dw) * 128u + (uint32_t)((fq ^ ((q0 + dw) & 7)) << 4);
+            bs[dw][0] = rel;
+            bs[dw][1] = rel ^ 64u;           // ch + 4 = ch ^ 4 (fq < 4)
+          }
+        };
+        auto load_b = [&](const uint32_t (*bs)[2], int s) -> bf16x8 {
+          const int tap = s >> 1;
+          return *(const bf16x8*)(smem + bs[tap % 3][s & 1] + (tap / 3) * C21_PITCH * 128);
+        };
+        auto load_a8 = [&](int s) -> bf16x8 {
+          return *(const bf16x8*)(w8 + (s * 64 + lane) * 16);
+        };
+        // B (and ninth-tile A) fragments prefetched PF steps ahead (one wave
+        // per SIMD: nothing else hides the LDS latency). Prefetching across
+        // chunk boundaries as well pushed the kernel past 512 registers.
+        constexpr int PF = 4, RING = PF + 1;
+        for (int c = 0; c < nch; ++c) {
+          const bool own8 = (c & 3) == wave;
+          uint32_t base[3][2];
+          chunk_base(c, base);
+          f32x4 acc0 = bs0, acc1 = bs1, acc8 = bs8;
+          bf16x8 bq[RING];
+#pragma unroll
+          for (int s = 0; s < PF; ++s) bq[s] = load_b(base, s);
+          if (own8) {
+            bf16x8 aq[RING];
+#pragma unroll
+            for (int s = 0; s < PF; ++s) aq[s] = load_a8(s);
+#pragma unroll
+            for (int s = 0; s < C21_NS; ++s) {
+              if (s + PF < C21_NS) {
+                bq[(s + PF) % RING] = load_b(base, s + PF);
+                aq[(s + PF) % RING] = load_a8(s + PF);
+              }
+              const bf16x8 bv = bq[s % RING];
+              acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[0][s], bv, acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[1][s], bv, acc1, 0, 0, 0);
+              acc8 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[s % RING], bv, acc8, 0, 0, 0);
+            }
+          } else {
+#pragma unroll
+            for (int s = 0; s < C21_NS; ++s) {
+              if (s + PF < C21_NS) bq[(s + PF) % RING] = load_b(base, s + PF);
+              const bf16x8 bv = bq[s % RING];
+              acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[0][s], bv, acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[1][s], bv, acc1, 0, 0, 0);
+            }
+          }
+          // ReLU -> bf16 -> ring: channels 32 wave + 8 fq .. +7 of pixel i
+          // (plane 4 wave + fq); ninth tile: channels 128 + 4 fq .. +3
+          const int i = c * 16 + frow;
+          i32x4v o;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            o[j] = (int)ep_pack(ep_relu(acc0[2 * j]), ep_relu(acc0[2 * j + 1]));
+            o[2 + j] = (int)ep_pack(ep_relu(acc1[2 * j]), ep_relu(acc1[2 * j + 1]));
+          }
+          *(i32x4v*)(slot + (4 * wave + fq) * C21_PLANE + i * 16) = o;
+          if (own8) {
+            i32x2v o8;
+            o8[0] = (int)ep_pack(ep_relu(acc8[0]), ep_relu(acc8[1]));
+            o8[1] = (int)ep_pack(ep_relu(acc8[2]), ep_relu(acc8[3]));
+            *(i32x2v*)(slot + (16 + (fq >> 1)) * C21_PLANE + i * 16 + (fq & 1) * 8) = o8;
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        // the patch is free: prefetch the next frame (or the next unit's first)
+        if (t + 1 < p.T)
+          issue_patch(unit, t + 1);
+        else if (unit + 1 < u_end)
+          issue_patch(unit + 1, 0);
+      }
+      if (t >= 1) {
+        // ---------------- (T) temporal conv of output frame t - 1 ----------
+        // groups G = 3 k + dt (chunk k, tap dt) of 5 B fragments each, the
+        // next group's reads issued before the current group's MFMAs; a tap
+        // that reads the clip's zero padding (frame -1 or T) re-reads the
+        // centre frame and skips its MFMAs
+        const int to = t - 1;
+        auto load_grp = [&](int G, bf16x8* dst) {
+          const int k = G / 3, dt = G % 3;
+          int fi = to - 1 + dt;
+          if (fi < 0 || fi >= p.T) fi = to;
+          const char* src = ring + (fi % 3) * C21_SLOT + fq * C21_PLANE +
+                            ((half + 2 * k) * 16 + frow) * 16;
+#pragma unroll
+          for (int ks = 0; ks < 5; ++ks) dst[ks] = *(const bf16x8*)(src + ks * 4 * C21_PLANE);
+        };
+        bf16x8 gb[2][5];
+        f32x4 acc0, acc1;
+        if (nmine > 0) load_grp(0, gb[0]);
+#pragma unroll
+        for (int G = 0; G < 12; ++G) {
+          const int k = G / 3, dt = G % 3;
+          if (k < nmine) {                   // (no break: the loop must fully unroll)
+            if (G + 1 < 12 && (G + 1) / 3 < nmine) load_grp(G + 1, gb[(G + 1) & 1]);
+            if (dt == 0) {
+              acc0 = bt0;
+              acc1 = bt1;
+            }
+            const int fi = to - 1 + dt;
+            if (fi >= 0 && fi < p.T) {
+#pragma unroll
+              for (int ks = 0; ks < 5; ++ks) {
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wtv[0][dt * 5 + ks],
+                                                               gb[G & 1][ks], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wtv[1][dt * 5 + ks],
+                                                               gb[G & 1][ks], acc1, 0, 0, 0);
+              }
+            }
+            if (dt == 2) {
+              const int i = (half + 2 * k) * 16 + frow;
+              ep_out8(e, ep_off(i < npx, m0 + i, e.y_stride, 32 * pp + 8 * fq), acc0, acc1,
+                      rres[k], true);
+              ++nvm;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+static void c21_magic(uint32_t d, uint32_t* m, uint32_t* s) {
+  if (d <= 1) { *m = 0; *s = 0; return; }
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t q = 31 + l;
+  *m = (uint32_t)(((1ull << q) + d - 1) / d);
+  *s = (uint32_t)(q - 32);
+}
+
+static int c21_num_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+extern "C" {
+
+int rnb_conv21_params_size() { return (int)sizeof(Conv21Params); }
+
+// 1 if the fused kernel serves frames of H x W (any T >= 1, W <= 56), else 0
+int rnb_conv21_supported(int T, int H, int W) {
+  return (T >= 1 && H >= 1 && W >= 1 && W <= C21_MAXW) ? 1 : 0;
+}
+
+int rnb_conv21_lds_bytes() { return C21_LDS; }
+
+int rnb_conv21_launch(const Conv21Params* pp, hipStream_t stream) {
+  Conv21Params p = *pp;
+  if (!rnb_conv21_supported(p.T, p.H, p.W)) return -3;
+  if (p.ks_pad < 9 * 64 || p.y_stride < 64 || (p.res && p.res_stride < 64)) return -2;
+  if (p.N <= 0) return 0;
+  const long long M = (long long)p.N * p.T * p.H * p.W;
+  if (M * 64 * 2 > 0x7FFFFF00LL) return -5;
+  if (M * p.y_stride * 2 > 0xFFFFFF00LL || M * (p.res ? p.res_stride : 0) * 2 > 0xFFFFFF00LL)
+    return -7;
+  p.bands = (p.H + C21_ROWS - 1) / C21_ROWS;
+  p.n_units = p.N * p.bands;
+  p.x_bytes = (uint32_t)(M * 64 * 2);
+  c21_magic((uint32_t)p.bands, &p.mB, &p.sB);
+  c21_magic((uint32_t)p.W, &p.mW, &p.sW);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)conv21_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    attr_set = true;
+  }
+  int grid = c21_num_cus();
+  if (grid > p.n_units) grid = p.n_units;
+  hipLaunchKernelGGL(conv21_kernel, dim3((unsigned)grid), dim3(256), C21_LDS, stream, p);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -35,6 +35,7 @@ import torch
 
 from ...ops.bn import BatchNormBatch
 from ...ops.conv import ConvGeom, ConvLayer, fold_bn, pad_to, CH_ALIGN
+from ...ops.conv21 import FusedSTConv
 from ...ops.video import Head, IN_CHANNELS_P, ndhwc_to_ncdhw, ncdhw_to_ndhwc
 from .network import (LAYER_CHANNELS, LAYER_INPUT_CTHW, LAYER_OUTPUT_CTHW,
                       R2Plus1DLayerWrapper, SpatioTemporalConv)
@@ -57,12 +58,15 @@ def boundary_shape(layer_idx: int, n: int) -> Tuple[int, ...]:
 
 class PlanOp:
     """One conv of the plan; ``bn`` is set in bn_mode='batch' (BatchNorm with
-    batch statistics applied after the unfolded conv, then residual + ReLU)."""
-    __slots__ = ("kind", "layer", "src", "dst", "res", "bn", "bn_relu")
+    batch statistics applied after the unfolded conv, then residual + ReLU).
+    ``fuse`` (on a spatial conv) is the FusedSTConv that runs it together with
+    the next op, its temporal conv, on the hip backend."""
+    __slots__ = ("kind", "layer", "src", "dst", "res", "bn", "bn_relu", "fuse")
 
     def __init__(self, kind, layer, src, dst, res=None, bn=None, bn_relu=False):
         self.kind, self.layer, self.src, self.dst, self.res = kind, layer, src, dst, res
         self.bn, self.bn_relu = bn, bn_relu
+        self.fuse = None
 
 
 class R2P1DEngine:
@@ -122,6 +126,10 @@ class R2P1DEngine:
         self._append(st.spatial_conv, st.bn, True, None, name + ".spatial", src, mid)
         dst = self._name()
         self._append(st.temporal_conv, post_bn, relu, res, name + ".temporal", mid, dst)
+        sp, tp = self.ops[-2], self.ops[-1]
+        if sp.bn is None and tp.bn is None and FusedSTConv.eligible(sp.layer, tp.layer):
+            # conv2-stage pair: one kernel, intermediate kept on chip (conv21.hip)
+            sp.fuse = FusedSTConv(sp.layer, tp.layer)
         return dst
 
     def _append(self, conv, bn, relu: bool, res: Optional[str], name: str, src: str, dst: str):
@@ -205,8 +213,18 @@ class R2P1DEngine:
                                device=x.device)
         hip = self.backend == "hip"
         bufs: Dict[str, torch.Tensor] = {"x": x}
-        for op in self.ops:
+        skip = False
+        for i, op in enumerate(self.ops):
+            if skip:                      # temporal half of a fused pair
+                skip = False
+                continue
             src = bufs[op.src]
+            if hip and op.fuse is not None and op.fuse.use_for(src.shape):
+                nxt = self.ops[i + 1]
+                res = bufs[nxt.res] if nxt.res is not None else None
+                bufs[nxt.dst] = op.fuse.forward_hip(src, res)
+                skip = True
+                continue
             res = bufs[op.res] if op.res is not None else None
             if op.bn is not None:
                 if hip:
@@ -243,8 +261,31 @@ class R2P1DEngine:
                 res = None               # the residual is added after the BN
             chosen[op.layer.name] = op.layer.autotune(src, res, reps)
             bufs[op.dst] = op.layer.forward_hip(src, res)
+        # fused (2+1)D pairs: keep the fused kernel only where it beats the
+        # two tuned kernels
+        for i, op in enumerate(self.ops):
+            if op.fuse is None or not op.fuse.supported(bufs[op.src].shape):
+                continue
+            nxt = self.ops[i + 1]
+            src = bufs[op.src]
+            res = bufs[nxt.res] if nxt.res is not None else None
+            t_fused = _time(lambda: op.fuse.forward_hip(src, res), reps)
+            t_split = _time(lambda: nxt.layer.forward_hip(op.layer.forward_hip(src), res), reps)
+            op.fuse._use[tuple(src.shape[:4])] = t_fused <= t_split
+            chosen[op.fuse.name] = int(t_fused <= t_split)
         torch.cuda.synchronize(self.device)
         return chosen
+
+
+def _time(fn, reps: int) -> float:
+    fn()                                          # warm
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record()
+    for _ in range(reps):
+        fn()
+    end.record()
+    end.synchronize()
+    return start.elapsed_time(end) / reps
 
 
 class GraphedEngine:

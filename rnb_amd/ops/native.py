@@ -128,6 +128,20 @@ class HaloParams(ctypes.Structure):
     ]
 
 
+class Conv21Params(ctypes.Structure):
+    """Mirror of ``struct Conv21Params`` in csrc/conv21.hip."""
+    _fields_ = [
+        ("x", ctypes.c_void_p), ("ws", ctypes.c_void_p), ("bs", ctypes.c_void_p),
+        ("wt", ctypes.c_void_p), ("bt", ctypes.c_void_p), ("res", ctypes.c_void_p),
+        ("y", ctypes.c_void_p),
+        ("N", ctypes.c_int), ("T", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+        ("ks_pad", ctypes.c_int), ("y_stride", ctypes.c_int), ("res_stride", ctypes.c_int),
+        ("relu", ctypes.c_int), ("n_units", ctypes.c_int), ("bands", ctypes.c_int),
+        ("x_bytes", ctypes.c_uint32), ("mB", ctypes.c_uint32), ("sB", ctypes.c_uint32),
+        ("mW", ctypes.c_uint32), ("sW", ctypes.c_uint32),
+    ]
+
+
 class TemporalParams(ctypes.Structure):
     """Mirror of ``struct TemporalParams`` in csrc/conv_temporal.hip."""
     _fields_ = [
@@ -185,6 +199,11 @@ class Kernels:
                                             ctypes.c_int, ctypes.c_void_p]
         lib.rnb_temporal_launch.restype = ctypes.c_int
         lib.rnb_temporal_lds_bytes.argtypes = [ctypes.c_int] * 3
+        lib.rnb_conv21_launch.argtypes = [ctypes.POINTER(Conv21Params), ctypes.c_void_p]
+        lib.rnb_conv21_launch.restype = ctypes.c_int
+        lib.rnb_conv21_supported.argtypes = [ctypes.c_int] * 3
+        if lib.rnb_conv21_params_size() != ctypes.sizeof(Conv21Params):
+            raise NativeUnavailable("Conv21Params layout mismatch: rebuild")
         if lib.rnb_temporal_params_size() != ctypes.sizeof(TemporalParams):
             raise NativeUnavailable("TemporalParams layout mismatch: rebuild")
         if lib.rnb_halo_params_size() != ctypes.sizeof(HaloParams):
@@ -214,6 +233,13 @@ class Kernels:
                  stream: int) -> None:
         _check(self.lib.rnb_temporal_launch(ctypes.byref(params), num_cus, blocks_per_cu,
                                             stream), "conv_temporal")
+
+    def conv21(self, params: Conv21Params, stream: int) -> None:
+        """Fused spatial 1x3x3 (64 -> 144) + temporal 3x1x1 (144 -> 64)."""
+        _check(self.lib.rnb_conv21_launch(ctypes.byref(params), stream), "conv21")
+
+    def conv21_supported(self, T: int, H: int, W: int) -> bool:
+        return bool(self.lib.rnb_conv21_supported(T, H, W))
 
     def temporal_lds_bytes(self, T: int, cin_p: int, cout_p: int) -> int:
         return self.lib.rnb_temporal_lds_bytes(T, cin_p, cout_p)

@@ -37,10 +37,17 @@ def main():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--compare", action="store_true",
                     help="time every tile config per layer; report best per family")
+    ap.add_argument("--fuse", action="store_true",
+                    help="time the conv2 (2+1)D pairs with the fused kernel (without "
+                         "--autotune: always; with it: where the autotuner picked it)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     eng = R2P1DEngine(build_network(1, 5, depth=args.depth), dev, backend="hip")
     n = args.clips
+    if args.fuse and not args.autotune:
+        for op in eng.ops:
+            if op.fuse is not None:
+                op.fuse.force(True)
     if args.autotune:
         eng.autotune(n)
     x = torch.randn(eng.input_shape(n), device=dev).to(torch.bfloat16)
@@ -49,8 +56,33 @@ def main():
     rows = []
     from rnb_amd.ops.native import kernels
     cfgs = kernels().configs
-    for op in eng.ops:
+    skip = False
+    for i, op in enumerate(eng.ops):
+        if skip:
+            skip = False
+            continue
         src = bufs[op.src]
+        if op.fuse is not None and op.fuse.use_for(src.shape) and args.fuse:
+            # fused (2+1)D pair (csrc/conv21.hip): one row for both convs
+            nxt = eng.ops[i + 1]
+            res = bufs[nxt.res] if nxt.res is not None else None
+            y = op.fuse.forward_hip(src, res)
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(args.reps):
+                op.fuse.forward_hip(src, res, out=y)
+            e.record()
+            e.synchronize()
+            ms = s.elapsed_time(e) / args.reps
+            N, T, H, W, _ = src.shape
+            flops = op.fuse.flops(N, T, H, W)
+            rows.append({"name": op.fuse.name, "M": N * T * H * W, "N": 144, "K": 576,
+                         "tile": "conv21", "ms": ms, "tflops": flops / ms / 1e9,
+                         "gflop": flops / 1e9})
+            bufs[nxt.dst] = y
+            skip = True
+            continue
         res = bufs[op.res] if op.res is not None else None
         y = op.layer.forward_hip(src, res)
         torch.cuda.synchronize()
