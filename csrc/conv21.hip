@@ -34,12 +34,23 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "conv_epilogue.h"
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x2v __attribute__((ext_vector_type(2)));
 typedef int i32x4v __attribute__((ext_vector_type(4)));
+
+// bottleneck experiments (scripts/c21_exp.py; results are garbage by design):
+// 1 no spatial phase, 2 no temporal phase, 3 no patch DMA after the first,
+// 4 no global stores / residual loads, 5 no waits + barriers,
+// 6 spatial phase only (2 + 3 + 4)
+#ifndef C21_EXP
+#define C21_EXP 0
+#endif
+#define C21_X(n) (C21_EXP == (n))
 
 #define C21_INVALID 0xFFFFFFF0u
 #define C21_NS 18                  // spatial K-steps: 9 taps x 64 channels / 32
@@ -90,11 +101,17 @@ void conv21_kernel(const Conv21Params p) {
   bf16x8 wv[2][C21_NS], wtv[2][C21_KT];
   {
     const uint16_t* wr = p.ws + (size_t)(32 * wave + frow) * p.ks_pad + 8 * fq;
+    // the spatial weights live in AGPRs (MFMA reads its A operand from there
+    // directly); left to itself the compiler put the temporal weights there
+    // instead and copied them to VGPRs before every use, which squeezed the
+    // B-fragment prefetch ring down to one register
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int s = 0; s < C21_NS; ++s)
-        wv[t][s] = *(const bf16x8*)(wr + (size_t)16 * t * p.ks_pad + 32 * s);
+      for (int s = 0; s < C21_NS; ++s) {
+        const bf16x8 v = *(const bf16x8*)(wr + (size_t)16 * t * p.ks_pad + 32 * s);
+        asm("; weights -> agpr %0" : "=a"(wv[t][s]) : "0"(v));
+      }
     const uint16_t* w8g = p.ws + (size_t)(128 + frow) * p.ks_pad + 8 * fq;
     for (int s = wave; s < C21_NS; s += 4)
       *(bf16x8*)(w8 + (s * 64 + lane) * 16) = *(const bf16x8*)(w8g + 32 * s);
@@ -102,8 +119,13 @@ void conv21_kernel(const Conv21Params p) {
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int s = 0; s < C21_KT; ++s)
-        wtv[b][s] = *(const bf16x8*)(wt + (size_t)16 * b * 480 + 32 * s);
+      for (int s = 0; s < C21_KT; ++s) {
+        const bf16x8 v = *(const bf16x8*)(wt + (size_t)16 * b * 480 + 32 * s);
+        if (b == 0)
+          asm("; weights -> agpr %0" : "=a"(wtv[b][s]) : "0"(v));
+        else
+          wtv[b][s] = v;
+      }
   }
   // biases (the initial accumulators) stay in registers
   const f32x4 bs0 = *(const f32x4*)(p.bs + 32 * wave + 4 * fq);
@@ -164,7 +186,7 @@ void conv21_kernel(const Conv21Params p) {
       // under the spatial phase (16 B per lane and chunk: channels 32 pp + 8 fq)
       ep_i32x4 rres[4];
       const long long m0 = ((long long)(n * p.T + max(t - 1, 0)) * p.H + h0) * p.W;
-      if (t >= 1) {
+      if (t >= 1 && !C21_X(4) && !C21_X(6)) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int i = (half + 2 * k) * 16 + frow;
@@ -177,7 +199,8 @@ void conv21_kernel(const Conv21Params p) {
       if (t < p.T) {
         // ---------------- (S) spatial conv of frame t -> ring slot t % 3 ----
         // this wave's DMA pieces are older than its nvm newest vm ops
-        if (nvm >= 4)
+        if (C21_X(5)) {
+        } else if (nvm >= 4)
           asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         else if (nvm >= 2)
           asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -212,7 +235,7 @@ void conv21_kernel(const Conv21Params p) {
         // per SIMD: nothing else hides the LDS latency). Prefetching across
         // chunk boundaries as well pushed the kernel past 512 registers.
         constexpr int PF = 4, RING = PF + 1;
-        for (int c = 0; c < nch; ++c) {
+        for (int c = 0; c < (C21_X(1) ? 0 : nch); ++c) {
           const bool own8 = (c & 3) == wave;
           uint32_t base[3][2];
           chunk_base(c, base);
@@ -235,6 +258,13 @@ void conv21_kernel(const Conv21Params p) {
               acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[1][s], bv, acc1, 0, 0, 0);
               acc8 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[s % RING], bv, acc8, 0, 0, 0);
             }
+            // pin the software pipeline: the scheduler otherwise sinks each
+            // read next to its MFMAs (register pressure of the unified file)
+#pragma unroll
+            for (int s = 0; s < C21_NS; ++s) {
+              if (s + PF < C21_NS) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+            }
           } else {
 #pragma unroll
             for (int s = 0; s < C21_NS; ++s) {
@@ -242,6 +272,11 @@ void conv21_kernel(const Conv21Params p) {
               const bf16x8 bv = bq[s % RING];
               acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[0][s], bv, acc0, 0, 0, 0);
               acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[1][s], bv, acc1, 0, 0, 0);
+            }
+#pragma unroll
+            for (int s = 0; s < C21_NS; ++s) {
+              if (s + PF < C21_NS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
             }
           }
           // ReLU -> bf16 -> ring: channels 32 wave + 8 fq .. +7 of pixel i
@@ -261,14 +296,15 @@ void conv21_kernel(const Conv21Params p) {
             *(i32x2v*)(slot + (16 + (fq >> 1)) * C21_PLANE + i * 16 + (fq & 1) * 8) = o8;
           }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (!C21_X(5)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         // the patch is free: prefetch the next frame (or the next unit's first)
-        if (t + 1 < p.T)
+        if (C21_X(3) || C21_X(6)) {
+        } else if (t + 1 < p.T)
           issue_patch(unit, t + 1);
         else if (unit + 1 < u_end)
           issue_patch(unit + 1, 0);
       }
-      if (t >= 1) {
+      if (t >= 1 && !C21_X(2) && !C21_X(6)) {
         // ---------------- (T) temporal conv of output frame t - 1 ----------
         // groups G = 3 k + dt (chunk k, tap dt) of 5 B fragments each, the
         // next group's reads issued before the current group's MFMAs; a tap
@@ -309,12 +345,312 @@ void conv21_kernel(const Conv21Params p) {
             if (dt == 2) {
               const int i = (half + 2 * k) * 16 + frow;
               ep_out8(e, ep_off(i < npx, m0 + i, e.y_stride, 32 * pp + 8 * fq), acc0, acc1,
-                      rres[k], true);
+                      rres[k], !C21_X(4));
               ++nvm;
             }
           }
         }
       }
+    }
+  }
+}
+
+// ===========================================================================
+// Role-specialised variant (conv21s): 8 waves per CU, 2 per SIMD. Waves 0-3
+// are SPATIAL waves, waves 4-7 TEMPORAL waves; each SIMD runs one of each,
+// so one wave's LDS/barrier stalls are filled by the other's MFMAs, and each
+// wave keeps only its own role's weights stationary (spatial 144 VGPRs,
+// temporal 60), which is what lets two waves share a SIMD's 512 registers.
+//
+// The block walks its units' frames as one stream f = 0 .. F-1 (unit major,
+// frame minor) in lock step, one barrier per step s = 0 .. F:
+//   spatial  s: DMA the input patch of frame s + 1 into patch[(s + 1) & 1],
+//               compute the 144-channel intermediate of frame s from
+//               patch[s & 1] into ring slot s & 1;
+//   temporal s: consume the intermediate of frame s - 1 (slot (s - 1) & 1):
+//               with out[t] = sum_dt W_dt mid[t - 1 + dt] it adds W_2 mid[t]
+//               to out[t - 1], W_1 mid[t] to out[t] and W_0 mid[t] to
+//               out[t + 1] (three accumulator sets in registers), then stores
+//               out[t - 1] (and out[T - 1] at the clip's last frame).
+// Accumulating into outputs instead of gathering 3 intermediate frames
+// needs only 2 ring slots, which leaves LDS for a double-buffered patch: the
+// DMA of frame s + 1 lands under frame s's compute.
+// Temporal waves own one 16-channel output tile each (physical rows
+// 16 w .. +15 of the pair-permuted matrix -> 4 consecutive channels per
+// lane, 8-byte stores) for all of the unit's <= 7 pixel chunks.
+// ===========================================================================
+#define C21S_LDS (2 * C21_PATCH + 2 * C21_SLOT + C21_W8)     // 152 KB
+#define C21S_CH 7                                            // chunks per unit (112 px)
+
+__global__ __launch_bounds__(512, 1)
+void conv21s_kernel(const Conv21Params p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wq = wave & 3;
+  const bool spatial = wave < 4;
+  const int frow = lane & 15;
+  const int fq = lane >> 4;
+  char* ring = smem + 2 * C21_PATCH;
+  char* w8 = ring + 2 * C21_SLOT;            // [18 steps][64 lanes][16 B]
+
+  // ---- this block's units: XCD-grouped contiguous range ----
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int u_begin = (int)((long long)wgid * p.n_units / nwg);
+  const int u_end = (int)((long long)(wgid + 1) * p.n_units / nwg);
+  const int F = (u_end - u_begin) * p.T;
+
+  // zero pad planes 18, 19 of both slots; ninth spatial tile -> LDS
+  for (int i = tid; i < 2 * 2 * C21_PLANE / 16; i += 512) {
+    const int slot = i / (2 * C21_PLANE / 16), r = i - slot * (2 * C21_PLANE / 16);
+    *(i32x4v*)(ring + slot * C21_SLOT + 18 * C21_PLANE + r * 16) = (i32x4v){0, 0, 0, 0};
+  }
+  {
+    const uint16_t* w8g = p.ws + (size_t)(128 + frow) * p.ks_pad + 8 * fq;
+    for (int s = wave; s < C21_NS; s += 8)
+      *(bf16x8*)(w8 + (s * 64 + lane) * 16) = *(const bf16x8*)(w8g + 32 * s);
+  }
+
+  if (spatial) {
+    // ======================= spatial waves =======================
+    bf16x8 wv[2][C21_NS];
+    {
+      const uint16_t* wr = p.ws + (size_t)(32 * wq + frow) * p.ks_pad + 8 * fq;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < C21_NS; ++s)
+          wv[t][s] = *(const bf16x8*)(wr + (size_t)16 * t * p.ks_pad + 32 * s);
+    }
+    const f32x4 bs0 = *(const f32x4*)(p.bs + 32 * wq + 4 * fq);
+    const f32x4 bs1 = *(const f32x4*)(p.bs + 32 * wq + 16 + 4 * fq);
+    const f32x4 bs8 = *(const f32x4*)(p.bs + 128 + 4 * fq);
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+    const int lrow = lane >> 3;
+    const int kc = (lane & 7) ^ lrow;        // swizzle on the DMA source side
+    // patch pixel q = pr * 64 + pc <-> image (h0 - 1 + pr, pc - 1) of frame t
+    auto issue_patch = [&](int unit, int t, int buf) {
+      const int n = c21div(unit, p.mB, p.sB);
+      const int h0 = (unit - n * p.bands) * C21_ROWS;
+      const int fbase = (n * p.T + t) * p.H;
+#pragma unroll
+      for (int i = 0; i < C21_PI; ++i) {
+        const int instr = wq + 4 * i;
+        const int q = instr * 8 + lrow;
+        const int h = h0 - 1 + q / C21_PITCH, wc = q % C21_PITCH - 1;
+        const uint32_t off = ((unsigned)h < (unsigned)p.H && (unsigned)wc < (unsigned)p.W)
+                                 ? (uint32_t)((((fbase + h) * p.W + wc) * 64 + kc * 8) * 2)
+                                 : C21_INVALID;
+        if (!C21_X(3))
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              xr,
+              (__attribute__((address_space(3))) void*)(smem + buf * C21_PATCH + instr * 1024),
+              16, off, 0, 0, 0);
+      }
+    };
+    if (F > 0) issue_patch(u_begin, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    int unit = u_begin, t = 0;
+    for (int s = 0; s <= F; ++s) {
+      if (s < F) {
+        // next frame's patch into the other buffer (read by the previous step)
+        int nu = unit, nt = t + 1;
+        if (nt == p.T) { nt = 0; ++nu; }
+        if (nu < u_end) issue_patch(nu, nt, (s + 1) & 1);
+        const int n = c21div(unit, p.mB, p.sB);
+        const int h0 = (unit - n * p.bands) * C21_ROWS;
+        const int npx = min(C21_ROWS, p.H - h0) * p.W;
+        const int nch = (npx + 15) >> 4;
+        const uint32_t pb = (uint32_t)((s & 1) * C21_PATCH);
+        char* slot = ring + (s & 1) * C21_SLOT;
+        constexpr int PF = 4, RING = PF + 1;
+        for (int c = 0; c < (C21_X(1) ? 0 : nch); ++c) {
+          const bool own8 = (c & 3) == wq;
+          uint32_t base[3][2];
+          {
+            const int i = min(c * 16 + frow, npx - 1);
+            const int hh = c21div(i, p.mW, p.sW);
+            const int q0 = hh * C21_PITCH + (i - hh * p.W);
+#pragma unroll
+            for (int dw = 0; dw < 3; ++dw) {
+              const uint32_t rel =
+                  (uint32_t)(q0 + dw) * 128u + (uint32_t)((fq ^ ((q0 + dw) & 7)) << 4);
+              base[dw][0] = pb + rel;
+              base[dw][1] = pb + (rel ^ 64u);
+            }
+          }
+          auto load_b = [&](int k) -> bf16x8 {
+            const int tap = k >> 1;
+            return *(const bf16x8*)(smem + base[tap % 3][k & 1] + (tap / 3) * C21_PITCH * 128);
+          };
+          auto load_a8 = [&](int k) -> bf16x8 {
+            return *(const bf16x8*)(w8 + (k * 64 + lane) * 16);
+          };
+          f32x4 acc0 = bs0, acc1 = bs1, acc8 = bs8;
+          bf16x8 bq[RING];
+#pragma unroll
+          for (int k = 0; k < PF; ++k) bq[k] = load_b(k);
+          if (own8) {
+            bf16x8 aq[RING];
+#pragma unroll
+            for (int k = 0; k < PF; ++k) aq[k] = load_a8(k);
+#pragma unroll
+            for (int k = 0; k < C21_NS; ++k) {
+              if (k + PF < C21_NS) {
+                bq[(k + PF) % RING] = load_b(k + PF);
+                aq[(k + PF) % RING] = load_a8(k + PF);
+              }
+              const bf16x8 bv = bq[k % RING];
+              acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[0][k], bv, acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[1][k], bv, acc1, 0, 0, 0);
+              acc8 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[k % RING], bv, acc8, 0, 0, 0);
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < C21_NS; ++k) {
+              if (k + PF < C21_NS) bq[(k + PF) % RING] = load_b(k + PF);
+              const bf16x8 bv = bq[k % RING];
+              acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[0][k], bv, acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[1][k], bv, acc1, 0, 0, 0);
+            }
+          }
+          // ReLU -> bf16 -> ring: channels 32 wq + 8 fq .. +7 of pixel i
+          // (plane 4 wq + fq); ninth tile: channels 128 + 4 fq .. +3
+          const int i = c * 16 + frow;
+          i32x4v o;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            o[j] = (int)ep_pack(ep_relu(acc0[2 * j]), ep_relu(acc0[2 * j + 1]));
+            o[2 + j] = (int)ep_pack(ep_relu(acc1[2 * j]), ep_relu(acc1[2 * j + 1]));
+          }
+          *(i32x4v*)(slot + (4 * wq + fq) * C21_PLANE + i * 16) = o;
+          if (own8) {
+            i32x2v o8;
+            o8[0] = (int)ep_pack(ep_relu(acc8[0]), ep_relu(acc8[1]));
+            o8[1] = (int)ep_pack(ep_relu(acc8[2]), ep_relu(acc8[3]));
+            *(i32x2v*)(slot + (16 + (fq >> 1)) * C21_PLANE + i * 16 + (fq & 1) * 8) = o8;
+          }
+        }
+        unit = nu;
+        t = nt;
+        // the next patch has landed, the intermediate is in the ring
+        if (!C21_X(5)) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+    }
+  } else {
+    // ======================= temporal waves =======================
+    // physical output tile wq: rows 16 wq + 4 fq .. +3 = channels
+    // 32 (wq >> 1) + 8 fq + 4 (wq & 1) .. +3 (pair permutation)
+    bf16x8 wtv[C21_KT];
+    {
+      const uint16_t* wt = p.wt + (size_t)(16 * wq + frow) * 480 + 8 * fq;
+#pragma unroll
+      for (int k = 0; k < C21_KT; ++k) wtv[k] = *(const bf16x8*)(wt + 32 * k);
+    }
+    const f32x4 bt = *(const f32x4*)(p.bt + 16 * wq + 4 * fq);
+    const int ch = 32 * (wq >> 1) + 8 * fq + 4 * (wq & 1);
+    const EpCtx e = ep_make(p.y, p.y_stride, p.res, p.res_stride,
+                            (long long)p.N * p.T * p.H * p.W, 64, p.relu != 0);
+    f32x4 accP[C21S_CH], accC[C21S_CH], accN[C21S_CH];
+#pragma unroll
+    for (int c = 0; c < C21S_CH; ++c) accP[c] = accC[c] = accN[c] = bt;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    int unit = u_begin, t = 0;
+    for (int s = 0; s <= F; ++s) {
+      if (s >= 1) {
+        // consume mid[t] of (unit, t) = frame s - 1, ring slot (s - 1) & 1
+        const int n = c21div(unit, p.mB, p.sB);
+        const int h0 = (unit - n * p.bands) * C21_ROWS;
+        const int npx = min(C21_ROWS, p.H - h0) * p.W;
+        const int nch = (npx + 15) >> 4;
+        const bool doP = t >= 1, doN = t + 1 < p.T, last = t + 1 == p.T;
+        const long long mP = ((long long)(n * p.T + t - 1) * p.H + h0) * p.W;
+        const long long mC = mP + (long long)p.H * p.W;
+        // residuals of the outputs this step completes, loaded before the MFMAs
+        ep_i32x2 rP[C21S_CH], rC[C21S_CH];
+#pragma unroll
+        for (int c = 0; c < C21S_CH; ++c) rP[c] = rC[c] = (ep_i32x2){0, 0};
+        if (e.has_res && doP && !C21_X(4)) {
+#pragma unroll
+          for (int c = 0; c < C21S_CH; ++c) {
+            const int i = c * 16 + frow;
+            rP[c] = __builtin_amdgcn_raw_buffer_load_b64(
+                e.res, ep_off(i < npx, mP + i, e.res_stride, ch), 0, 0);
+          }
+        }
+        const char* src = ring + ((s - 1) & 1) * C21_SLOT + fq * C21_PLANE + frow * 16;
+        // one straight-line body per (previous, next output frame) case
+        auto consume = [&](auto P_, auto N_) {
+          constexpr bool P = decltype(P_)::value, N = decltype(N_)::value;
+          // (no cross-chunk prefetch: the SIMD's spatial wave hides this
+          // wave's LDS latency, and the registers are needed for accumulators)
+#pragma unroll
+          for (int c = 0; c < C21S_CH; ++c) {
+            if (c < nch) {
+              bf16x8 b[5];
+#pragma unroll
+              for (int k = 0; k < 5; ++k)
+                b[k] = *(const bf16x8*)(src + k * 4 * C21_PLANE + c * 256);
+#pragma unroll
+              for (int k = 0; k < 5; ++k) {
+                if (P)
+                  accP[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wtv[10 + k], b[k],
+                                                                    accP[c], 0, 0, 0);
+                accC[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wtv[5 + k], b[k], accC[c],
+                                                                  0, 0, 0);
+                if (N)
+                  accN[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wtv[k], b[k], accN[c],
+                                                                    0, 0, 0);
+              }
+            }
+          }
+        };
+        using T1 = std::integral_constant<bool, true>;
+        using F0 = std::integral_constant<bool, false>;
+        if (!C21_X(2)) {
+          if (doP && doN) consume(T1{}, T1{});
+          else if (doP) consume(T1{}, F0{});
+          else if (doN) consume(F0{}, T1{});
+          else consume(F0{}, F0{});
+        }
+        // out[t - 1] is complete; at the clip's last frame out[t] as well
+        if (doP) {
+#pragma unroll
+          for (int c = 0; c < C21S_CH; ++c) {
+            const int i = c * 16 + frow;
+            ep_out4(e, ep_off(i < npx, mP + i, e.y_stride, ch), accP[c], rP[c], !C21_X(4));
+          }
+        }
+        if (last) {
+          // (once per clip: these loads' latency is exposed, but their
+          // registers are free during the MFMAs)
+          if (e.has_res && !C21_X(4)) {
+#pragma unroll
+            for (int c = 0; c < C21S_CH; ++c) {
+              const int i = c * 16 + frow;
+              rC[c] = __builtin_amdgcn_raw_buffer_load_b64(
+                  e.res, ep_off(i < npx, mC + i, e.res_stride, ch), 0, 0);
+            }
+          }
+#pragma unroll
+          for (int c = 0; c < C21S_CH; ++c) {
+            const int i = c * 16 + frow;
+            ep_out4(e, ep_off(i < npx, mC + i, e.y_stride, ch), accC[c], rC[c], !C21_X(4));
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < C21S_CH; ++c) {
+          accP[c] = accC[c];
+          accC[c] = accN[c];
+          accN[c] = bt;
+        }
+        if (++t == p.T) { t = 0; ++unit; }
+      }
+      if (s < F && !C21_X(5)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
   }
 }
@@ -369,7 +705,7 @@ int rnb_conv21_launch(const Conv21Params* pp, hipStream_t stream) {
   c21_magic((uint32_t)p.W, &p.mW, &p.sW);
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)conv21_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv21_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                         160 * 1024);
     attr_set = true;
   }
@@ -379,4 +715,32 @@ int rnb_conv21_launch(const Conv21Params* pp, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// role-specialised variant (8 waves: 4 spatial + 4 temporal), same arguments
+int rnb_conv21s_launch(const Conv21Params* pp, hipStream_t stream) {
+  Conv21Params p = *pp;
+  if (!rnb_conv21_supported(p.T, p.H, p.W)) return -3;
+  if (p.ks_pad < 9 * 64 || p.y_stride < 64 || (p.res && p.res_stride < 64)) return -2;
+  if (p.N <= 0) return 0;
+  const long long M = (long long)p.N * p.T * p.H * p.W;
+  if (M * 64 * 2 > 0x7FFFFF00LL) return -5;
+  if (M * p.y_stride * 2 > 0xFFFFFF00LL || M * (p.res ? p.res_stride : 0) * 2 > 0xFFFFFF00LL)
+    return -7;
+  p.bands = (p.H + C21_ROWS - 1) / C21_ROWS;
+  p.n_units = p.N * p.bands;
+  p.x_bytes = (uint32_t)(M * 64 * 2);
+  c21_magic((uint32_t)p.bands, &p.mB, &p.sB);
+  c21_magic((uint32_t)p.W, &p.mW, &p.sW);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)conv21s_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    attr_set = true;
+  }
+  int grid = c21_num_cus();
+  if (grid > p.n_units) grid = p.n_units;
+  hipLaunchKernelGGL(conv21s_kernel, dim3((unsigned)grid), dim3(512), C21S_LDS, stream, p);
+  return (int)hipGetLastError();
+}
+
 }  // extern "C"
+

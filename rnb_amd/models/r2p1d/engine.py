@@ -269,10 +269,14 @@ class R2P1DEngine:
             nxt = self.ops[i + 1]
             src = bufs[op.src]
             res = bufs[nxt.res] if nxt.res is not None else None
-            t_fused = _time(lambda: op.fuse.forward_hip(src, res), reps)
-            t_split = _time(lambda: nxt.layer.forward_hip(op.layer.forward_hip(src), res), reps)
-            op.fuse._use[tuple(src.shape[:4])] = t_fused <= t_split
-            chosen[op.fuse.name] = int(t_fused <= t_split)
+            best, t_best = None, _time(
+                lambda: nxt.layer.forward_hip(op.layer.forward_hip(src), res), reps)
+            for v in op.fuse.VARIANTS:
+                t = _time(lambda: op.fuse.forward_hip(src, res, variant=v), reps)
+                if t < t_best:
+                    best, t_best = v, t
+            op.fuse.set_choice(src.shape, best)
+            chosen[op.fuse.name] = -1 if best is None else best
         torch.cuda.synchronize(self.device)
         return chosen
 

@@ -42,9 +42,10 @@ class FusedSTConv:
         self.wt = wt.reshape(64, 3 * MID_PAD).contiguous()
         self.bt = temporal.bias[:64].contiguous()
         self.relu = temporal.relu
-        self._use: Dict[Tuple[int, int, int, int], bool] = {}
+        # per input shape: 0 = two-kernel path, else kernel variant + 1
+        self._use: Dict[Tuple[int, int, int, int], int] = {}
         self.enabled = True
-        self._default = False
+        self._default = 0
 
     @staticmethod
     def eligible(spatial: ConvLayer, temporal: ConvLayer) -> bool:
@@ -59,21 +60,31 @@ class FusedSTConv:
         N, T, H, W, C = x_shape
         return C == 64 and kernels().conv21_supported(T, H, W)
 
+    VARIANTS = (1, 0)     # conv21.hip: 1 = role-specialised 8 waves, 0 = 4 waves
+
     def use_for(self, x_shape) -> bool:
         """Fused path for this input shape. Off until the engine's autotune
         times it against the two tuned kernels (``R2P1DEngine.autotune``), or
         on for every supported shape after ``force(True)``."""
+        return self.variant_for(x_shape) is not None
+
+    def variant_for(self, x_shape) -> Optional[int]:
+        """Kernel variant serving this shape, or None for the two-kernel path."""
         if not self.enabled:
-            return False
+            return None
         key = tuple(x_shape[:4])
         use = self._use.get(key)
         if use is None:
-            use = self._use[key] = self._default and self.supported(x_shape)
-        return use
+            use = self._use[key] = self._default if self.supported(x_shape) else 0
+        return use - 1 if use else None
 
-    def force(self, on: bool) -> None:
+    def set_choice(self, x_shape, variant: Optional[int]) -> None:
+        """Record the autotuner's pick for this shape (None = two kernels)."""
+        self._use[tuple(x_shape[:4])] = 0 if variant is None else variant + 1
+
+    def force(self, on: bool, variant: int = 1) -> None:
         """Use (or never use) the fused kernel for every supported shape."""
-        self._default = on
+        self._default = variant + 1 if on else 0
         self._use.clear()
 
     def out_shape(self, x_shape):
@@ -81,8 +92,9 @@ class FusedSTConv:
         return (N, T, H, W, 64)
 
     def forward_hip(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        from .native import Conv21Params, kernels
+                    out: Optional[torch.Tensor] = None,
+                    variant: Optional[int] = None) -> torch.Tensor:
+        from .native import kernels
         if x.dtype != torch.bfloat16 or not x.is_contiguous() or x.shape[-1] != 64:
             raise ValueError("%s: expected contiguous bf16 NDHWC input with 64 channels"
                              % self.name)
@@ -94,6 +106,19 @@ class FusedSTConv:
                                      or residual.shape[-1] < 64):
             raise ValueError("%s: residual %s does not match output %s"
                              % (self.name, tuple(residual.shape), tuple(y.shape)))
+        if variant is None:
+            variant = self.variant_for(x.shape)
+            if variant is None:
+                variant = self.VARIANTS[0]
+        p = self.params(x, y, residual)
+        kernels().conv21(p, torch.cuda.current_stream(x.device).cuda_stream, variant)
+        return y
+
+    def params(self, x: torch.Tensor, y: torch.Tensor,
+               residual: Optional[torch.Tensor] = None):
+        """Kernel arguments (``struct Conv21Params``) for x -> y."""
+        from .native import Conv21Params
+        N, T, H, W, _ = x.shape
         s = self.spatial
         p = Conv21Params()
         p.x = x.data_ptr()
@@ -106,8 +131,7 @@ class FusedSTConv:
         p.y_stride = y.shape[-1]
         p.res_stride = residual.shape[-1] if residual is not None else 0
         p.relu = 1 if self.relu else 0
-        kernels().conv21(p, torch.cuda.current_stream(x.device).cuda_stream)
-        return y
+        return p
 
     def forward_torch(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None):
         return self.temporal.forward_torch(self.spatial.forward_torch(x), residual)

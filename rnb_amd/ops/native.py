@@ -201,6 +201,8 @@ class Kernels:
         lib.rnb_temporal_lds_bytes.argtypes = [ctypes.c_int] * 3
         lib.rnb_conv21_launch.argtypes = [ctypes.POINTER(Conv21Params), ctypes.c_void_p]
         lib.rnb_conv21_launch.restype = ctypes.c_int
+        lib.rnb_conv21s_launch.argtypes = [ctypes.POINTER(Conv21Params), ctypes.c_void_p]
+        lib.rnb_conv21s_launch.restype = ctypes.c_int
         lib.rnb_conv21_supported.argtypes = [ctypes.c_int] * 3
         if lib.rnb_conv21_params_size() != ctypes.sizeof(Conv21Params):
             raise NativeUnavailable("Conv21Params layout mismatch: rebuild")
@@ -234,9 +236,11 @@ class Kernels:
         _check(self.lib.rnb_temporal_launch(ctypes.byref(params), num_cus, blocks_per_cu,
                                             stream), "conv_temporal")
 
-    def conv21(self, params: Conv21Params, stream: int) -> None:
-        """Fused spatial 1x3x3 (64 -> 144) + temporal 3x1x1 (144 -> 64)."""
-        _check(self.lib.rnb_conv21_launch(ctypes.byref(params), stream), "conv21")
+    def conv21(self, params: Conv21Params, stream: int, variant: int = 1) -> None:
+        """Fused spatial 1x3x3 (64 -> 144) + temporal 3x1x1 (144 -> 64).
+        variant 1: role-specialised 8-wave kernel (conv21s), 0: 4-wave kernel."""
+        fn = self.lib.rnb_conv21s_launch if variant == 1 else self.lib.rnb_conv21_launch
+        _check(fn(ctypes.byref(params), stream), "conv21 (variant %d)" % variant)
 
     def conv21_supported(self, T: int, H: int, W: int) -> bool:
         return bool(self.lib.rnb_conv21_supported(T, H, W))

@@ -29,7 +29,7 @@ def build():
     procs = []
     for v in VARIANTS:
         out = os.path.join(EXP_DIR, "libexp%d.so" % v)
-        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wl,-Bsymbolic",
                "-DHALO_EXP=%d" % v, "-DCONV_EXP=%d" % v, "-DTEMP_EXP=%d" % v,
                "-DWS_EXP=%d" % v, os.path.join(ROOT, "csrc", "conv_halo_ws.hip"),
                os.path.join(ROOT, "csrc", "conv_igemm.hip"),

@@ -78,7 +78,8 @@ def main():
             N, T, H, W, _ = src.shape
             flops = op.fuse.flops(N, T, H, W)
             rows.append({"name": op.fuse.name, "M": N * T * H * W, "N": 144, "K": 576,
-                         "tile": "conv21", "ms": ms, "tflops": flops / ms / 1e9,
+                         "tile": "conv21s" if op.fuse.variant_for(src.shape) == 1 else "conv21",
+                         "ms": ms, "tflops": flops / ms / 1e9,
                          "gflop": flops / 1e9})
             bufs[nxt.dst] = y
             skip = True

@@ -35,6 +35,7 @@ def _x(shape, integer=True, seed=1):
     return x.to(torch.bfloat16).to(DEV)
 
 
+@pytest.mark.parametrize("variant", [1, 0])
 @pytest.mark.parametrize("n,thw,with_res", [
     (2, (8, 56, 56), True),      # conv2 block conv2: residual + ReLU
     (2, (8, 56, 56), False),     # conv2 block conv1
@@ -42,13 +43,13 @@ def _x(shape, integer=True, seed=1):
     (1, (1, 4, 56), False),      # single frame, widest supported W
     (12, (2, 56, 56), True),     # 336 units: several per persistent block
 ])
-def test_conv21_exact(n, thw, with_res):
+def test_conv21_exact(n, thw, with_res, variant):
     f = _pair()
     x = _x((n,) + thw + (64,))
     res = _x((n,) + thw + (64,), seed=5) if with_res else None
     assert f.supported(x.shape)
     ref = f.forward_torch(x, res)
-    y = f.forward_hip(x, res)
+    y = f.forward_hip(x, res, variant=variant)
     split = f.temporal.forward_hip(f.spatial.forward_hip(x), res)
     torch.cuda.synchronize()
     assert torch.equal(split, ref)
@@ -61,11 +62,12 @@ def test_conv21_rejects_wide_frames():
     assert not f.use_for((1, 2, 4, 57, 64))
 
 
-def test_conv21_random_weights_close_to_fp32():
+@pytest.mark.parametrize("variant", [1, 0])
+def test_conv21_random_weights_close_to_fp32(variant):
     f = _pair(integer=False)
     x = _x((2, 8, 56, 56, 64), integer=False)
     res = _x((2, 8, 56, 56, 64), integer=False, seed=3)
-    y = f.forward_hip(x, res).float()
+    y = f.forward_hip(x, res, variant=variant).float()
     # fp32 intermediate (no bf16 rounding between the convs)
     s, t = f.spatial, f.temporal
     xin = x.float().permute(0, 4, 1, 2, 3)
