@@ -46,7 +46,10 @@ typedef int i32x4v __attribute__((ext_vector_type(4)));
 // bottleneck experiments (scripts/c21_exp.py; results are garbage by design):
 // 1 no spatial phase, 2 no temporal phase, 3 no patch DMA after the first,
 // 4 no global stores / residual loads, 5 no waits + barriers,
-// 6 spatial phase only (2 + 3 + 4)
+// 6 spatial phase only (2 + 3 + 4); conv21s only: 7 temporal residual loads /
+// stores at lane-linear addresses (whole lines, same bytes), 8 no residual loads,
+// 9 = product with the spatial waves at raised issue priority, 10 = product
+// with the spatial B prefetch 8 K-steps ahead (instead of 5)
 #ifndef C21_EXP
 #define C21_EXP 0
 #endif
@@ -379,7 +382,7 @@ void conv21_kernel(const Conv21Params p) {
 // 16 w .. +15 of the pair-permuted matrix -> 4 consecutive channels per
 // lane, 8-byte stores) for all of the unit's <= 7 pixel chunks.
 // ===========================================================================
-#define C21S_LDS (2 * C21_PATCH + 2 * C21_SLOT + C21_W8)     // 152 KB
+#define C21S_LDS (2 * C21_PATCH + 2 * C21_SLOT + C21_W8 + 576)   // 153 KB (+ spatial bias)
 #define C21S_CH 7                                            // chunks per unit (112 px)
 
 __global__ __launch_bounds__(512, 1)
@@ -412,10 +415,12 @@ void conv21s_kernel(const Conv21Params p) {
     const uint16_t* w8g = p.ws + (size_t)(128 + frow) * p.ks_pad + 8 * fq;
     for (int s = wave; s < C21_NS; s += 8)
       *(bf16x8*)(w8 + (s * 64 + lane) * 16) = *(const bf16x8*)(w8g + 32 * s);
+    if (tid < 144) ((float*)(w8 + C21_W8))[tid] = p.bs[tid];
   }
 
   if (spatial) {
     // ======================= spatial waves =======================
+    if (C21_X(9)) __builtin_amdgcn_s_setprio(3);   // the critical path issues first
     bf16x8 wv[2][C21_NS];
     {
       const uint16_t* wr = p.ws + (size_t)(32 * wq + frow) * p.ks_pad + 8 * fq;
@@ -425,31 +430,40 @@ void conv21s_kernel(const Conv21Params p) {
         for (int s = 0; s < C21_NS; ++s)
           wv[t][s] = *(const bf16x8*)(wr + (size_t)16 * t * p.ks_pad + 32 * s);
     }
-    const f32x4 bs0 = *(const f32x4*)(p.bs + 32 * wq + 4 * fq);
-    const f32x4 bs1 = *(const f32x4*)(p.bs + 32 * wq + 16 + 4 * fq);
-    const f32x4 bs8 = *(const f32x4*)(p.bs + 128 + 4 * fq);
-    const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+    // the spatial bias (the accumulators' initial value) is re-read from LDS
+    // per chunk: registers go to the B-fragment prefetch ring instead
+    const float* bias_l = (const float*)(w8 + C21_W8);
     const int lrow = lane >> 3;
     const int kc = (lane & 7) ^ lrow;        // swizzle on the DMA source side
-    // patch pixel q = pr * 64 + pc <-> image (h0 - 1 + pr, pc - 1) of frame t
+    // patch pixel q = pr * 64 + pc <-> image (h0 - 1 + pr, pc - 1). A piece's
+    // in-frame byte offset depends only on the unit, so it is computed once
+    // per unit (8 VGPRs); per frame only the buffer resource moves (SALU).
+    const uint32_t frame_bytes = (uint32_t)(p.H * p.W * 128);
     auto issue_patch = [&](int unit, int t, int buf) {
       const int n = c21div(unit, p.mB, p.sB);
-      const int h0 = (unit - n * p.bands) * C21_ROWS;
-      const int fbase = (n * p.T + t) * p.H;
+      uint32_t doff[C21_PI];
+      {
+        const int h0 = (unit - n * p.bands) * C21_ROWS;
+#pragma unroll
+        for (int i = 0; i < C21_PI; ++i) {
+          const int q = (wq + 4 * i) * 8 + lrow;
+          const int h = h0 - 1 + (q >> 6), wc = (q & 63) - 1;
+          doff[i] = ((unsigned)h < (unsigned)p.H && (unsigned)wc < (unsigned)p.W)
+                        ? (uint32_t)((h * p.W + wc) * 128 + kc * 16)
+                        : C21_INVALID;
+        }
+      }
+      const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((const char*)p.x + (size_t)(n * p.T + t) * frame_bytes), (short)0,
+          frame_bytes, 0x00020000);
 #pragma unroll
       for (int i = 0; i < C21_PI; ++i) {
-        const int instr = wq + 4 * i;
-        const int q = instr * 8 + lrow;
-        const int h = h0 - 1 + q / C21_PITCH, wc = q % C21_PITCH - 1;
-        const uint32_t off = ((unsigned)h < (unsigned)p.H && (unsigned)wc < (unsigned)p.W)
-                                 ? (uint32_t)((((fbase + h) * p.W + wc) * 64 + kc * 8) * 2)
-                                 : C21_INVALID;
         if (!C21_X(3))
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
               xr,
-              (__attribute__((address_space(3))) void*)(smem + buf * C21_PATCH + instr * 1024),
-              16, off, 0, 0, 0);
+              (__attribute__((address_space(3))) void*)(smem + buf * C21_PATCH +
+                                                        (wq + 4 * i) * 1024),
+              16, doff[i], 0, 0, 0);
       }
     };
     if (F > 0) issue_patch(u_begin, 0, 0);
@@ -467,56 +481,88 @@ void conv21s_kernel(const Conv21Params p) {
         const int nch = (npx + 15) >> 4;
         const uint32_t pb = (uint32_t)((s & 1) * C21_PATCH);
         char* slot = ring + (s & 1) * C21_SLOT;
-        constexpr int PF = 4, RING = PF + 1;
+        // B fragments prefetched PF K-steps ahead ACROSS chunk boundaries
+        // (RING divides the 18 K-steps, so a step's ring slot is the same in
+        // every chunk); the ninth tile's A fragments APF steps ahead within
+        // the chunk. sched_group_barrier pins the issue order: left alone,
+        // the scheduler sinks every read next to its MFMAs and the lone
+        // spatial wave of the SIMD waits out each read's LDS latency.
+        constexpr int PF = C21_X(10) ? 8 : 5, RING = PF + 1, APF = C21_X(10) ? 2 : 3, ARING = APF + 1;
+        static_assert(C21_NS % RING == 0, "ring slot must repeat per chunk");
+        auto chunk_base = [&](int c, uint32_t (*bs)[2]) {
+          // a unit has at most 2 image rows: row = (i >= W), no division
+          const int i = min(c * 16 + frow, npx - 1);
+          const int q0 = i + (i >= p.W ? C21_PITCH - p.W : 0);
+#pragma unroll
+          for (int dw = 0; dw < 3; ++dw) {
+            const uint32_t q = (uint32_t)(q0 + dw);
+            const uint32_t rel = (q << 7) | (((q ^ (uint32_t)fq) & 7u) << 4);
+            bs[dw][0] = pb + rel;
+            bs[dw][1] = pb + (rel ^ 64u);
+          }
+        };
+        auto load_b = [&](const uint32_t (*bs)[2], int k) -> bf16x8 {
+          const int tap = k >> 1;
+          return *(const bf16x8*)(smem + bs[tap % 3][k & 1] + (tap / 3) * C21_PITCH * 128);
+        };
+        auto load_a8 = [&](int k) -> bf16x8 {
+          return *(const bf16x8*)(w8 + (k * 64 + lane) * 16);
+        };
+        uint32_t base[3][2], nbase[3][2];
+        bf16x8 bq[RING];
+        chunk_base(0, base);
+#pragma unroll
+        for (int k = 0; k < PF; ++k) bq[k] = load_b(base, k);
         for (int c = 0; c < (C21_X(1) ? 0 : nch); ++c) {
           const bool own8 = (c & 3) == wq;
-          uint32_t base[3][2];
-          {
-            const int i = min(c * 16 + frow, npx - 1);
-            const int hh = c21div(i, p.mW, p.sW);
-            const int q0 = hh * C21_PITCH + (i - hh * p.W);
-#pragma unroll
-            for (int dw = 0; dw < 3; ++dw) {
-              const uint32_t rel =
-                  (uint32_t)(q0 + dw) * 128u + (uint32_t)((fq ^ ((q0 + dw) & 7)) << 4);
-              base[dw][0] = pb + rel;
-              base[dw][1] = pb + (rel ^ 64u);
-            }
-          }
-          auto load_b = [&](int k) -> bf16x8 {
-            const int tap = k >> 1;
-            return *(const bf16x8*)(smem + base[tap % 3][k & 1] + (tap / 3) * C21_PITCH * 128);
-          };
-          auto load_a8 = [&](int k) -> bf16x8 {
-            return *(const bf16x8*)(w8 + (k * 64 + lane) * 16);
-          };
-          f32x4 acc0 = bs0, acc1 = bs1, acc8 = bs8;
-          bf16x8 bq[RING];
-#pragma unroll
-          for (int k = 0; k < PF; ++k) bq[k] = load_b(k);
+          // (past the last chunk: harmless re-reads of the last chunk)
+          chunk_base(min(c + 1, nch - 1), nbase);
+          f32x4 acc0 = *(const f32x4*)(bias_l + 32 * wq + 4 * fq);
+          f32x4 acc1 = *(const f32x4*)(bias_l + 32 * wq + 16 + 4 * fq);
+          f32x4 acc8 = *(const f32x4*)(bias_l + 128 + 4 * fq);
           if (own8) {
-            bf16x8 aq[RING];
+            bf16x8 aq[ARING];
 #pragma unroll
-            for (int k = 0; k < PF; ++k) aq[k] = load_a8(k);
+            for (int k = 0; k < APF; ++k) aq[k] = load_a8(k);
 #pragma unroll
             for (int k = 0; k < C21_NS; ++k) {
-              if (k + PF < C21_NS) {
-                bq[(k + PF) % RING] = load_b(k + PF);
-                aq[(k + PF) % RING] = load_a8(k + PF);
-              }
+              bq[(k + PF) % RING] =
+                  k + PF < C21_NS ? load_b(base, k + PF) : load_b(nbase, k + PF - C21_NS);
+              if (k + APF < C21_NS) aq[(k + APF) % ARING] = load_a8(k + APF);
               const bf16x8 bv = bq[k % RING];
               acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[0][k], bv, acc0, 0, 0, 0);
               acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[1][k], bv, acc1, 0, 0, 0);
-              acc8 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[k % RING], bv, acc8, 0, 0, 0);
+              acc8 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[k % ARING], bv, acc8, 0, 0, 0);
+            }
+#pragma unroll
+            for (int k = 0; k < C21_NS - APF; ++k) {
+              __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+            }
+#pragma unroll
+            for (int k = C21_NS - APF; k < C21_NS; ++k) {
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
             }
           } else {
 #pragma unroll
             for (int k = 0; k < C21_NS; ++k) {
-              if (k + PF < C21_NS) bq[(k + PF) % RING] = load_b(k + PF);
+              bq[(k + PF) % RING] =
+                  k + PF < C21_NS ? load_b(base, k + PF) : load_b(nbase, k + PF - C21_NS);
               const bf16x8 bv = bq[k % RING];
               acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[0][k], bv, acc0, 0, 0, 0);
               acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[1][k], bv, acc1, 0, 0, 0);
             }
+#pragma unroll
+            for (int k = 0; k < C21_NS; ++k) {
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            }
+          }
+#pragma unroll
+          for (int dw = 0; dw < 3; ++dw) {
+            base[dw][0] = nbase[dw][0];
+            base[dw][1] = nbase[dw][1];
           }
           // ReLU -> bf16 -> ring: channels 32 wq + 8 fq .. +7 of pixel i
           // (plane 4 wq + fq); ninth tile: channels 128 + 4 fq .. +3
@@ -555,102 +601,106 @@ void conv21s_kernel(const Conv21Params p) {
     const int ch = 32 * (wq >> 1) + 8 * fq + 4 * (wq & 1);
     const EpCtx e = ep_make(p.y, p.y_stride, p.res, p.res_stride,
                             (long long)p.N * p.T * p.H * p.W, 64, p.relu != 0);
-    f32x4 accP[C21S_CH], accC[C21S_CH], accN[C21S_CH];
+    // Two accumulator sets whose roles alternate per step: X holds out[t-1]
+    // (P), which is stored as soon as its last contribution is in, and then
+    // receives out[t+1] = bias + W_0 mid[t] (N) in the same registers; Y holds
+    // out[t] (C). Next step P = Y and C = X: no register moves.
+    f32x4 accA[C21S_CH], accB[C21S_CH];
 #pragma unroll
-    for (int c = 0; c < C21S_CH; ++c) accP[c] = accC[c] = accN[c] = bt;
+    for (int c = 0; c < C21S_CH; ++c) accA[c] = accB[c] = bt;
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     int unit = u_begin, t = 0;
-    for (int s = 0; s <= F; ++s) {
-      if (s >= 1) {
-        // consume mid[t] of (unit, t) = frame s - 1, ring slot (s - 1) & 1
-        const int n = c21div(unit, p.mB, p.sB);
-        const int h0 = (unit - n * p.bands) * C21_ROWS;
-        const int npx = min(C21_ROWS, p.H - h0) * p.W;
-        const int nch = (npx + 15) >> 4;
-        const bool doP = t >= 1, doN = t + 1 < p.T, last = t + 1 == p.T;
-        const long long mP = ((long long)(n * p.T + t - 1) * p.H + h0) * p.W;
-        const long long mC = mP + (long long)p.H * p.W;
-        // residuals of the outputs this step completes, loaded before the MFMAs
-        ep_i32x2 rP[C21S_CH], rC[C21S_CH];
+    // consume mid[t] of frame (unit, t) from ring slot `slot_i`
+    auto consume = [&](f32x4* X, f32x4* Y, int slot_i) {
+      const int n = c21div(unit, p.mB, p.sB);
+      const int h0 = (unit - n * p.bands) * C21_ROWS;
+      const int npx = min(C21_ROWS, p.H - h0) * p.W;
+      const int nch = (npx + 15) >> 4;
+      const bool doP = t >= 1, last = t + 1 == p.T;
+      const long long mP = ((long long)(n * p.T + t - 1) * p.H + h0) * p.W;
+      const long long mC = mP + (long long)p.H * p.W;
+      if (t == 0) {                          // a new clip: out[0] starts at the bias
 #pragma unroll
-        for (int c = 0; c < C21S_CH; ++c) rP[c] = rC[c] = (ep_i32x2){0, 0};
-        if (e.has_res && doP && !C21_X(4)) {
+        for (int c = 0; c < C21S_CH; ++c) Y[c] = bt;
+      }
+      // residuals of out[t - 1], loaded before the MFMAs
+      // (experiment 7: same bytes, lane-linear addresses = whole 128-B lines)
+      auto lin = [&](int c) -> uint32_t {
+        return (uint32_t)(mP * 128 + ((c * 4 + wq) * 64 + lane) * 8);
+      };
+      ep_i32x2 rP[C21S_CH];
 #pragma unroll
-          for (int c = 0; c < C21S_CH; ++c) {
+      for (int c = 0; c < C21S_CH; ++c) rP[c] = (ep_i32x2){0, 0};
+      if (e.has_res && doP && !C21_X(4) && !C21_X(8)) {
+#pragma unroll
+        for (int c = 0; c < C21S_CH; ++c) {
+          const int i = c * 16 + frow;
+          rP[c] = __builtin_amdgcn_raw_buffer_load_b64(
+              e.res, C21_X(7) ? lin(c) : ep_off(i < npx, mP + i, e.res_stride, ch), 0, 0);
+        }
+      }
+      const char* src = ring + slot_i * C21_SLOT + fq * C21_PLANE + frow * 16;
+#pragma unroll
+      for (int c = 0; c < C21S_CH; ++c) {
+        if (c < nch) {
+          bf16x8 b[5];
+#pragma unroll
+          for (int k = 0; k < 5; ++k)
+            b[k] = *(const bf16x8*)(src + k * 4 * C21_PLANE + c * 256);
+          if (!C21_X(2)) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+              X[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wtv[10 + k], b[k], X[c], 0, 0, 0);
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+              Y[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wtv[5 + k], b[k], Y[c], 0, 0, 0);
+          }
+          // out[t - 1] is complete (at t = 0, X is the previous clip's spent P)
+          if (doP) {
             const int i = c * 16 + frow;
-            rP[c] = __builtin_amdgcn_raw_buffer_load_b64(
-                e.res, ep_off(i < npx, mP + i, e.res_stride, ch), 0, 0);
+            ep_out4(e, C21_X(7) ? lin(c) : ep_off(i < npx, mP + i, e.y_stride, ch), X[c],
+                    rP[c], !C21_X(4));
+          }
+          if (!C21_X(2)) {
+            X[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wtv[0], b[0], bt, 0, 0, 0);
+#pragma unroll
+            for (int k = 1; k < 5; ++k)
+              X[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wtv[k], b[k], X[c], 0, 0, 0);
           }
         }
-        const char* src = ring + ((s - 1) & 1) * C21_SLOT + fq * C21_PLANE + frow * 16;
-        // one straight-line body per (previous, next output frame) case
-        auto consume = [&](auto P_, auto N_) {
-          constexpr bool P = decltype(P_)::value, N = decltype(N_)::value;
-          // (no cross-chunk prefetch: the SIMD's spatial wave hides this
-          // wave's LDS latency, and the registers are needed for accumulators)
+      }
+      if (last) {
+        // out[T - 1] is complete as well (once per clip: these residual
+        // loads' latency is exposed, but their registers are free meanwhile)
+        ep_i32x2 rC[C21S_CH];
 #pragma unroll
-          for (int c = 0; c < C21S_CH; ++c) {
-            if (c < nch) {
-              bf16x8 b[5];
-#pragma unroll
-              for (int k = 0; k < 5; ++k)
-                b[k] = *(const bf16x8*)(src + k * 4 * C21_PLANE + c * 256);
-#pragma unroll
-              for (int k = 0; k < 5; ++k) {
-                if (P)
-                  accP[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wtv[10 + k], b[k],
-                                                                    accP[c], 0, 0, 0);
-                accC[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wtv[5 + k], b[k], accC[c],
-                                                                  0, 0, 0);
-                if (N)
-                  accN[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wtv[k], b[k], accN[c],
-                                                                    0, 0, 0);
-              }
-            }
-          }
-        };
-        using T1 = std::integral_constant<bool, true>;
-        using F0 = std::integral_constant<bool, false>;
-        if (!C21_X(2)) {
-          if (doP && doN) consume(T1{}, T1{});
-          else if (doP) consume(T1{}, F0{});
-          else if (doN) consume(F0{}, T1{});
-          else consume(F0{}, F0{});
-        }
-        // out[t - 1] is complete; at the clip's last frame out[t] as well
-        if (doP) {
-#pragma unroll
-          for (int c = 0; c < C21S_CH; ++c) {
-            const int i = c * 16 + frow;
-            ep_out4(e, ep_off(i < npx, mP + i, e.y_stride, ch), accP[c], rP[c], !C21_X(4));
-          }
-        }
-        if (last) {
-          // (once per clip: these loads' latency is exposed, but their
-          // registers are free during the MFMAs)
-          if (e.has_res && !C21_X(4)) {
-#pragma unroll
-            for (int c = 0; c < C21S_CH; ++c) {
-              const int i = c * 16 + frow;
-              rC[c] = __builtin_amdgcn_raw_buffer_load_b64(
-                  e.res, ep_off(i < npx, mC + i, e.res_stride, ch), 0, 0);
-            }
-          }
-#pragma unroll
-          for (int c = 0; c < C21S_CH; ++c) {
-            const int i = c * 16 + frow;
-            ep_out4(e, ep_off(i < npx, mC + i, e.y_stride, ch), accC[c], rC[c], !C21_X(4));
-          }
+        for (int c = 0; c < C21S_CH; ++c) {
+          const int i = c * 16 + frow;
+          rC[c] = (e.has_res && !C21_X(4))
+                      ? __builtin_amdgcn_raw_buffer_load_b64(
+                            e.res, ep_off(i < npx, mC + i, e.res_stride, ch), 0, 0)
+                      : (ep_i32x2){0, 0};
         }
 #pragma unroll
         for (int c = 0; c < C21S_CH; ++c) {
-          accP[c] = accC[c];
-          accC[c] = accN[c];
-          accN[c] = bt;
+          const int i = c * 16 + frow;
+          ep_out4(e, ep_off(i < npx, mC + i, e.y_stride, ch), Y[c], rC[c], !C21_X(4));
         }
-        if (++t == p.T) { t = 0; ++unit; }
       }
+    };
+    // step s consumes frame s - 1 (ring slot (s - 1) & 1); the loop is unrolled
+    // by two so that the X/Y role swap is static (no register selects)
+    if (F > 0 && !C21_X(5)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int s = 1; s <= F; s += 2) {
+      consume(accA, accB, 0);
+      if (++t == p.T) { t = 0; ++unit; }
       if (s < F && !C21_X(5)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (s + 1 <= F) {
+        consume(accB, accA, 1);
+        if (++t == p.T) { t = 0; ++unit; }
+        if (s + 1 < F && !C21_X(5))
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
     }
   }
 }

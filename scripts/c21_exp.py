@@ -17,7 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 EXP_DIR = os.path.join(ROOT, "rnb_amd", "_native", "exp")
 VARIANTS = {0: "product", 1: "no-spatial", 2: "no-temporal", 3: "no-dma", 4: "no-store",
-            5: "no-sync", 6: "spatial-only"}
+            5: "no-sync", 6: "spatial-only", 7: "linear-stores", 8: "no-res-loads",
+            9: "spatial-prio", 10: "prefetch-8"}
 
 
 def build():
@@ -76,13 +77,34 @@ def run(args):
         print("%-14s %12.1f %12.1f" % (name, row[0], row[1]), flush=True)
 
 
+def one(args):
+    """Only the product 8-wave kernel, for rocprofv3 --pmc passes."""
+    import torch
+    from rnb_amd.models.r2p1d.model import build_network
+    from rnb_amd.models.r2p1d.engine import R2P1DEngine
+    dev = torch.device("cuda:0")
+    eng = R2P1DEngine(build_network(1, 2, depth=34), dev, backend="hip")
+    f = [o for o in eng.ops if o.fuse is not None][0].fuse
+    x = torch.randn((args.clips, 8, 56, 56, 64), device=dev).to(torch.bfloat16)
+    res = torch.randn_like(x)
+    y = torch.empty_like(x)
+    for _ in range(args.reps):
+        f.forward_hip(x, res, out=y, variant=1)
+    torch.cuda.synchronize()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["build", "run"])
+    ap.add_argument("cmd", choices=["build", "run", "one"])
     ap.add_argument("--clips", type=int, default=128)
     ap.add_argument("--reps", type=int, default=20)
     args = ap.parse_args()
-    build() if args.cmd == "build" else run(args)
+    if args.cmd == "build":
+        build()
+    elif args.cmd == "one":
+        one(args)
+    else:
+        run(args)
 
 
 if __name__ == "__main__":
