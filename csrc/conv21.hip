@@ -49,7 +49,7 @@ typedef int i32x4v __attribute__((ext_vector_type(4)));
 // 6 spatial phase only (2 + 3 + 4); conv21s only: 7 temporal residual loads /
 // stores at lane-linear addresses (whole lines, same bytes), 8 no residual loads,
 // 9 = product with the spatial waves at raised issue priority, 10 = product
-// with the spatial B prefetch 8 K-steps ahead (instead of 5)
+// with the spatial B prefetch 5 K-steps ahead (instead of 8)
 #ifndef C21_EXP
 #define C21_EXP 0
 #endif
@@ -418,6 +418,10 @@ void conv21s_kernel(const Conv21Params p) {
     if (tid < 144) ((float*)(w8 + C21_W8))[tid] = p.bs[tid];
   }
 
+  // the spatial bias (the accumulators' initial value) is re-read from LDS
+  // per chunk: registers go to the B-fragment prefetch rings instead
+  const float* bias_l = (const float*)(w8 + C21_W8);
+
   if (spatial) {
     // ======================= spatial waves =======================
     if (C21_X(9)) __builtin_amdgcn_s_setprio(3);   // the critical path issues first
@@ -430,9 +434,6 @@ void conv21s_kernel(const Conv21Params p) {
         for (int s = 0; s < C21_NS; ++s)
           wv[t][s] = *(const bf16x8*)(wr + (size_t)16 * t * p.ks_pad + 32 * s);
     }
-    // the spatial bias (the accumulators' initial value) is re-read from LDS
-    // per chunk: registers go to the B-fragment prefetch ring instead
-    const float* bias_l = (const float*)(w8 + C21_W8);
     const int lrow = lane >> 3;
     const int kc = (lane & 7) ^ lrow;        // swizzle on the DMA source side
     // patch pixel q = pr * 64 + pc <-> image (h0 - 1 + pr, pc - 1). A piece's
@@ -483,11 +484,10 @@ void conv21s_kernel(const Conv21Params p) {
         char* slot = ring + (s & 1) * C21_SLOT;
         // B fragments prefetched PF K-steps ahead ACROSS chunk boundaries
         // (RING divides the 18 K-steps, so a step's ring slot is the same in
-        // every chunk); the ninth tile's A fragments APF steps ahead within
-        // the chunk. sched_group_barrier pins the issue order: left alone,
+        // every chunk). sched_group_barrier pins the issue order: left alone,
         // the scheduler sinks every read next to its MFMAs and the lone
         // spatial wave of the SIMD waits out each read's LDS latency.
-        constexpr int PF = C21_X(10) ? 8 : 5, RING = PF + 1, APF = C21_X(10) ? 2 : 3, ARING = APF + 1;
+        constexpr int PF = C21_X(10) ? 5 : 8, RING = PF + 1;
         static_assert(C21_NS % RING == 0, "ring slot must repeat per chunk");
         auto chunk_base = [&](int c, uint32_t (*bs)[2]) {
           // a unit has at most 2 image rows: row = (i >= W), no division
@@ -505,59 +505,28 @@ void conv21s_kernel(const Conv21Params p) {
           const int tap = k >> 1;
           return *(const bf16x8*)(smem + bs[tap % 3][k & 1] + (tap / 3) * C21_PITCH * 128);
         };
-        auto load_a8 = [&](int k) -> bf16x8 {
-          return *(const bf16x8*)(w8 + (k * 64 + lane) * 16);
-        };
         uint32_t base[3][2], nbase[3][2];
         bf16x8 bq[RING];
         chunk_base(0, base);
 #pragma unroll
         for (int k = 0; k < PF; ++k) bq[k] = load_b(base, k);
         for (int c = 0; c < (C21_X(1) ? 0 : nch); ++c) {
-          const bool own8 = (c & 3) == wq;
           // (past the last chunk: harmless re-reads of the last chunk)
           chunk_base(min(c + 1, nch - 1), nbase);
           f32x4 acc0 = *(const f32x4*)(bias_l + 32 * wq + 4 * fq);
           f32x4 acc1 = *(const f32x4*)(bias_l + 32 * wq + 16 + 4 * fq);
-          f32x4 acc8 = *(const f32x4*)(bias_l + 128 + 4 * fq);
-          if (own8) {
-            bf16x8 aq[ARING];
 #pragma unroll
-            for (int k = 0; k < APF; ++k) aq[k] = load_a8(k);
+          for (int k = 0; k < C21_NS; ++k) {
+            bq[(k + PF) % RING] =
+                k + PF < C21_NS ? load_b(base, k + PF) : load_b(nbase, k + PF - C21_NS);
+            const bf16x8 bv = bq[k % RING];
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[0][k], bv, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[1][k], bv, acc1, 0, 0, 0);
+          }
 #pragma unroll
-            for (int k = 0; k < C21_NS; ++k) {
-              bq[(k + PF) % RING] =
-                  k + PF < C21_NS ? load_b(base, k + PF) : load_b(nbase, k + PF - C21_NS);
-              if (k + APF < C21_NS) aq[(k + APF) % ARING] = load_a8(k + APF);
-              const bf16x8 bv = bq[k % RING];
-              acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[0][k], bv, acc0, 0, 0, 0);
-              acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[1][k], bv, acc1, 0, 0, 0);
-              acc8 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[k % ARING], bv, acc8, 0, 0, 0);
-            }
-#pragma unroll
-            for (int k = 0; k < C21_NS - APF; ++k) {
-              __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-              __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-            }
-#pragma unroll
-            for (int k = C21_NS - APF; k < C21_NS; ++k) {
-              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-              __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-            }
-          } else {
-#pragma unroll
-            for (int k = 0; k < C21_NS; ++k) {
-              bq[(k + PF) % RING] =
-                  k + PF < C21_NS ? load_b(base, k + PF) : load_b(nbase, k + PF - C21_NS);
-              const bf16x8 bv = bq[k % RING];
-              acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[0][k], bv, acc0, 0, 0, 0);
-              acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[1][k], bv, acc1, 0, 0, 0);
-            }
-#pragma unroll
-            for (int k = 0; k < C21_NS; ++k) {
-              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-              __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            }
+          for (int k = 0; k < C21_NS; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
           }
 #pragma unroll
           for (int dw = 0; dw < 3; ++dw) {
@@ -565,7 +534,7 @@ void conv21s_kernel(const Conv21Params p) {
             base[dw][1] = nbase[dw][1];
           }
           // ReLU -> bf16 -> ring: channels 32 wq + 8 fq .. +7 of pixel i
-          // (plane 4 wq + fq); ninth tile: channels 128 + 4 fq .. +3
+          // (plane 4 wq + fq)
           const int i = c * 16 + frow;
           i32x4v o;
 #pragma unroll
@@ -574,12 +543,6 @@ void conv21s_kernel(const Conv21Params p) {
             o[2 + j] = (int)ep_pack(ep_relu(acc1[2 * j]), ep_relu(acc1[2 * j + 1]));
           }
           *(i32x4v*)(slot + (4 * wq + fq) * C21_PLANE + i * 16) = o;
-          if (own8) {
-            i32x2v o8;
-            o8[0] = (int)ep_pack(ep_relu(acc8[0]), ep_relu(acc8[1]));
-            o8[1] = (int)ep_pack(ep_relu(acc8[2]), ep_relu(acc8[3]));
-            *(i32x2v*)(slot + (16 + (fq >> 1)) * C21_PLANE + i * 16 + (fq & 1) * 8) = o8;
-          }
         }
         unit = nu;
         t = nt;
@@ -611,7 +574,7 @@ void conv21s_kernel(const Conv21Params p) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     int unit = u_begin, t = 0;
     // consume mid[t] of frame (unit, t) from ring slot `slot_i`
-    auto consume = [&](f32x4* X, f32x4* Y, int slot_i) {
+    auto consume = [&](f32x4* X, f32x4* Y, int slot_i, auto&& pre) {
       const int n = c21div(unit, p.mB, p.sB);
       const int h0 = (unit - n * p.bands) * C21_ROWS;
       const int npx = min(C21_ROWS, p.H - h0) * p.W;
@@ -639,6 +602,7 @@ void conv21s_kernel(const Conv21Params p) {
               e.res, C21_X(7) ? lin(c) : ep_off(i < npx, mP + i, e.res_stride, ch), 0, 0);
         }
       }
+      pre();                                 // (under the residual loads' latency)
       const char* src = ring + slot_i * C21_SLOT + fq * C21_PLANE + frow * 16;
 #pragma unroll
       for (int c = 0; c < C21S_CH; ++c) {
@@ -688,16 +652,84 @@ void conv21s_kernel(const Conv21Params p) {
         }
       }
     };
-    // step s consumes frame s - 1 (ring slot (s - 1) & 1); the loop is unrolled
-    // by two so that the X/Y role swap is static (no register selects)
-    if (F > 0 && !C21_X(5)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // ninth spatial tile (intermediate channels 128..143) of frame (un, *) for
+    // this wave's chunks c = wq, wq + 4: B fragments from patch[par], A from
+    // LDS, into ring slot par (planes 16, 17). The spatial waves then all do
+    // the same 36 MFMAs per chunk, and the temporal waves' spare MFMA slots
+    // take the ninth tile.
+    auto ninth = [&](int un, int par) {
+      const int n = c21div(un, p.mB, p.sB);
+      const int h0 = (un - n * p.bands) * C21_ROWS;
+      const int npx = min(C21_ROWS, p.H - h0) * p.W;
+      const int nch = (npx + 15) >> 4;
+      const uint32_t pb = (uint32_t)(par * C21_PATCH);
+      char* slot = ring + par * C21_SLOT;
+      for (int c = wq; c < nch; c += 4) {
+        uint32_t bs[3][2];
+        {
+          const int i = min(c * 16 + frow, npx - 1);
+          const int q0 = i + (i >= p.W ? C21_PITCH - p.W : 0);
+#pragma unroll
+          for (int dw = 0; dw < 3; ++dw) {
+            const uint32_t q = (uint32_t)(q0 + dw);
+            const uint32_t rel = (q << 7) | (((q ^ (uint32_t)fq) & 7u) << 4);
+            bs[dw][0] = pb + rel;
+            bs[dw][1] = pb + (rel ^ 64u);
+          }
+        }
+        auto load_b = [&](int k) -> bf16x8 {
+          const int tap = k >> 1;
+          return *(const bf16x8*)(smem + bs[tap % 3][k & 1] + (tap / 3) * C21_PITCH * 128);
+        };
+        auto load_a8 = [&](int k) -> bf16x8 {
+          return *(const bf16x8*)(w8 + (k * 64 + lane) * 16);
+        };
+        constexpr int NPF = 3, NRING = 4;
+        bf16x8 bq[NRING], aq[NRING];
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) {
+          bq[k] = load_b(k);
+          aq[k] = load_a8(k);
+        }
+        f32x4 acc8 = *(const f32x4*)(bias_l + 128 + 4 * fq);
+#pragma unroll
+        for (int k = 0; k < C21_NS; ++k) {
+          if (k + NPF < C21_NS) {
+            bq[(k + NPF) % NRING] = load_b(k + NPF);
+            aq[(k + NPF) % NRING] = load_a8(k + NPF);
+          }
+          if (!C21_X(1))
+            acc8 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[k % NRING], bq[k % NRING], acc8,
+                                                           0, 0, 0);
+        }
+        const int i = c * 16 + frow;
+        i32x2v o8;
+        o8[0] = (int)ep_pack(ep_relu(acc8[0]), ep_relu(acc8[1]));
+        o8[1] = (int)ep_pack(ep_relu(acc8[2]), ep_relu(acc8[3]));
+        *(i32x2v*)(slot + (16 + (fq >> 1)) * C21_PLANE + i * 16 + (fq & 1) * 8) = o8;
+      }
+    };
+    // step s: the ninth tile of frame s (s < F), then frame s - 1 is consumed
+    // (ring slot (s - 1) & 1); the loop is unrolled by two so that the X/Y
+    // role swap is static (no register selects)
+    int nu = u_begin, ntt = 0;               // frame s
+    auto adv = [&](int& u, int& tt) {
+      if (++tt == p.T) { tt = 0; ++u; }
+    };
+    if (F > 0) {
+      ninth(nu, 0);
+      adv(nu, ntt);
+      if (!C21_X(5)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
     for (int s = 1; s <= F; s += 2) {
-      consume(accA, accB, 0);
-      if (++t == p.T) { t = 0; ++unit; }
+      consume(accA, accB, 0, [&] { if (s < F) ninth(nu, 1); });
+      adv(nu, ntt);
+      adv(unit, t);
       if (s < F && !C21_X(5)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (s + 1 <= F) {
-        consume(accB, accA, 1);
-        if (++t == p.T) { t = 0; ++unit; }
+        consume(accB, accA, 1, [&] { if (s + 1 < F) ninth(nu, 0); });
+        adv(nu, ntt);
+        adv(unit, t);
         if (s + 1 < F && !C21_X(5))
           asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       }

@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 EXP_DIR = os.path.join(ROOT, "rnb_amd", "_native", "exp")
 VARIANTS = {0: "product", 1: "no-spatial", 2: "no-temporal", 3: "no-dma", 4: "no-store",
             5: "no-sync", 6: "spatial-only", 7: "linear-stores", 8: "no-res-loads",
-            9: "spatial-prio", 10: "prefetch-8"}
+            9: "spatial-prio", 10: "prefetch-5"}
 
 
 def build():
