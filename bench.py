@@ -14,7 +14,8 @@ accumulation, eval-mode BN folded.
 One step = ``--videos-per-step`` videos per GPU arriving at once (weak
 scaling), served in batches of ``--video-batch`` videos by ``--replicas``
 concurrent streams (R and B of RnB). Every video goes through the full
-decode -> 72 conv kernels -> head -> per-video argmax chain; the argmax of
+decode -> 66 conv kernels (72 convs, the 6 conv2-stage (2+1)D pairs fused,
+csrc/conv21.hip) -> head -> per-video argmax chain; the argmax of
 every video is copied back to the host inside the timed region. Latency of a
 video = completion of its batch - arrival (step start).
 

@@ -368,13 +368,15 @@ void conv21_kernel(const Conv21Params p) {
 // The block walks its units' frames as one stream f = 0 .. F-1 (unit major,
 // frame minor) in lock step, one barrier per step s = 0 .. F:
 //   spatial  s: DMA the input patch of frame s + 1 into patch[(s + 1) & 1],
-//               compute the 144-channel intermediate of frame s from
-//               patch[s & 1] into ring slot s & 1;
-//   temporal s: consume the intermediate of frame s - 1 (slot (s - 1) & 1):
-//               with out[t] = sum_dt W_dt mid[t - 1 + dt] it adds W_2 mid[t]
-//               to out[t - 1], W_1 mid[t] to out[t] and W_0 mid[t] to
-//               out[t + 1] (three accumulator sets in registers), then stores
-//               out[t - 1] (and out[T - 1] at the clip's last frame).
+//               compute intermediate channels 0..127 of frame s from
+//               patch[s & 1] into ring slot s & 1 (wave w: channels 32 w ..);
+//   temporal s: compute intermediate channels 128..143 (the ninth 16-row
+//               tile, weights in LDS) of frame s for pixel chunks w, w + 4,
+//               then consume the intermediate of frame s - 1 (slot
+//               (s - 1) & 1): with out[t] = sum_dt W_dt mid[t - 1 + dt] it
+//               adds W_2 mid[t] to out[t - 1], W_1 mid[t] to out[t] and
+//               W_0 mid[t] to out[t + 1], storing out[t - 1] as soon as it is
+//               complete (and out[T - 1] at the clip's last frame).
 // Accumulating into outputs instead of gathering 3 intermediate frames
 // needs only 2 ring slots, which leaves LDS for a double-buffered patch: the
 // DMA of frame s + 1 lands under frame s's compute.

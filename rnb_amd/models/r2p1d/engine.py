@@ -85,6 +85,8 @@ class R2P1DEngine:
         self.ops: List[PlanOp] = []
         self.head: Optional[Head] = None
         self._n = 0
+        # (2+1)D pair -> conv21 variant picked by autotune, None = two kernels
+        self.fused_choices: Dict[str, Optional[int]] = {}
         if backend == "module":
             self.module = net.to(device)
             self.module.train(bn_mode == "batch")
@@ -251,6 +253,7 @@ class R2P1DEngine:
     def autotune(self, n: int, reps: int = 3) -> Dict[str, int]:
         """Pick the fastest tile per conv for ``n`` clips (GPU only)."""
         assert self.backend == "hip"
+        self.fused_choices = {}
         x = torch.randn(self.input_shape(n), device=self.device).to(torch.bfloat16)
         bufs = {"x": x}
         chosen = {}
@@ -276,7 +279,7 @@ class R2P1DEngine:
                 if t < t_best:
                     best, t_best = v, t
             op.fuse.set_choice(src.shape, best)
-            chosen[op.fuse.name] = -1 if best is None else best
+            self.fused_choices[op.fuse.name] = best
         torch.cuda.synchronize(self.device)
         return chosen
 

@@ -42,10 +42,13 @@ class FusedSTConv:
         self.wt = wt.reshape(64, 3 * MID_PAD).contiguous()
         self.bt = temporal.bias[:64].contiguous()
         self.relu = temporal.relu
-        # per input shape: 0 = two-kernel path, else kernel variant + 1
+        # per input shape: 0 = two-kernel path, else kernel variant + 1; the
+        # role-specialised kernel beats the two tuned kernels at every clip
+        # count measured (profiles/r1_layers_r34_128clips_v10_conv21s.txt), so
+        # it is the default until the engine's autotune decides per shape
         self._use: Dict[Tuple[int, int, int, int], int] = {}
         self.enabled = True
-        self._default = 0
+        self._default = self.VARIANTS[0] + 1
 
     @staticmethod
     def eligible(spatial: ConvLayer, temporal: ConvLayer) -> bool:
@@ -63,9 +66,9 @@ class FusedSTConv:
     VARIANTS = (1, 0)     # conv21.hip: 1 = role-specialised 8 waves, 0 = 4 waves
 
     def use_for(self, x_shape) -> bool:
-        """Fused path for this input shape. Off until the engine's autotune
-        times it against the two tuned kernels (``R2P1DEngine.autotune``), or
-        on for every supported shape after ``force(True)``."""
+        """Fused path for this input shape: the default variant for every
+        supported shape until the engine's autotune times the variants against
+        the two tuned kernels (``R2P1DEngine.autotune``); ``force`` overrides."""
         return self.variant_for(x_shape) is not None
 
     def variant_for(self, x_shape) -> Optional[int]:

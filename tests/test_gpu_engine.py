@@ -82,6 +82,8 @@ def test_autotune_picks_valid_config():
     from rnb_amd.ops.native import kernels
     from rnb_amd.ops.conv import SPECIAL_NAMES
     assert all(0 <= c < len(kernels().configs) or c in SPECIAL_NAMES for c in chosen.values())
+    # fused (2+1)D pairs: a conv21.hip variant or None (two-kernel path)
+    assert hip.fused_choices and all(v in (None, 0, 1) for v in hip.fused_choices.values())
 
 
 def _ipc_child(q_in, q_out):
