@@ -7,6 +7,8 @@
 //  * rnb_preprocess      uint8 NFHWC3 -> normalised bf16 NDHWC8 (channels 3..7
 //                        zero), the fused form of the reference's
 //                        .float().permute() + slot copy.
+//  * rnb_stem_pack       NDHWC8 -> zero-bordered pixel-pair-packed layout of
+//                        the stem conv (ops/conv.StemConv).
 //  * rnb_head            AdaptiveAvgPool3d(1) + Linear(512 -> classes): a
 //                        pooling kernel (one thread per clip x channel pair)
 //                        and a linear kernel (16 clips x 64 classes per block)
@@ -102,6 +104,31 @@ __global__ void preprocess_kernel(const uint8_t* __restrict__ in, uint16_t* __re
       emit(i, px[0], px[1], px[2]);
     }
   }
+}
+
+// Stem repack for the pair-packed conv1 spatial conv (ops/conv.StemConv):
+// NDHWC8 bf16 [F][H][W][8] (channels 0..2 used) -> zero-bordered
+// [F][H+6][(W+6)/2][8], where packed pixel (y, xp) holds channels 0..3 of
+// padded pixels 2xp and 2xp+1 (padded x = x + 3, padded y = y + 3). One
+// thread = one 16-byte packed pixel: two 8-byte loads, one 16-byte store.
+__global__ __launch_bounds__(256) void stem_pack_kernel(const uint16_t* __restrict__ in,
+                                                        uint16_t* __restrict__ out,
+                                                        long long nout, int H, int W, int Hp,
+                                                        int Wq) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nout) return;
+  const long long r = i / Wq;
+  const int xp = (int)(i - r * Wq);
+  const long long f = r / Hp;
+  const int yr = (int)(r - f * Hp) - 3;
+  const int x0 = 2 * xp - 3;
+  uint2 a = make_uint2(0u, 0u), b = make_uint2(0u, 0u);
+  if (yr >= 0 && yr < H) {
+    const uint16_t* row = in + (f * H + yr) * (long long)W * 8;
+    if (x0 >= 0 && x0 < W) a = *(const uint2*)(row + (long long)x0 * 8);
+    if (x0 + 1 >= 0 && x0 + 1 < W) b = *(const uint2*)(row + (long long)(x0 + 1) * 8);
+  }
+  *(uint4*)(out + i * 8) = make_uint4(a.x, a.y, b.x, b.y);
 }
 
 // Head, part 1: average pool. x: [N][S][Cs] bf16 (NDHWC, S = T*H*W) ->
@@ -286,6 +313,19 @@ int rnb_video_reduce(const float* logits, const int* offsets, float* sums, int* 
   if (nvid <= 0) return 0;
   hipLaunchKernelGGL(video_reduce_kernel, dim3(nvid), dim3(256), 0, stream, logits, offsets,
                      sums, argmax, ncls);
+  return (int)hipGetLastError();
+}
+
+// in: [frames][H][W][8] bf16, out: [frames][H+6][(W+6)/2][8] bf16 (W even)
+int rnb_stem_pack(const void* in, void* out, long long frames, int H, int W,
+                  hipStream_t stream) {
+  if (frames <= 0) return 0;
+  if (W % 2 != 0 || H <= 0 || W <= 0) return -2;
+  if ((((uintptr_t)in) & 7u) != 0 || (((uintptr_t)out) & 15u) != 0) return -2;
+  const int Hp = H + 6, Wq = (W + 6) / 2;
+  const long long nout = frames * Hp * Wq;
+  hipLaunchKernelGGL(stem_pack_kernel, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0,
+                     stream, (const uint16_t*)in, (uint16_t*)out, nout, H, W, Hp, Wq);
   return (int)hipGetLastError();
 }
 

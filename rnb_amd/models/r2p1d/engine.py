@@ -28,13 +28,14 @@ up to its bucket and the padded rows are discarded.
 from __future__ import annotations
 
 import bisect
+import os
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
 from ...ops.bn import BatchNormBatch
-from ...ops.conv import ConvGeom, ConvLayer, fold_bn, pad_to, CH_ALIGN
+from ...ops.conv import ConvGeom, ConvLayer, StemConv, fold_bn, pad_to, CH_ALIGN
 from ...ops.conv21 import FusedSTConv
 from ...ops.video import Head, IN_CHANNELS_P, ndhwc_to_ncdhw, ncdhw_to_ndhwc
 from .network import (LAYER_CHANNELS, LAYER_INPUT_CTHW, LAYER_OUTPUT_CTHW,
@@ -80,6 +81,8 @@ class R2P1DEngine:
         self.device = device
         self.backend = backend
         self.bn_mode = bn_mode
+        # conv1 spatial on the pair-packed input (ops/conv.StemConv)
+        self.pack_stem = os.environ.get("RNB_STEM_PACK", "1") != "0"
         self.start_idx, self.end_idx = net.start_idx, net.end_idx
         self.num_classes = getattr(net, "num_classes", 400)
         self.ops: List[PlanOp] = []
@@ -118,7 +121,10 @@ class R2P1DEngine:
             w = w[:, :, pt:pt + 1].contiguous()
             geom = ConvGeom(cin=geom.cin, cout=geom.cout, kernel=(1,) + geom.kernel[1:],
                             stride=geom.stride, padding=(0,) + geom.padding[1:])
-        layer = ConvLayer(w, b, geom, relu, self.device, name)
+        if self.pack_stem and StemConv.eligible(geom):
+            layer = StemConv(w, b, geom, relu, self.device, name)
+        else:
+            layer = ConvLayer(w, b, geom, relu, self.device, name)
         layer.nominal_geom = nominal
         return layer
 

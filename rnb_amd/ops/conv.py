@@ -410,3 +410,135 @@ class ConvLayer:
         if g.cout_p != g.cout:
             y = F.pad(y, (0, g.cout_p - g.cout))
         return y.to(out_dtype).contiguous()
+
+
+# ----------------------------------------------------------------------
+# Stem: the R(2+1)D conv1 spatial conv (3 -> 83 channels, 1x7x7, stride
+# (1,2,2), pad (0,3,3)) run as a pixel-pair-packed conv.
+def stem_pack(x: torch.Tensor) -> torch.Tensor:
+    """NDHWC8 [N,T,H,W,8] -> zero-bordered pair-packed [N,T,H+6,(W+6)/2,8].
+
+    Packed pixel (y, xp), channel j = channel j % 4 of padded pixel
+    (y, 2*xp + j // 4) (padding 3 on each side). The HIP kernel is
+    ``video_ops.hip: stem_pack_kernel``; the CPU path is its mirror.
+    """
+    N, T, H, W, C = x.shape
+    if C != CH_ALIGN or W % 2:
+        raise ValueError("stem_pack expects [N,T,H,W,8] with even W, got %s" % (tuple(x.shape),))
+    Hp, Wq = H + 6, (W + 6) // 2
+    if x.is_cuda:
+        from .native import kernels
+        if x.dtype != torch.bfloat16 or not x.is_contiguous():
+            raise ValueError("stem_pack expects contiguous bf16 input")
+        out = torch.empty((N, T, Hp, Wq, C), dtype=torch.bfloat16, device=x.device)
+        kernels().stem_pack(x.data_ptr(), out.data_ptr(), N * T, H, W,
+                            torch.cuda.current_stream(x.device).cuda_stream)
+        return out
+    pad = torch.zeros((N, T, Hp, 2 * Wq, 4), dtype=x.dtype)
+    pad[:, :, 3:3 + H, 3:3 + W] = x[..., :4]
+    return pad.reshape(N, T, Hp, Wq, 8).contiguous()
+
+
+class StemConv(ConvLayer):
+    """conv1's 1x7x7 stride-(1,2,2) spatial conv on a pair-packed input.
+
+    With 3 input channels padded to 8 the generic gather moves 49 16-byte
+    chunks per output pixel of which 3/8 is data, and the MFMA K loop runs
+    over 448 entries for 147 useful ones (measured 0.44 ms at 128 clips,
+    178 TFLOP/s, the least efficient conv of the plan). ``stem_pack`` stores
+    two horizontally adjacent padded pixels x 4 channels per 16 bytes, which
+    turns the conv into a 1x7x4 conv with stride (1,2,1) and no padding over
+    8 packed channels: K = 7*4*8 = 224 (256 padded), every gathered chunk
+    holds 6 data values of 8, and the zero border replaces validity masks.
+    Packed weight W'[o, j, 0, dy, q] = W[o, j % 4, 0, dy, 2q + j // 4] (zero
+    for channel 3 and tap 7).
+    """
+
+    def __init__(self, weight: torch.Tensor, bias: torch.Tensor, geom: ConvGeom,
+                 relu: bool, device: torch.device, name: str = ""):
+        if not StemConv.eligible(geom):
+            raise ValueError("not a stem geometry: %s" % (geom,))
+        cout = geom.cout
+        w = weight.detach().float()
+        wp = torch.zeros(cout, CH_ALIGN, 1, 7, 4, dtype=torch.float32)
+        for j in range(CH_ALIGN):
+            c, h = j % 4, j // 4
+            if c >= geom.cin:
+                continue
+            for q in range(4):
+                dx = 2 * q + h
+                if dx < 7:
+                    wp[:, j, 0, :, q] = w[:, c, 0, :, dx]
+        packed = ConvGeom(cin=CH_ALIGN, cout=cout, kernel=(1, 7, 4), stride=(1, 2, 1),
+                          padding=(0, 0, 0))
+        super().__init__(wp, bias, packed, relu, device, name)
+        self.real_geom = geom
+        # torch path runs the real conv on the bf16-rounded original weight
+        self.w_ref = weight.detach().to(torch.bfloat16).float().to(device)
+        self.use_halo = self.use_temporal = self.use_halo_ws = False
+        self._in_packed = False
+
+    @staticmethod
+    def eligible(geom: ConvGeom) -> bool:
+        return (geom.kernel == (1, 7, 7) and geom.stride == (1, 2, 2)
+                and geom.padding == (0, 3, 3) and geom.cin <= 4)
+
+    def out_shape(self, x_shape):
+        """Output shape for a real [N,T,H,W,8] input (or a packed one while
+        the base class launches on it)."""
+        if self._in_packed:
+            return super().out_shape(x_shape)
+        N, T, H, W, _ = x_shape
+        To, Ho, Wo = self.real_geom.out_thw(T, H, W)
+        return (N, To, Ho, Wo, self.geom.cout_p)
+
+    def _on_packed(self, fn, x, *args):
+        xp = stem_pack(x)
+        self._in_packed = True
+        try:
+            return fn(xp, *args)
+        finally:
+            self._in_packed = False
+
+    def autotune(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                 reps: int = 5) -> int:
+        return self._on_packed(super().autotune, x, residual, reps)
+
+    def config_for(self, x_shape) -> int:
+        if not self._in_packed:
+            N, T, H, W, C = x_shape
+            x_shape = (N, T, H + 6, (W + 6) // 2, C)
+        return super().config_for(x_shape)
+
+    def forward_hip(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                    out: Optional[torch.Tensor] = None, config: Optional[int] = None):
+        """x: real NDHWC8 input; packed into a temporary, then the generic kernel."""
+        if x.dtype != torch.bfloat16 or not x.is_contiguous():
+            raise ValueError("%s: expected contiguous bf16 NDHWC input" % self.name)
+        return self._on_packed(super().forward_hip, x, residual, out, config)
+
+    def forward_packed_torch(self, xp: torch.Tensor) -> torch.Tensor:
+        """fp32 conv of the packed weight over a packed input (layout check)."""
+        g = self.geom
+        wp = self.wmat[:g.cout_p].float().cpu()
+        inv = torch.argsort(pair_permutation(g.cout_p))
+        wp = wp[inv][:g.cout, :g.k_total].reshape(g.cout, 1, 7, 4, CH_ALIGN)
+        wp = wp.permute(0, 4, 1, 2, 3)
+        y = F.conv3d(xp.float().permute(0, 4, 1, 2, 3), wp.to(xp.device),
+                     self.b_ref.to(xp.device), stride=g.stride)
+        return y.permute(0, 2, 3, 4, 1)
+
+    def forward_torch(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                      out_dtype=torch.bfloat16):
+        g = self.real_geom
+        xin = x[..., :g.cin].float().permute(0, 4, 1, 2, 3)
+        y = F.conv3d(xin, self.w_ref.to(x.device), self.b_ref.to(x.device),
+                     stride=g.stride, padding=g.padding)
+        y = y.permute(0, 2, 3, 4, 1)
+        if residual is not None:
+            y = y + residual[..., :g.cout].float()
+        if self.relu:
+            y = torch.relu(y)
+        if self.geom.cout_p != g.cout:
+            y = F.pad(y, (0, self.geom.cout_p - g.cout))
+        return y.to(out_dtype).contiguous()

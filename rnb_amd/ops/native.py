@@ -175,6 +175,8 @@ class Kernels:
         lib.rnb_preprocess.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
                                        ctypes.POINTER(ctypes.c_float),
                                        ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
+        lib.rnb_stem_pack.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
+                                      ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         lib.rnb_head.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
@@ -272,6 +274,9 @@ class Kernels:
         m = (ctypes.c_float * 3)(*mean)
         s = (ctypes.c_float * 3)(*std)
         _check(self.lib.rnb_preprocess(in_ptr, out_ptr, npix, m, s, stream), "preprocess")
+
+    def stem_pack(self, in_ptr, out_ptr, frames, H, W, stream):
+        _check(self.lib.rnb_stem_pack(in_ptr, out_ptr, frames, H, W, stream), "stem_pack")
 
     def head(self, x_ptr, w_ptr, b_ptr, out_ptr, pooled_ptr, N, S, C, Cs, ncls, stream):
         _check(self.lib.rnb_head(x_ptr, w_ptr, b_ptr, out_ptr, pooled_ptr, N, S, C, Cs, ncls,

@@ -94,7 +94,7 @@ def main():
         e.record()
         e.synchronize()
         ms = s.elapsed_time(e) / args.reps
-        g = op.layer.geom
+        g = getattr(op.layer, "real_geom", op.layer.geom)
         N, T, H, W, _ = src.shape
         flops = g.flops(N, T, H, W)
         To, Ho, Wo = g.out_thw(T, H, W)

@@ -307,3 +307,47 @@ def test_temporal_tap_skipping_every_config(thw, cin, stride):
         y = layer.forward_hip(x, config=cfg)
         torch.cuda.synchronize()
         assert torch.equal(y, ref), (cfg, (y.float() - ref.float()).abs().max().item())
+
+
+@pytest.mark.parametrize("thw", [(8, 112, 112), (3, 10, 14)])
+def test_stem_pack_matches_cpu_mirror(thw):
+    from rnb_amd.ops.conv import stem_pack
+    x = torch.randn((2,) + thw + (8,)).to(torch.bfloat16)
+    got = stem_pack(x.to(DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(got.cpu(), stem_pack(x))
+
+
+def test_stem_conv_every_tile_config_exact_integers():
+    """Pair-packed stem conv (ops/conv.StemConv) == the 1x7x7 stride-2 conv."""
+    from rnb_amd.ops.conv import StemConv
+    from rnb_amd.ops.native import kernels
+    g = torch.Generator().manual_seed(3)
+    w = torch.randint(-2, 3, (83, 3, 1, 7, 7), generator=g).float()
+    b = torch.randint(-4, 5, (83,), generator=g).float()
+    stem = StemConv(w, b, ConvGeom(3, 83, (1, 7, 7), (1, 2, 2), (0, 3, 3)), True, DEV,
+                    "conv1.spatial")
+    x = _input(2, (2, 22, 30), 8, 3, integer=True)
+    ref = stem.forward_torch(x, out_dtype=torch.bfloat16)
+    for cfg in range(len(kernels().configs)):
+        y = stem.forward_hip(x, config=cfg)
+        torch.cuda.synchronize()
+        assert torch.equal(y, ref), (cfg, (y.float() - ref.float()).abs().max().item())
+
+
+def test_stem_conv_matches_torch_full_size():
+    from rnb_amd.ops.conv import StemConv
+    g = torch.Generator().manual_seed(4)
+    w = torch.randn((83, 3, 1, 7, 7), generator=g) * (2.0 / 147) ** 0.5
+    b = torch.randn(83, generator=g) * 0.1
+    stem = StemConv(w, b, ConvGeom(3, 83, (1, 7, 7), (1, 2, 2), (0, 3, 3)), True, DEV,
+                    "conv1.spatial")
+    x = _input(3, (8, 112, 112), 8, 3)
+    cid = stem.autotune(x, reps=1)
+    y = stem.forward_hip(x)
+    ref = stem.forward_torch(x, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert stem.config_for(x.shape) == cid
+    err = (y.float() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= 1e-2 * scale + 1e-2, (err, scale)

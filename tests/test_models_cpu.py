@@ -150,3 +150,30 @@ def test_layout_converters_roundtrip():
     y = ncdhw_to_ndhwc(x, 8, dtype=torch.float32)
     assert y.shape == (2, 4, 5, 6, 8)
     assert torch.equal(ndhwc_to_ncdhw(y, 3), x)
+
+
+def test_stem_pair_packed_conv_is_the_stem_conv():
+    """conv1 spatial as the pair-packed 1x7x4 conv (ops/conv.StemConv) equals
+    the 1x7x7 stride-(1,2,2) conv exactly in fp32, whatever the pad channels hold."""
+    from rnb_amd.ops.conv import ConvGeom, StemConv, stem_pack
+    g = ConvGeom(3, 83, (1, 7, 7), (1, 2, 2), (0, 3, 3))
+    gen = torch.Generator().manual_seed(0)
+    w, b = torch.randn(83, 3, 1, 7, 7, generator=gen), torch.randn(83, generator=gen)
+    stem = StemConv(w, b, g, True, torch.device("cpu"), "conv1.spatial")
+    assert stem.geom.k_total == 224 and stem.geom.k_pad == 256
+    for thw in [(2, 112, 112), (3, 10, 14)]:
+        x = torch.randn((2,) + thw + (8,), generator=gen).to(torch.bfloat16)
+        xp = stem_pack(x)
+        assert xp.shape == (2, thw[0], thw[1] + 6, (thw[2] + 6) // 2, 8)
+        ref = stem.forward_torch(x, out_dtype=torch.float32)
+        assert tuple(ref.shape) == stem.out_shape(x.shape)
+        got = torch.relu(stem.forward_packed_torch(xp))
+        assert torch.equal(ref[..., :83], got)
+
+
+def test_engine_uses_packed_stem():
+    from rnb_amd.ops.conv import StemConv
+    net = R2Plus1DLayerWrapper(1, 5, 400, normalize_layer_sizes(1, 5, None, 18)).eval()
+    eng = R2P1DEngine(net, torch.device("cpu"), backend="torch")
+    assert isinstance(eng.ops[0].layer, StemConv)
+    assert eng.flops_per_clip() > 0
