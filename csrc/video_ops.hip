@@ -9,6 +9,8 @@
 //                        .float().permute() + slot copy.
 //  * rnb_stem_pack       NDHWC8 -> zero-bordered pixel-pair-packed layout of
 //                        the stem conv (ops/conv.StemConv).
+//  * rnb_preprocess_packed  rnb_preprocess + rnb_stem_pack in one pass: uint8
+//                        frames straight to the stem's packed input.
 //  * rnb_head            AdaptiveAvgPool3d(1) + Linear(512 -> classes): a
 //                        pooling kernel (one thread per clip x channel pair)
 //                        and a linear kernel (16 clips x 64 classes per block)
@@ -129,6 +131,40 @@ __global__ __launch_bounds__(256) void stem_pack_kernel(const uint16_t* __restri
     if (x0 + 1 >= 0 && x0 + 1 < W) b = *(const uint2*)(row + (long long)(x0 + 1) * 8);
   }
   *(uint4*)(out + i * 8) = make_uint4(a.x, a.y, b.x, b.y);
+}
+
+// preprocess fused with the stem repack: uint8 [F][H][W][3] -> zero-bordered
+// pair-packed bf16 [F][H+6][(W+6)/2][8] (the layout of stem_pack_kernel), so
+// the decoder writes the stem conv's input directly. One thread = one packed
+// pixel: up to 6 byte loads, one 16-byte store; the border is written as zero.
+__global__ __launch_bounds__(256) void preprocess_packed_kernel(const uint8_t* __restrict__ in,
+                                                                uint16_t* __restrict__ out,
+                                                                long long nout, int H, int W,
+                                                                int Hp, int Wq, NormParams np) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nout) return;
+  const long long r = i / Wq;
+  const int xp = (int)(i - r * Wq);
+  const long long f = r / Hp;
+  const int yr = (int)(r - f * Hp) - 3;
+  const int x0 = 2 * xp - 3;
+  uint32_t v[4] = {0u, 0u, 0u, 0u};
+  if (yr >= 0 && yr < H) {
+    const uint8_t* row = in + (f * H + yr) * (long long)W * 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int x = x0 + h;
+      if (x >= 0 && x < W) {
+        const uint8_t* px = row + (long long)x * 3;
+        const uint32_t rr = f2bf_bits((float)px[0] * np.scale[0] + np.shift[0]);
+        const uint32_t gg = f2bf_bits((float)px[1] * np.scale[1] + np.shift[1]);
+        const uint32_t bb = f2bf_bits((float)px[2] * np.scale[2] + np.shift[2]);
+        v[2 * h] = rr | (gg << 16);
+        v[2 * h + 1] = bb;
+      }
+    }
+  }
+  *(uint4*)(out + i * 8) = make_uint4(v[0], v[1], v[2], v[3]);
 }
 
 // Head, part 1: average pool. x: [N][S][Cs] bf16 (NDHWC, S = T*H*W) ->
@@ -326,6 +362,24 @@ int rnb_stem_pack(const void* in, void* out, long long frames, int H, int W,
   const long long nout = frames * Hp * Wq;
   hipLaunchKernelGGL(stem_pack_kernel, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0,
                      stream, (const uint16_t*)in, (uint16_t*)out, nout, H, W, Hp, Wq);
+  return (int)hipGetLastError();
+}
+
+// in: uint8 [frames][H][W][3], out: [frames][H+6][(W+6)/2][8] bf16 (W even)
+int rnb_preprocess_packed(const void* in, void* out, long long frames, int H, int W,
+                          const float* mean, const float* stdv, hipStream_t stream) {
+  if (frames <= 0) return 0;
+  if (W % 2 != 0 || H <= 0 || W <= 0) return -2;
+  if ((((uintptr_t)out) & 15u) != 0) return -2;
+  NormParams np;
+  for (int c = 0; c < 3; ++c) {
+    np.scale[c] = 1.0f / (255.0f * stdv[c]);
+    np.shift[c] = -mean[c] / stdv[c];
+  }
+  const int Hp = H + 6, Wq = (W + 6) / 2;
+  const long long nout = frames * Hp * Wq;
+  hipLaunchKernelGGL(preprocess_packed_kernel, dim3((unsigned)((nout + 255) / 256)), dim3(256),
+                     0, stream, (const uint8_t*)in, (uint16_t*)out, nout, H, W, Hp, Wq, np);
   return (int)hipGetLastError();
 }
 

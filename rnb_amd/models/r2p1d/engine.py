@@ -37,7 +37,8 @@ import torch
 from ...ops.bn import BatchNormBatch
 from ...ops.conv import ConvGeom, ConvLayer, StemConv, fold_bn, pad_to, CH_ALIGN
 from ...ops.conv21 import FusedSTConv
-from ...ops.video import Head, IN_CHANNELS_P, ndhwc_to_ncdhw, ncdhw_to_ndhwc
+from ...ops.video import (Head, IN_CHANNELS_P, ndhwc_to_ncdhw, ncdhw_to_ndhwc,
+                          packed_input_shape)
 from .network import (LAYER_CHANNELS, LAYER_INPUT_CTHW, LAYER_OUTPUT_CTHW,
                       R2Plus1DLayerWrapper, SpatioTemporalConv)
 
@@ -178,8 +179,22 @@ class R2P1DEngine:
     def in_channels_p(self) -> int:
         return boundary_channels_p(self.start_idx)
 
-    def input_shape(self, n: int) -> Tuple[int, ...]:
-        return boundary_shape(self.start_idx, n)
+    def input_shape(self, n: int, packed: bool = False) -> Tuple[int, ...]:
+        """Boundary input shape; ``packed`` = the stem's pair-packed layout
+        (only when ``accepts_packed_input``)."""
+        shape = boundary_shape(self.start_idx, n)
+        if not packed:
+            return shape
+        if not self.accepts_packed_input:
+            raise ValueError("this engine's first op does not take a packed input")
+        return packed_input_shape(*shape[:4])
+
+    @property
+    def accepts_packed_input(self) -> bool:
+        """True when the first op is the pair-packed stem conv, so a decoder
+        can write its input layout directly (``forward(x, packed=True)``)."""
+        return (self.backend != "module" and bool(self.ops)
+                and isinstance(self.ops[0].layer, StemConv) and self.ops[0].bn is None)
 
     def output_shape(self, n: int) -> Tuple[int, ...]:
         if self.end_idx == 5:
@@ -207,8 +222,12 @@ class R2P1DEngine:
         return [op.layer for op in self.ops if op.kind == "conv"]
 
     # -------------------------------------------------------------- forward
-    def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """x: NDHWC bf16 boundary tensor (or NCDHW fp32 for backend=module)."""
+    def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
+                packed: bool = False) -> torch.Tensor:
+        """x: NDHWC bf16 boundary tensor (or NCDHW fp32 for backend=module);
+        with ``packed``, the stem's pair-packed input (``input_shape(n, True)``)."""
+        if packed and not self.accepts_packed_input:
+            raise ValueError("this engine's first op does not take a packed input")
         if self.backend == "module":
             if x.dim() == 5 and x.shape[-1] == self.in_channels_p and x.dtype == torch.bfloat16:
                 x = ndhwc_to_ncdhw(x, LAYER_INPUT_CTHW[self.start_idx][0])
@@ -241,6 +260,9 @@ class R2P1DEngine:
                 else:
                     y = op.layer.forward_torch(src, None)
                     y = op.bn.forward_torch(y, res, op.bn_relu)
+            elif packed and i == 0:
+                y = (op.layer.forward_hip(src, res, prepacked=True) if hip
+                     else op.layer.forward_torch(src, res, prepacked=True))
             elif hip:
                 y = op.layer.forward_hip(src, res)
             else:

@@ -21,6 +21,7 @@ run concurrently with the others on the same GPU.
 from __future__ import annotations
 
 import bisect
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -45,6 +46,10 @@ class Replica:
         self.device = engine.device
         self.max_videos = max_videos
         self.buckets = sorted({b for b in buckets if b < max_clips} | {max_clips})
+        # the preprocess kernel writes the stem's pair-packed input directly
+        # (no separate stem_pack pass); RNB_PACKED_INPUT=0 turns it off
+        self.packed = (engine.accepts_packed_input
+                       and os.environ.get("RNB_PACKED_INPUT", "1") != "0")
         self.stream = torch.cuda.Stream(self.device)
         self.pool = torch.cuda.graph_pool_handle()
         self.graphs: Dict[int, _BucketGraph] = {}
@@ -64,8 +69,8 @@ class Replica:
     def _body(self, bg: _BucketGraph, b: int):
         F, H, W = CLIP_SHAPE
         surf = vops.clipgen_u8(bg.meta[0], bg.meta[1], F, H, W)
-        vops.preprocess(surf, out=bg.frames)
-        logits = self.engine.forward(bg.frames)
+        vops.preprocess(surf, out=bg.frames, packed=self.packed)
+        logits = self.engine.forward(bg.frames, packed=self.packed)
         bg.logits = logits
         vops.video_reduce(logits, bg.offsets, sums=bg.sums)[1]
 
@@ -76,7 +81,8 @@ class Replica:
         bg = _BucketGraph()
         bg.meta = torch.zeros((2, b), dtype=torch.int32, device=dev)
         bg.offsets = torch.zeros((self.max_videos + 1,), dtype=torch.int32, device=dev)
-        bg.frames = torch.empty(self.engine.input_shape(b), dtype=torch.bfloat16, device=dev)
+        bg.frames = torch.empty(self.engine.input_shape(b, self.packed), dtype=torch.bfloat16,
+                                device=dev)
         bg.sums = torch.empty((self.max_videos, self.engine.num_classes),
                               dtype=torch.float32, device=dev)
         with torch.cuda.stream(self.stream):
@@ -87,8 +93,8 @@ class Replica:
             with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
                 F, H, W = CLIP_SHAPE
                 surf = vops.clipgen_u8(bg.meta[0], bg.meta[1], F, H, W)
-                vops.preprocess(surf, out=bg.frames)
-                bg.logits = self.engine.forward(bg.frames)
+                vops.preprocess(surf, out=bg.frames, packed=self.packed)
+                bg.logits = self.engine.forward(bg.frames, packed=self.packed)
                 _, bg.argmax = vops.video_reduce(bg.logits, bg.offsets, sums=bg.sums)
             self.stream.synchronize()
         bg.graph = g
@@ -98,8 +104,8 @@ class Replica:
     def _run_eager(self, bg):
         F, H, W = CLIP_SHAPE
         surf = vops.clipgen_u8(bg.meta[0], bg.meta[1], F, H, W)
-        vops.preprocess(surf, out=bg.frames)
-        logits = self.engine.forward(bg.frames)
+        vops.preprocess(surf, out=bg.frames, packed=self.packed)
+        logits = self.engine.forward(bg.frames, packed=self.packed)
         vops.video_reduce(logits, bg.offsets, sums=bg.sums)
 
     def submit(self, videos: Sequence[Tuple[int, Sequence[int]]],

@@ -511,11 +511,20 @@ class StemConv(ConvLayer):
         return super().config_for(x_shape)
 
     def forward_hip(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                    out: Optional[torch.Tensor] = None, config: Optional[int] = None):
-        """x: real NDHWC8 input; packed into a temporary, then the generic kernel."""
+                    out: Optional[torch.Tensor] = None, config: Optional[int] = None,
+                    prepacked: bool = False):
+        """x: real NDHWC8 input, packed into a temporary, then the generic
+        kernel; or (``prepacked``) an input already in the packed layout, as
+        ``ops.video.preprocess(..., packed=True)`` writes it."""
         if x.dtype != torch.bfloat16 or not x.is_contiguous():
             raise ValueError("%s: expected contiguous bf16 NDHWC input" % self.name)
-        return self._on_packed(super().forward_hip, x, residual, out, config)
+        if not prepacked:
+            return self._on_packed(super().forward_hip, x, residual, out, config)
+        self._in_packed = True
+        try:
+            return super().forward_hip(x, residual, out, config)
+        finally:
+            self._in_packed = False
 
     def forward_packed_torch(self, xp: torch.Tensor) -> torch.Tensor:
         """fp32 conv of the packed weight over a packed input (layout check)."""
@@ -529,12 +538,17 @@ class StemConv(ConvLayer):
         return y.permute(0, 2, 3, 4, 1)
 
     def forward_torch(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                      out_dtype=torch.bfloat16):
+                      out_dtype=torch.bfloat16, prepacked: bool = False):
+        """fp32 reference: the 1x7x7 conv on a real input, or (``prepacked``)
+        the packed conv on a packed one."""
         g = self.real_geom
-        xin = x[..., :g.cin].float().permute(0, 4, 1, 2, 3)
-        y = F.conv3d(xin, self.w_ref.to(x.device), self.b_ref.to(x.device),
-                     stride=g.stride, padding=g.padding)
-        y = y.permute(0, 2, 3, 4, 1)
+        if prepacked:
+            y = self.forward_packed_torch(x)
+        else:
+            xin = x[..., :g.cin].float().permute(0, 4, 1, 2, 3)
+            y = F.conv3d(xin, self.w_ref.to(x.device), self.b_ref.to(x.device),
+                         stride=g.stride, padding=g.padding)
+            y = y.permute(0, 2, 3, 4, 1)
         if residual is not None:
             y = y + residual[..., :g.cout].float()
         if self.relu:

@@ -177,6 +177,10 @@ class Kernels:
                                        ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
         lib.rnb_stem_pack.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        lib.rnb_preprocess_packed.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
+                                              ctypes.POINTER(ctypes.c_float),
+                                              ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
         lib.rnb_head.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
@@ -277,6 +281,12 @@ class Kernels:
 
     def stem_pack(self, in_ptr, out_ptr, frames, H, W, stream):
         _check(self.lib.rnb_stem_pack(in_ptr, out_ptr, frames, H, W, stream), "stem_pack")
+
+    def preprocess_packed(self, in_ptr, out_ptr, frames, H, W, mean, std, stream):
+        m = (ctypes.c_float * 3)(*mean)
+        s = (ctypes.c_float * 3)(*std)
+        _check(self.lib.rnb_preprocess_packed(in_ptr, out_ptr, frames, H, W, m, s, stream),
+               "preprocess_packed")
 
     def head(self, x_ptr, w_ptr, b_ptr, out_ptr, pooled_ptr, N, S, C, Cs, ncls, stream):
         _check(self.lib.rnb_head(x_ptr, w_ptr, b_ptr, out_ptr, pooled_ptr, N, S, C, Cs, ncls,

@@ -53,10 +53,17 @@ def clipgen_u8(vids: torch.Tensor, starts: torch.Tensor, F: int, H: int, W: int,
 
 
 def preprocess(frames_u8: torch.Tensor, mean=KINETICS_MEAN, std=KINETICS_STD,
-               out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """uint8 [n, F, H, W, 3] -> normalised bf16 [n, F, H, W, 8] (NDHWC)."""
+               out: Optional[torch.Tensor] = None, packed: bool = False) -> torch.Tensor:
+    """uint8 [n, F, H, W, 3] -> normalised bf16 [n, F, H, W, 8] (NDHWC).
+
+    ``packed=True`` writes the stem conv's zero-bordered pixel-pair layout
+    [n, F, H+6, (W+6)/2, 8] instead (``ops.conv.stem_pack`` of the NDHWC
+    result, in one pass: ``video_ops.hip: preprocess_packed_kernel``).
+    """
     n, F, H, W, C = frames_u8.shape
     assert C == 3
+    if packed:
+        return _preprocess_packed(frames_u8, mean, std, out)
     if frames_u8.is_cuda:
         from .native import kernels
         if out is None:
@@ -71,6 +78,34 @@ def preprocess(frames_u8: torch.Tensor, mean=KINETICS_MEAN, std=KINETICS_STD,
     y = frames_u8.float() * scale + shift
     res = torch.zeros((n, F, H, W, IN_CHANNELS_P), dtype=torch.bfloat16)
     res[..., :3] = y.to(torch.bfloat16)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+def packed_input_shape(n: int, F: int, H: int, W: int) -> Tuple[int, ...]:
+    """Shape of the stem's pair-packed input for n clips of F x H x W."""
+    return (n, F, H + 6, (W + 6) // 2, IN_CHANNELS_P)
+
+
+def _preprocess_packed(frames_u8, mean, std, out):
+    n, F, H, W, _ = frames_u8.shape
+    if W % 2:
+        raise ValueError("packed preprocess needs an even frame width, got %d" % W)
+    shape = packed_input_shape(n, F, H, W)
+    if frames_u8.is_cuda:
+        from .native import kernels
+        if out is None:
+            out = torch.empty(shape, dtype=torch.bfloat16, device=frames_u8.device)
+        elif tuple(out.shape) != shape or out.dtype != torch.bfloat16 or not out.is_contiguous():
+            raise ValueError("packed preprocess: out must be contiguous bf16 %s" % (shape,))
+        kernels().preprocess_packed(frames_u8.contiguous().data_ptr(), out.data_ptr(),
+                                    n * F, H, W, mean, std,
+                                    torch.cuda.current_stream(frames_u8.device).cuda_stream)
+        return out
+    from .conv import stem_pack
+    res = stem_pack(preprocess(frames_u8, mean, std))
     if out is not None:
         out.copy_(res)
         return out

@@ -351,3 +351,35 @@ def test_stem_conv_matches_torch_full_size():
     err = (y.float() - ref).abs().max().item()
     scale = ref.abs().max().item()
     assert err <= 1e-2 * scale + 1e-2, (err, scale)
+
+
+@pytest.mark.parametrize("shape", [(2, 8, 112, 112, 3), (1, 3, 5, 10, 3)])
+def test_preprocess_packed_is_preprocess_then_stem_pack(shape):
+    """Fused preprocess + stem repack (video_ops.hip: preprocess_packed_kernel)
+    == stem_pack(preprocess(u8)) bit for bit, on the GPU and vs the CPU mirror."""
+    from rnb_amd.ops.conv import stem_pack
+    u8 = torch.randint(0, 256, shape, dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
+    ug = u8.to(DEV)
+    got = vops.preprocess(ug, packed=True)
+    two_pass = stem_pack(vops.preprocess(ug))
+    torch.cuda.synchronize()
+    assert tuple(got.shape) == vops.packed_input_shape(*shape[:4])
+    assert torch.equal(got, two_pass)
+    assert torch.equal(got.cpu().float(), vops.preprocess(u8, packed=True).float())
+
+
+def test_engine_packed_input_bit_identical():
+    """engine.forward(preprocess(u8, packed=True), packed=True) gives the same
+    logits as the unpacked input through the engine's own stem_pack."""
+    from rnb_amd.models.r2p1d.model import build_network
+    from rnb_amd.models.r2p1d.engine import R2P1DEngine
+    net = build_network(1, 5, depth=18, seed=0)
+    eng = R2P1DEngine(net, DEV, backend="hip")
+    assert eng.accepts_packed_input
+    u8 = vops.clipgen_u8(torch.tensor([1, 2, 9], dtype=torch.int32, device=DEV),
+                         torch.tensor([0, 5, 30], dtype=torch.int32, device=DEV), 8, 112, 112)
+    with torch.no_grad():
+        a = eng.forward(vops.preprocess(u8))
+        b = eng.forward(vops.preprocess(u8, packed=True), packed=True)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), (a - b).abs().max().item()

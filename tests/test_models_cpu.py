@@ -177,3 +177,25 @@ def test_engine_uses_packed_stem():
     eng = R2P1DEngine(net, torch.device("cpu"), backend="torch")
     assert isinstance(eng.ops[0].layer, StemConv)
     assert eng.flops_per_clip() > 0
+
+
+def test_engine_packed_input_matches_unpacked():
+    """The decoder can write the stem's pair-packed layout directly
+    (ops.video.preprocess(packed=True)); the engine's logits match."""
+    from rnb_amd.ops import video as vops
+    net = build_network(1, 5, depth=18, seed=0)
+    eng = R2P1DEngine(net, torch.device("cpu"), backend="torch")
+    assert eng.accepts_packed_input
+    u8 = torch.randint(0, 256, (1, 8, 112, 112, 3), dtype=torch.uint8,
+                       generator=torch.Generator().manual_seed(2))
+    xp = vops.preprocess(u8, packed=True)
+    assert tuple(xp.shape) == eng.input_shape(1, packed=True) == (1, 8, 118, 59, 8)
+    with torch.no_grad():
+        a = eng.forward(vops.preprocess(u8))
+        b = eng.forward(xp, packed=True)
+    err = (a - b).abs().max().item()
+    assert err <= 2e-2 * a.abs().max().item(), err
+    mod = R2P1DEngine(net, torch.device("cpu"), backend="module")
+    assert not mod.accepts_packed_input
+    with pytest.raises(ValueError):
+        mod.input_shape(1, packed=True)
