@@ -48,6 +48,10 @@ def parse_args(argv=None):
                     help="clip budget per model invocation: videos are packed in "
                          "arrival order until the next one would exceed it, so "
                          "batches fill a captured graph bucket exactly")
+    ap.add_argument("--packing", choices=["first-fit", "arrival"], default="first-fit",
+                    help="how a step's videos are split into batches (pack_step)")
+    ap.add_argument("--bucket-step", type=int, default=4,
+                    help="HIP-graph clip buckets every this many clips")
     ap.add_argument("--replicas", type=int, default=3,
                     help="concurrent serving streams per GPU (RnB replication)")
     ap.add_argument("--seed", type=int, default=1234)
@@ -57,6 +61,39 @@ def parse_args(argv=None):
                     help="write a per-kernel time table of the timed steps (rocprofiler-"
                          "sdk tracer, rnb_amd.profiling.tracer) to this path")
     return ap.parse_args(argv)
+
+
+def pack_step(videos, clip_cap: int, video_cap: int, mode: str = "first-fit"):
+    """Split one step's arriving videos into model batches of at most
+    ``clip_cap`` clips and ``video_cap`` videos.
+
+    ``arrival``: consecutive runs in arrival order (a batch closes when the
+    next video does not fit). ``first-fit``: each video, in arrival order,
+    joins the first open batch it fits in, so the 1-clip videos fill the
+    gaps a 15-clip video leaves and all batches but the last are (nearly)
+    full -- less padding up to the graph bucket. A step's videos arrive
+    together, so either order serves them from the same burst.
+    """
+    if mode not in ("arrival", "first-fit"):
+        raise ValueError("unknown packing %r" % (mode,))
+    out, clips = [], []
+
+    def fits(i, n):
+        return clips[i] + n <= clip_cap and len(out[i]) < video_cap
+
+    for v in videos:
+        n = len(v[1])
+        if mode == "arrival":
+            target = len(out) - 1 if out and fits(len(out) - 1, n) else None
+        else:
+            target = next((i for i in range(len(out)) if fits(i, n)), None)
+        if target is None:
+            out.append([v])
+            clips.append(n)
+        else:
+            out[target].append(v)
+            clips[target] += n
+    return out
 
 
 def make_workload(n_videos: int, seed: int):
@@ -110,27 +147,17 @@ def main(argv=None) -> int:
     vps, vb = args.videos_per_step, args.video_batch
     total_steps = args.warmup + args.steps
     workload = make_workload(vps * total_steps, args.seed + 7919 * rank)
-    # per step: pack the step's videos (arrival order) into batches of at most
-    # --clips-per-batch clips and --video-batch videos
-    step_batches = []
-    for st in range(total_steps):
-        vids, cur, cur_clips, out = workload[st * vps:(st + 1) * vps], [], 0, []
-        for v in vids:
-            n = len(v[1])
-            if cur and (cur_clips + n > args.clips_per_batch or len(cur) >= vb):
-                out.append(cur)
-                cur, cur_clips = [], 0
-            cur.append(v)
-            cur_clips += n
-        if cur:
-            out.append(cur)
-        step_batches.append(out)
+    # per step: pack the step's videos into batches of at most
+    # --clips-per-batch clips and --video-batch videos (pack_step)
+    step_batches = [pack_step(workload[st * vps:(st + 1) * vps], args.clips_per_batch, vb,
+                              args.packing) for st in range(total_steps)]
     batches = [b for sb in step_batches for b in sb]
     max_clips = max(max(sum(len(s) for _, s in b) for b in batches), args.clips_per_batch)
-    # graph buckets every 8 clips: a batch pads to the next bucket, so the
-    # padding stays < 8 clips per batch (2.3 % of the clips vs 6.2 % with
-    # power-of-two-ish buckets on the reference clip mix)
-    buckets = sorted(set(range(8, args.clips_per_batch + 1, 8))
+    # graph buckets every --bucket-step clips: a batch pads to the next
+    # bucket (every 8 clips with arrival-order packing: 2.3 % of the clips
+    # padded vs 6.2 % with power-of-two-ish buckets on the reference clip mix)
+    bstep = max(1, args.bucket_step)
+    buckets = sorted(set(range(bstep, args.clips_per_batch + 1, bstep))
                      | {args.clips_per_batch, max_clips})
     eng = FusedR2P1D(device, depth=args.depth, replicas=args.replicas,
                      max_clips=max(max_clips, 1), max_videos=vb, buckets=buckets,
@@ -236,6 +263,7 @@ def main(argv=None) -> int:
                        "parallelism": "dp%d (replicated runners)" % world,
                        "pipeline": "r2p1d-whole (loader+model per GPU, fused)",
                        "video_batch": vb, "clips_per_batch": args.clips_per_batch,
+                       "packing": args.packing, "bucket_step": bstep,
                        "replicas_per_gpu": args.replicas,
                        "clip": "8x112x112", "clips_dist": "1 w.p. 10/11, 15 w.p. 1/11",
                        "prepare_s": round(prep_s, 1)},
