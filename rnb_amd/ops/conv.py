@@ -16,6 +16,7 @@ CPU execution path.
 from __future__ import annotations
 
 import math
+import threading
 from dataclasses import dataclass
 from typing import Dict, Optional, Tuple
 
@@ -476,7 +477,18 @@ class StemConv(ConvLayer):
         # torch path runs the real conv on the bf16-rounded original weight
         self.w_ref = weight.detach().to(torch.bfloat16).float().to(device)
         self.use_halo = self.use_temporal = self.use_halo_ws = False
-        self._in_packed = False
+        self._tls = threading.local()
+
+    @property
+    def _in_packed(self) -> bool:
+        """True while a base-class method runs on the packed input. Kept per
+        thread, so replicas driving one engine from several threads do not
+        see each other's state."""
+        return getattr(self._tls, "packed", False)
+
+    @_in_packed.setter
+    def _in_packed(self, v: bool):
+        self._tls.packed = v
 
     @staticmethod
     def eligible(geom: ConvGeom) -> bool:
