@@ -297,6 +297,65 @@ __global__ __launch_bounds__(256) void video_reduce_kernel(const float* __restri
   if (threadIdx.x == 0) argmax[v] = (c1 > c0) ? bi[0] : -1;
 }
 
+
+// fp32 path (reference precision): uint8 NFHWC3 -> normalised fp32 NDHWC4
+// (channel 3 zero), so one 16-byte chunk is one pixel and the stem conv's K
+// is 7*7*4 = 196. One thread per 4 pixels: three dword loads, 4 x 16 B out.
+__global__ void preprocess_f32_kernel(const uint8_t* __restrict__ in, float* __restrict__ out,
+                                      long long npix, NormParams np) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long i0 = q * 4;
+  if (i0 >= npix) return;
+  auto emit = [&](long long i, uint32_t r8, uint32_t g8, uint32_t b8) {
+    *(float4*)(out + i * 4) = make_float4((float)r8 * np.scale[0] + np.shift[0],
+                                          (float)g8 * np.scale[1] + np.shift[1],
+                                          (float)b8 * np.scale[2] + np.shift[2], 0.f);
+  };
+  if (i0 + 4 <= npix) {
+    const uint32_t* w = (const uint32_t*)(in + i0 * 3);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    emit(i0 + 0, w0 & 255u, (w0 >> 8) & 255u, (w0 >> 16) & 255u);
+    emit(i0 + 1, w0 >> 24, w1 & 255u, (w1 >> 8) & 255u);
+    emit(i0 + 2, (w1 >> 16) & 255u, w1 >> 24, w2 & 255u);
+    emit(i0 + 3, (w2 >> 8) & 255u, (w2 >> 16) & 255u, w2 >> 24);
+  } else {
+    for (long long i = i0; i < npix; ++i) {
+      const uint8_t* px = in + i * 3;
+      emit(i, px[0], px[1], px[2]);
+    }
+  }
+}
+
+// fp32 head, part 1: average pool of an fp32 NDHWC tensor. One thread per
+// (clip, 4 channels): 16-byte loads, 7 in flight per thread.
+__global__ __launch_bounds__(256) void head_pool_f32_kernel(const float* __restrict__ x,
+                                                            float* __restrict__ pooled, int N,
+                                                            int S, int C, int Cs) {
+  const int cq = C / 4;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)N * cq) return;
+  const int n = (int)(i / cq);
+  const int c = (int)(i - (long long)n * cq) * 4;
+  const float* xc = x + (size_t)n * S * Cs + c;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  int t = 0;
+  for (; t + 7 <= S; t += 7) {
+    float4 v[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) v[j] = *(const float4*)(xc + (size_t)(t + j) * Cs);
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w;
+    }
+  }
+  for (; t < S; ++t) {
+    const float4 v = *(const float4*)(xc + (size_t)t * Cs);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  const float inv = 1.0f / (float)S;
+  *(float4*)(pooled + (size_t)n * C + c) = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
+}
+
 extern "C" {
 
 int rnb_clipgen_u8(void* out, const int* vids, const int* starts, int nclips, int F, int H,
@@ -380,6 +439,38 @@ int rnb_preprocess_packed(const void* in, void* out, long long frames, int H, in
   const long long nout = frames * Hp * Wq;
   hipLaunchKernelGGL(preprocess_packed_kernel, dim3((unsigned)((nout + 255) / 256)), dim3(256),
                      0, stream, (const uint8_t*)in, (uint16_t*)out, nout, H, W, Hp, Wq, np);
+  return (int)hipGetLastError();
+}
+
+int rnb_preprocess_f32(const void* in, void* out, long long npix, const float* mean,
+                       const float* stdv, hipStream_t stream) {
+  if (npix <= 0) return 0;
+  NormParams np;
+  for (int c = 0; c < 3; ++c) {
+    np.scale[c] = 1.0f / (255.0f * stdv[c]);
+    np.shift[c] = -mean[c] / stdv[c];
+  }
+  if (((uintptr_t)in & 3u) != 0 || ((uintptr_t)out & 15u) != 0) return -2;
+  const int block = 256;
+  const long long grid = ((npix + 3) / 4 + block - 1) / block;
+  hipLaunchKernelGGL(preprocess_f32_kernel, dim3((unsigned)grid), dim3(block), 0, stream,
+                     (const uint8_t*)in, (float*)out, npix, np);
+  return (int)hipGetLastError();
+}
+
+// x: fp32 [N][S][Cs]; w: TRANSPOSED linear weight [C][ncls]; pooled: [N][C] scratch
+int rnb_head_f32(const float* x, const float* w, const float* b, float* out, float* pooled,
+                 int N, int S, int C, int Cs, int ncls, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (C % 16 != 0 || Cs % 4 != 0 || Cs < C || !pooled) return -2;
+  const size_t lds = ((size_t)HEAD_CLIPS * C + 4 * HEAD_CLIPS * HEAD_CLS) * sizeof(float);
+  if (lds > 64 * 1024) return -3;
+  const long long threads = (long long)N * (C / 4);
+  hipLaunchKernelGGL(head_pool_f32_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256),
+                     0, stream, x, pooled, N, S, C, Cs);
+  const dim3 grid((ncls + HEAD_CLS - 1) / HEAD_CLS, (N + HEAD_CLIPS - 1) / HEAD_CLIPS);
+  hipLaunchKernelGGL(head_linear_kernel, grid, dim3(256), lds, stream, pooled, w, b, out, N, C,
+                     ncls);
   return (int)hipGetLastError();
 }
 

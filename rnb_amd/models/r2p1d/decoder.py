@@ -38,23 +38,27 @@ class Decoder:
 
 class SyntheticDecoder(Decoder):
     def __init__(self, device: torch.device, clip_length: int = 8, height: int = 112,
-                 width: int = 112):
+                 width: int = 112, dtype=torch.bfloat16):
         self.device = device
         self.F, self.H, self.W = clip_length, height, width
+        self.dtype = dtype
 
     def probe(self, path):
         return parse_synthetic_path(path)
 
+    def empty(self):
+        c = vops.IN_CHANNELS_P_F32 if self.dtype == torch.float32 else vops.IN_CHANNELS_P
+        return torch.zeros((0, self.F, self.H, self.W, c), dtype=self.dtype, device=self.device)
+
     def decode(self, vid, starts, out=None):
         n = len(starts)
         if n == 0:
-            return torch.zeros((0, self.F, self.H, self.W, vops.IN_CHANNELS_P),
-                               dtype=torch.bfloat16, device=self.device)
+            return self.empty()
         meta = torch.tensor([[vid] * n, list(starts)], dtype=torch.int32)
         if self.device.type == "cuda":
             meta = meta.pin_memory().to(self.device, non_blocking=True)
         surf = vops.clipgen_u8(meta[0], meta[1], self.F, self.H, self.W)
-        return vops.preprocess(surf, out=out)
+        return vops.preprocess(surf, out=out, dtype=self.dtype)
 
 
 class NpyDecoder(Decoder):

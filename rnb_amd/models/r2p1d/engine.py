@@ -37,6 +37,7 @@ import torch
 from ...ops.bn import BatchNormBatch
 from ...ops.conv import ConvGeom, ConvLayer, StemConv, fold_bn, pad_to, CH_ALIGN
 from ...ops.conv21 import FusedSTConv
+from ...ops.conv_f32 import F32_ALIGN, ConvLayerF32
 from ...ops.video import (Head, IN_CHANNELS_P, ndhwc_to_ncdhw, ncdhw_to_ndhwc,
                           packed_input_shape)
 from .network import (LAYER_CHANNELS, LAYER_INPUT_CTHW, LAYER_OUTPUT_CTHW,
@@ -46,16 +47,18 @@ DEFAULT_BUCKETS = (1, 2, 3, 4, 5, 6, 8, 10, 12, 15, 16, 20, 24, 30, 32, 40, 45, 
                    60, 64, 80, 96, 128)
 
 
-def boundary_channels_p(layer_idx: int) -> int:
-    """Channels (padded) of the NDHWC tensor entering layer ``layer_idx``."""
+def boundary_channels_p(layer_idx: int, dtype=torch.bfloat16) -> int:
+    """Channels (padded) of the NDHWC tensor entering layer ``layer_idx``:
+    multiples of 8 for bf16 (16-byte pixels), of 4 for fp32."""
+    align = F32_ALIGN if dtype == torch.float32 else CH_ALIGN
     if layer_idx == 1:
-        return IN_CHANNELS_P
-    return pad_to(LAYER_INPUT_CTHW[layer_idx][0], CH_ALIGN)
+        return align if dtype == torch.float32 else IN_CHANNELS_P
+    return pad_to(LAYER_INPUT_CTHW[layer_idx][0], align)
 
 
-def boundary_shape(layer_idx: int, n: int) -> Tuple[int, ...]:
+def boundary_shape(layer_idx: int, n: int, dtype=torch.bfloat16) -> Tuple[int, ...]:
     c, t, h, w = LAYER_INPUT_CTHW[layer_idx]
-    return (n, t, h, w, boundary_channels_p(layer_idx))
+    return (n, t, h, w, boundary_channels_p(layer_idx, dtype))
 
 
 class PlanOp:
@@ -73,17 +76,24 @@ class PlanOp:
 
 class R2P1DEngine:
     def __init__(self, net: R2Plus1DLayerWrapper, device: torch.device,
-                 backend: str = "hip", bn_mode: str = "eval"):
+                 backend: str = "hip", bn_mode: str = "eval", dtype=torch.bfloat16):
         if backend not in ("hip", "torch", "module"):
             raise ValueError("unknown backend %r" % backend)
         if bn_mode not in ("eval", "batch"):
             raise ValueError("bn_mode must be 'eval' or 'batch'")
+        dtype = _as_dtype(dtype)
+        if dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("dtype must be bfloat16 or float32, got %s" % dtype)
         self.net = net
         self.device = device
         self.backend = backend
         self.bn_mode = bn_mode
-        # conv1 spatial on the pair-packed input (ops/conv.StemConv)
-        self.pack_stem = os.environ.get("RNB_STEM_PACK", "1") != "0"
+        # activation / compute dtype: float32 = the reference's precision
+        # (csrc/conv_f32.hip, fp32 MFMA), bfloat16 = the fast serving path
+        self.dtype = dtype
+        self.f32 = dtype == torch.float32
+        # conv1 spatial on the pair-packed input (ops/conv.StemConv, bf16 only)
+        self.pack_stem = os.environ.get("RNB_STEM_PACK", "1") != "0" and not self.f32
         self.start_idx, self.end_idx = net.start_idx, net.end_idx
         self.num_classes = getattr(net, "num_classes", 400)
         self.ops: List[PlanOp] = []
@@ -109,7 +119,8 @@ class R2P1DEngine:
         w, b = fold_bn(conv.weight, conv.bias, bn)
         geom = ConvGeom(cin=conv.in_channels, cout=conv.out_channels,
                         kernel=tuple(conv.kernel_size), stride=tuple(conv.stride),
-                        padding=tuple(conv.padding))
+                        padding=tuple(conv.padding),
+                        align=F32_ALIGN if self.f32 else CH_ALIGN)
         T, H, W = self._thw[src]
         self._thw[dst] = geom.out_thw(T, H, W)
         nominal = geom
@@ -121,8 +132,11 @@ class R2P1DEngine:
             # 1/3 of the MACs (same result)
             w = w[:, :, pt:pt + 1].contiguous()
             geom = ConvGeom(cin=geom.cin, cout=geom.cout, kernel=(1,) + geom.kernel[1:],
-                            stride=geom.stride, padding=(0,) + geom.padding[1:])
-        if self.pack_stem and StemConv.eligible(geom):
+                            stride=geom.stride, padding=(0,) + geom.padding[1:],
+                            align=geom.align)
+        if self.f32:
+            layer = ConvLayerF32(w, b, geom, relu, self.device, name)
+        elif self.pack_stem and StemConv.eligible(geom):
             layer = StemConv(w, b, geom, relu, self.device, name)
         else:
             layer = ConvLayer(w, b, geom, relu, self.device, name)
@@ -136,7 +150,8 @@ class R2P1DEngine:
         dst = self._name()
         self._append(st.temporal_conv, post_bn, relu, res, name + ".temporal", mid, dst)
         sp, tp = self.ops[-2], self.ops[-1]
-        if sp.bn is None and tp.bn is None and FusedSTConv.eligible(sp.layer, tp.layer):
+        if (not self.f32 and sp.bn is None and tp.bn is None
+                and FusedSTConv.eligible(sp.layer, tp.layer)):
             # conv2-stage pair: one kernel, intermediate kept on chip (conv21.hip)
             sp.fuse = FusedSTConv(sp.layer, tp.layer)
         return dst
@@ -177,12 +192,12 @@ class R2P1DEngine:
     # ------------------------------------------------------------- metadata
     @property
     def in_channels_p(self) -> int:
-        return boundary_channels_p(self.start_idx)
+        return boundary_channels_p(self.start_idx, self.dtype)
 
     def input_shape(self, n: int, packed: bool = False) -> Tuple[int, ...]:
         """Boundary input shape; ``packed`` = the stem's pair-packed layout
         (only when ``accepts_packed_input``)."""
-        shape = boundary_shape(self.start_idx, n)
+        shape = boundary_shape(self.start_idx, n, self.dtype)
         if not packed:
             return shape
         if not self.accepts_packed_input:
@@ -199,10 +214,10 @@ class R2P1DEngine:
     def output_shape(self, n: int) -> Tuple[int, ...]:
         if self.end_idx == 5:
             return (n, self.num_classes)
-        return boundary_shape(self.end_idx + 1, n)
+        return boundary_shape(self.end_idx + 1, n, self.dtype)
 
     def output_dtype(self):
-        return torch.float32 if self.end_idx == 5 else torch.bfloat16
+        return torch.float32 if self.end_idx == 5 else self.dtype
 
     def flops_per_clip(self) -> int:
         """Useful FLOPs for one 8x112x112 clip through this layer range."""
@@ -229,12 +244,14 @@ class R2P1DEngine:
         if packed and not self.accepts_packed_input:
             raise ValueError("this engine's first op does not take a packed input")
         if self.backend == "module":
-            if x.dim() == 5 and x.shape[-1] == self.in_channels_p and x.dtype == torch.bfloat16:
-                x = ndhwc_to_ncdhw(x, LAYER_INPUT_CTHW[self.start_idx][0])
-            y = self.module(x.to(self.device))
+            cin = LAYER_INPUT_CTHW[self.start_idx][0]
+            if x.dim() == 5 and x.shape[-1] == self.in_channels_p and x.shape[1] != cin:
+                x = ndhwc_to_ncdhw(x, cin)
+            y = self.module(x.to(self.device).float())
             if self.end_idx == 5:
                 return y.float()
-            return ncdhw_to_ndhwc(y, boundary_channels_p(self.end_idx + 1))
+            return ncdhw_to_ndhwc(y, boundary_channels_p(self.end_idx + 1, self.dtype),
+                                  dtype=self.dtype)
         if x.shape[0] == 0:
             return torch.zeros(self.output_shape(0), dtype=self.output_dtype(),
                                device=x.device)
@@ -258,15 +275,15 @@ class R2P1DEngine:
                     y = op.layer.forward_hip(src, None)
                     y = op.bn.forward_hip(y, res, op.bn_relu, out=y)
                 else:
-                    y = op.layer.forward_torch(src, None)
-                    y = op.bn.forward_torch(y, res, op.bn_relu)
+                    y = op.layer.forward_torch(src, None, out_dtype=self.dtype)
+                    y = op.bn.forward_torch(y, res, op.bn_relu, out_dtype=self.dtype)
             elif packed and i == 0:
                 y = (op.layer.forward_hip(src, res, prepacked=True) if hip
                      else op.layer.forward_torch(src, res, prepacked=True))
             elif hip:
                 y = op.layer.forward_hip(src, res)
             else:
-                y = op.layer.forward_torch(src, res)
+                y = op.layer.forward_torch(src, res, out_dtype=self.dtype)
             bufs[op.dst] = y
         y = bufs[self.out_name]
         if self.head is not None:
@@ -282,7 +299,7 @@ class R2P1DEngine:
         """Pick the fastest tile per conv for ``n`` clips (GPU only)."""
         assert self.backend == "hip"
         self.fused_choices = {}
-        x = torch.randn(self.input_shape(n), device=self.device).to(torch.bfloat16)
+        x = torch.randn(self.input_shape(n), device=self.device).to(self.dtype)
         bufs = {"x": x}
         chosen = {}
         for op in self.ops:
@@ -310,6 +327,16 @@ class R2P1DEngine:
             self.fused_choices[op.fuse.name] = best
         torch.cuda.synchronize(self.device)
         return chosen
+
+
+def _as_dtype(d):
+    if isinstance(d, torch.dtype):
+        return d
+    names = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32,
+             "float32": torch.float32, "float": torch.float32}
+    if d not in names:
+        raise ValueError("unknown dtype %r (use 'fp32' or 'bf16')" % (d,))
+    return names[d]
 
 
 def _time(fn, reps: int) -> float:
@@ -354,7 +381,7 @@ class GraphedEngine:
         eng = self.engine
         if self.autotune:
             eng.autotune(b)
-        static_in = torch.zeros(eng.input_shape(b), dtype=torch.bfloat16, device=self.device)
+        static_in = torch.zeros(eng.input_shape(b), dtype=eng.dtype, device=self.device)
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):

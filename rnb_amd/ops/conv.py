@@ -75,14 +75,15 @@ class ConvGeom:
     kernel: Tuple[int, int, int]
     stride: Tuple[int, int, int]
     padding: Tuple[int, int, int]
+    align: int = CH_ALIGN      # channel padding (8 for bf16, 4 for fp32)
 
     @property
     def cin_p(self) -> int:
-        return pad_to(self.cin, CH_ALIGN)
+        return pad_to(self.cin, self.align)
 
     @property
     def cout_p(self) -> int:
-        return pad_to(self.cout, CH_ALIGN)
+        return pad_to(self.cout, self.align)
 
     @property
     def k_total(self) -> int:

@@ -1,0 +1,228 @@
+"""Channels-last (NDHWC) fp32 3-D convolution layer: the reference-precision path.
+
+The reference computes R(2+1)D in fp32 (reference models/r2p1d/model.py:
+149,225 ``.float()``; cuDNN fp32, runner.py:24-25). ``ConvLayerF32`` is the
+fp32 counterpart of ``ops.conv.ConvLayer``: one folded conv (+ residual add
+and ReLU) over fp32 NDHWC activations, computed by ``csrc/conv_f32.hip`` on
+the gfx950 fp32 matrix cores (exact fp32 products and fp32 accumulation).
+
+Layout: channels padded to ``F32_ALIGN`` = 4 (one 16-byte chunk = 4 fp32
+channels of one tap, the kernel's gather granule); the weight is the GEMM
+matrix ``[Cout_p + 256][K_pad]`` fp32 with k = ((dt*KH + dh)*KW + dw)*Cin_p + c
+and K_pad a multiple of 32 (one 128-byte LDS row); rows past Cout_p are zero.
+Large batches are split into clip chunks so every launch addresses less than
+2 GiB per tensor (32-bit buffer offsets), which makes the layer usable at any
+batch size.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from .conv import ConvGeom, pad_to
+
+F32_ALIGN = 4        # channel padding of fp32 NDHWC activations
+F32_BK = 32          # K per LDS row / K step of the fp32 kernel
+F32_ROW_SLACK = 256  # extra zero weight rows (>= largest channel tile)
+
+
+def f32_geom(cin: int, cout: int, kernel, stride, padding) -> ConvGeom:
+    return ConvGeom(cin=cin, cout=cout, kernel=tuple(kernel), stride=tuple(stride),
+                    padding=tuple(padding), align=F32_ALIGN)
+
+
+class ConvLayerF32:
+    """One folded fp32 conv (+ optional residual add and ReLU) of the plan."""
+
+    dtype = torch.float32
+
+    def __init__(self, weight: torch.Tensor, bias: torch.Tensor, geom: ConvGeom,
+                 relu: bool, device: torch.device, name: str = ""):
+        assert geom.align == F32_ALIGN, geom
+        assert weight.shape == (geom.cout, geom.cin) + tuple(geom.kernel), (weight.shape, geom)
+        self.geom = geom
+        self.relu = bool(relu)
+        self.name = name
+        self.device = device
+        kt, kh, kw = geom.kernel
+        cin_p, cout_p = geom.cin_p, geom.cout_p
+        self.k_total = kt * kh * kw * cin_p
+        self.k_pad = pad_to(self.k_total, F32_BK)
+        w = torch.zeros(geom.cout, kt, kh, kw, cin_p, dtype=torch.float32)
+        w[..., :geom.cin] = weight.detach().float().permute(0, 2, 3, 4, 1)
+        wmat = torch.zeros(cout_p + F32_ROW_SLACK, self.k_pad, dtype=torch.float32)
+        wmat[:geom.cout, :self.k_total] = w.reshape(geom.cout, -1)
+        b = torch.zeros(cout_p + F32_ROW_SLACK, dtype=torch.float32)
+        b[:geom.cout] = bias.detach().float()
+        self.wmat = wmat.to(device).contiguous()
+        self.bias = b.to(device).contiguous()
+        self.w_ref = weight.detach().float().to(device)
+        self.b_ref = bias.detach().float().to(device)
+        self._config: Dict[Tuple[int, int, int, int], int] = {}
+        self._ktab: Dict[Tuple[int, int, int], torch.Tensor] = {}
+
+    # ------------------------------------------------------------------
+    def out_shape(self, x_shape) -> Tuple[int, int, int, int, int]:
+        N, T, H, W, _ = x_shape
+        To, Ho, Wo = self.geom.out_thw(T, H, W)
+        return (N, To, Ho, Wo, self.geom.cout_p)
+
+    def ktab(self, T: int, H: int, W: int, device) -> torch.Tensor:
+        """Per-16-byte K chunk (4 channels of one tap) gather table: byte offset of
+        the chunk relative to the output pixel's input origin + validity bits
+        (bit dt, 8 + dh, 16 + dw); chunks past K_total require bit 31."""
+        key = (T, H, W)
+        tab = self._ktab.get(key)
+        if tab is None:
+            g = self.geom
+            kt, kh, kw = g.kernel
+            if max(kt, kh, kw) > 8:
+                raise ValueError("kernel extent > 8 not supported by the gather table")
+            k = torch.arange(self.k_pad // 4, dtype=torch.int64) * 4
+            tap, c = k // g.cin_p, k % g.cin_p
+            dw, dh, dt = tap % kw, (tap // kw) % kh, tap // (kw * kh)
+            delta = (((dt * H + dh) * W + dw) * g.cin_p + c) * 4
+            req = (1 << dt) | (1 << (8 + dh)) | (1 << (16 + dw))
+            valid = k < self.k_total
+            delta = torch.where(valid, delta, torch.zeros_like(delta))
+            req = torch.where(valid, req, torch.full_like(req, -(1 << 31)))
+            tab = torch.stack([delta, req], dim=1).to(torch.int32).contiguous().to(device)
+            self._ktab[key] = tab
+        return tab
+
+    def params(self, x: torch.Tensor, y: torch.Tensor, residual: Optional[torch.Tensor],
+               n0: int = 0, n1: Optional[int] = None):
+        """Launch parameters for clips [n0, n1) of the batch."""
+        from .native import ConvParams
+        g = self.geom
+        N, T, H, W, C = x.shape
+        n1 = N if n1 is None else n1
+        if C != g.cin_p:
+            raise ValueError("%s: input has %d channels, expected %d" % (self.name, C, g.cin_p))
+        _, To, Ho, Wo, Co = y.shape
+        xs, ys = T * H * W * C * 4, To * Ho * Wo * Co * 4
+        p = ConvParams()
+        p.x = x.data_ptr() + n0 * xs
+        p.w, p.bias = self.wmat.data_ptr(), self.bias.data_ptr()
+        if residual is not None:
+            p.res = residual.data_ptr() + n0 * To * Ho * Wo * residual.shape[-1] * 4
+        else:
+            p.res = None
+        p.y = y.data_ptr() + n0 * ys
+        p.N, p.T, p.H, p.W, p.Cin_p = n1 - n0, T, H, W, g.cin_p
+        p.To, p.Ho, p.Wo = To, Ho, Wo
+        p.KT, p.KH, p.KW = g.kernel
+        p.ST, p.SH, p.SW = g.stride
+        p.PT, p.PH, p.PW = g.padding
+        p.Cout_p = g.cout_p
+        p.y_stride = Co
+        p.res_stride = residual.shape[-1] if residual is not None else 0
+        p.K_total, p.K_pad = self.k_total, self.k_pad
+        p.M = (n1 - n0) * To * Ho * Wo
+        p.relu = 1 if self.relu else 0
+        p.w_rows = self.wmat.shape[0]
+        p.ktab = self.ktab(T, H, W, x.device).data_ptr()
+        p.row_mode = 0
+        return p
+
+    def chunk_clips(self, x_shape, y_shape, res_stride: int = 0) -> int:
+        """Most clips one launch may cover (32-bit buffer offsets)."""
+        from .native import kernels
+        limit = kernels().f32_max_bytes
+        _, T, H, W, C = x_shape
+        _, To, Ho, Wo, Co = y_shape
+        per = max(T * H * W * C, To * Ho * Wo * max(Co, res_stride)) * 4
+        return max(1, limit // per)
+
+    def heuristic_config(self, M: int) -> int:
+        from .native import kernels
+        best, best_cost = 0, None
+        cp = self.geom.cout_p
+        for cid, (pt, ct) in enumerate(kernels().f32_configs):
+            nblk = math.ceil(M / pt) * math.ceil(cp / ct)
+            work = math.ceil(M / pt) * pt * math.ceil(cp / ct) * ct
+            waves = math.ceil(nblk / 512.0)
+            cost = work * (1.0 + 8.0 / pt + 8.0 / ct) * (waves * 512.0 / max(nblk, 1)) ** 0.5
+            if best_cost is None or cost < best_cost:
+                best, best_cost = cid, cost
+        return best
+
+    def config_for(self, x_shape) -> int:
+        key = tuple(x_shape[:4])
+        cid = self._config.get(key)
+        if cid is None:
+            N, T, H, W, _ = x_shape
+            To, Ho, Wo = self.geom.out_thw(T, H, W)
+            cid = self._config[key] = self.heuristic_config(N * To * Ho * Wo)
+        return cid
+
+    def _launch_all(self, x, y, residual, cid, stream):
+        from .native import kernels
+        k = kernels()
+        N = x.shape[0]
+        step = self.chunk_clips(x.shape, y.shape,
+                                residual.shape[-1] if residual is not None else 0)
+        for n0 in range(0, N, step):
+            k.conv_f32(self.params(x, y, residual, n0, min(N, n0 + step)), cid,
+                       stream.cuda_stream)
+
+    def autotune(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                 reps: int = 3) -> int:
+        """Time every fp32 tile config on this input shape; keep the fastest."""
+        from .native import kernels
+        y = torch.empty(self.out_shape(x.shape), dtype=torch.float32, device=x.device)
+        stream = torch.cuda.current_stream(x.device)
+        best, best_t = None, None
+        for cid in range(len(kernels().f32_configs)):
+            self._launch_all(x, y, residual, cid, stream)       # warm
+            start = torch.cuda.Event(enable_timing=True)
+            end = torch.cuda.Event(enable_timing=True)
+            start.record(stream)
+            for _ in range(reps):
+                self._launch_all(x, y, residual, cid, stream)
+            end.record(stream)
+            end.synchronize()
+            t = start.elapsed_time(end) / reps
+            if best_t is None or t < best_t:
+                best, best_t = cid, t
+        self._config[tuple(x.shape[:4])] = best
+        return best
+
+    # ------------------------------------------------------------------
+    def forward_hip(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                    out: Optional[torch.Tensor] = None, config: Optional[int] = None):
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            raise ValueError("%s: expected contiguous fp32 NDHWC input" % self.name)
+        y = out if out is not None else torch.empty(self.out_shape(x.shape),
+                                                    dtype=torch.float32, device=x.device)
+        if tuple(y.shape[:4]) != tuple(self.out_shape(x.shape)[:4]) or y.dtype != torch.float32:
+            raise ValueError("%s: output %s does not match" % (self.name, tuple(y.shape)))
+        if residual is not None:
+            if residual.shape[:4] != y.shape[:4] or residual.dtype != torch.float32 \
+                    or not residual.is_contiguous():
+                raise ValueError("%s: residual %s does not match output %s"
+                                 % (self.name, tuple(residual.shape), tuple(y.shape)))
+        if x.shape[0] == 0:
+            return y
+        cid = self.config_for(x.shape) if config is None else config
+        self._launch_all(x, y, residual, cid, torch.cuda.current_stream(x.device))
+        return y
+
+    def forward_torch(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                      out_dtype=torch.float32):
+        """fp32 reference of the same op (F.conv3d on the folded fp32 weight)."""
+        g = self.geom
+        xin = x[..., :g.cin].float().permute(0, 4, 1, 2, 3)
+        y = F.conv3d(xin, self.w_ref.to(x.device), self.b_ref.to(x.device),
+                     stride=g.stride, padding=g.padding)
+        y = y.permute(0, 2, 3, 4, 1)
+        if residual is not None:
+            y = y + residual[..., :g.cout].float()
+        if self.relu:
+            y = torch.relu(y)
+        if g.cout_p != g.cout:
+            y = F.pad(y, (0, g.cout_p - g.cout))
+        return y.to(out_dtype).contiguous()

@@ -220,6 +220,27 @@ class Kernels:
             raise NativeUnavailable("ConvParams layout mismatch (%d vs %d): rebuild"
                                     % (lib.rnb_conv_params_size(),
                                        ctypes.sizeof(ConvParams)))
+        lib.rnb_conv_f32_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
+                                            ctypes.c_void_p]
+        lib.rnb_conv_f32_launch.restype = ctypes.c_int
+        lib.rnb_conv_f32_config_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                                 ctypes.POINTER(ctypes.c_int)]
+        lib.rnb_conv_f32_max_bytes.restype = ctypes.c_longlong
+        lib.rnb_preprocess_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
+                                           ctypes.POINTER(ctypes.c_float),
+                                           ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
+        lib.rnb_head_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_void_p]
+        if lib.rnb_conv_f32_params_size() != ctypes.sizeof(ConvParams):
+            raise NativeUnavailable("ConvF32Params layout mismatch: rebuild")
+        self.f32_configs = []      # (pixel tile, channel tile) per fp32 config id
+        for i in range(lib.rnb_conv_f32_num_configs()):
+            p, c = ctypes.c_int(), ctypes.c_int()
+            lib.rnb_conv_f32_config_info(i, ctypes.byref(p), ctypes.byref(c))
+            self.f32_configs.append((p.value, c.value))
+        self.f32_max_bytes = lib.rnb_conv_f32_max_bytes()
         self.configs = []          # (pixel tile, channel tile) per config id
         self.stages = []           # LDS staging depth per config id
         for i in range(lib.rnb_conv_num_configs()):
@@ -231,6 +252,20 @@ class Kernels:
     def conv(self, params: ConvParams, config_id: int, stream: int) -> None:
         _check(self.lib.rnb_conv_launch(ctypes.byref(params), config_id, stream),
                "conv (config %d)" % config_id)
+
+    def conv_f32(self, params: ConvParams, config_id: int, stream: int) -> None:
+        _check(self.lib.rnb_conv_f32_launch(ctypes.byref(params), config_id, stream),
+               "conv_f32 (config %d)" % config_id)
+
+    def preprocess_f32(self, in_ptr, out_ptr, npix, mean, std, stream):
+        m = (ctypes.c_float * 3)(*mean)
+        s = (ctypes.c_float * 3)(*std)
+        _check(self.lib.rnb_preprocess_f32(in_ptr, out_ptr, npix, m, s, stream),
+               "preprocess_f32")
+
+    def head_f32(self, x_ptr, w_ptr, b_ptr, out_ptr, pooled_ptr, N, S, C, Cs, ncls, stream):
+        _check(self.lib.rnb_head_f32(x_ptr, w_ptr, b_ptr, out_ptr, pooled_ptr, N, S, C, Cs,
+                                     ncls, stream), "head_f32")
 
     def halo(self, params: HaloParams, stream: int, variant: int = 2) -> None:
         """variant (csrc/conv_halo.hip kHalo): 2 = 32-pixel waves, 4 = 64-pixel

@@ -12,7 +12,8 @@ import torch
 # Kinetics-400 normalisation used by R(2+1)D
 KINETICS_MEAN = (0.43216, 0.394666, 0.37645)
 KINETICS_STD = (0.22803, 0.22145, 0.216989)
-IN_CHANNELS_P = 8   # RGB padded to 8 channels (16-byte NDHWC pixels)
+IN_CHANNELS_P = 8   # RGB padded to 8 channels (16-byte NDHWC bf16 pixels)
+IN_CHANNELS_P_F32 = 4   # RGB padded to 4 channels (16-byte NDHWC fp32 pixels)
 
 _M32 = 0xFFFFFFFF
 
@@ -53,15 +54,22 @@ def clipgen_u8(vids: torch.Tensor, starts: torch.Tensor, F: int, H: int, W: int,
 
 
 def preprocess(frames_u8: torch.Tensor, mean=KINETICS_MEAN, std=KINETICS_STD,
-               out: Optional[torch.Tensor] = None, packed: bool = False) -> torch.Tensor:
+               out: Optional[torch.Tensor] = None, packed: bool = False,
+               dtype=torch.bfloat16) -> torch.Tensor:
     """uint8 [n, F, H, W, 3] -> normalised bf16 [n, F, H, W, 8] (NDHWC).
 
     ``packed=True`` writes the stem conv's zero-bordered pixel-pair layout
     [n, F, H+6, (W+6)/2, 8] instead (``ops.conv.stem_pack`` of the NDHWC
     result, in one pass: ``video_ops.hip: preprocess_packed_kernel``).
+    ``dtype=torch.float32`` (the reference precision) writes fp32
+    [n, F, H, W, 4] (``preprocess_f32_kernel``).
     """
     n, F, H, W, C = frames_u8.shape
     assert C == 3
+    if dtype == torch.float32:
+        if packed:
+            raise ValueError("the packed stem layout is bf16 only")
+        return _preprocess_f32(frames_u8, mean, std, out)
     if packed:
         return _preprocess_packed(frames_u8, mean, std, out)
     if frames_u8.is_cuda:
@@ -78,6 +86,32 @@ def preprocess(frames_u8: torch.Tensor, mean=KINETICS_MEAN, std=KINETICS_STD,
     y = frames_u8.float() * scale + shift
     res = torch.zeros((n, F, H, W, IN_CHANNELS_P), dtype=torch.bfloat16)
     res[..., :3] = y.to(torch.bfloat16)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+def _preprocess_f32(frames_u8, mean, std, out):
+    n, F, H, W, _ = frames_u8.shape
+    shape = (n, F, H, W, IN_CHANNELS_P_F32)
+    if frames_u8.is_cuda:
+        from .native import kernels
+        if out is None:
+            out = torch.empty(shape, dtype=torch.float32, device=frames_u8.device)
+        elif tuple(out.shape) != shape or out.dtype != torch.float32 or not out.is_contiguous():
+            raise ValueError("fp32 preprocess: out must be contiguous fp32 %s" % (shape,))
+        kernels().preprocess_f32(frames_u8.contiguous().data_ptr(), out.data_ptr(),
+                                 n * F * H * W, mean, std,
+                                 torch.cuda.current_stream(frames_u8.device).cuda_stream)
+        return out
+    # same arithmetic as the kernel, which contracts x * scale + shift into one
+    # fp32 fma (single rounding): the product of a u8 and an fp32 scale is exact
+    # in fp64, so the fp64 sum rounded once to fp32 is the fma's result
+    scale = torch.tensor([1.0 / (255.0 * s) for s in std], dtype=torch.float32)
+    shift = torch.tensor([-m / s for m, s in zip(mean, std)], dtype=torch.float32)
+    res = torch.zeros(shape, dtype=torch.float32)
+    res[..., :3] = (frames_u8.double() * scale.double() + shift.double()).float()
     if out is not None:
         out.copy_(res)
         return out
@@ -142,9 +176,12 @@ class Head:
             if out is None:
                 out = torch.empty((N, self.num_classes), dtype=torch.float32, device=x.device)
             pooled = torch.empty((N, self.channels), dtype=torch.float32, device=x.device)
-            kernels().head(x.data_ptr(), self.weight_t.data_ptr(), self.bias.data_ptr(),
-                           out.data_ptr(), pooled.data_ptr(), N, T * H * W, self.channels, Cs,
-                           self.num_classes, torch.cuda.current_stream(x.device).cuda_stream)
+            fn = kernels().head_f32 if x.dtype == torch.float32 else kernels().head
+            if x.dtype not in (torch.float32, torch.bfloat16) or not x.is_contiguous():
+                raise ValueError("head: expected a contiguous fp32/bf16 NDHWC tensor")
+            fn(x.data_ptr(), self.weight_t.data_ptr(), self.bias.data_ptr(),
+               out.data_ptr(), pooled.data_ptr(), N, T * H * W, self.channels, Cs,
+               self.num_classes, torch.cuda.current_stream(x.device).cuda_stream)
             return out
         return self.forward_torch(x)
 

@@ -19,9 +19,11 @@ from rnb_amd.models.r2p1d.model import build_network  # noqa: E402
 from rnb_amd.models.r2p1d.engine import R2P1DEngine  # noqa: E402
 
 
-def tile_name(cid):
+def tile_name(cid, f32=False):
     from rnb_amd.ops.native import kernels
     k = kernels()
+    if f32:
+        return "%dx%d" % k.f32_configs[cid]
     if cid >= len(k.configs):
         from rnb_amd.ops.conv import SPECIAL_NAMES
         return SPECIAL_NAMES.get(cid, str(cid))
@@ -35,6 +37,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--autotune", action="store_true")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--compare", action="store_true",
                     help="time every tile config per layer; report best per family")
     ap.add_argument("--fuse", action="store_true",
@@ -42,7 +45,9 @@ def main():
                          "--autotune: always; with it: where the autotuner picked it)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    eng = R2P1DEngine(build_network(1, 5, depth=args.depth), dev, backend="hip")
+    eng = R2P1DEngine(build_network(1, 5, depth=args.depth), dev, backend="hip",
+                      dtype=args.dtype)
+    f32 = eng.f32
     n = args.clips
     if args.fuse and not args.autotune:
         for op in eng.ops:
@@ -50,7 +55,7 @@ def main():
                 op.fuse.force(True)
     if args.autotune:
         eng.autotune(n)
-    x = torch.randn(eng.input_shape(n), device=dev).to(torch.bfloat16)
+    x = torch.randn(eng.input_shape(n), device=dev).to(eng.dtype)
     x[..., 3:] = 0
     bufs = {"x": x}
     rows = []
@@ -101,11 +106,12 @@ def main():
         cid = op.layer.config_for(src.shape)
         rows.append({"name": op.layer.name, "M": N * To * Ho * Wo, "N": g.cout,
                      "K": g.cin * g.kernel[0] * g.kernel[1] * g.kernel[2],
-                     "tile": tile_name(cid), "ms": ms,
+                     "tile": tile_name(cid, f32), "ms": ms,
                      "tflops": flops / ms / 1e9, "gflop": flops / 1e9})
         if args.compare:
             best = {}
-            cands = list(range(len(cfgs))) + op.layer.special_candidates(src.shape)
+            cands = (list(range(len(kernels().f32_configs))) if f32 else
+                     list(range(len(cfgs))) + op.layer.special_candidates(src.shape))
             for c in cands:
                 s.record()
                 for _ in range(args.reps):
@@ -116,7 +122,7 @@ def main():
                 fam = "best"
                 if fam not in best or t < best[fam][1]:
                     best[fam] = (c, t)
-            rows[-1]["best"] = {k: (tile_name(v[0]), v[1]) for k, v in best.items()}
+            rows[-1]["best"] = {k: (tile_name(v[0], f32), v[1]) for k, v in best.items()}
         bufs[op.dst] = y
     tot_ms = sum(r["ms"] for r in rows)
     tot_gf = sum(r["gflop"] for r in rows)
@@ -132,7 +138,7 @@ def main():
           % (len(rows), tot_ms, n, tot_gf / tot_ms, n / tot_ms * 1e3))
     if args.json_out:
         with open(args.json_out, "w") as f:
-            json.dump({"clips": n, "depth": args.depth, "rows": rows,
+            json.dump({"clips": n, "depth": args.depth, "dtype": args.dtype, "rows": rows,
                        "total_ms": tot_ms, "tflops": tot_gf / tot_ms}, f, indent=1)
 
 
