@@ -1,23 +1,39 @@
 """Driver benchmark: node-wide videos/s + p50/p99 latency, R(2+1)D-34.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--pipeline P] [--dtype D]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
-Metric (BASELINE.json): "videos/sec (whole node) + p50/p99 end-to-end
-latency, R(2+1)D-34 8-frame clips". Each rank is one replicated RnB serving
-pipeline on its own MI355X (the r2p1d-whole / aggressive configs: loader +
-whole R(2+1)D-34 per GPU, replication across GPUs): synthetic clips decoded
-on the GPU (clip counts drawn from the reference sampler: 1 clip w.p. 10/11,
-15 clips w.p. 1/11), random-init weights, bf16 compute with fp32
-accumulation, eval-mode BN folded.
+Metric (BASELINE.json): "videos/sec (whole node) + p50/p99 end-to-end latency,
+R(2+1)D-34 8-frame clips". The number comes from the RnB framework itself:
+rank 0 runs ``benchmark.py``'s launcher (rnb_amd/launcher.py) on a pipeline
+config over the N GPUs -- client process, loader processes decoding
+synthetic clips on every GPU, a frame queue, R(2+1)D-34 runner processes that
+batch queued videos on the consumer side and replay HIP graphs -- exactly the
+multi-process path ``benchmark.py -c <config>`` runs. The other torchrun ranks
+only join the final barrier (the launcher spawns one or more processes per
+GPU itself, as the reference does).
 
-One step = ``--videos-per-step`` videos per GPU arriving at once (weak
-scaling), served in batches of ``--video-batch`` videos by ``--replicas``
-concurrent streams (R and B of RnB). Every video goes through the full
-decode -> 66 conv kernels (72 convs, the 6 conv2-stage (2+1)D pairs fused,
-csrc/conv21.hip) -> head -> per-video argmax chain; the argmax of
-every video is copied back to the host inside the timed region. Latency of a
-video = completion of its batch - arrival (step start).
+Precision: ``--dtype fp32`` (default) is the reference's precision (reference
+models/r2p1d/model.py:149,225): fp32 activations and weights, fp32 MFMA
+(csrc/conv_f32.hip), eval-mode BatchNorm folded into the convs in fp64 on the
+host. ``--dtype bf16`` selects the bf16 serving kernels.
+
+Phases of one launcher run (``-mi 0``):
+1. warm-up: W steps of videos, all completed before timing starts;
+2. timed: K steps of V videos per GPU enqueued at once (saturation); the
+   window runs from the end of warm-up to the completion (stream-synchronised)
+   of the last timed video; ``value`` = K*V*N / window;
+3. latency: Poisson arrivals at ``--latency-load`` x the measured throughput
+   for ``--latency-seconds``; ``p50_ms``/``p99_ms`` are enqueue -> result of
+   those requests (the reference's end-to-end keys, rnb_logging.py:171-185).
+
+``--pipeline``: ``global`` (default; reference config/r2p1d-aggressive-global
+.json: a loader and R runners per GPU around ONE global frame queue, so a
+runner pulls clips decoded on any GPU -- peer copies over xGMI when N > 1),
+``aggressive`` (per-GPU queues, BASELINE config #5), ``whole`` (r2p1d-whole:
+loader + runner, one video per model call, BASELINE config #2), ``rnb``
+(LargeSmall routing + Batcher step), ``fused`` (single-process in-process
+engine, the upper bound the pipeline is compared with).
 
 The reference's only published number is 11.30 videos/s (R(2+1)D-18, fp32,
 one older NVIDIA GPU, load-bound at 11.1 req/s offered).
@@ -31,36 +47,190 @@ import sys
 import time
 
 BASELINE_VIDEOS_PER_S = 11.30
+METRIC = "videos/sec (whole node) + p50/p99 end-to-end latency, R(2+1)D-34 8-frame clips"
+ITERATOR = "rnb_amd.models.r2p1d.model.R2P1DVideoPathIterator"
+LOADER = "rnb_amd.models.r2p1d.model.R2P1DLoader"
+RUNNER = "rnb_amd.models.r2p1d.model.R2P1DRunner"
 
 
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__,
                                  formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pipeline", default="global",
+                    choices=["global", "aggressive", "whole", "rnb", "fused"])
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--depth", type=int, default=34)
     ap.add_argument("--videos-per-step", type=int, default=256,
                     help="videos arriving per GPU per step")
+    ap.add_argument("--replicas", type=int, default=2,
+                    help="R(2+1)D runner processes per GPU (the R of RnB)")
+    ap.add_argument("--loaders", type=int, default=1, help="loader processes per GPU")
     ap.add_argument("--video-batch", type=int, default=64,
-                    help="max videos per model invocation (RnB batching)")
+                    help="max videos per model invocation (consumer-side batching)")
     ap.add_argument("--clips-per-batch", type=int, default=128,
-                    help="clip budget per model invocation: videos are packed in "
-                         "arrival order until the next one would exceed it, so "
-                         "batches fill a captured graph bucket exactly")
-    ap.add_argument("--packing", choices=["first-fit", "arrival"], default="first-fit",
-                    help="how a step's videos are split into batches (pack_step)")
-    ap.add_argument("--bucket-step", type=int, default=4,
+                    help="clip capacity of one model invocation (largest graph bucket)")
+    ap.add_argument("--bucket-step", type=int, default=8,
                     help="HIP-graph clip buckets every this many clips")
-    ap.add_argument("--replicas", type=int, default=3,
-                    help="concurrent serving streams per GPU (RnB replication)")
+    ap.add_argument("--batch-wait-ms", type=float, default=0.0,
+                    help="how long a runner waits for more queued videos to batch")
+    ap.add_argument("--slots", type=int, default=None,
+                    help="slots per loader ring (default: sized from the step's work)")
+    ap.add_argument("--latency-seconds", type=float, default=3.0,
+                    help="duration of the Poisson latency phase (0: skip)")
+    ap.add_argument("--latency-load", type=float, default=0.5,
+                    help="offered Poisson load as a fraction of the measured throughput")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-autotune", action="store_true")
     ap.add_argument("--json-out", type=str, default=None)
+    ap.add_argument("--barrier-timeout", type=float, default=900.0)
+    # fused (in-process) engine options
+    ap.add_argument("--packing", choices=["first-fit", "arrival"], default="first-fit")
+    ap.add_argument("--fused-replicas", type=int, default=3)
     ap.add_argument("--trace", type=str, default=None,
-                    help="write a per-kernel time table of the timed steps (rocprofiler-"
-                         "sdk tracer, rnb_amd.profiling.tracer) to this path")
+                    help="(fused) write a per-kernel time table of the timed steps")
     return ap.parse_args(argv)
+
+
+def pipeline_config(args, n_gpus: int) -> dict:
+    """The pipeline JSON (benchmark.py format) for ``--pipeline``."""
+    gpus = list(range(n_gpus))
+    runner = {"model": RUNNER, "start_index": 1, "end_index": 5,
+              "max_clips": args.clips_per_batch, "bucket_step": args.bucket_step,
+              "max_batch_videos": args.video_batch, "batch_wait_ms": args.batch_wait_ms}
+    loader_gpus = [g for g in gpus for _ in range(args.loaders)]
+    runner_gpus = [g for g in gpus for _ in range(args.replicas)]
+    defaults = {"depth": args.depth, "dtype": args.dtype,
+                "autotune": not args.no_autotune}
+    if args.pipeline == "global":
+        steps = [{"model": LOADER, "queue_groups": [{"gpus": loader_gpus, "out_queues": [0]}]},
+                 dict(runner, queue_groups=[{"gpus": runner_gpus, "in_queue": 0}])]
+    elif args.pipeline == "aggressive":
+        steps = [{"model": LOADER,
+                  "queue_groups": [{"gpus": [g] * args.loaders, "out_queues": [g]}
+                                   for g in gpus]},
+                 dict(runner, queue_groups=[{"gpus": [g] * args.replicas, "in_queue": g}
+                                            for g in gpus])]
+    elif args.pipeline == "whole":
+        # r2p1d-whole: one video per model call (BASELINE config #2: batch=1)
+        runner.update(max_clips=15, max_batch_videos=1, bucket_step=1)
+        steps = [{"model": LOADER, "queue_groups": [{"gpus": loader_gpus, "out_queues": [0]}]},
+                 dict(runner, queue_groups=[{"gpus": runner_gpus, "in_queue": 0}])]
+    elif args.pipeline == "rnb":
+        # reference config/rnb.json: 15-clip videos bypass the Batcher step
+        steps = [{"model": LOADER,
+                  "queue_groups": [{"gpus": loader_gpus, "out_queues": [0, 1],
+                                    "queue_selector":
+                                        "rnb_amd.models.r2p1d.model.LargeSmallSelector"}]},
+                 {"model": "rnb_amd.batcher.Batcher", "max_rows": args.clips_per_batch,
+                  "queue_groups": [{"gpus": gpus, "in_queue": 0, "out_queues": [0],
+                                    "batch": args.video_batch},
+                                   {"gpus": gpus, "in_queue": 1, "out_queues": [0]}]},
+                 dict(runner, max_batch_videos=1,
+                      queue_groups=[{"gpus": runner_gpus, "in_queue": 0}])]
+    else:
+        raise ValueError(args.pipeline)
+    if args.slots:
+        for st in steps[:-1]:
+            st["num_shared_tensors"] = args.slots
+    return {"video_path_iterator": ITERATOR, "defaults": defaults, "pipeline": steps}
+
+
+def run_pipeline(args, world: int) -> dict:
+    """Rank 0: one launcher run (benchmark.py path) over ``args.gpus`` GPUs."""
+    from rnb_amd import launcher
+    root = os.path.dirname(os.path.abspath(__file__))
+    out_dir = os.path.join(root, "logs", "bench")
+    os.makedirs(out_dir, exist_ok=True)
+    name = "bench-%s-%s-%dgpu" % (args.pipeline, args.dtype, args.gpus)
+    cfg_path = os.path.join(out_dir, name + ".json")
+    with open(cfg_path, "w") as f:
+        json.dump(pipeline_config(args, args.gpus), f, indent=1)
+    os.environ.setdefault("RNB_TUNE_CACHE", os.path.join(out_dir, "tune_cache.json"))
+    os.environ.setdefault("RNB_NO_TQDM", "1")
+    per_step = args.videos_per_step * args.gpus
+    res_path = os.path.join(out_dir, name + ".result.json")
+    largv = ["-c", cfg_path, "-mi", "0", "-v", str(per_step * args.steps),
+             "--warmup-videos", str(per_step * args.warmup), "--seed", str(args.seed),
+             "--barrier-timeout", str(args.barrier_timeout), "--json-out", res_path,
+             "--log-root", os.path.join(root, "logs")]
+    if args.latency_seconds > 0:
+        largv += ["--latency-seconds", str(args.latency_seconds),
+                  "--latency-load", str(args.latency_load)]
+    t0 = time.time()
+    res = launcher.run(launcher.build_parser().parse_args(largv))
+    res["wall_s"] = time.time() - t0
+    res["config_path"] = os.path.relpath(cfg_path, root)
+    return res
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    # pipelines: the launcher on rank 0 drives all --gpus GPUs, so it runs
+    # with or without torchrun; under torchrun the world must match --gpus.
+    # fused: one engine per rank, so --gpus N needs N ranks.
+    if (world > 1 and world != args.gpus) or \
+            (args.pipeline == "fused" and world != args.gpus):
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        return 2
+    if args.pipeline == "fused":
+        return run_fused(args)
+    import torch.distributed as dist
+    if world > 1:
+        # coordination only (gloo, CPU): the GPUs belong to the launcher's processes
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    rc, line = 0, None
+    if rank == 0:
+        res = run_pipeline(args, world)
+        ok = bool(res.get("ok"))
+        rc = 0 if ok else 1
+        lat = res.get("latency_phase") or {}
+        n_videos = args.videos_per_step * args.gpus * args.steps
+        window = res.get("window_s") or float("nan")
+        value = n_videos / window if ok and window > 0 else 0.0
+        rec = {
+            "metric": METRIC, "value": round(value, 2), "unit": "videos/s",
+            "n_gpus": args.gpus, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * window / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_VIDEOS_PER_S, 2),
+            "dtype": args.dtype,
+            "data": "synthetic clips (GPU-decoded, reference sampler clip counts), "
+                    "random-init weights",
+            "p50_ms": round(lat.get("p50_ms", float("nan")), 3),
+            "p99_ms": round(lat.get("p99_ms", float("nan")), 3),
+            "latency_offered_videos_per_s": round(lat.get("offered_videos_per_s", 0.0), 1),
+            "latency_requests": lat.get("count", 0),
+            "bulk_p50_ms": round(res.get("latency", {}).get("p50_ms", float("nan")), 3),
+            "bulk_p99_ms": round(res.get("latency", {}).get("p99_ms", float("nan")), 3),
+            "barrier_videos_per_s": round(res.get("videos_per_s", 0.0), 2),
+            "termination": res.get("termination_flag"),
+            "config": {"model": "R(2+1)D-%d" % args.depth,
+                       "global_batch": args.videos_per_step * args.gpus, "seq_len": 8,
+                       "parallelism": "rnb pipeline: %d loader + %d runner processes per GPU"
+                                      % (args.loaders, args.replicas),
+                       "pipeline": args.pipeline, "launcher_config": res.get("config_path"),
+                       "bn": "eval (folded, fp64 fold)", "clip": "8x112x112",
+                       "clips_dist": "1 w.p. 10/11, 15 w.p. 1/11",
+                       "max_batch_videos": args.video_batch,
+                       "clips_per_batch": args.clips_per_batch,
+                       "bucket_step": args.bucket_step,
+                       "job_wall_s": round(res.get("wall_s", 0.0), 1)},
+        }
+        line = json.dumps(rec)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    return rc
 
 
 def pack_step(videos, clip_cap: int, video_cap: int, mode: str = "first-fit"):
@@ -110,8 +280,9 @@ def make_workload(n_videos: int, seed: int):
     return videos
 
 
-def main(argv=None) -> int:
-    args = parse_args(argv)
+def run_fused(args) -> int:
+    """In-process fused engine (decode -> R(2+1)D -> argmax in HIP graphs on
+    replica streams): the upper bound the RnB pipeline is compared with."""
     if args.trace:
         from rnb_amd.profiling import tracer
         tracer.initialize()            # before the HIP runtime starts
@@ -159,9 +330,9 @@ def main(argv=None) -> int:
     bstep = max(1, args.bucket_step)
     buckets = sorted(set(range(bstep, args.clips_per_batch + 1, bstep))
                      | {args.clips_per_batch, max_clips})
-    eng = FusedR2P1D(device, depth=args.depth, replicas=args.replicas,
+    eng = FusedR2P1D(device, depth=args.depth, replicas=args.fused_replicas,
                      max_clips=max(max_clips, 1), max_videos=vb, buckets=buckets,
-                     autotune=not args.no_autotune, seed=0)
+                     autotune=not args.no_autotune, seed=0, dtype=args.dtype)
     t_prep = time.time()
     eng.prepare([sum(len(s) for _, s in b) for b in batches])
     prep_s = time.time() - t_prep
@@ -253,7 +424,7 @@ def main(argv=None) -> int:
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(value / BASELINE_VIDEOS_PER_S, 2),
-            "dtype": "bf16", "data": "synthetic clips (GPU-decoded), random-init weights",
+            "dtype": args.dtype, "data": "synthetic clips (GPU-decoded), random-init weights",
             "p50_ms": round(p50, 3), "p99_ms": round(p99, 3),
             "clips_per_s": round(clips_all / elapsed, 1),
             "effective_tflops": round(flops / 1e12, 1),
@@ -261,10 +432,10 @@ def main(argv=None) -> int:
             "config": {"model": "R(2+1)D-%d" % args.depth,
                        "global_batch": vps * world, "seq_len": 8,
                        "parallelism": "dp%d (replicated runners)" % world,
-                       "pipeline": "r2p1d-whole (loader+model per GPU, fused)",
+                       "pipeline": "fused (single-process engine, not the RnB launcher)",
                        "video_batch": vb, "clips_per_batch": args.clips_per_batch,
                        "packing": args.packing, "bucket_step": bstep,
-                       "replicas_per_gpu": args.replicas,
+                       "replicas_per_gpu": args.fused_replicas,
                        "clip": "8x112x112", "clips_dist": "1 w.p. 10/11, 15 w.p. 1/11",
                        "prepare_s": round(prep_s, 1)},
         }

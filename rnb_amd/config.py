@@ -61,6 +61,9 @@ class StepSpec:
     num_shared_tensors: int = DEFAULT_NUM_SHARED_TENSORS
     kwargs: Dict[str, Any] = field(default_factory=dict)
     slot_dtype: Optional[str] = None
+    # True when the config did not fix num_shared_tensors (or said "auto"):
+    # the launcher then sizes the rings from HBM (control.plan_ring_depths)
+    auto_slots: bool = False
 
 
 @dataclass
@@ -156,9 +159,10 @@ def parse_pipeline(config: Dict[str, Any]) -> PipelineSpec:
         if final and num_segments != 1:
             raise ConfigError("The last step may not have multiple segments.")
         if "num_shared_tensors" in step:
-            _require(isinstance(step["num_shared_tensors"], int)
-                     and step["num_shared_tensors"] >= 1,
-                     "step %d: num_shared_tensors must be a positive int"
+            _require(step["num_shared_tensors"] == "auto" or
+                     (isinstance(step["num_shared_tensors"], int)
+                      and step["num_shared_tensors"] >= 1),
+                     "step %d: num_shared_tensors must be a positive int or \"auto\""
                      % step_idx)
             if final:
                 raise ConfigError("The last step does not need shared output "
@@ -209,9 +213,11 @@ def parse_pipeline(config: Dict[str, Any]) -> PipelineSpec:
             prev_out = {q for g in groups for q in g.out_queues}
         steps.append(StepSpec(
             model=step["model"], groups=groups, num_segments=num_segments,
-            num_shared_tensors=step.get("num_shared_tensors",
-                                        DEFAULT_NUM_SHARED_TENSORS),
-            kwargs=step_kwargs, slot_dtype=step.get("slot_dtype")))
+            num_shared_tensors=(step["num_shared_tensors"]
+                                if isinstance(step.get("num_shared_tensors"), int)
+                                else DEFAULT_NUM_SHARED_TENSORS),
+            kwargs=step_kwargs, slot_dtype=step.get("slot_dtype"),
+            auto_slots=not isinstance(step.get("num_shared_tensors"), int)))
     return PipelineSpec(video_path_iterator=config["video_path_iterator"],
                         steps=steps,
                         iterator_kwargs=config.get("video_path_iterator_kwargs",
@@ -268,6 +274,28 @@ def gpu_memory_used_bytes() -> Optional[List[int]]:
                 except Exception:
                     used.append(0)
             return used
+        finally:
+            amdsmi.amdsmi_shut_down()
+    except Exception:
+        return None
+
+
+def gpu_memory_free_bytes() -> Optional[List[int]]:
+    """Per-physical-GPU free VRAM (total - used) via amdsmi, without creating a
+    HIP context in the calling process. ``None`` if unavailable."""
+    try:
+        import amdsmi  # type: ignore
+    except Exception:
+        return None
+    try:
+        amdsmi.amdsmi_init()
+        try:
+            out = []
+            for h in amdsmi.amdsmi_get_processor_handles():
+                info = amdsmi.amdsmi_get_gpu_vram_usage(h)
+                out.append(max(0, int(info.get("vram_total", 0))
+                               - int(info.get("vram_used", 0))) * 1024 * 1024)
+            return out
         finally:
             amdsmi.amdsmi_shut_down()
     except Exception:

@@ -96,6 +96,90 @@ def step_output_spec(step, group=None):
     return get_segmented_shapes(shapes, step.num_segments), tuple(dtypes)
 
 
+RING_HBM_FRACTION = 0.25        # share of a GPU's free HBM the slot rings may take
+ASSUMED_FREE_BYTES = 64 << 30   # when amdsmi cannot report free VRAM
+
+
+def _consumer_capacity(group) -> int:
+    """Items one consumer instance takes per model call (consumer-side batching)."""
+    kw = group.kwargs
+    for key in ("max_batch_videos", "batch"):
+        v = kw.get(key)
+        if isinstance(v, int) and v > 1:
+            return v
+    return 1
+
+
+def plan_ring_depths(spec: PipelineSpec, free_bytes=None, fraction=RING_HBM_FRACTION,
+                     verbose=True):
+    """Size the slot rings of steps without a fixed ``num_shared_tensors``.
+
+    The reference uses a static 10 slots per producer (control.py:8). Here a
+    producer's ring must cover what its consumers can hold in flight: each
+    consumer instance takes up to ``max_batch_videos``/``batch`` items per
+    model call and may have one call queued behind the current one, so the
+    ring gets 2 x (total consumer capacity of its queues) / (producers of those
+    queues) + 2 slots, at least 10. Rings that live on one GPU together get at
+    most ``fraction`` of that GPU's free HBM (288 GB on MI355X: the cap rarely
+    binds, it only protects smaller devices). Returns the plan
+    [(step, group, gpu, slots, slot_bytes)].
+    """
+    import math
+    plan = []
+    demand_bytes: Dict[int, int] = {}
+    for s_idx, step in enumerate(spec.steps[:-1]):
+        if not step.auto_slots:
+            continue
+        nxt = spec.steps[s_idx + 1]
+        shapes, dtypes = step_output_spec(step, step.groups[0])
+        if shapes is None:
+            continue
+        slot_bytes = sum(math.prod(sh) * _itemsize(dt) for sh, dt in zip(shapes, dtypes))
+        for g_idx, group in enumerate(step.groups):
+            outs = set(group.out_queues)
+            cap = sum(_consumer_capacity(cg) * len(cg.gpus) for cg in nxt.groups
+                      if cg.in_queue in outs)
+            producers = sum(len(pg.gpus) for pg in step.groups
+                            if set(pg.out_queues) & outs)
+            depth = max(DEFAULT_NUM_SHARED_TENSORS,
+                        math.ceil(2.0 * cap * step.num_segments / max(1, producers)) + 2)
+            for gpu in group.gpus:
+                plan.append([s_idx, g_idx, gpu, depth, slot_bytes])
+                demand_bytes[gpu] = demand_bytes.get(gpu, 0) + depth * slot_bytes
+    for gpu, need in demand_bytes.items():
+        if gpu < 0:
+            continue
+        free = None
+        if free_bytes is not None and gpu < len(free_bytes):
+            free = free_bytes[gpu]
+        budget = fraction * (free if free else ASSUMED_FREE_BYTES)
+        if need > budget:
+            scale = budget / need
+            for row in plan:
+                if row[2] == gpu:
+                    row[3] = max(2, int(row[3] * scale))
+    # a step's rings are uniform across its groups' instances: take the min
+    for s_idx, step in enumerate(spec.steps[:-1]):
+        rows = [r for r in plan if r[0] == s_idx]
+        if rows:
+            step.num_shared_tensors = min(r[3] for r in rows)
+            for r in rows:
+                r[3] = step.num_shared_tensors
+    if verbose and plan:
+        for s_idx in sorted({r[0] for r in plan}):
+            rows = [r for r in plan if r[0] == s_idx]
+            print("[ring plan] step %d (%s): %d slots x %.1f MB per producer, %d producers, "
+                  "%.2f GB total" % (s_idx, spec.steps[s_idx].model.rsplit(".", 1)[-1],
+                                     rows[0][3], rows[0][4] / 1e6, len(rows),
+                                     sum(r[3] * r[4] for r in rows) / 1e9), flush=True)
+    return [tuple(r) for r in plan]
+
+
+def _itemsize(dtype) -> int:
+    import torch
+    return torch.empty((), dtype=dtype).element_size()
+
+
 class SharedQueuesAndTensors:
     """Creates all queues and slot-ring control blocks of a pipeline.
 
@@ -152,6 +236,16 @@ class SharedQueuesAndTensors:
             self.rings.append(step_rings)
             self.done.append(step_done)
             self.num_producers.append(step_np)
+        # every ring learns which consumer instances may pull from it (the IPC
+        # ring creates one set of release events per consumer)
+        for step_idx in range(self.num_steps - 1):
+            for group_idx, (_, outs) in enumerate(self.queue_indices[step_idx]):
+                consumers = [(step_idx + 1, cg, ci)
+                             for cg, grp in enumerate(spec.steps[step_idx + 1].groups)
+                             if grp.in_queue in outs for ci in range(len(grp.gpus))]
+                for ring in self.rings[step_idx][group_idx]:
+                    if ring is not None:
+                        ring.set_consumers(consumers)
 
     def _consumers_use_cpu(self, step_idx: int, group) -> bool:
         nxt = self.spec.steps[step_idx + 1]

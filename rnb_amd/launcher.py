@@ -53,6 +53,14 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--log-root", type=str, default=None, help="Log directory root")
     p.add_argument("--cpu-only", action="store_true",
                    help="Place every replica on the CPU, keeping the topology (no GPU needed)")
+    p.add_argument("--warmup-videos", type=nonnegative_int, default=0,
+                   help="Videos run (and completed) before the timed window starts; "
+                        "they are excluded from throughput and latency")
+    p.add_argument("--latency-seconds", type=float, default=0.0,
+                   help="(-mi 0 with --warmup-videos) after the timed bulk phase, offer "
+                        "Poisson arrivals for about this long at --latency-load x the "
+                        "measured throughput and report their request latency")
+    p.add_argument("--latency-load", type=float, default=0.5)
     p.add_argument("--set", dest="overrides", action="append", default=[],
                    metavar="KEY=JSON",
                    help="Override a model kwarg in every step, e.g. --set depth=18")
@@ -170,6 +178,15 @@ def run(args) -> dict:
         spec = spec.override_kwargs(_parse_overrides(args.overrides))
     check_gpus(spec)
     _apply_batch_default(spec, args.batch_size)
+    # slot rings sized from the consumers' batching and free HBM (amdsmi: no
+    # HIP context in this process)
+    from .config import gpu_memory_free_bytes, visible_devices
+    from .control import plan_ring_depths
+    free = gpu_memory_free_bytes()
+    mapping = visible_devices()
+    if free is not None and mapping is not None:
+        free = [free[p] if p < len(free) else 0 for p in mapping]
+    plan_ring_depths(spec, free)
 
     ctx = tmp.get_context("spawn")
     job_id = "%s-mi%d-b%d-v%d-qs%d" % (datetime.today().strftime("%y%m%d_%H%M%S"),
@@ -180,13 +197,23 @@ def run(args) -> dict:
     fin_bar = ctx.Barrier(num_runners + 2)
     counter = ctx.Value("i", 0)
     flag = ctx.Value("i", TerminationFlag.UNSET)
+    phase_start = ctx.Array("d", 3)     # timed start, latency-phase start, offered rate
+    warm = int(getattr(args, "warmup_videos", 0) or 0)
+    total_videos = args.videos + warm
+    lat_s = float(getattr(args, "latency_seconds", 0.0) or 0.0)
+    if lat_s and (args.mean_interval_ms != 0 or not warm):
+        from .config import ConfigError
+        raise ConfigError("--latency-seconds needs -mi 0 and --warmup-videos")
+    # videos the final step must count; with a latency phase the client sets
+    # it once it knows how many Poisson requests follow the bulk phase
+    target = ctx.Value("i", total_videos if not lat_s else 2 ** 31 - 1)
     # bulk mode: every video (times its segments) plus every producer's exit
     # markers must fit at once, or a marker burst from a finished replica can
     # fill a queue another replica still needs (-> spurious FRAME_QUEUE_FULL)
     from .runner import NUM_EXIT_MARKERS
     max_segments = max(step.num_segments for step in spec.steps)
     queue_size = args.queue_size if args.mean_interval_ms > 0 \
-        else args.videos * max_segments + (NUM_EXIT_MARKERS + 1) * (num_runners + 1)
+        else total_videos * max_segments + (NUM_EXIT_MARKERS + 1) * (num_runners + 1)
     qt = SharedQueuesAndTensors(spec, ctx.Queue, queue_size, ctx)
     result_queue = ctx.Queue()
     it_kwargs = spec.iterator_kwargs
@@ -197,7 +224,8 @@ def run(args) -> dict:
                                    sta_bar, fin_bar),
                              kwargs=dict(seed=args.seed,
                                          barrier_timeout=args.barrier_timeout,
-                                         iterator_kwargs=it_kwargs))
+                                         iterator_kwargs=it_kwargs, warmup_videos=warm,
+                                         counter=counter, phase_start=phase_start))
     else:
         client = ctx.Process(target=_client_main, name="client",
                              args=(bulk_client, spec.video_path_iterator,
@@ -206,7 +234,11 @@ def run(args) -> dict:
                              kwargs=dict(seed=args.seed,
                                          barrier_timeout=args.barrier_timeout,
                                          iterator_kwargs=it_kwargs,
-                                         done_counter=qt.filename_done))
+                                         done_counter=qt.filename_done,
+                                         warmup_videos=warm, counter=counter,
+                                         phase_start=phase_start, latency_seconds=lat_s,
+                                         latency_load=getattr(args, "latency_load", 0.5),
+                                         target=target))
     procs = [("client", client)]
     last = len(spec.steps) - 1
     dist_infos = _assign_rccl_ranks(spec, qt, job_id)
@@ -220,7 +252,7 @@ def run(args) -> dict:
                     target=runner,
                     name="runner-s%d-g%d-i%d" % (step_idx, group_idx, instance_idx),
                     args=(in_q, out_qs, group.queue_selector, first_final, job_id, gpu,
-                          group_idx, instance_idx, counter, args.videos, flag, step_idx,
+                          group_idx, instance_idx, counter, target, flag, step_idx,
                           sta_bar, fin_bar, step.model, step.num_segments, in_r, out_r),
                     kwargs=dict(group.kwargs, result_queue=result_queue,
                                 barrier_timeout=args.barrier_timeout,
@@ -248,7 +280,7 @@ def run(args) -> dict:
         with flag.get_lock():
             if flag.value == TerminationFlag.UNSET:
                 flag.value = TerminationFlag.BARRIER_TIMEOUT
-        print("[ERROR] job aborted: %s" % (dog.failed or "barrier timeout"), flush=True)
+        print("[ERROR] job aborted: %s" % (dog.failed or "barrier timeout",), flush=True)
 
     summaries = TimeCardSummary()
     n_final = sum(len(g.gpus) for g in spec.steps[-1].groups)
@@ -273,20 +305,45 @@ def run(args) -> dict:
 
     result = {"job_id": job_id, "config": os.path.basename(args.config_file_path),
               "termination_flag": TerminationFlag.NAMES.get(flag.value, flag.value),
-              "videos_target": args.videos, "videos_done": counter.value,
+              "videos_target": args.videos, "videos_done": max(0, counter.value - warm),
+              "warmup_videos": warm,
               "mean_interval_ms": args.mean_interval_ms, "ok": False}
     if time_start is not None and time_end is not None:
+        if warm and phase_start[0] > 0:
+            time_start = phase_start[0]          # timed window starts after warm-up
         total = time_end - time_start
-        done = min(counter.value, args.videos)
+        done = min(max(0, counter.value - warm), args.videos)
         print("Time: %f sec" % total)
         print("Number of videos: %d videos" % args.videos)
-        lat = summaries.latency_stats(num_skips=min(10, max(0, len(summaries) - 1)))
+        last = warm + args.videos
+        if warm:
+            lat = summaries.latency_stats(min_id=warm + 1, max_id=last)
+            fin = summaries.finish_times(min_id=warm + 1, max_id=last)
+        else:
+            lat = summaries.latency_stats(num_skips=min(10, max(0, len(summaries) - 1)))
+            fin = summaries.finish_times()
+        # window from the start of the timed phase to the completion of its
+        # last request (the barrier-based time also covers the shutdown)
+        window = float(fin.max() - time_start) if fin.size else total
+        if lat_s and phase_start[1] > 0:
+            result["latency_phase"] = dict(
+                summaries.latency_stats(min_id=last + 1),
+                offered_videos_per_s=phase_start[2], seconds=lat_s)
+            print("Latency phase: %.1f videos/s offered (Poisson), p50 %.2f ms p99 %.2f ms "
+                  "(%d requests)" % (phase_start[2], result["latency_phase"]["p50_ms"],
+                                     result["latency_phase"]["p99_ms"],
+                                     result["latency_phase"]["count"]), flush=True)
+        if lat_s:
+            total = window      # the barrier also waits for the latency phase
         result.update({"time_s": total, "videos_per_s": done / total if total > 0 else 0.0,
+                       "window_s": window,
+                       "videos_per_s_window": done / window if window > 0 else 0.0,
                        "latency": lat, "ok": flag.value ==
                        TerminationFlag.TARGET_NUM_VIDEOS_REACHED})
-        print("Throughput: %.2f videos/s; latency p50 %.2f ms p99 %.2f ms (%d requests)"
-              % (result["videos_per_s"], lat["p50_ms"], lat["p99_ms"], lat["count"]),
-              flush=True)
+        print("Throughput: %.2f videos/s (%.2f over the completion window); latency p50 "
+              "%.2f ms p99 %.2f ms (%d requests)"
+              % (result["videos_per_s"], result["videos_per_s_window"], lat["p50_ms"],
+                 lat["p99_ms"], lat["count"]), flush=True)
     with open(logmeta(job_id), "w") as f:
         f.write("Args: %s\n" % str(args))
         f.write("%f %f\n" % (time_start or 0.0, time_end or 0.0))

@@ -376,11 +376,23 @@ class GraphedEngine:
                              % (n, self.buckets[-1]))
         return self.buckets[i]
 
+    def _tune_here(self, b: int) -> bool:
+        """fp32 engines time tiles at a few batch sizes only (the largest bucket
+        and the power-of-two buckets); the other buckets take the nearest tuned
+        size's tiles (ops/tuning.nearest). bf16 engines tune every bucket."""
+        if not self.autotune:
+            return False
+        if not self.engine.f32:
+            return True
+        return b == self.buckets[-1] or (b & (b - 1)) == 0
+
     def _capture(self, b: int):
         t0 = time.time()
         eng = self.engine
-        if self.autotune:
-            eng.autotune(b)
+        if self._tune_here(b):
+            from ...ops import tuning
+            with tuning.FileLock("autotune"):
+                eng.autotune(b)
         static_in = torch.zeros(eng.input_shape(b), dtype=eng.dtype, device=self.device)
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))

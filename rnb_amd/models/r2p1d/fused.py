@@ -50,6 +50,7 @@ class Replica:
         # (no separate stem_pack pass); RNB_PACKED_INPUT=0 turns it off
         self.packed = (engine.accepts_packed_input
                        and os.environ.get("RNB_PACKED_INPUT", "1") != "0")
+        self.dtype = engine.dtype
         self.stream = torch.cuda.Stream(self.device)
         self.pool = torch.cuda.graph_pool_handle()
         self.graphs: Dict[int, _BucketGraph] = {}
@@ -69,7 +70,7 @@ class Replica:
     def _body(self, bg: _BucketGraph, b: int):
         F, H, W = CLIP_SHAPE
         surf = vops.clipgen_u8(bg.meta[0], bg.meta[1], F, H, W)
-        vops.preprocess(surf, out=bg.frames, packed=self.packed)
+        vops.preprocess(surf, out=bg.frames, packed=self.packed, dtype=self.dtype)
         logits = self.engine.forward(bg.frames, packed=self.packed)
         bg.logits = logits
         vops.video_reduce(logits, bg.offsets, sums=bg.sums)[1]
@@ -81,7 +82,7 @@ class Replica:
         bg = _BucketGraph()
         bg.meta = torch.zeros((2, b), dtype=torch.int32, device=dev)
         bg.offsets = torch.zeros((self.max_videos + 1,), dtype=torch.int32, device=dev)
-        bg.frames = torch.empty(self.engine.input_shape(b, self.packed), dtype=torch.bfloat16,
+        bg.frames = torch.empty(self.engine.input_shape(b, self.packed), dtype=self.dtype,
                                 device=dev)
         bg.sums = torch.empty((self.max_videos, self.engine.num_classes),
                               dtype=torch.float32, device=dev)
@@ -93,7 +94,7 @@ class Replica:
             with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
                 F, H, W = CLIP_SHAPE
                 surf = vops.clipgen_u8(bg.meta[0], bg.meta[1], F, H, W)
-                vops.preprocess(surf, out=bg.frames, packed=self.packed)
+                vops.preprocess(surf, out=bg.frames, packed=self.packed, dtype=self.dtype)
                 bg.logits = self.engine.forward(bg.frames, packed=self.packed)
                 _, bg.argmax = vops.video_reduce(bg.logits, bg.offsets, sums=bg.sums)
             self.stream.synchronize()
@@ -104,7 +105,7 @@ class Replica:
     def _run_eager(self, bg):
         F, H, W = CLIP_SHAPE
         surf = vops.clipgen_u8(bg.meta[0], bg.meta[1], F, H, W)
-        vops.preprocess(surf, out=bg.frames, packed=self.packed)
+        vops.preprocess(surf, out=bg.frames, packed=self.packed, dtype=self.dtype)
         logits = self.engine.forward(bg.frames, packed=self.packed)
         vops.video_reduce(logits, bg.offsets, sums=bg.sums)
 
@@ -156,9 +157,9 @@ class FusedR2P1D:
     def __init__(self, device: torch.device, depth: int = 34, num_classes: int = 400,
                  replicas: int = 1, max_clips: int = 256, max_videos: int = 64,
                  buckets: Sequence[int] = DEFAULT_BUCKETS, autotune: bool = True,
-                 seed: int = 0, ckpt_path: Optional[str] = None):
+                 seed: int = 0, ckpt_path: Optional[str] = None, dtype="bf16"):
         net = build_network(1, 5, num_classes, depth=depth, seed=seed, ckpt_path=ckpt_path)
-        self.engine = R2P1DEngine(net, device, backend="hip")
+        self.engine = R2P1DEngine(net, device, backend="hip", dtype=dtype)
         self.device = device
         self.autotune = autotune
         self.replicas = [Replica(self.engine, max_clips, max_videos, buckets)
@@ -169,7 +170,9 @@ class FusedR2P1D:
         """Autotune + capture the buckets needed for these clip counts."""
         buckets = sorted({self.replicas[0].bucket_for(max(c, 1)) for c in clip_counts})
         for b in buckets:
-            if self.autotune and b not in self._tuned:
+            tune = self.autotune and (not self.engine.f32 or b == buckets[-1]
+                                      or (b & (b - 1)) == 0)
+            if tune and b not in self._tuned:
                 self.engine.autotune(b)
                 self._tuned.add(b)
             for r in self.replicas:

@@ -17,8 +17,15 @@ MI355X-specific behaviour (documented deviations):
   ``ckpt_path`` points at a reference checkpoint (loaded with
   ``torch.load(weights_only=True)``); the reference's hard-coded site paths
   are unavailable.
-* Stage boundaries are NDHWC bf16 (channels padded to 8) instead of NCDHW
-  fp32; runners also accept the reference NCDHW fp32 layout and convert.
+* Stage boundaries are NDHWC (channels padded to 4 for fp32, 8 for bf16)
+  instead of NCDHW; runners also accept the reference NCDHW fp32 layout and
+  convert. ``dtype`` (every stage) selects the compute precision: ``"fp32"``
+  (default; the reference's precision, fp32 MFMA kernels) or ``"bf16"``.
+* ``R2P1DRunner`` batches on the consumer side: with ``max_batch_videos`` > 1
+  one call takes every queued video that fits ``max_clips`` rows and the
+  runner pulls their slots straight into the HIP-graph input buffer
+  (``gather_limits`` / ``gather_buffers``, runner.py), the in-process form of
+  the reference's Batcher step (reference batcher.py:5-34).
 * Runner output slots are sized from ``start_index/end_index`` (fixes the
   reference's TODO #69) and ``max_clips`` (default 15, the sampler maximum;
   the reference's 10-row slots overflow on 15-clip videos).
@@ -46,6 +53,18 @@ from .sampler import R2P1DSampler
 
 DEFAULT_MAX_CLIPS = 15
 CLIP_SHAPE = (8, 112, 112)
+DEFAULT_DTYPE = "fp32"       # the reference computes in fp32 (model.py:149,225)
+
+
+def _dtype(d):
+    from .engine import _as_dtype
+    return _as_dtype(d if d is not None else DEFAULT_DTYPE)
+
+
+def clip_channels(dtype) -> int:
+    """Channels of a decoded NDHWC clip pixel (RGB padded to 16 bytes)."""
+    from ...ops.video import IN_CHANNELS_P, IN_CHANNELS_P_F32
+    return IN_CHANNELS_P_F32 if _dtype(dtype) == torch.float32 else IN_CHANNELS_P
 
 
 def _resolve_backend(backend: str, device: torch.device) -> str:
@@ -72,26 +91,27 @@ def build_network(start_index: int, end_index: int, num_classes: int = 400,
 def build_engine(device: torch.device, start_index=1, end_index=5, num_classes=400,
                  layer_sizes=None, depth=None, backend="auto", bn_mode="eval", seed=0,
                  ckpt_path=None, max_clips=DEFAULT_MAX_CLIPS, use_graphs=True,
-                 autotune=True):
+                 autotune=True, dtype=None, buckets=None):
     net = build_network(start_index, end_index, num_classes, layer_sizes, depth, seed,
                         ckpt_path)
     backend = _resolve_backend(backend, device)
-    eng = R2P1DEngine(net, device, backend=backend, bn_mode=bn_mode)
+    eng = R2P1DEngine(net, device, backend=backend, bn_mode=bn_mode, dtype=_dtype(dtype))
     # batch-statistics BN runs eagerly: bucket graphs pad the clip batch
     if backend == "hip" and use_graphs and bn_mode == "eval":
-        return GraphedEngine(eng, max_clips, autotune=autotune)
+        kw = {} if buckets is None else {"buckets": buckets}
+        return GraphedEngine(eng, max_clips, autotune=autotune, **kw)
     return eng
 
 
-def _to_boundary(x: torch.Tensor, start_index: int) -> torch.Tensor:
-    """Accept the reference NCDHW fp32 layout as well as NDHWC bf16."""
-    cp = boundary_channels_p(start_index)
-    if x.dim() == 5 and x.shape[-1] == cp and x.dtype == torch.bfloat16:
-        return x.contiguous()
+def _to_boundary(x: torch.Tensor, start_index: int, dtype=torch.float32) -> torch.Tensor:
+    """Accept the reference NCDHW fp32 layout as well as the NDHWC boundary."""
+    cp = boundary_channels_p(start_index, dtype)
+    if x.dim() == 5 and x.shape[-1] == cp and x.shape[1] != LAYER_INPUT_CTHW[start_index][0]:
+        return x.to(dtype).contiguous()
     c = LAYER_INPUT_CTHW[start_index][0]
     if x.dim() == 5 and x.shape[1] == c:
         from ...ops.video import ncdhw_to_ndhwc
-        return ncdhw_to_ndhwc(x, cp)
+        return ncdhw_to_ndhwc(x, cp, dtype=dtype)
     raise ValueError("unexpected input of shape %s for layer %d" % (tuple(x.shape),
                                                                      start_index))
 
@@ -102,7 +122,8 @@ class R2P1DRunner(RunnerModel):
     def __init__(self, device, start_index=1, end_index=5, num_classes=400,
                  layer_sizes=None, depth=None, block_type=None, backend="auto",
                  bn_mode="eval", seed=0, ckpt_path=None, max_clips=DEFAULT_MAX_CLIPS,
-                 warmup=3, use_graphs=True, autotune=True, **unused):
+                 warmup=3, use_graphs=True, autotune=True, dtype=None,
+                 max_batch_videos=1, batch_wait_ms=0.0, bucket_step=None, **unused):
         super().__init__(device)
         if start_index < 1:
             raise ValueError("Wrong layer index for the starting layer! The start_index "
@@ -111,21 +132,49 @@ class R2P1DRunner(RunnerModel):
             raise ValueError("Wrong layer index for the ending layer! The end_index (%d) "
                              "should be less than or equal to 5." % end_index)
         self.start_index, self.end_index = start_index, end_index
-        self.max_clips = max_clips
+        self.max_clips = int(max_clips)
+        self.dtype = _dtype(dtype)
+        self.max_batch_videos = int(max_batch_videos)
+        self.batch_wait_s = float(batch_wait_ms) / 1000.0
+        buckets = None
+        if bucket_step:
+            step = int(bucket_step)
+            buckets = sorted(set(range(step, self.max_clips + 1, step)) | {1, self.max_clips})
         self.engine = build_engine(device, start_index, end_index, num_classes,
                                    layer_sizes, depth, backend, bn_mode, seed, ckpt_path,
-                                   max_clips, use_graphs, autotune)
+                                   self.max_clips, use_graphs, autotune, self.dtype, buckets)
         if isinstance(self.engine, GraphedEngine):
             self.engine.prepare()
-        n = min(10, max_clips)
-        tmp = torch.randn(boundary_shape(start_index, n)).to(torch.bfloat16).to(device)
+        n = min(10, self.max_clips)
+        tmp = torch.randn(boundary_shape(start_index, n, self.dtype)).to(self.dtype).to(device)
         for _ in range(warmup):
             self.engine(tmp)
         if device.type == "cuda":
             torch.cuda.current_stream(device).synchronize()
+        self._gather_ptr = None
+        self._gather_buf = None
+
+    # consumer-side batching (runner.py): up to max_batch_videos queued
+    # videos per call, their rows pulled into the graph's static input
+    def gather_limits(self):
+        if self.max_batch_videos <= 1 and not isinstance(self.engine, GraphedEngine):
+            return None
+        return (max(1, self.max_batch_videos), self.max_clips, self.batch_wait_s)
+
+    def gather_buffers(self, rows: int):
+        if isinstance(self.engine, GraphedEngine) and rows > 0:
+            static_in, _ = self.engine.input_buffer(rows)
+        else:
+            if self._gather_buf is None:
+                self._gather_buf = torch.empty(
+                    boundary_shape(self.start_index, self.max_clips, self.dtype),
+                    dtype=self.dtype, device=self.device)
+            static_in = self._gather_buf
+        self._gather_ptr = static_in.data_ptr()
+        return (static_in,)
 
     def input_shape(self):
-        return (boundary_shape(self.start_index, self.max_clips),)
+        return (boundary_shape(self.start_index, self.max_clips, self.dtype),)
 
     @staticmethod
     def output_shape():
@@ -133,18 +182,25 @@ class R2P1DRunner(RunnerModel):
 
     @classmethod
     def output_shape_for(cls, start_index=1, end_index=5, num_classes=400,
-                         max_clips=DEFAULT_MAX_CLIPS, **kwargs):
+                         max_clips=DEFAULT_MAX_CLIPS, dtype=None, **kwargs):
         if end_index == 5:
             return ((max_clips, num_classes),)
-        return (boundary_shape(end_index + 1, max_clips),)
+        return (boundary_shape(end_index + 1, max_clips, _dtype(dtype)),)
 
     @classmethod
-    def output_dtypes_for(cls, end_index=5, **kwargs):
-        return (torch.float32,) if end_index == 5 else (torch.bfloat16,)
+    def output_dtypes_for(cls, end_index=5, dtype=None, **kwargs):
+        return (torch.float32,) if end_index == 5 else (_dtype(dtype),)
 
     def __call__(self, tensors, non_tensors, time_card):
-        x = _to_boundary(tensors[0], self.start_index)
-        y = self.engine(x)
+        x = tensors[0]
+        if (self._gather_ptr is not None and x.data_ptr() == self._gather_ptr
+                and isinstance(self.engine, GraphedEngine) and x.shape[0] > 0):
+            # rows already sit in the bucket graph's static input: replay only
+            self._gather_ptr = None
+            y = self.engine.replay(x.shape[0])
+        else:
+            self._gather_ptr = None
+            y = self.engine(_to_boundary(x, self.start_index, self.dtype))
         return (y,), non_tensors, time_card
 
 
@@ -164,31 +220,39 @@ class R2P1DVideoPathIterator(VideoPathIterator):
 
 
 class R2P1DLoader(RunnerModel):
-    """Video path -> sampled clips, NDHWC bf16 [n, 8, 112, 112, 8]."""
+    """Video path -> sampled clips, NDHWC [n, 8, 112, 112, C] (fp32 C=4, bf16 C=8)."""
 
     def __init__(self, device, num_clips_population=(1, 15), num_clips_weights=(10, 1),
                  decoder="synthetic", seed=None, max_clips=DEFAULT_MAX_CLIPS,
-                 warmup=3, **unused):
+                 warmup=3, dtype=None, **unused):
         super().__init__(device)
         self.sampler = R2P1DSampler(clip_length=CLIP_SHAPE[0],
                                     num_clips_population=num_clips_population,
                                     num_clips_weights=num_clips_weights, seed=seed)
-        self.decoder = make_decoder(decoder, device, *CLIP_SHAPE)
+        self.dtype = _dtype(dtype)
+        self.decoder = make_decoder(decoder, device, *CLIP_SHAPE, dtype=self.dtype)
         self.max_clips = max_clips
-        for i in range(warmup):
-            self.decoder.decode(i, [0])
+        self.decoder.warmup(warmup)
         if device.type == "cuda":
             torch.cuda.current_stream(device).synchronize()
 
-    def load(self, path: str):
+    def load(self, path: str, out: Optional[torch.Tensor] = None):
         vid, length = self.decoder.probe(path)
         starts = self.sampler.sample(length) or []
         if len(starts) > self.max_clips:
             starts = starts[:self.max_clips]
-        return self.decoder.decode(vid, starts)
+        return self.decoder.decode(vid, starts, out=None if out is None else
+                                   out[:len(starts)])
 
     def __call__(self, tensors, non_tensors, time_card):
         frames = self.load(non_tensors)
+        time_card.num_clips = int(frames.shape[0])
+        return (frames,), None, time_card
+
+    def call_into(self, tensors, non_tensors, time_card, out):
+        """Decode straight into the output slot ``out[0]`` (runner.py direct_out:
+        no staging tensor, no slot copy)."""
+        frames = self.load(non_tensors, out=out[0])
         time_card.num_clips = int(frames.shape[0])
         return (frames,), None, time_card
 
@@ -197,15 +261,15 @@ class R2P1DLoader(RunnerModel):
 
     @staticmethod
     def output_shape():
-        return ((DEFAULT_MAX_CLIPS,) + CLIP_SHAPE + (8,),)
+        return ((DEFAULT_MAX_CLIPS,) + CLIP_SHAPE + (clip_channels(None),),)
 
     @classmethod
-    def output_shape_for(cls, max_clips=DEFAULT_MAX_CLIPS, **kwargs):
-        return ((max_clips,) + CLIP_SHAPE + (8,),)
+    def output_shape_for(cls, max_clips=DEFAULT_MAX_CLIPS, dtype=None, **kwargs):
+        return ((max_clips,) + CLIP_SHAPE + (clip_channels(dtype),),)
 
     @classmethod
-    def output_dtypes_for(cls, **kwargs):
-        return (torch.bfloat16,)
+    def output_dtypes_for(cls, dtype=None, **kwargs):
+        return (_dtype(dtype),)
 
 
 class R2P1DSingleStep(RunnerModel):
@@ -215,18 +279,31 @@ class R2P1DSingleStep(RunnerModel):
                  block_type=None, num_clips_population=(1, 15), num_clips_weights=(10, 1),
                  decoder="synthetic", seed=None, model_seed=0, backend="auto",
                  bn_mode="eval", ckpt_path=None, max_clips=DEFAULT_MAX_CLIPS, warmup=3,
-                 use_graphs=True, autotune=True, **unused):
+                 use_graphs=True, autotune=True, dtype=None, **unused):
         super().__init__(device)
         self.loader = R2P1DLoader(device, num_clips_population, num_clips_weights,
                                   decoder=decoder, seed=seed, max_clips=max_clips,
-                                  warmup=warmup)
+                                  warmup=warmup, dtype=dtype)
         self.runner = R2P1DRunner(device, 1, 5, num_classes,
                                   layer_sizes=layer_sizes, depth=depth, backend=backend,
                                   bn_mode=bn_mode, seed=model_seed, ckpt_path=ckpt_path,
                                   max_clips=max_clips, warmup=warmup,
-                                  use_graphs=use_graphs, autotune=autotune)
+                                  use_graphs=use_graphs, autotune=autotune, dtype=dtype)
 
     def __call__(self, tensors, non_tensors, time_card):
+        eng = self.runner.engine
+        if isinstance(eng, GraphedEngine) and self.runner.device.type == "cuda":
+            # decode straight into the bucket graph's input buffer
+            vid, length = self.loader.decoder.probe(non_tensors)
+            starts = (self.loader.sampler.sample(length) or [])[:self.loader.max_clips]
+            time_card.num_clips = len(starts)
+            if starts:
+                static_in, _ = eng.input_buffer(len(starts))
+                self.loader.decoder.decode(vid, starts, out=static_in[:len(starts)])
+                return (eng.replay(len(starts)),), None, time_card
+            frames = self.loader.decoder.empty()
+            (logits,), _, _ = self.runner((frames,), None, time_card)
+            return (logits,), None, time_card
         frames = self.loader.load(non_tensors)
         time_card.num_clips = int(frames.shape[0])
         (logits,), _, _ = self.runner((frames,), None, time_card)

@@ -22,11 +22,29 @@ from typing import Dict, Optional, Tuple
 import torch
 import torch.nn.functional as F
 
+from . import tuning
 from .conv import ConvGeom, pad_to
 
 F32_ALIGN = 4        # channel padding of fp32 NDHWC activations
 F32_BK = 32          # K per LDS row / K step of the fp32 kernel
 F32_ROW_SLACK = 256  # extra zero weight rows (>= largest channel tile)
+
+
+_DEV_NAMES: Dict[int, str] = {}
+
+
+def _device_name(device) -> str:
+    if device is None or getattr(device, "type", "cpu") != "cuda":
+        return "cpu"
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _DEV_NAMES:
+        _DEV_NAMES[idx] = torch.cuda.get_device_name(idx).replace("|", "/")
+    return _DEV_NAMES[idx]
+
+
+def _configs():
+    from .native import kernels
+    return kernels().f32_configs
 
 
 def f32_geom(cin: int, cout: int, kernel, stride, padding) -> ConvGeom:
@@ -150,13 +168,26 @@ class ConvLayerF32:
                 best, best_cost = cid, cost
         return best
 
+    def _tune_key(self, x_shape, device) -> str:
+        return tuning.make_key("f32", self.geom, tuple(x_shape[:4]), _device_name(device))
+
     def config_for(self, x_shape) -> int:
+        """Tile config for this input shape: tuned (this layer, or any layer of
+        the same geometry via the tuning cache), else the nearest tuned batch
+        of the same geometry, else the cost heuristic."""
         key = tuple(x_shape[:4])
         cid = self._config.get(key)
         if cid is None:
-            N, T, H, W, _ = x_shape
-            To, Ho, Wo = self.geom.out_thw(T, H, W)
-            cid = self._config[key] = self.heuristic_config(N * To * Ho * Wo)
+            tkey = self._tune_key(x_shape, self.device)
+            cid = tuning.get(tkey)
+            if cid is None:
+                N, T, H, W, _ = x_shape
+                cid = tuning.nearest(tkey, N * T * H * W)
+            if cid is None or cid >= len(_configs()):
+                N, T, H, W, _ = x_shape
+                To, Ho, Wo = self.geom.out_thw(T, H, W)
+                cid = self.heuristic_config(N * To * Ho * Wo)
+            self._config[key] = cid
         return cid
 
     def _launch_all(self, x, y, residual, cid, stream):
@@ -171,8 +202,14 @@ class ConvLayerF32:
 
     def autotune(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                  reps: int = 3) -> int:
-        """Time every fp32 tile config on this input shape; keep the fastest."""
+        """Time every fp32 tile config on this input shape; keep the fastest
+        (shared through ``ops.tuning``: a geometry/shape is timed once)."""
         from .native import kernels
+        tkey = self._tune_key(x.shape, x.device)
+        cached = tuning.get(tkey)
+        if cached is not None and cached < len(kernels().f32_configs):
+            self._config[tuple(x.shape[:4])] = cached
+            return cached
         y = torch.empty(self.out_shape(x.shape), dtype=torch.float32, device=x.device)
         stream = torch.cuda.current_stream(x.device)
         best, best_t = None, None
@@ -189,6 +226,7 @@ class ConvLayerF32:
             if best_t is None or t < best_t:
                 best, best_t = cid, t
         self._config[tuple(x.shape[:4])] = best
+        tuning.put(tkey, best)
         return best
 
     # ------------------------------------------------------------------

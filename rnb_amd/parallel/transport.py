@@ -19,7 +19,8 @@ Backends (chosen per edge by ``make_ring``):
               native runtime and exported with ``hipIpcGetMemHandle``; the
               handles travel inside each ``Signal`` so consumers open them
               lazily; pulls are ``hipMemcpyAsync`` (peer copy over xGMI when
-              the consumer sits on another GPU, an on-device copy otherwise).
+              the consumer sits on another GPU, an on-device copy otherwise),
+              ordered on the GPU by interprocess events (no host syncs).
 
 The RCCL send/recv channel for static 1:1 edges lives in
 ``parallel/rccl_channel.py``.
@@ -57,6 +58,8 @@ def _nbytes(shape, dtype) -> int:
 
 
 class RingBase:
+    gpu_ordered = False
+
     """Slot ring control block shared by all backends.
 
     ``events[i]`` set  <=> slot i is free (producer may write);
@@ -110,8 +113,14 @@ class RingBase:
         return None
 
     # ---- consumer side -------------------------------------------------
-    def consumer_attach(self, device: torch.device) -> None:
+    def consumer_attach(self, device: torch.device, key=None) -> None:
         self.consumer_device = device
+
+    def set_consumers(self, consumers) -> None:
+        self.consumers = [tuple(c) for c in consumers]
+
+    def rows_of(self, idx: int) -> int:
+        return self.valid_rows(idx)[0]
 
     def is_free(self, idx: int) -> bool:
         return self.events[idx].is_set()
@@ -183,8 +192,51 @@ class HostRing(RingBase):
         return out
 
 
+EVENT_HANDLE_BYTES = 64     # sizeof(hipIpcEventHandle_t); checked at attach
+ORDER_ENV = "RNB_RING_ORDER"  # "event" (default): GPU-side ordering; "host": stream syncs
+
+
+class _CudaArray:
+    """Zero-copy torch view of raw device memory (``__cuda_array_interface__``)."""
+
+    _TYPESTR = {torch.float32: "<f4", torch.bfloat16: "<V2", torch.float16: "<f2",
+                torch.uint8: "|u1", torch.int32: "<i4"}
+
+    def __init__(self, ptr: int, shape, dtype):
+        self.__cuda_array_interface__ = {
+            "shape": tuple(int(x) for x in shape), "typestr": self._TYPESTR[dtype],
+            "data": (int(ptr), False), "version": 2}
+
+
+def device_view(ptr: int, shape, dtype, device) -> torch.Tensor:
+    """A torch tensor aliasing ``ptr`` (device memory of ``device``)."""
+    if dtype == torch.bfloat16:
+        # CAI has no bf16 type string: view the bytes as int16 and reinterpret
+        t = torch.as_tensor(_CudaArray(ptr, shape, torch.float16), device=device)
+        return t.view(torch.bfloat16)
+    return torch.as_tensor(_CudaArray(ptr, shape, dtype), device=device)
+
+
 class IpcRing(RingBase):
-    """Producer-owned HBM slots exported through HIP IPC (native runtime)."""
+    """Producer-owned HBM slots exported through HIP IPC (native runtime).
+
+    Ordering is done on the GPU, without host stream synchronisation
+    (reference control.py:19-46 used host events only and
+    raced, §5.2):
+
+    * every slot has a "written" interprocess event, owned by the producer:
+      the producer records it on its stream after the slot's data and then
+      publishes the slot (host flag + queue signal); a consumer makes its
+      stream wait on it before the pull copy;
+    * every (consumer, slot) pair has a "released" interprocess event, owned
+      by the consumer: it is recorded after the pull copy, and the consumer
+      then marks the slot free naming itself in ``released_by``; the producer
+      makes its stream wait on that event before it writes the slot again.
+
+    The host flags only carry "who may touch the slot next"; the data
+    dependencies are GPU-to-GPU waits, so neither side blocks on the other's
+    kernels. ``RNB_RING_ORDER=host`` restores host-synchronised copies.
+    """
 
     kind = "ipc"
 
@@ -193,17 +245,49 @@ class IpcRing(RingBase):
         self._ptrs = None          # producer: [slot][tensor] device pointers
         self._desc = None
         self._opened: Dict[Tuple, List[List[int]]] = {}
+        self.consumers: List[Tuple[int, int, int]] = []   # (step, group, instance)
+        self._ctx = ctx
+        self.released_by = ctx.Array("i", [-1] * self.num_slots, lock=False)
+        self.rel_handles = None    # set by set_consumers (before spawn)
+        self.order = os.environ.get(ORDER_ENV, "event")
+        # per process
+        self._wev = None           # producer: written events [slot]
+        self._rel_open: Dict[int, List[Optional[int]]] = {}   # producer: cid -> events
+        self._cid = None           # consumer id of this process
+        self._rev = None           # consumer: own release events [slot]
+        self._wopen: Dict[Tuple, List[int]] = {}              # consumer: opened written events
+        self._dev = None
+
+    def set_consumers(self, consumers) -> None:
+        """Declare the consumer instances (before the processes are spawned)."""
+        self.consumers = [tuple(c) for c in consumers]
+        n = max(1, len(self.consumers))
+        self.rel_handles = self._ctx.Array("c", n * self.num_slots * EVENT_HANDLE_BYTES,
+                                           lock=False)
+        self.rel_ready = self._ctx.Array("i", n, lock=False)
 
     def __getstate__(self):
         st = dict(self.__dict__)
         st["_ptrs"] = None
         st["_opened"] = {}
+        st["_ctx"] = None
+        st["_wev"] = None
+        st["_rel_open"] = {}
+        st["_rev"] = None
+        st["_wopen"] = {}
+        st["_cid"] = None
         return st
 
+    @property
+    def gpu_ordered(self) -> bool:
+        return self.order == "event"
+
+    # ---- producer ---------------------------------------------------------
     def producer_attach(self, device):
         from ..ops import native
         rt = native.runtime()
         rt.set_device(device.index)
+        self._dev = device
         self._ptrs, handles = [], []
         for _ in range(self.num_slots):
             row_ptrs, row_h = [], []
@@ -213,16 +297,68 @@ class IpcRing(RingBase):
                 row_h.append(rt.ipc_get_handle(ptr))
             self._ptrs.append(row_ptrs)
             handles.append(tuple(row_h))
-        self._desc = (self.name, os.getpid(), device.index, tuple(handles))
+        wh = ()
+        if self.gpu_ordered:
+            if rt.event_handle_size > EVENT_HANDLE_BYTES:
+                raise RuntimeError("hipIpcEventHandle_t is %d bytes (> %d)"
+                                   % (rt.event_handle_size, EVENT_HANDLE_BYTES))
+            self._wev = [rt.event_create_ipc() for _ in range(self.num_slots)]
+            wh = tuple(rt.event_get_handle(e) for e in self._wev)
+        self._desc = (self.name, os.getpid(), device.index, tuple(handles), wh)
 
     def descriptor(self):
         return self._desc
+
+    def slot_views(self, idx: int) -> List[torch.Tensor]:
+        """Torch views of slot ``idx``'s tensors (producer side, full capacity)."""
+        return [device_view(p, s, d, self._dev)
+                for p, s, d in zip(self._ptrs[idx], self.shapes, self.dtypes)]
+
+    def _release_event(self, cid: int, idx: int) -> int:
+        from ..ops import native
+        evs = self._rel_open.get(cid)
+        if evs is None:
+            evs = self._rel_open[cid] = [None] * self.num_slots
+        if evs[idx] is None:
+            if not self.rel_ready[cid]:
+                raise RuntimeError("ring %s: consumer %d released a slot before "
+                                   "publishing its events" % (self.name, cid))
+            off = (cid * self.num_slots + idx) * EVENT_HANDLE_BYTES
+            h = bytes(self.rel_handles[off:off + EVENT_HANDLE_BYTES])
+            evs[idx] = native.runtime().event_open_handle(h)
+        return evs[idx]
+
+    def begin_write(self, idx: int, stream=None) -> None:
+        """Order the producer stream after the last consumer's pull of ``idx``
+        (call after ``wait_free``, before anything writes the slot)."""
+        if not self.gpu_ordered:
+            return
+        cid = self.released_by[idx]
+        if cid < 0:
+            return
+        from ..ops import native
+        stream = stream or torch.cuda.current_stream(self._dev)
+        native.runtime().stream_wait_event(stream.cuda_stream, self._release_event(cid, idx))
+
+    def commit(self, idx: int, rows: Sequence[int], stream=None) -> int:
+        """Publish slot ``idx`` holding ``rows`` valid rows per tensor (its data
+        was enqueued on ``stream``)."""
+        from ..ops import native
+        stream = stream or torch.cuda.current_stream(self._dev)
+        if self.gpu_ordered:
+            native.runtime().event_record(self._wev[idx], stream.cuda_stream)
+        else:
+            stream.synchronize()   # push completes before the slot is marked full
+        self._set_valid(idx, rows)
+        self.released_by[idx] = -1
+        return self._publish(idx)
 
     def write(self, idx, tensors):
         from ..ops import native
         rt = native.runtime()
         rows = []
-        stream = torch.cuda.current_stream()
+        stream = torch.cuda.current_stream(self._dev)
+        self.begin_write(idx, stream)
         for t, src in enumerate(tensors):
             b = src.shape[0]
             cap = self.shapes[t][0]
@@ -234,12 +370,27 @@ class IpcRing(RingBase):
                 if src.dtype != self.dtypes[t]:
                     src = src.to(self.dtypes[t])
                 rt.memcpy_async(self._ptrs[idx][t], src.data_ptr(),
-                                src.numel() * src.element_size(),
-                                stream.cuda_stream)
+                                src.numel() * src.element_size(), stream.cuda_stream)
             rows.append(b)
-        stream.synchronize()       # push completes before the slot is marked full
-        self._set_valid(idx, rows)
-        return self._publish(idx)
+        return self.commit(idx, rows, stream)
+
+    # ---- consumer ---------------------------------------------------------
+    def consumer_attach(self, device, key=None):
+        """``key`` = (step, group, instance) of this consumer (see set_consumers)."""
+        super().consumer_attach(device)
+        if not self.gpu_ordered or device.type != "cuda":
+            return
+        from ..ops import native
+        rt = native.runtime()
+        if key is None or tuple(key) not in self.consumers:
+            raise RuntimeError("ring %s: consumer %s was not declared" % (self.name, key))
+        self._cid = self.consumers.index(tuple(key))
+        self._rev = [rt.event_create_ipc() for _ in range(self.num_slots)]
+        for i, e in enumerate(self._rev):
+            h = rt.event_get_handle(e)
+            off = (self._cid * self.num_slots + i) * EVENT_HANDLE_BYTES
+            self.rel_handles[off:off + len(h)] = h
+        self.rel_ready[self._cid] = 1
 
     def _open(self, desc):
         from ..ops import native
@@ -249,9 +400,18 @@ class IpcRing(RingBase):
             rt = native.runtime()
             ptrs = [[rt.ipc_open_handle(h) for h in row] for row in desc[3]]
             self._opened[key] = ptrs
+            if self.gpu_ordered and len(desc) > 4 and desc[4]:
+                self._wopen[key] = [rt.event_open_handle(h) for h in desc[4]]
         return ptrs
 
+    def rows_of(self, idx: int) -> int:
+        return self.valid_rows(idx)[0]
+
     def read_into(self, idx, placeholders, descriptor=None):
+        """Pull slot ``idx``'s valid rows into ``placeholders`` (rows [0, b)) on the
+        current stream. GPU-ordered mode: the copy waits for the producer's
+        "written" event on the GPU and nothing blocks the host; call
+        ``release`` afterwards."""
         from ..ops import native
         if descriptor is None:
             raise RuntimeError("IPC ring %s read without a descriptor" % self.name)
@@ -259,23 +419,37 @@ class IpcRing(RingBase):
         ptrs = self._open(descriptor)
         out = []
         dev = placeholders[0].device
+        gpu = dev.type == "cuda"
+        if gpu:
+            stream = torch.cuda.current_stream(dev)
+            if self.gpu_ordered:
+                rt.stream_wait_event(stream.cuda_stream, self._wopen[descriptor[:2]][idx])
         for t, (ph, b) in enumerate(zip(placeholders, self.valid_rows(idx))):
             if b:
+                if b > ph.shape[0] or not ph.is_contiguous():
+                    raise ValueError("ring %s: %d rows do not fit the destination %s"
+                                     % (self.name, b, tuple(ph.shape)))
                 nbytes = _nbytes((b,) + tuple(self.shapes[t][1:]), self.dtypes[t])
                 if ph.is_cuda:
-                    stream = torch.cuda.current_stream(dev)
-                    rt.memcpy_async(ph.data_ptr(), ptrs[idx][t], nbytes,
-                                    stream.cuda_stream)
+                    rt.memcpy_async(ph.data_ptr(), ptrs[idx][t], nbytes, stream.cuda_stream)
                 else:
                     rt.memcpy_d2h(ph.data_ptr(), ptrs[idx][t], nbytes)
             out.append(ph[:b])
-        if dev.type == "cuda":
+        if gpu and not self.gpu_ordered:
             torch.cuda.current_stream(dev).synchronize()  # pull done before release
         return out
 
+    def release(self, idx: int) -> None:
+        if self.gpu_ordered and self._rev is not None:
+            from ..ops import native
+            stream = torch.cuda.current_stream(self.consumer_device)
+            native.runtime().event_record(self._rev[idx], stream.cuda_stream)
+            self.released_by[idx] = self._cid
+        super().release(idx)
+
     def close(self):
         from ..ops import native
-        if self._ptrs is None and not self._opened:
+        if self._ptrs is None and not self._opened and self._rev is None:
             return
         rt = native.runtime()
         for ptrs in self._opened.values():
@@ -284,6 +458,7 @@ class IpcRing(RingBase):
                     rt.ipc_close_handle(p)
         self._opened = {}
         if self._ptrs is not None:
+            torch.cuda.synchronize(self._dev)
             for row in self._ptrs:
                 for p in row:
                     rt.free(p)

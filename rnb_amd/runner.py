@@ -116,6 +116,15 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             selector = sel_cls(len(output_queues))
         if shared_output_ring is not None:
             shared_output_ring.producer_attach(device)
+        # consumer-side batching ("B" of RnB inside the consumer): the model
+        # declares how many queued items one call may take and provides the
+        # buffer their rows are pulled into (RunnerModel.gather_limits)
+        gather = getattr(model, "gather_limits", None)
+        gather = gather() if callable(gather) else None
+        # producer writes straight into its output slot (no staging copy)
+        direct_out = (shared_output_ring is not None and num_segments == 1
+                      and callable(getattr(model, "call_into", None))
+                      and callable(getattr(shared_output_ring, "slot_views", None)))
 
         placeholders = None
         if shared_input_rings is not None:
@@ -124,14 +133,15 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 for ring in rings:
                     if ring is None:
                         continue
-                    ring.consumer_attach(device)
+                    ring.consumer_attach(device, (step_idx, group_idx, instance_idx))
                     if shapes is None:
                         shapes, dtypes = ring.shapes, ring.dtypes
                     else:
                         shapes = tuple(tuple(max(a, b) for a, b in zip(s1, s2))
                                        for s1, s2 in zip(shapes, ring.shapes))
-            placeholders = tuple(torch.zeros(s, dtype=d, device=device)
-                                 for s, d in zip(shapes, dtypes))
+            if gather is None:
+                placeholders = tuple(torch.zeros(s, dtype=d, device=device)
+                                     for s, d in zip(shapes, dtypes))
 
         def aborted():
             return termination_flag.value != TerminationFlag.UNSET
@@ -141,19 +151,29 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         if print_summary and os.environ.get("RNB_NO_TQDM") != "1":
             try:
                 from tqdm import tqdm
-                progress = tqdm(total=num_videos, file=sys.stdout, mininterval=1.0)
+                progress = tqdm(total=getattr(num_videos, "value", num_videos),
+                                file=sys.stdout, mininterval=1.0)
             except Exception:
                 progress = None
-        items = 0
+        count = {"items": 0}
 
         state = {"out_counter": 0, "last_count": 0}
 
-        def emit(outputs):
-            """Route one model output; False means stop the runner loop."""
+        # host synchronisation per item is needed where the host reads results
+        # (final step: completion time + count) or where the output ring is
+        # not GPU-ordered; GPU-ordered rings order the consumer on the GPU
+        sync_each = is_final_step or shared_output_ring is None or \
+            not shared_output_ring.gpu_ordered or os.environ.get("RNB_STAGE_SYNC") == "1"
+
+        def emit(outputs, slot=None):
+            """Route one model output; False means stop the runner loop.
+            ``slot``: the output slot the model already wrote (direct_out)."""
             tensor_outputs, non_tensor_outputs, time_card = outputs
-            if stream is not None:
+            if stream is not None and sync_each:
                 stream.synchronize()
             if time_card is None:
+                if slot is not None:
+                    shared_output_ring.release(slot)    # nothing written
                 return True
             time_card.record("inference%d_finish" % step_idx)
             if is_final_step:
@@ -162,15 +182,16 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                     prev = global_inference_counter.value
                     global_inference_counter.value = prev + n_inf
                     now = global_inference_counter.value
-                if now >= num_videos:
-                    if prev < num_videos:
-                        print("Finished processing %d videos" % num_videos, flush=True)
+                goal = num_videos.value if hasattr(num_videos, "value") else num_videos
+                if now >= goal:
+                    if prev < goal:
+                        print("Finished processing %d videos" % goal, flush=True)
                         _set_flag(termination_flag,
                                   TerminationFlag.TARGET_NUM_VIDEOS_REACHED)
                     else:
                         return False
                 if progress is not None and now > state["last_count"]:
-                    progress.update(min(now, num_videos) - min(state["last_count"], num_videos))
+                    progress.update(min(now, goal) - min(state["last_count"], goal))
                     state["last_count"] = now
                 cards = time_card.time_cards if isinstance(time_card, TimeCardList) \
                     else [time_card]
@@ -181,7 +202,14 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             out_q = output_queues[selector.select(tensor_outputs, non_tensor_outputs,
                                                   time_card)]
             msgs = []
-            for seg in range(num_segments):
+            if slot is not None:
+                gen = shared_output_ring.commit(slot, [t.shape[0] for t in tensor_outputs])
+                state["out_counter"] = (state["out_counter"] + 1) % len(shared_output_ring)
+                signal_out = Signal(group_idx, instance_idx, slot,
+                                    shared_output_ring.descriptor(),
+                                    gen if shared_output_ring.check else None)
+                msgs.append((signal_out, non_tensor_outputs, time_card))
+            for seg in range(num_segments if slot is None else 0):
                 signal_out = None
                 if shared_output_ring is not None:
                     seg_tensors = []
@@ -214,13 +242,45 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             # without accounting (direct callers) fall back to marker semantics
             return in_state is None or in_state[0].value >= in_state[1]
 
+        def pull(signal, dst):
+            """Pull one item's slot into ``dst`` (tuple of tensors) and release
+            the slot; returns the row views."""
+            ring = shared_input_rings[signal.group_idx][signal.instance_idx]
+            ring.verify(signal.tensor_idx, signal.gen, "before pull")
+            if fault == "early_release":
+                # test hook: the reference's bug (slot released before the
+                # pull completes, runner.py:112-117) -> the race checker
+                # must catch the producer's overwrite
+                ring.release(signal.tensor_idx)
+                time.sleep(0.3)
+            out = ring.read_into(signal.tensor_idx, dst, signal.ring)
+            if fault != "early_release":
+                ring.verify(signal.tensor_idx, signal.gen, "after pull")
+            elif signal.gen is not None and ring.gen[signal.tensor_idx] != signal.gen:
+                from .parallel.transport import RingRaceError
+                raise RingRaceError("ring %s slot %d overwritten during the pull"
+                                    % (ring.name, signal.tensor_idx))
+            ring.release(signal.tensor_idx)
+            return out
+
+        def rows_of(signal):
+            return shared_input_rings[signal.group_idx][signal.instance_idx].rows_of(
+                signal.tensor_idx)
+
+        def cards_of(tc):
+            return list(tc.time_cards) if isinstance(tc, TimeCardList) else [tc]
+
+        pending = []                  # an item taken out of the queue but not run yet
         while termination_flag.value == TerminationFlag.UNSET:
-            try:
-                tpl = input_queue.get(timeout=QUEUE_POLL_S)
-            except Empty:
-                if in_state is not None and upstream_finished():
-                    break          # every producer flushed and the queue is drained
-                continue
+            if pending:
+                tpl = pending.pop()
+            else:
+                try:
+                    tpl = input_queue.get(timeout=QUEUE_POLL_S)
+                except Empty:
+                    if in_state is not None and upstream_finished():
+                        break      # every producer flushed and the queue is drained
+                    continue
             if tpl is None:
                 if upstream_finished():
                     try:           # drain whatever is still queued behind markers
@@ -235,33 +295,75 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             time_card.add_gpu(g_idx)
             time_card.record("runner%d_start" % step_idx)
 
-            if signal is not None:
-                ring = shared_input_rings[signal.group_idx][signal.instance_idx]
-                if ring.is_free(signal.tensor_idx) and aborted():
-                    break
-                ring.verify(signal.tensor_idx, signal.gen, "before pull")
-                if fault == "early_release":
-                    # test hook: the reference's bug (slot released before the
-                    # pull completes, runner.py:112-117) -> the race checker
-                    # must catch the producer's overwrite
-                    ring.release(signal.tensor_idx)
-                    time.sleep(0.3)
-                tensor_inputs = ring.read_into(signal.tensor_idx, placeholders, signal.ring)
-                if fault != "early_release":
-                    ring.verify(signal.tensor_idx, signal.gen, "after pull")
-                elif signal.gen is not None and ring.gen[signal.tensor_idx] != signal.gen:
-                    from .parallel.transport import RingRaceError
-                    raise RingRaceError("ring %s slot %d overwritten during the pull"
-                                        % (ring.name, signal.tensor_idx))
-                ring.release(signal.tensor_idx)
+            if gather is not None and signal is not None:
+                # consumer-side batching: take what is queued (up to the model's
+                # item / row limits, waiting at most max_wait_s for more), pull
+                # every item's rows straight into the model's input buffer
+                max_items, max_rows, max_wait_s = gather
+                items, rows = [tpl], rows_of(signal)
+                deadline = time.time() + max_wait_s
+                while len(items) < max_items and rows < max_rows:
+                    try:
+                        wait = deadline - time.time()
+                        nxt = input_queue.get_nowait() if wait <= 0 else \
+                            input_queue.get(timeout=wait)
+                    except Empty:
+                        break
+                    if nxt is None:
+                        continue            # end-of-stream wake-up marker
+                    if nxt[0] is None or rows + rows_of(nxt[0]) > max_rows:
+                        pending.append(nxt)
+                        break
+                    nxt[2].add_gpu(g_idx)
+                    nxt[2].record("runner%d_start" % step_idx)
+                    items.append(nxt)
+                    rows += rows_of(nxt[0])
+                gslot = None
+                if direct_out and getattr(model, "gather_into_output", False):
+                    # batching stage: assemble the batch in the output slot itself
+                    gslot = state["out_counter"] % len(shared_output_ring)
+                    if not shared_output_ring.wait_free(gslot, aborted):
+                        break
+                    shared_output_ring.begin_write(gslot, stream)
+                    dst = tuple(shared_output_ring.slot_views(gslot))
+                else:
+                    dst = model.gather_buffers(rows)
+                off, cards, nts = 0, [], []
+                for sig, nt, tc in items:
+                    r = rows_of(sig)
+                    pull(sig, tuple(d[off:off + r] for d in dst))
+                    off += r
+                    cards.extend(cards_of(tc))
+                    nts.append(nt)
+                tensor_inputs = tuple(d[:rows] for d in dst)
+                time_card = TimeCardList(cards)
+                non_tensor_inputs = nts
+            elif signal is not None:
+                tensor_inputs = pull(signal, placeholders)
             else:
                 tensor_inputs = None
 
             time_card.record("inference%d_start" % step_idx)
-            items += 1
-            if fault == "runner%d_item%d" % (step_idx, items):
+            count["items"] += 1         # model calls (fault-injection index)
+            if fault == "runner%d_item%d" % (step_idx, count["items"]):
                 raise RuntimeError("injected fault in runner%d at item %d"
-                                   % (step_idx, items))
+                                   % (step_idx, count["items"]))
+            if gather is not None and signal is not None:
+                call = getattr(model, "call_gathered", model)
+                outputs = call(tensor_inputs, non_tensor_inputs, time_card)
+                if not emit(outputs, gslot):
+                    break
+                continue
+            if direct_out:
+                slot = state["out_counter"] % len(shared_output_ring)
+                if not shared_output_ring.wait_free(slot, aborted):
+                    break
+                shared_output_ring.begin_write(slot, stream)
+                outputs = model.call_into(tensor_inputs, non_tensor_inputs, time_card,
+                                          shared_output_ring.slot_views(slot))
+                if not emit(outputs, slot):
+                    break
+                continue
             outputs = model(tensor_inputs, non_tensor_inputs, time_card)
             if not emit(outputs):
                 break

@@ -233,16 +233,38 @@ class TimeCardSummary:
             out["%s -> %s" % (prv, nxt)] = float(d.mean())
         return out
 
-    def end_to_end(self, num_skips: int = 0) -> np.ndarray:
-        """Per-request latency (first key -> max over all later keys), s."""
+    def _select(self, min_id: Optional[int], max_id: Optional[int]) -> np.ndarray:
+        ids = np.asarray(self.ids, dtype=np.int64)
+        keep = np.ones(len(ids), dtype=bool)
+        if min_id is not None:
+            keep &= ids >= min_id
+        if max_id is not None:
+            keep &= ids <= max_id
+        return keep
+
+    def end_to_end(self, num_skips: int = 0, min_id: Optional[int] = None,
+                   max_id: Optional[int] = None) -> np.ndarray:
+        """Per-request latency (first key -> max over all later keys), s;
+        ``min_id``/``max_id`` restrict to a request-id range (a bench phase)."""
         if not self.keys:
             return np.zeros(0)
         mat = np.asarray([self.summary[k] for k in self.keys], dtype=np.float64)
         lat = mat.max(axis=0) - mat[0]
+        if min_id is not None or max_id is not None:
+            return lat[self._select(min_id, max_id)]
         return lat[num_skips:]
 
-    def latency_stats(self, num_skips: int = 0) -> Dict[str, float]:
-        return percentile_stats(self.end_to_end(num_skips))
+    def finish_times(self, min_id: Optional[int] = None,
+                     max_id: Optional[int] = None) -> np.ndarray:
+        """Completion time (latest key) of each request in the id range, s."""
+        if not self.keys:
+            return np.zeros(0)
+        mat = np.asarray([self.summary[k] for k in self.keys], dtype=np.float64)
+        return mat.max(axis=0)[self._select(min_id, max_id)]
+
+    def latency_stats(self, num_skips: int = 0, min_id: Optional[int] = None,
+                      max_id: Optional[int] = None) -> Dict[str, float]:
+        return percentile_stats(self.end_to_end(num_skips, min_id, max_id))
 
     def print_summary(self, num_skips: int) -> None:
         """Mean Δ between consecutive keys (reference format) + percentiles."""

@@ -186,7 +186,8 @@ def test_shared_queues_and_rings_wiring_rnb():
     assert in_q is qt.get_filename_queue() and len(out_qs) == 2
     in_r, out_r = qt.get_tensors(0, 0, 5)
     assert in_r is None and out_r.kind == "host" and len(out_r) == 20
-    assert out_r.shapes == ((15, 8, 112, 112, 8),)
+    # fp32 NDHWC4 clips by default (reference precision)
+    assert out_r.shapes == ((15, 8, 112, 112, 4),)
     # batcher group 1 reads loader queue 1, both batcher groups feed queue 0
     bq_in, bq_out = qt.get_queues(1, 1)
     assert bq_in is out_qs[1]
@@ -204,4 +205,8 @@ def test_runner_slot_shape_follows_layer_range():
     shapes, dtypes = step_output_spec(spec.steps[1], spec.steps[1].groups[0])
     assert shapes == ((15, 8, 56, 56, 64),)
     import torch
-    assert dtypes == (torch.bfloat16,)
+    assert dtypes == (torch.float32,)
+    cfg["defaults"]["dtype"] = "bf16"
+    spec = parse_pipeline(cfg)
+    shapes, dtypes = step_output_spec(spec.steps[1], spec.steps[1].groups[0])
+    assert shapes == ((15, 8, 56, 56, 64),) and dtypes == (torch.bfloat16,)

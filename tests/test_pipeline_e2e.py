@@ -191,3 +191,65 @@ def test_ring_race_checker_catches_early_release(tmp_path):
     assert proc.returncode != 0
     assert "RingRaceError" in proc.stdout + proc.stderr
     assert res is not None and res["termination_flag"] == "CHILD_FAILED"
+
+
+def test_consumer_side_batching_warmup_and_latency_phase(tmp_path):
+    """R2P1DRunner takes several queued videos per call (gather_limits), the
+    launcher excludes the warm-up videos from the timed window and runs a
+    Poisson latency phase after the bulk phase (bench.py's three phases)."""
+    cfg = {"video_path_iterator": IT, "defaults": SMALL, "pipeline": [
+        {"model": M + "R2P1DLoader", "queue_groups": [{"gpus": [-1, -1], "out_queues": [0]}]},
+        {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [-1], "in_queue": 0}],
+         "max_clips": 8, "max_batch_videos": 4}]}
+    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "6", "-mi", "0", "--warmup-videos", "2",
+                           "--latency-seconds", "1", "--latency-load", "0.5")
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert res["ok"] and res["warmup_videos"] == 2
+    assert res["latency"]["count"] == 6              # timed ids 3..8 only
+    assert res["latency_phase"]["count"] >= 1
+    assert res["window_s"] > 0 and res["videos_per_s_window"] > 0
+    # the runner log holds every request: warm-up + timed + latency phase
+    logs = [f for f in os.listdir(tmp_path / "logs" / res["job_id"]) if f.startswith("g")]
+    rows = sum(len(open(tmp_path / "logs" / res["job_id"] / f).read().splitlines()) - 1
+               for f in logs)
+    assert rows == 8 + res["latency_phase"]["count"]
+
+
+def test_batcher_gathers_without_staging_copies(tmp_path):
+    """Batcher under the runner: up to ``batch`` queued items per call, pulled
+    straight into the batch (no clone / cat), TimeCardList downstream."""
+    cfg = {"video_path_iterator": IT, "defaults": SMALL, "pipeline": [
+        {"model": M + "R2P1DLoader", "queue_groups": [{"gpus": [-1], "out_queues": [0]}]},
+        {"model": "rnb_amd.batcher.Batcher", "max_rows": 9, "max_wait_ms": 200,
+         "queue_groups": [{"gpus": [-1], "in_queue": 0, "out_queues": [0], "batch": 3}]},
+        {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [-1], "in_queue": 0}],
+         "max_clips": 9}]}
+    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "9", "-mi", "0")
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert res["ok"] and res["videos_done"] == 9
+
+
+def test_ring_depth_plan_from_consumer_batching():
+    """Rings without a fixed num_shared_tensors are sized from what their
+    consumers batch, capped by free HBM (control.plan_ring_depths)."""
+    from rnb_amd.config import parse_pipeline
+    from rnb_amd.control import plan_ring_depths
+    cfg = {"video_path_iterator": IT, "defaults": {"dtype": "fp32"}, "pipeline": [
+        {"model": M + "R2P1DLoader", "queue_groups": [{"gpus": [0, 1], "out_queues": [0]}]},
+        {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [0, 0, 1, 1], "in_queue": 0}],
+         "max_batch_videos": 64}]}
+    spec = parse_pipeline(cfg)
+    plan = plan_ring_depths(spec, [300 << 30, 300 << 30], verbose=False)
+    assert spec.steps[0].num_shared_tensors == 2 * 64 * 4 // 2 + 2 == plan[0][3]
+    slot = plan[0][4]
+    assert slot == 15 * 8 * 112 * 112 * 4 * 4        # 15 fp32 NDHWC4 clips
+    # a small device: the rings shrink to the HBM share
+    spec = parse_pipeline(cfg)
+    plan_ring_depths(spec, [2 << 30, 2 << 30], verbose=False)
+    assert 2 <= spec.steps[0].num_shared_tensors < 258
+    assert spec.steps[0].num_shared_tensors * slot <= 0.25 * (2 << 30)
+    # an explicit depth is kept
+    cfg["pipeline"][0]["num_shared_tensors"] = 7
+    spec = parse_pipeline(cfg)
+    plan_ring_depths(spec, None, verbose=False)
+    assert spec.steps[0].num_shared_tensors == 7
