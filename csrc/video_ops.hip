@@ -69,6 +69,50 @@ __global__ void clipgen_u8_kernel(uint8_t* __restrict__ out, const int* __restri
   }
 }
 
+// Same generator for ONE video whose clip start frames travel in the kernel
+// arguments (no metadata upload, no host synchronisation: the loader stage
+// issues it per video; rnb_amd/models/r2p1d/decoder.py).
+#define CLIPGEN_MAX_CLIPS 32
+struct ClipgenArgs {
+  int vid, nclips;
+  int starts[CLIPGEN_MAX_CLIPS];
+};
+
+__global__ void clipgen_video_kernel(uint8_t* __restrict__ out, ClipgenArgs a, int F, int H,
+                                     int W) {
+  const long long hw = (long long)H * W;
+  const long long total_px = hw * F * a.nclips;
+  const long long px0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (px0 >= total_px) return;
+  const long long frame = px0 / hw;
+  const int clip = (int)(frame / F);
+  const uint32_t vid = (uint32_t)a.vid;
+  const uint32_t fr = (uint32_t)(a.starts[clip] + (int)(frame - (long long)clip * F));
+  const uint32_t pix0 = (uint32_t)(px0 - frame * hw);
+  const int n = (int)min(16LL, min(total_px - px0, hw - (long long)pix0));
+  uint32_t words[12];
+#pragma unroll
+  for (int w = 0; w < 12; ++w) words[w] = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int b = i * 3 + c;
+      const uint32_t v = i < n ? pixel_hash(vid, fr, pix0 + i, c) : 0u;
+      words[b >> 2] |= v << (8 * (b & 3));
+    }
+  }
+  uint8_t* dst = out + px0 * 3;
+  if (n == 16) {
+    uint4* d4 = (uint4*)dst;
+    d4[0] = make_uint4(words[0], words[1], words[2], words[3]);
+    d4[1] = make_uint4(words[4], words[5], words[6], words[7]);
+    d4[2] = make_uint4(words[8], words[9], words[10], words[11]);
+  } else {
+    for (int b = 0; b < n * 3; ++b) dst[b] = (uint8_t)(words[b >> 2] >> (8 * (b & 3)));
+  }
+}
+
 struct NormParams {
   float scale[3];   // 1 / (255 * std)
   float shift[3];   // -mean / std
@@ -368,6 +412,21 @@ int rnb_clipgen_u8(void* out, const int* vids, const int* starts, int nclips, in
   const long long grid = (threads + block - 1) / block;
   hipLaunchKernelGGL(clipgen_u8_kernel, dim3((unsigned)grid), dim3(block), 0, stream,
                      (uint8_t*)out, vids, starts, nclips, F, H, W);
+  return (int)hipGetLastError();
+}
+
+int rnb_clipgen_video(void* out, int vid, const int* starts, int nclips, int F, int H, int W,
+                      hipStream_t stream) {
+  if (nclips <= 0) return 0;
+  if (nclips > CLIPGEN_MAX_CLIPS) return -3;
+  if (((long long)H * W) % 16 != 0) return -2;
+  ClipgenArgs a;
+  a.vid = vid;
+  a.nclips = nclips;
+  for (int i = 0; i < CLIPGEN_MAX_CLIPS; ++i) a.starts[i] = i < nclips ? starts[i] : 0;
+  const long long threads = ((long long)nclips * F * H * W + 15) / 16;
+  hipLaunchKernelGGL(clipgen_video_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     stream, (uint8_t*)out, a, F, H, W);
   return (int)hipGetLastError();
 }
 

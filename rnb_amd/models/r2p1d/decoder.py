@@ -57,38 +57,23 @@ class SyntheticDecoder(Decoder):
         self.device = device
         self.F, self.H, self.W = clip_length, height, width
         self.dtype = dtype
-        # pinned staging ring for the per-video metadata upload (pinning a
-        # fresh host tensor per video costs more than the decode kernels)
-        self._pinned = None
-        self._pin_i = 0
+        self._surface = None
 
     def probe(self, path):
         return parse_synthetic_path(path)
-
-    def _meta(self, vid, starts):
-        n = len(starts)
-        if self.device.type != "cuda":
-            return torch.tensor([[vid] * n, list(starts)], dtype=torch.int32)
-        if self._pinned is None:
-            self._pinned = [(torch.zeros((2, 64), dtype=torch.int32).pin_memory(),
-                             torch.cuda.Event()) for _ in range(8)]
-        host, ev = self._pinned[self._pin_i]
-        self._pin_i = (self._pin_i + 1) % len(self._pinned)
-        if n > host.shape[1]:
-            return torch.tensor([[vid] * n, list(starts)], dtype=torch.int32).to(self.device)
-        ev.synchronize()                      # the previous upload from this buffer is done
-        host[0, :n] = vid
-        host[1, :n] = torch.as_tensor(list(starts), dtype=torch.int32)
-        meta = host[:, :n].to(self.device, non_blocking=True)
-        ev.record(torch.cuda.current_stream(self.device))
-        return meta
 
     def decode(self, vid, starts, out=None):
         n = len(starts)
         if n == 0:
             return self.empty()
-        meta = self._meta(vid, starts)
-        surf = vops.clipgen_u8(meta[0], meta[1], self.F, self.H, self.W)
+        surf = None
+        if self.device.type == "cuda":
+            # one reusable decoder surface: uses of it are ordered on the stream
+            if self._surface is None or self._surface.shape[0] < n:
+                self._surface = torch.empty((max(n, 15), self.F, self.H, self.W, 3),
+                                            dtype=torch.uint8, device=self.device)
+            surf = self._surface[:n]
+        surf = vops.clipgen_video(vid, starts, self.F, self.H, self.W, self.device, out=surf)
         return vops.preprocess(surf, out=out, dtype=self.dtype)
 
 

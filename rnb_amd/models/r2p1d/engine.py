@@ -188,6 +188,19 @@ class R2P1DEngine:
                 for j, blk in enumerate(layer.blocks):
                     cur = self._block(blk, cur, "conv%d.blocks.%d" % (idx, j))
         self.out_name = cur
+        # liveness: buffers no later op reads are dropped right after their
+        # last reader, so a forward (and a captured graph) holds only the
+        # live activations, not all ~70 of them (R(2+1)D-34 fp32 at 128
+        # clips: ~6 GB peak instead of ~60 GB)
+        last = {}
+        for i, op in enumerate(self.ops):
+            last[op.src] = i
+            if op.res is not None:
+                last[op.res] = i
+        self._free_after = [[] for _ in self.ops]
+        for name, i in last.items():
+            if name not in ("x", self.out_name):
+                self._free_after[i].append(name)
 
     # ------------------------------------------------------------- metadata
     @property
@@ -258,9 +271,12 @@ class R2P1DEngine:
         hip = self.backend == "hip"
         bufs: Dict[str, torch.Tensor] = {"x": x}
         skip = False
+        free_after = self._free_after
         for i, op in enumerate(self.ops):
             if skip:                      # temporal half of a fused pair
                 skip = False
+                for name in free_after[i]:
+                    bufs.pop(name, None)
                 continue
             src = bufs[op.src]
             if hip and op.fuse is not None and op.fuse.use_for(src.shape):
@@ -268,6 +284,8 @@ class R2P1DEngine:
                 res = bufs[nxt.res] if nxt.res is not None else None
                 bufs[nxt.dst] = op.fuse.forward_hip(src, res)
                 skip = True
+                for name in free_after[i]:
+                    bufs.pop(name, None)
                 continue
             res = bufs[op.res] if op.res is not None else None
             if op.bn is not None:
@@ -285,6 +303,9 @@ class R2P1DEngine:
             else:
                 y = op.layer.forward_torch(src, res, out_dtype=self.dtype)
             bufs[op.dst] = y
+            del src, res
+            for name in free_after[i]:
+                bufs.pop(name, None)
         y = bufs[self.out_name]
         if self.head is not None:
             y = self.head.forward(y, out) if hip else self.head.forward_torch(y)
@@ -302,13 +323,17 @@ class R2P1DEngine:
         x = torch.randn(self.input_shape(n), device=self.device).to(self.dtype)
         bufs = {"x": x}
         chosen = {}
-        for op in self.ops:
+        for i, op in enumerate(self.ops):
             src = bufs[op.src]
             res = bufs[op.res] if op.res is not None else None
             if op.bn is not None:
                 res = None               # the residual is added after the BN
             chosen[op.layer.name] = op.layer.autotune(src, res, reps)
             bufs[op.dst] = op.layer.forward_hip(src, res)
+            if self.f32:                 # no fused pairs to tune afterwards
+                del src, res
+                for name in self._free_after[i]:
+                    bufs.pop(name, None)
         # fused (2+1)D pairs: keep the fused kernel only where it beats the
         # two tuned kernels
         for i, op in enumerate(self.ops):
@@ -326,6 +351,8 @@ class R2P1DEngine:
             op.fuse.set_choice(src.shape, best)
             self.fused_choices[op.fuse.name] = best
         torch.cuda.synchronize(self.device)
+        del bufs
+        torch.cuda.empty_cache()         # tuning scratch back to the device
         return chosen
 
 

@@ -222,6 +222,10 @@ class R2P1DVideoPathIterator(VideoPathIterator):
 class R2P1DLoader(RunnerModel):
     """Video path -> sampled clips, NDHWC [n, 8, 112, 112, C] (fp32 C=4, bf16 C=8)."""
 
+    # decode kernels are tiny and gate the consumers: run them on a
+    # high-priority HIP stream so they do not queue behind the conv kernels
+    stream_priority = -1
+
     def __init__(self, device, num_clips_population=(1, 15), num_clips_weights=(10, 1),
                  decoder="synthetic", seed=None, max_clips=DEFAULT_MAX_CLIPS,
                  warmup=3, dtype=None, **unused):

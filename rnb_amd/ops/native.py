@@ -172,6 +172,10 @@ class Kernels:
         lib.rnb_clipgen_u8.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_void_p]
+        lib.rnb_clipgen_video.argtypes = [ctypes.c_void_p, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p]
         lib.rnb_preprocess.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
                                        ctypes.POINTER(ctypes.c_float),
                                        ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
@@ -308,6 +312,11 @@ class Kernels:
     def clipgen_u8(self, out_ptr, vids_ptr, starts_ptr, nclips, F, H, W, stream):
         _check(self.lib.rnb_clipgen_u8(out_ptr, vids_ptr, starts_ptr, nclips, F, H, W,
                                        stream), "clipgen_u8")
+
+    def clipgen_video(self, out_ptr, vid, starts, F, H, W, stream):
+        arr = (ctypes.c_int * max(1, len(starts)))(*starts)
+        _check(self.lib.rnb_clipgen_video(out_ptr, int(vid), arr, len(starts), F, H, W,
+                                          stream), "clipgen_video")
 
     def preprocess(self, in_ptr, out_ptr, npix, mean, std, stream):
         m = (ctypes.c_float * 3)(*mean)

@@ -53,6 +53,27 @@ def clipgen_u8(vids: torch.Tensor, starts: torch.Tensor, F: int, H: int, W: int,
     return res.contiguous()
 
 
+def clipgen_video(vid: int, starts, F: int, H: int, W: int, device,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One video's synthetic clips (uint8 [n, F, H, W, 3]); the start frames
+    travel as kernel arguments, so nothing is uploaded and the host never
+    waits (the per-video form of ``clipgen_u8``; same pixels)."""
+    n = len(starts)
+    if device.type == "cuda":
+        from .native import kernels
+        if out is None:
+            out = torch.empty((n, F, H, W, 3), dtype=torch.uint8, device=device)
+        if n > 32:
+            return clipgen_u8(torch.full((n,), vid, dtype=torch.int32, device=device),
+                              torch.as_tensor(list(starts), dtype=torch.int32).to(device),
+                              F, H, W, out=out)
+        kernels().clipgen_video(out.data_ptr(), vid, list(starts), F, H, W,
+                                torch.cuda.current_stream(device).cuda_stream)
+        return out
+    return clipgen_u8(torch.full((n,), vid, dtype=torch.int32),
+                      torch.as_tensor(list(starts), dtype=torch.int32), F, H, W, out=out)
+
+
 def preprocess(frames_u8: torch.Tensor, mean=KINETICS_MEAN, std=KINETICS_STD,
                out: Optional[torch.Tensor] = None, packed: bool = False,
                dtype=torch.bfloat16) -> torch.Tensor:

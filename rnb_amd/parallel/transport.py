@@ -249,6 +249,13 @@ class IpcRing(RingBase):
         self._ctx = ctx
         self.released_by = ctx.Array("i", [-1] * self.num_slots, lock=False)
         self.rel_handles = None    # set by set_consumers (before spawn)
+        # the producer's import descriptor (mem + event handles of every slot,
+        # ~25 KB for a deep ring) is published once in shared memory; queue
+        # signals carry only the small token (name, producer pid)
+        n_t = len(self.shapes)
+        self._desc_cap = 512 + self.num_slots * (n_t + 1) * 96
+        self._desc_shm = ctx.Array("c", self._desc_cap, lock=False)
+        self._desc_len = ctx.Value("i", 0, lock=False)
         self.order = os.environ.get(ORDER_ENV, "event")
         # per process
         self._wev = None           # producer: written events [slot]
@@ -257,6 +264,8 @@ class IpcRing(RingBase):
         self._rev = None           # consumer: own release events [slot]
         self._wopen: Dict[Tuple, List[int]] = {}              # consumer: opened written events
         self._dev = None
+        self._views = None
+        self._token = None
 
     def set_consumers(self, consumers) -> None:
         """Declare the consumer instances (before the processes are spawned)."""
@@ -276,6 +285,8 @@ class IpcRing(RingBase):
         st["_rev"] = None
         st["_wopen"] = {}
         st["_cid"] = None
+        st["_views"] = None
+        st["_token"] = None
         return st
 
     @property
@@ -305,14 +316,27 @@ class IpcRing(RingBase):
             self._wev = [rt.event_create_ipc() for _ in range(self.num_slots)]
             wh = tuple(rt.event_get_handle(e) for e in self._wev)
         self._desc = (self.name, os.getpid(), device.index, tuple(handles), wh)
+        import pickle
+        blob = pickle.dumps(self._desc, protocol=pickle.HIGHEST_PROTOCOL)
+        if len(blob) > self._desc_cap:
+            raise RuntimeError("ring %s: descriptor of %d bytes exceeds %d"
+                               % (self.name, len(blob), self._desc_cap))
+        self._desc_shm[:len(blob)] = blob
+        self._desc_len.value = len(blob)
+        self._token = (self.name, os.getpid())
 
     def descriptor(self):
-        return self._desc
+        """Token identifying this producer's slots (the full handles are read
+        once from shared memory by each consumer: ``_open``)."""
+        return self._token
 
     def slot_views(self, idx: int) -> List[torch.Tensor]:
         """Torch views of slot ``idx``'s tensors (producer side, full capacity)."""
-        return [device_view(p, s, d, self._dev)
-                for p, s, d in zip(self._ptrs[idx], self.shapes, self.dtypes)]
+        if self._views is None:
+            self._views = [[device_view(p, s, d, self._dev)
+                            for p, s, d in zip(row, self.shapes, self.dtypes)]
+                           for row in self._ptrs]
+        return self._views[idx]
 
     def _release_event(self, cid: int, idx: int) -> int:
         from ..ops import native
@@ -392,11 +416,17 @@ class IpcRing(RingBase):
             self.rel_handles[off:off + len(h)] = h
         self.rel_ready[self._cid] = 1
 
-    def _open(self, desc):
+    def _open(self, token):
         from ..ops import native
-        key = desc[:2]
+        key = tuple(token[:2])
         ptrs = self._opened.get(key)
         if ptrs is None:
+            import pickle
+            n = self._desc_len.value
+            desc = pickle.loads(bytes(self._desc_shm[:n])) if n else None
+            if desc is None or tuple(desc[:2]) != key:
+                raise RuntimeError("ring %s: no published descriptor for producer %s"
+                                   % (self.name, key))
             rt = native.runtime()
             ptrs = [[rt.ipc_open_handle(h) for h in row] for row in desc[3]]
             self._opened[key] = ptrs
@@ -423,7 +453,7 @@ class IpcRing(RingBase):
         if gpu:
             stream = torch.cuda.current_stream(dev)
             if self.gpu_ordered:
-                rt.stream_wait_event(stream.cuda_stream, self._wopen[descriptor[:2]][idx])
+                rt.stream_wait_event(stream.cuda_stream, self._wopen[tuple(descriptor[:2])][idx])
         for t, (ph, b) in enumerate(zip(placeholders, self.valid_rows(idx))):
             if b:
                 if b > ph.shape[0] or not ph.is_contiguous():
@@ -459,6 +489,7 @@ class IpcRing(RingBase):
         self._opened = {}
         if self._ptrs is not None:
             torch.cuda.synchronize(self._dev)
+            self._views = None
             for row in self._ptrs:
                 for p in row:
                     rt.free(p)

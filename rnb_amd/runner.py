@@ -93,7 +93,11 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
     if use_gpu:
         torch.cuda.set_device(g_idx)
         device = torch.device("cuda:%d" % g_idx)
-        stream = torch.cuda.Stream(device=device)
+        # stages whose GPU work gates everyone else (decoding) ask for a
+        # high-priority stream (RunnerModel.stream_priority, lower = higher)
+        from .utils.class_utils import load_class as _lc
+        prio = int(getattr(_lc(model_module_path), "stream_priority", 0))
+        stream = torch.cuda.Stream(device=device, priority=prio)
         stream_ctx = torch.cuda.stream(stream)
     else:
         device = torch.device("cpu")
@@ -271,6 +275,17 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             return list(tc.time_cards) if isinstance(tc, TimeCardList) else [tc]
 
         pending = []                  # an item taken out of the queue but not run yet
+        gstats = {"calls": 0, "items": 0, "rows": 0}
+        # RNB_PROFILE_STAGES=1: where this runner's host time goes (seconds per
+        # phase: queue wait, slot pulls, model call, output publish)
+        prof = {} if os.environ.get("RNB_PROFILE_STAGES") == "1" else None
+        pclock = [time.perf_counter()]
+
+        def tick(name):
+            if prof is not None:
+                now = time.perf_counter()
+                prof[name] = prof.get(name, 0.0) + now - pclock[0]
+                pclock[0] = now
         while termination_flag.value == TerminationFlag.UNSET:
             if pending:
                 tpl = pending.pop()
@@ -291,6 +306,7 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                         continue
                 else:
                     continue
+            tick("queue")
             signal, non_tensor_inputs, time_card = tpl
             time_card.add_gpu(g_idx)
             time_card.record("runner%d_start" % step_idx)
@@ -337,12 +353,16 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                     nts.append(nt)
                 tensor_inputs = tuple(d[:rows] for d in dst)
                 time_card = TimeCardList(cards)
+                gstats["calls"] += 1
+                gstats["items"] += len(items)
+                gstats["rows"] += rows
                 non_tensor_inputs = nts
             elif signal is not None:
                 tensor_inputs = pull(signal, placeholders)
             else:
                 tensor_inputs = None
 
+            tick("pull")
             time_card.record("inference%d_start" % step_idx)
             count["items"] += 1         # model calls (fault-injection index)
             if fault == "runner%d_item%d" % (step_idx, count["items"]):
@@ -351,22 +371,30 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             if gather is not None and signal is not None:
                 call = getattr(model, "call_gathered", model)
                 outputs = call(tensor_inputs, non_tensor_inputs, time_card)
+                tick("model")
                 if not emit(outputs, gslot):
                     break
+                tick("emit")
                 continue
             if direct_out:
                 slot = state["out_counter"] % len(shared_output_ring)
                 if not shared_output_ring.wait_free(slot, aborted):
                     break
+                tick("slot_wait")
                 shared_output_ring.begin_write(slot, stream)
+                tick("begin_write")
                 outputs = model.call_into(tensor_inputs, non_tensor_inputs, time_card,
                                           shared_output_ring.slot_views(slot))
+                tick("model")
                 if not emit(outputs, slot):
                     break
+                tick("emit")
                 continue
             outputs = model(tensor_inputs, non_tensor_inputs, time_card)
+            tick("model")
             if not emit(outputs):
                 break
+            tick("emit")
         if termination_flag.value == TerminationFlag.UNSET and hasattr(model, "flush"):
             # natural end of stream: let batching/aggregating stages emit what
             # they still hold (the reference's Batcher would hold it forever)
@@ -374,6 +402,18 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             if outputs is not None:
                 emit(outputs)
 
+        if prof:
+            tot = sum(prof.values())
+            print("[runner %d/%d/%d gpu %d] host time %.2f s over %d calls: %s"
+                  % (step_idx, group_idx, instance_idx, g_idx, tot, count["items"],
+                     ", ".join("%s %.0f us" % (k, 1e6 * v / max(1, count["items"]))
+                               for k, v in sorted(prof.items(), key=lambda kv: -kv[1]))),
+                  flush=True)
+        if gstats["calls"]:
+            print("[runner %d/%d/%d gpu %d] %d batched calls: %.1f items, %.1f rows per call"
+                  % (step_idx, group_idx, instance_idx, g_idx, gstats["calls"],
+                     gstats["items"] / gstats["calls"], gstats["rows"] / gstats["calls"]),
+                  flush=True)
         # ---- shutdown
         if not is_final_step:
             try:

@@ -193,3 +193,13 @@ def test_f32_graphed_engine_matches_eager():
     ref = eng.forward(x)
     torch.cuda.synchronize()
     assert torch.equal(y, ref)
+
+
+def test_clipgen_video_args_kernel_matches_clipgen_u8():
+    from rnb_amd.ops import video as vops
+    starts = [0, 17, 40, 99, 3]
+    a = vops.clipgen_video(77, starts, 8, 112, 112, DEV)
+    b = vops.clipgen_u8(torch.full((5,), 77, dtype=torch.int32, device=DEV),
+                        torch.tensor(starts, dtype=torch.int32, device=DEV), 8, 112, 112)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
