@@ -65,9 +65,9 @@ def parse_args(argv=None):
     ap.add_argument("--depth", type=int, default=34)
     ap.add_argument("--videos-per-step", type=int, default=256,
                     help="videos arriving per GPU per step")
-    ap.add_argument("--replicas", type=int, default=2,
+    ap.add_argument("--replicas", type=int, default=3,
                     help="R(2+1)D runner processes per GPU (the R of RnB)")
-    ap.add_argument("--loaders", type=int, default=1, help="loader processes per GPU")
+    ap.add_argument("--loaders", type=int, default=3, help="loader processes per GPU")
     ap.add_argument("--video-batch", type=int, default=64,
                     help="max videos per model invocation (consumer-side batching)")
     ap.add_argument("--clips-per-batch", type=int, default=128,

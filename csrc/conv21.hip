@@ -771,6 +771,16 @@ int rnb_conv21_supported(int T, int H, int W) {
   return (T >= 1 && H >= 1 && W >= 1 && W <= C21_MAXW) ? 1 : 0;
 }
 
+// Full launch contract for N clips (the size checks of the launchers below):
+// callers fall back to the two-kernel path when this is 0.
+int rnb_conv21_fits(int N, int T, int H, int W, int y_stride, int res_stride) {
+  if (!rnb_conv21_supported(T, H, W) || N < 0) return 0;
+  const long long M = (long long)N * T * H * W;
+  if (M * 64 * 2 > 0x7FFFFF00LL) return 0;
+  if (M * y_stride * 2 > 0xFFFFFF00LL || M * res_stride * 2 > 0xFFFFFF00LL) return 0;
+  return 1;
+}
+
 int rnb_conv21_lds_bytes() { return C21_LDS; }
 
 int rnb_conv21_launch(const Conv21Params* pp, hipStream_t stream) {
@@ -787,11 +797,14 @@ int rnb_conv21_launch(const Conv21Params* pp, hipStream_t stream) {
   p.x_bytes = (uint32_t)(M * 64 * 2);
   c21_magic((uint32_t)p.bands, &p.mB, &p.sB);
   c21_magic((uint32_t)p.W, &p.mW, &p.sW);
-  static bool attr_set = false;
-  if (!attr_set) {
+  // the LDS limit is a per-device function attribute: set it once per device
+  static bool attr_set[64] = {false};
+  int adev = 0;
+  if (hipGetDevice(&adev) != hipSuccess || adev < 0 || adev >= 64) adev = 0;
+  if (!attr_set[adev]) {
     (void)hipFuncSetAttribute((const void*)conv21_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                         160 * 1024);
-    attr_set = true;
+    attr_set[adev] = true;
   }
   int grid = c21_num_cus();
   if (grid > p.n_units) grid = p.n_units;
@@ -814,11 +827,14 @@ int rnb_conv21s_launch(const Conv21Params* pp, hipStream_t stream) {
   p.x_bytes = (uint32_t)(M * 64 * 2);
   c21_magic((uint32_t)p.bands, &p.mB, &p.sB);
   c21_magic((uint32_t)p.W, &p.mW, &p.sW);
-  static bool attr_set = false;
-  if (!attr_set) {
+  // the LDS limit is a per-device function attribute: set it once per device
+  static bool attr_set[64] = {false};
+  int adev = 0;
+  if (hipGetDevice(&adev) != hipSuccess || adev < 0 || adev >= 64) adev = 0;
+  if (!attr_set[adev]) {
     (void)hipFuncSetAttribute((const void*)conv21s_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                         160 * 1024);
-    attr_set = true;
+    attr_set[adev] = true;
   }
   int grid = c21_num_cus();
   if (grid > p.n_units) grid = p.n_units;

@@ -113,6 +113,126 @@ __global__ void clipgen_video_kernel(uint8_t* __restrict__ out, ClipgenArgs a, i
   }
 }
 
+// ---------------------------------------------------------------------------
+// NV12 decoder surfaces -> normalised clips: the per-frame work NVVL's
+// RnBLoader does after NVDEC (colour conversion + scaling to 112x112;
+// reference models/r2p1d/model.py:123-125, README.md:42-110).
+//
+//  * nv12gen_video_kernel   synthetic decoder output: NV12 frames (Y plane of
+//                           H rows, then an interleaved UV plane of H/2 rows,
+//                           W bytes per row) at the source resolution, e.g.
+//                           Kinetics' 340x256; stands in for the VCN surface.
+//  * nv12_clip_kernel       bilinear scale (align_corners = false, from a crop
+//                           box of the source frame) of Y and of the half-
+//                           resolution U/V planes, BT.601 video-range YUV ->
+//                           RGB, clamp to [0, 255], Kinetics normalisation,
+//                           written straight into the stage's NDHWC layout
+//                           (fp32 4 channels or bf16 8 channels per pixel).
+// ---------------------------------------------------------------------------
+template <bool FROM_ARRAYS>
+__global__ void nv12gen_kernel(uint8_t* __restrict__ out, ClipgenArgs a,
+                               const int* __restrict__ vids, const int* __restrict__ starts,
+                               int F, int H, int W) {
+  // one thread = 16 bytes of one frame's NV12 image (H*W*3/2 bytes per frame)
+  const long long fbytes = (long long)H * W * 3 / 2;
+  const long long total = fbytes * F * a.nclips;
+  const long long b0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (b0 >= total) return;
+  const long long frame = b0 / fbytes;
+  const int clip = (int)(frame / F);
+  const int start = FROM_ARRAYS ? starts[clip] : a.starts[clip];
+  const uint32_t vid = (uint32_t)(FROM_ARRAYS ? vids[clip] : a.vid);
+  const uint32_t fr = (uint32_t)(start + (int)(frame - (long long)clip * F));
+  const long long off0 = b0 - frame * fbytes;
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const long long off = off0 + i;
+    uint32_t v = 0;
+    if (off < fbytes) {
+      if (off < (long long)H * W) {
+        v = pixel_hash(vid, fr, (uint32_t)off, 0u);
+      } else {
+        const long long c = off - (long long)H * W;     // UV plane byte
+        v = pixel_hash(vid, fr, (uint32_t)(c >> 1), 1u + (uint32_t)(c & 1));
+        v = 64u + (v >> 1);                              // keep chroma near neutral
+      }
+    }
+    w[i >> 2] |= v << (8 * (i & 3));
+  }
+  uint8_t* dst = out + b0;
+  if (off0 + 16 <= fbytes && ((uintptr_t)dst & 15u) == 0) {
+    *(uint4*)dst = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    for (int i = 0; i < 16 && off0 + i < fbytes; ++i) dst[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+  }
+}
+
+struct Nv12ClipArgs {
+  int src_w, src_h, out_w, out_h;
+  float crop_x, crop_y, crop_w, crop_h;   // source box scaled to the output
+  float scale[3], shift[3];               // normalisation (x / (255 std) - mean / std)
+  int bf16;                               // 0: fp32 NDHWC4, 1: bf16 NDHWC8
+};
+
+static __device__ __forceinline__ uint32_t nv12_bf_bits(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+
+static __device__ __forceinline__ float nv12_sample(const uint8_t* __restrict__ plane, int w,
+                                                    int h, int stride, int comps, int comp,
+                                                    float sx, float sy) {
+  // bilinear with edge clamping, align_corners = false mapping done by caller
+  sx = fminf(fmaxf(sx, 0.f), (float)(w - 1));
+  sy = fminf(fmaxf(sy, 0.f), (float)(h - 1));
+  const int x0 = (int)sx, y0 = (int)sy;
+  const int x1 = min(x0 + 1, w - 1), y1 = min(y0 + 1, h - 1);
+  const float fx = sx - (float)x0, fy = sy - (float)y0;
+  const float p00 = plane[y0 * stride + x0 * comps + comp];
+  const float p01 = plane[y0 * stride + x1 * comps + comp];
+  const float p10 = plane[y1 * stride + x0 * comps + comp];
+  const float p11 = plane[y1 * stride + x1 * comps + comp];
+  const float top = p00 + (p01 - p00) * fx;
+  const float bot = p10 + (p11 - p10) * fx;
+  return top + (bot - top) * fy;
+}
+
+__global__ __launch_bounds__(256) void nv12_clip_kernel(const uint8_t* __restrict__ nv12,
+                                                        void* __restrict__ out, long long npix,
+                                                        Nv12ClipArgs a) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npix) return;
+  const int ohw = a.out_w * a.out_h;
+  const long long frame = i / ohw;
+  const int p = (int)(i - frame * ohw);
+  const int oy = p / a.out_w, ox = p - oy * a.out_w;
+  const uint8_t* y_plane = nv12 + frame * ((long long)a.src_w * a.src_h * 3 / 2);
+  const uint8_t* uv_plane = y_plane + (long long)a.src_w * a.src_h;
+  // output pixel centre -> source coordinate (align_corners = false)
+  const float sx = a.crop_x + ((float)ox + 0.5f) * (a.crop_w / (float)a.out_w) - 0.5f;
+  const float sy = a.crop_y + ((float)oy + 0.5f) * (a.crop_h / (float)a.out_h) - 0.5f;
+  const float yv = nv12_sample(y_plane, a.src_w, a.src_h, a.src_w, 1, 0, sx, sy);
+  // chroma grid: half resolution, sample centres at 2x + 0.5
+  const float cx = (sx + 0.5f) * 0.5f - 0.5f, cy = (sy + 0.5f) * 0.5f - 0.5f;
+  const int cw = a.src_w / 2, ch = a.src_h / 2;
+  const float u = nv12_sample(uv_plane, cw, ch, a.src_w, 2, 0, cx, cy) - 128.f;
+  const float v = nv12_sample(uv_plane, cw, ch, a.src_w, 2, 1, cx, cy) - 128.f;
+  const float yy = 1.164f * (yv - 16.f);
+  float r = yy + 1.596f * v;
+  float g = yy - 0.392f * u - 0.813f * v;
+  float b = yy + 2.017f * u;
+  r = fminf(fmaxf(r, 0.f), 255.f) * a.scale[0] + a.shift[0];
+  g = fminf(fmaxf(g, 0.f), 255.f) * a.scale[1] + a.shift[1];
+  b = fminf(fmaxf(b, 0.f), 255.f) * a.scale[2] + a.shift[2];
+  if (a.bf16) {
+    uint16_t* o = (uint16_t*)out + i * 8;
+    *(uint4*)o = make_uint4(nv12_bf_bits(r) | (nv12_bf_bits(g) << 16), nv12_bf_bits(b), 0u, 0u);
+  } else {
+    *(float4*)((float*)out + i * 4) = make_float4(r, g, b, 0.f);
+  }
+}
+
 struct NormParams {
   float scale[3];   // 1 / (255 * std)
   float shift[3];   // -mean / std
@@ -427,6 +547,58 @@ int rnb_clipgen_video(void* out, int vid, const int* starts, int nclips, int F, 
   const long long threads = ((long long)nclips * F * H * W + 15) / 16;
   hipLaunchKernelGGL(clipgen_video_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                      stream, (uint8_t*)out, a, F, H, W);
+  return (int)hipGetLastError();
+}
+
+int rnb_nv12gen_video(void* out, int vid, const int* starts, int nclips, int F, int H, int W,
+                      hipStream_t stream) {
+  if (nclips <= 0) return 0;
+  if (nclips > CLIPGEN_MAX_CLIPS || H % 2 || W % 2) return -3;
+  ClipgenArgs a;
+  a.vid = vid;
+  a.nclips = nclips;
+  for (int i = 0; i < CLIPGEN_MAX_CLIPS; ++i) a.starts[i] = i < nclips ? starts[i] : 0;
+  const long long bytes = (long long)nclips * F * H * W * 3 / 2;
+  const long long threads = (bytes + 15) / 16;
+  hipLaunchKernelGGL(nv12gen_kernel<false>, dim3((unsigned)((threads + 255) / 256)), dim3(256),
+                     0, stream, (uint8_t*)out, a, (const int*)nullptr, (const int*)nullptr, F, H,
+                     W);
+  return (int)hipGetLastError();
+}
+
+// batched form (per-clip video id / start frame in device arrays: graph-capturable)
+int rnb_nv12gen(void* out, const int* vids, const int* starts, int nclips, int F, int H, int W,
+                hipStream_t stream) {
+  if (nclips <= 0) return 0;
+  if (H % 2 || W % 2) return -3;
+  ClipgenArgs a;
+  a.vid = 0;
+  a.nclips = nclips;
+  const long long bytes = (long long)nclips * F * H * W * 3 / 2;
+  const long long threads = (bytes + 15) / 16;
+  hipLaunchKernelGGL(nv12gen_kernel<true>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     stream, (uint8_t*)out, a, vids, starts, F, H, W);
+  return (int)hipGetLastError();
+}
+
+// nv12: [frames][H*3/2][W] bytes -> out: [frames][oh][ow][4] fp32 or [..][8] bf16
+int rnb_nv12_to_clip(const void* nv12, void* out, long long frames, int src_w, int src_h,
+                     int out_w, int out_h, const float* crop, const float* mean,
+                     const float* stdv, int bf16, hipStream_t stream) {
+  if (frames <= 0) return 0;
+  if (src_w % 2 || src_h % 2 || out_w <= 0 || out_h <= 0) return -2;
+  if (((uintptr_t)out & 15u) != 0) return -2;
+  Nv12ClipArgs a;
+  a.src_w = src_w; a.src_h = src_h; a.out_w = out_w; a.out_h = out_h;
+  a.crop_x = crop[0]; a.crop_y = crop[1]; a.crop_w = crop[2]; a.crop_h = crop[3];
+  for (int c = 0; c < 3; ++c) {
+    a.scale[c] = 1.0f / (255.0f * stdv[c]);
+    a.shift[c] = -mean[c] / stdv[c];
+  }
+  a.bf16 = bf16;
+  const long long npix = frames * out_w * out_h;
+  hipLaunchKernelGGL(nv12_clip_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0,
+                     stream, (const uint8_t*)nv12, out, npix, a);
   return (int)hipGetLastError();
 }
 

@@ -4,9 +4,11 @@ The reference decodes with NVVL's ``RnBLoader`` (ffmpeg demux + NVDEC + CUDA
 colour/resize kernels; reference model.py:116-158, README.md:42-110). On the
 MI355X pool there is neither a video decoder library (rocDecode is not
 installed) nor a dataset, so the default backend synthesises the decoder's
-output surface on the GPU with the ``clipgen_u8`` HIP kernel (deterministic
-pixels per (video, frame)), then runs the same ``preprocess`` HIP kernel a real
-decoder's output would go through. ``NpyDecoder`` is a real-I/O backend that
+output surfaces on the GPU -- NV12 frames at the source resolution, 340x256,
+deterministic per (video, frame) -- and runs the per-frame work a real
+decoder's output goes through in NVVL: colour conversion and scaling to
+112x112 (``nv12_to_clip`` HIP kernel). ``synthetic-rgb`` generates 112x112 RGB
+frames directly (``clipgen`` + ``preprocess``). ``NpyDecoder`` is a real-I/O backend that
 reads pre-decoded ``uint8 [frames, H, W, 3]`` ``.npy`` files (memory-mapped,
 so only the sampled frames are read) and uploads them.
 
@@ -52,11 +54,26 @@ class Decoder:
 
 
 class SyntheticDecoder(Decoder):
+    """Synthetic video source on the GPU.
+
+    ``source="nv12"`` (default): per video, the sampled frames are produced as
+    NV12 decoder surfaces at the source resolution (340x256, as Kinetics is
+    stored; ``nv12gen``) and then go through the same per-frame work NVVL
+    does after NVDEC: bilinear scaling to 112x112, BT.601 YUV -> RGB,
+    normalisation, written straight into the output (slot) layout
+    (``nv12_to_clip``). ``source="rgb"``: 112x112 RGB frames directly
+    (``clipgen`` + ``preprocess``; the round-1 loader)."""
+
     def __init__(self, device: torch.device, clip_length: int = 8, height: int = 112,
-                 width: int = 112, dtype=torch.bfloat16):
+                 width: int = 112, dtype=torch.bfloat16, source: str = "nv12",
+                 src_width: int = vops.SOURCE_W, src_height: int = vops.SOURCE_H):
+        if source not in ("nv12", "rgb"):
+            raise ValueError("unknown synthetic source %r" % (source,))
         self.device = device
         self.F, self.H, self.W = clip_length, height, width
         self.dtype = dtype
+        self.source = source
+        self.src_w, self.src_h = src_width, src_height
         self._surface = None
 
     def probe(self, path):
@@ -66,6 +83,8 @@ class SyntheticDecoder(Decoder):
         n = len(starts)
         if n == 0:
             return self.empty()
+        if self.source == "nv12":
+            return self._decode_nv12(vid, starts, out)
         surf = None
         if self.device.type == "cuda":
             # one reusable decoder surface: uses of it are ordered on the stream
@@ -75,6 +94,29 @@ class SyntheticDecoder(Decoder):
             surf = self._surface[:n]
         surf = vops.clipgen_video(vid, starts, self.F, self.H, self.W, self.device, out=surf)
         return vops.preprocess(surf, out=out, dtype=self.dtype)
+
+    def warmup(self, n: int) -> None:
+        for i in range(n):
+            self.decode(i, [0])
+
+    def _decode_nv12(self, vid, starts, out):
+        n = len(starts)
+        surf = None
+        if self.device.type == "cuda":
+            rows = self.src_h * 3 // 2
+            if self._surface is None or self._surface.shape[0] < n * self.F:
+                self._surface = torch.empty((max(n, 15) * self.F, rows, self.src_w),
+                                            dtype=torch.uint8, device=self.device)
+            surf = self._surface[:n * self.F]
+        surf = vops.nv12gen(int(vid), list(starts), self.F, self.src_h, self.src_w,
+                            self.device, out=surf)
+        C = vops.IN_CHANNELS_P_F32 if self.dtype == torch.float32 else vops.IN_CHANNELS_P
+        if out is None:
+            out = torch.empty((n, self.F, self.H, self.W, C), dtype=self.dtype,
+                              device=self.device)
+        vops.nv12_to_clip(surf, self.src_w, self.src_h, self.W, self.H, dtype=self.dtype,
+                          out=out)
+        return out
 
 
 class NpyDecoder(Decoder):
@@ -112,8 +154,10 @@ class NpyDecoder(Decoder):
 
 def make_decoder(backend: str, device: torch.device, clip_length=8, height=112, width=112,
                  dtype=torch.bfloat16) -> Decoder:
-    if backend == "synthetic":
-        return SyntheticDecoder(device, clip_length, height, width, dtype)
+    if backend in ("synthetic", "synthetic-nv12"):
+        return SyntheticDecoder(device, clip_length, height, width, dtype, source="nv12")
+    if backend == "synthetic-rgb":
+        return SyntheticDecoder(device, clip_length, height, width, dtype, source="rgb")
     if backend == "npy":
         return NpyDecoder(device, clip_length, height, width, dtype)
     if backend in ("rocdecode", "nvvl"):

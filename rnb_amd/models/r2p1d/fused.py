@@ -67,10 +67,23 @@ class Replica:
             raise ValueError("%d clips exceed the largest bucket %d" % (n, self.buckets[-1]))
         return self.buckets[i]
 
+    def _decode(self, bg: _BucketGraph):
+        """Decoder stage of the graph: fp32 runs NVVL's per-frame work on NV12
+        surfaces at 340x256 (as the pipeline loader does); the bf16 path keeps
+        the 112x112 generator + the stem's packed preprocess."""
+        F, H, W = CLIP_SHAPE
+        if self.dtype == torch.float32:
+            surf = vops.nv12gen(bg.meta[0], bg.meta[1], F, vops.SOURCE_H, vops.SOURCE_W,
+                                self.device)
+            vops.nv12_to_clip(surf, vops.SOURCE_W, vops.SOURCE_H, W, H, dtype=self.dtype,
+                              out=bg.frames)
+        else:
+            surf = vops.clipgen_u8(bg.meta[0], bg.meta[1], F, H, W)
+            vops.preprocess(surf, out=bg.frames, packed=self.packed, dtype=self.dtype)
+
     def _body(self, bg: _BucketGraph, b: int):
         F, H, W = CLIP_SHAPE
-        surf = vops.clipgen_u8(bg.meta[0], bg.meta[1], F, H, W)
-        vops.preprocess(surf, out=bg.frames, packed=self.packed, dtype=self.dtype)
+        self._decode(bg)
         logits = self.engine.forward(bg.frames, packed=self.packed)
         bg.logits = logits
         vops.video_reduce(logits, bg.offsets, sums=bg.sums)[1]
@@ -93,8 +106,7 @@ class Replica:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
                 F, H, W = CLIP_SHAPE
-                surf = vops.clipgen_u8(bg.meta[0], bg.meta[1], F, H, W)
-                vops.preprocess(surf, out=bg.frames, packed=self.packed, dtype=self.dtype)
+                self._decode(bg)
                 bg.logits = self.engine.forward(bg.frames, packed=self.packed)
                 _, bg.argmax = vops.video_reduce(bg.logits, bg.offsets, sums=bg.sums)
             self.stream.synchronize()
@@ -104,8 +116,7 @@ class Replica:
 
     def _run_eager(self, bg):
         F, H, W = CLIP_SHAPE
-        surf = vops.clipgen_u8(bg.meta[0], bg.meta[1], F, H, W)
-        vops.preprocess(surf, out=bg.frames, packed=self.packed, dtype=self.dtype)
+        self._decode(bg)
         logits = self.engine.forward(bg.frames, packed=self.packed)
         vops.video_reduce(logits, bg.offsets, sums=bg.sums)
 

@@ -61,7 +61,9 @@ class FusedSTConv:
     def supported(self, x_shape) -> bool:
         from .native import kernels
         N, T, H, W, C = x_shape
-        return C == 64 and kernels().conv21_supported(T, H, W)
+        # the N-aware check: past ~660 clips of 56x56x8 the 32-bit buffer
+        # offsets overflow and the two-kernel path must run instead
+        return C == 64 and kernels().conv21_fits(N, T, H, W, 64, 64)
 
     VARIANTS = (1, 0)     # conv21.hip: 1 = role-specialised 8 waves, 0 = 4 waves
 

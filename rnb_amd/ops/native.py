@@ -176,6 +176,19 @@ class Kernels:
                                           ctypes.POINTER(ctypes.c_int), ctypes.c_int,
                                           ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_void_p]
+        lib.rnb_nv12gen_video.argtypes = [ctypes.c_void_p, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p]
+        lib.rnb_nv12gen.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_void_p]
+        lib.rnb_nv12_to_clip.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.POINTER(ctypes.c_float),
+                                         ctypes.POINTER(ctypes.c_float),
+                                         ctypes.POINTER(ctypes.c_float), ctypes.c_int,
+                                         ctypes.c_void_p]
         lib.rnb_preprocess.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
                                        ctypes.POINTER(ctypes.c_float),
                                        ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
@@ -214,6 +227,7 @@ class Kernels:
         lib.rnb_conv21s_launch.argtypes = [ctypes.POINTER(Conv21Params), ctypes.c_void_p]
         lib.rnb_conv21s_launch.restype = ctypes.c_int
         lib.rnb_conv21_supported.argtypes = [ctypes.c_int] * 3
+        lib.rnb_conv21_fits.argtypes = [ctypes.c_int] * 6
         if lib.rnb_conv21_params_size() != ctypes.sizeof(Conv21Params):
             raise NativeUnavailable("Conv21Params layout mismatch: rebuild")
         if lib.rnb_temporal_params_size() != ctypes.sizeof(TemporalParams):
@@ -290,6 +304,11 @@ class Kernels:
     def conv21_supported(self, T: int, H: int, W: int) -> bool:
         return bool(self.lib.rnb_conv21_supported(T, H, W))
 
+    def conv21_fits(self, N: int, T: int, H: int, W: int, y_stride: int = 64,
+                    res_stride: int = 64) -> bool:
+        """Whole launch contract for N clips (buffer-offset limits included)."""
+        return bool(self.lib.rnb_conv21_fits(N, T, H, W, y_stride, res_stride))
+
     def temporal_lds_bytes(self, T: int, cin_p: int, cout_p: int) -> int:
         return self.lib.rnb_temporal_lds_bytes(T, cin_p, cout_p)
 
@@ -317,6 +336,23 @@ class Kernels:
         arr = (ctypes.c_int * max(1, len(starts)))(*starts)
         _check(self.lib.rnb_clipgen_video(out_ptr, int(vid), arr, len(starts), F, H, W,
                                           stream), "clipgen_video")
+
+    def nv12gen_video(self, out_ptr, vid, starts, F, H, W, stream):
+        arr = (ctypes.c_int * max(1, len(starts)))(*starts)
+        _check(self.lib.rnb_nv12gen_video(out_ptr, int(vid), arr, len(starts), F, H, W,
+                                          stream), "nv12gen_video")
+
+    def nv12gen(self, out_ptr, vids_ptr, starts_ptr, nclips, F, H, W, stream):
+        _check(self.lib.rnb_nv12gen(out_ptr, vids_ptr, starts_ptr, nclips, F, H, W, stream),
+               "nv12gen")
+
+    def nv12_to_clip(self, in_ptr, out_ptr, frames, src_w, src_h, out_w, out_h, crop, mean,
+                     std, bf16, stream):
+        c = (ctypes.c_float * 4)(*crop)
+        m = (ctypes.c_float * 3)(*mean)
+        s = (ctypes.c_float * 3)(*std)
+        _check(self.lib.rnb_nv12_to_clip(in_ptr, out_ptr, frames, src_w, src_h, out_w, out_h,
+                                         c, m, s, 1 if bf16 else 0, stream), "nv12_to_clip")
 
     def preprocess(self, in_ptr, out_ptr, npix, mean, std, stream):
         m = (ctypes.c_float * 3)(*mean)

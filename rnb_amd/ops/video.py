@@ -5,6 +5,7 @@ mirror (the mirrors are what the numerics tests compare the kernels with).
 """
 from __future__ import annotations
 
+import math
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -74,6 +75,127 @@ def clipgen_video(vid: int, starts, F: int, H: int, W: int, device,
                       torch.as_tensor(list(starts), dtype=torch.int32), F, H, W, out=out)
 
 
+# ---------------------------------------------------------------------------
+# NV12 decoder surfaces (VCN / NVDEC output format) -> normalised clips
+# ---------------------------------------------------------------------------
+SOURCE_W, SOURCE_H = 340, 256      # Kinetics-400 videos as usually stored
+
+
+def nv12_frame_bytes(W: int, H: int) -> int:
+    return W * H * 3 // 2
+
+
+def nv12gen(vids, starts, F: int, H: int, W: int, device,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Synthetic decoder surfaces: uint8 [n*F, H*3/2, W] NV12 frames (Y rows,
+    then interleaved UV rows), deterministic per (video, frame). ``vids`` may
+    be one id (start frames then go in kernel arguments) or a per-clip array."""
+    single = isinstance(vids, int)
+    n = len(starts)
+    shape = (n * F, H * 3 // 2, W)
+    if device.type == "cuda":
+        from .native import kernels
+        if out is None:
+            out = torch.empty(shape, dtype=torch.uint8, device=device)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        if single and n <= 32:
+            kernels().nv12gen_video(out.data_ptr(), vids, list(starts), F, H, W, stream)
+        else:
+            v = torch.full((n,), vids, dtype=torch.int32, device=device) if single else \
+                vids.to(device=device, dtype=torch.int32).contiguous()
+            st = starts if isinstance(starts, torch.Tensor) else \
+                torch.as_tensor(list(starts), dtype=torch.int32)
+            st = st.to(device=device, dtype=torch.int32).contiguous()
+            kernels().nv12gen(out.data_ptr(), v.data_ptr(), st.data_ptr(), n, F, H, W, stream)
+        return out
+    # CPU mirror of nv12gen_kernel
+    v = torch.full((n,), vids, dtype=torch.int64) if single else \
+        torch.as_tensor(vids, dtype=torch.int64).view(-1)
+    st = torch.as_tensor(list(starts) if not isinstance(starts, torch.Tensor) else starts,
+                         dtype=torch.int64).view(-1)
+    fr = (st.view(n, 1) + torch.arange(F).view(1, F)).reshape(-1)           # [n*F]
+    vv = v.view(n, 1).expand(n, F).reshape(-1)
+    ypix = torch.arange(H * W, dtype=torch.int64).view(1, -1)
+    y = _pixel_hash_torch(vv.view(-1, 1), fr.view(-1, 1), ypix, torch.zeros(1, dtype=torch.int64))
+    c = torch.arange(H * W // 2, dtype=torch.int64).view(1, -1)
+    uv = _pixel_hash_torch(vv.view(-1, 1), fr.view(-1, 1), c >> 1, 1 + (c & 1))
+    uv = (64 + (uv.to(torch.int64) >> 1)).to(torch.uint8)
+    res = torch.cat([y.view(-1, H, W), uv.view(-1, H // 2, W)], dim=1).contiguous()
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+def _norm32(mean, std):
+    """Normalisation constants as the kernels compute them (fp32 arithmetic)."""
+    m32 = torch.tensor(mean, dtype=torch.float32)
+    s32 = torch.tensor(std, dtype=torch.float32)
+    return torch.tensor(1.0, dtype=torch.float32) / (torch.tensor(255.0) * s32), -m32 / s32
+
+
+def _bilinear_torch(plane: torch.Tensor, sx: torch.Tensor, sy: torch.Tensor) -> torch.Tensor:
+    """plane [F, h, w] float; sample at (sy[:, None], sx[None, :]) with edge clamp."""
+    Fn, h, w = plane.shape
+    sx = sx.clamp(0, w - 1)
+    sy = sy.clamp(0, h - 1)
+    x0, y0 = sx.floor().long(), sy.floor().long()
+    x1, y1 = (x0 + 1).clamp(max=w - 1), (y0 + 1).clamp(max=h - 1)
+    fx, fy = (sx - x0.float()).view(1, 1, -1), (sy - y0.float()).view(1, -1, 1)
+    p00 = plane[:, y0][:, :, x0]
+    p01 = plane[:, y0][:, :, x1]
+    p10 = plane[:, y1][:, :, x0]
+    p11 = plane[:, y1][:, :, x1]
+    top = p00 + (p01 - p00) * fx
+    bot = p10 + (p11 - p10) * fx
+    return top + (bot - top) * fy
+
+
+def nv12_to_clip(nv12: torch.Tensor, src_w: int, src_h: int, out_w: int = 112,
+                 out_h: int = 112, crop=None, dtype=torch.float32, mean=KINETICS_MEAN,
+                 std=KINETICS_STD, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """NV12 frames [frames, H*3/2, W] -> normalised NDHWC frames
+    [frames, out_h, out_w, C] (fp32 C=4 / bf16 C=8): bilinear scaling of the
+    ``crop`` box (x, y, w, h; default the whole frame) with align_corners =
+    false, BT.601 video-range YUV -> RGB, clamp, Kinetics normalisation (what
+    NVVL does after NVDEC; reference model.py:123-125)."""
+    frames = nv12.shape[0]
+    crop = tuple(float(c) for c in (crop or (0, 0, src_w, src_h)))
+    C = IN_CHANNELS_P_F32 if dtype == torch.float32 else IN_CHANNELS_P
+    shape = (frames, out_h, out_w, C)
+    if nv12.is_cuda:
+        from .native import kernels
+        if out is None:
+            out = torch.empty(shape, dtype=dtype, device=nv12.device)
+        elif out.dtype != dtype or not out.is_contiguous() or out.numel() != math.prod(shape):
+            raise ValueError("nv12_to_clip: out must be contiguous %s %s" % (dtype, shape))
+        kernels().nv12_to_clip(nv12.data_ptr(), out.data_ptr(), frames, src_w, src_h, out_w,
+                               out_h, crop, mean, std, dtype == torch.bfloat16,
+                               torch.cuda.current_stream(nv12.device).cuda_stream)
+        return out
+    y_plane = nv12[:, :src_h].float()
+    uv = nv12[:, src_h:].float().view(frames, src_h // 2, src_w // 2, 2)
+    ox = torch.arange(out_w, dtype=torch.float32)
+    oy = torch.arange(out_h, dtype=torch.float32)
+    sx = crop[0] + (ox + 0.5) * (crop[2] / out_w) - 0.5
+    sy = crop[1] + (oy + 0.5) * (crop[3] / out_h) - 0.5
+    yv = _bilinear_torch(y_plane, sx, sy)
+    cx, cy = (sx + 0.5) * 0.5 - 0.5, (sy + 0.5) * 0.5 - 0.5
+    u = _bilinear_torch(uv[..., 0], cx, cy) - 128.0
+    v = _bilinear_torch(uv[..., 1], cx, cy) - 128.0
+    yy = 1.164 * (yv - 16.0)
+    rgb = torch.stack([yy + 1.596 * v, yy - 0.392 * u - 0.813 * v, yy + 2.017 * u], dim=-1)
+    scale, shift = _norm32(mean, std)
+    rgb = rgb.clamp(0.0, 255.0) * scale + shift
+    res = torch.zeros(shape, dtype=torch.float32)
+    res[..., :3] = rgb
+    res = res.to(dtype)
+    if out is not None:
+        out.copy_(res.view(out.shape))
+        return out
+    return res
+
+
 def preprocess(frames_u8: torch.Tensor, mean=KINETICS_MEAN, std=KINETICS_STD,
                out: Optional[torch.Tensor] = None, packed: bool = False,
                dtype=torch.bfloat16) -> torch.Tensor:
@@ -129,8 +251,11 @@ def _preprocess_f32(frames_u8, mean, std, out):
     # same arithmetic as the kernel, which contracts x * scale + shift into one
     # fp32 fma (single rounding): the product of a u8 and an fp32 scale is exact
     # in fp64, so the fp64 sum rounded once to fp32 is the fma's result
-    scale = torch.tensor([1.0 / (255.0 * s) for s in std], dtype=torch.float32)
-    shift = torch.tensor([-m / s for m, s in zip(mean, std)], dtype=torch.float32)
+    # (the launcher computes scale/shift in fp32 arithmetic, as here)
+    m32 = torch.tensor(mean, dtype=torch.float32)
+    s32 = torch.tensor(std, dtype=torch.float32)
+    scale = torch.tensor(1.0, dtype=torch.float32) / (torch.tensor(255.0) * s32)
+    shift = -m32 / s32
     res = torch.zeros(shape, dtype=torch.float32)
     res[..., :3] = (frames_u8.double() * scale.double() + shift.double()).float()
     if out is not None:

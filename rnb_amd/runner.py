@@ -117,7 +117,15 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             selector = None
         else:
             sel_cls = load_class(queue_selector_path)
-            selector = sel_cls(len(output_queues))
+            import inspect
+            try:
+                takes_queues = "queues" in inspect.signature(sel_cls).parameters
+            except (TypeError, ValueError):
+                takes_queues = False
+            # selectors that look at queue depths (ShortestQueueSelector) get
+            # the queues themselves; plain ones keep the reference signature
+            selector = (sel_cls(len(output_queues), queues=output_queues) if takes_queues
+                        else sel_cls(len(output_queues)))
         if shared_output_ring is not None:
             shared_output_ring.producer_attach(device)
         # consumer-side batching ("B" of RnB inside the consumer): the model

@@ -20,10 +20,12 @@ def main():
     ap.add_argument("--clips", type=int, default=64)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--config", type=int, default=None)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    eng = R2P1DEngine(build_network(1, 5, depth=args.depth), dev, backend="hip")
-    x = torch.randn(eng.input_shape(args.clips), device=dev).to(torch.bfloat16)
+    eng = R2P1DEngine(build_network(1, 5, depth=args.depth), dev, backend="hip",
+                      dtype=args.dtype)
+    x = torch.randn(eng.input_shape(args.clips), device=dev).to(eng.dtype)
     x[..., 3:] = 0
     bufs = {"x": x}
     for op in eng.ops:

@@ -18,4 +18,4 @@ step() {  # step <name> <timeout> <cmd...>
 step build 600 python -m rnb_amd.build
 step pytest_gpu "${PYTEST_TIMEOUT:-900}" python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench "${BENCH_TIMEOUT:-600}" python bench.py --steps "${BENCH_STEPS:-10}" --warmup 2 --trace gpurun_out/bench_kernels.txt
+step bench "${BENCH_TIMEOUT:-900}" python bench.py --steps "${BENCH_STEPS:-10}" --warmup 2 --json-out gpurun_out/bench.json

@@ -27,8 +27,15 @@ if "SQ_WAVE_CYCLES" in vals:
         if k in vals:
             print("%s / WAVE_CYCLES = %.2f" % (k, vals[k] / w))
 if "SQ_VALU_MFMA_BUSY_CYCLES" in vals and "GRBM_GUI_ACTIVE" in vals:
-    # busy cycles are summed over SIMDs; 256 CUs x 4 SIMDs
-    print("MFMA busy / (GUI_ACTIVE x 1024 SIMDs) = %.2f"
-          % (vals["SQ_VALU_MFMA_BUSY_CYCLES"] / (vals["GRBM_GUI_ACTIVE"] * 1024.0)))
+    # SQ_VALU_MFMA_BUSY_CYCLES is summed over all 1024 SIMDs (256 CUs x 4);
+    # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS
+    # give-back), so the kernel's busy clock is GRBM_GUI_ACTIVE / 8. Round 1
+    # divided by GRBM_GUI_ACTIVE x 1024 and under-reported MFMA busy by 8x.
+    clk = vals["GRBM_GUI_ACTIVE"] / 8.0
+    print("MFMA busy per SIMD = BUSY / (GRBM_GUI_ACTIVE/8 x 1024) = %.2f"
+          % (vals["SQ_VALU_MFMA_BUSY_CYCLES"] / (clk * 1024.0)))
+    if "SQ_INSTS_MFMA" in vals and vals["SQ_INSTS_MFMA"]:
+        print("busy cycles per MFMA = %.1f"
+              % (vals["SQ_VALU_MFMA_BUSY_CYCLES"] / vals["SQ_INSTS_MFMA"]))
 if "SQ_WAIT_INST_LDS" in vals and "SQ_WAVE_CYCLES" in vals:
     print("SQ_WAIT_INST_LDS / WAVE_CYCLES = %.2f" % (vals["SQ_WAIT_INST_LDS"] / vals["SQ_WAVE_CYCLES"]))

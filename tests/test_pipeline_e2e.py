@@ -253,3 +253,32 @@ def test_ring_depth_plan_from_consumer_batching():
     spec = parse_pipeline(cfg)
     plan_ring_depths(spec, None, verbose=False)
     assert spec.steps[0].num_shared_tensors == 7
+
+
+def test_shortest_queue_selector_gets_the_queues(tmp_path):
+    """The runner hands queue-depth selectors their queues (round 1 built them
+    with the count only, so ShortestQueueSelector silently fell back to round
+    robin); both consumer groups receive work."""
+    cfg = {"video_path_iterator": IT, "defaults": SMALL, "pipeline": [
+        {"model": M + "R2P1DLoader", "queue_groups": [
+            {"gpus": [-1], "out_queues": [0, 1],
+             "queue_selector": "rnb_amd.selector.ShortestQueueSelector"}]},
+        {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [-1], "in_queue": 0},
+                                                       {"gpus": [-1], "in_queue": 1}]}]}
+    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "8", "-mi", "0")
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert res["ok"]
+    d = tmp_path / "logs" / res["job_id"]
+    rows = {f: len(open(d / f).read().splitlines()) - 1 for f in os.listdir(d)
+            if f.startswith("g")}
+    assert len(rows) == 2 and all(n > 0 for n in rows.values()), rows
+
+
+def test_conv21_fits_checks_the_clip_count():
+    from rnb_amd.ops import native
+    if not native.available():
+        pytest.skip("native library not built")
+    k = native.kernels()
+    assert k.conv21_fits(128, 8, 56, 56)
+    assert not k.conv21_fits(700, 8, 56, 56)       # 32-bit offsets would overflow
+    assert not k.conv21_fits(4, 8, 56, 57 + 64)    # too wide for the kernel

@@ -238,3 +238,24 @@ def test_host_ring_roundtrip():
         flag["n"] += 1
         return flag["n"] > 2
     assert ring.wait_free(1, abort) is False
+
+
+def test_nv12_mirror_equals_interpolate_of_planes():
+    """The NV12 -> clip CPU mirror (the HIP kernel's reference) is a bilinear
+    resize (F.interpolate, align_corners=False) of Y and of the half-res U/V
+    planes followed by BT.601 conversion and the Kinetics normalisation."""
+    import torch.nn.functional as F
+    from rnb_amd.ops import video as vops
+    nv = vops.nv12gen(3, [5], 2, 64, 96, torch.device("cpu"))      # 2 frames 96x64
+    got = vops.nv12_to_clip(nv, 96, 64, 24, 16)
+    y = nv[:, :64].float().unsqueeze(1)
+    uv = nv[:, 64:].float().view(2, 32, 48, 2).permute(0, 3, 1, 2)
+    yi = F.interpolate(y, size=(16, 24), mode="bilinear", align_corners=False)[:, 0]
+    uvi = F.interpolate(uv, size=(16, 24), mode="bilinear", align_corners=False)
+    u, v = uvi[:, 0] - 128, uvi[:, 1] - 128
+    yy = 1.164 * (yi - 16)
+    rgb = torch.stack([yy + 1.596 * v, yy - 0.392 * u - 0.813 * v, yy + 2.017 * u], -1)
+    scale, shift = vops._norm32(vops.KINETICS_MEAN, vops.KINETICS_STD)
+    ref = rgb.clamp(0, 255) * scale + shift
+    assert (got[..., :3] - ref).abs().max().item() < 1e-4
+    assert got.shape == (2, 16, 24, 4)
