@@ -60,7 +60,10 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pipeline", default="global",
-                    choices=["global", "aggressive", "whole", "rnb", "fused"])
+                    choices=["global", "aggressive", "whole", "rnb", "two-stage", "segment",
+                             "fused"])
+    ap.add_argument("--segments", type=int, default=None,
+                    help="(segment) segments per video (default min(4, GPUs), >= 2)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--depth", type=int, default=34)
     ap.add_argument("--videos-per-step", type=int, default=256,
@@ -130,6 +133,28 @@ def pipeline_config(args, n_gpus: int) -> dict:
                                    {"gpus": gpus, "in_queue": 1, "out_queues": [0]}]},
                  dict(runner, max_batch_videos=1,
                       queue_groups=[{"gpus": runner_gpus, "in_queue": 0}])]
+    elif args.pipeline == "two-stage":
+        # BASELINE config #3: loader GPU -> model GPU over RCCL send/recv (per
+        # pair of GPUs; RCCL allows one rank per GPU, so one process each)
+        if n_gpus < 2 or n_gpus % 2:
+            raise SystemExit("two-stage needs an even number of GPUs (pairs)")
+        pairs = [(2 * k, 2 * k + 1) for k in range(n_gpus // 2)]
+        steps = [{"model": LOADER, "transport": "rccl",
+                  "queue_groups": [{"gpus": [a], "out_queues": [k]}
+                                   for k, (a, _) in enumerate(pairs)]},
+                 dict(runner, queue_groups=[{"gpus": [b], "in_queue": k}
+                                            for k, (_, b) in enumerate(pairs)])]
+    elif args.pipeline == "segment":
+        # BASELINE config #4 (reference config/r2p1d-segment.json): every video
+        # is split into S segments that runners on any GPU take (peer copies
+        # over xGMI), re-joined by the aggregator on the CPU
+        seg = args.segments or max(2, min(4, n_gpus))
+        steps = [{"model": LOADER, "num_segments": seg,
+                  "queue_groups": [{"gpus": loader_gpus, "out_queues": [0]}]},
+                 dict(runner, queue_groups=[{"gpus": runner_gpus, "in_queue": 0,
+                                             "out_queues": [0]}]),
+                 {"model": "rnb_amd.models.r2p1d.model.R2P1DAggregator", "aggregate": seg,
+                  "queue_groups": [{"gpus": [-1], "in_queue": 0}]}]
     else:
         raise ValueError(args.pipeline)
     if args.slots:

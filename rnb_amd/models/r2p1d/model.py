@@ -326,7 +326,14 @@ class R2P1DSingleStep(RunnerModel):
 
 
 class R2P1DAggregator(RunnerModel):
-    """Sums clip logits per video; re-joins ``aggregate`` segments by id."""
+    """Sums clip logits per video; re-joins ``aggregate`` segments by id.
+
+    Accepts a single request's rows or a batch (``TimeCardList``, e.g. from a
+    batching runner upstream): a batch is split per request by the rows each
+    one brought (``extra["rows"]``, set by the gathering runner) or, for whole
+    videos, by their clip counts. Segments of one video may arrive in
+    different batches; a video is emitted once all ``aggregate`` segments
+    arrived (reference model.py:238-285, with batching added)."""
 
     def __init__(self, device, aggregate=1, **unused):
         super().__init__(device)
@@ -339,28 +346,41 @@ class R2P1DAggregator(RunnerModel):
     def __call__(self, tensors, non_tensors, time_card):
         tensor = tensors[0]
         if isinstance(time_card, TimeCardList):
-            # a batch of whole videos: split rows by each card's clip count
-            outs, row = [], 0
-            for tc in time_card.time_cards:
-                n = tc.num_clips if tc.num_clips is not None else 1
-                outs.append(int(self._sum(tensor[row:row + n]).argmax()) if n else -1)
+            cards = time_card.time_cards
+            arr = tensor.detach().float().cpu().numpy()
+            parts, row = [], 0
+            for tc in cards:
+                n = tc.extra.get("rows")
+                if n is None:
+                    n = tc.num_clips if tc.num_clips is not None else 1
+                parts.append(arr[row:row + n])
                 row += n
-            return None, outs, time_card
-        result = self._sum(tensor) if tensor.shape[0] else \
-            np.zeros(tensor.shape[1:], dtype=np.float32)
-        if self.aggregate == 1:
-            return None, int(result.argmax()), time_card
-        prev = self.results.get(time_card.id)
-        if prev is None:
-            self.results[time_card.id] = (result, [time_card])
+        else:
+            cards = [time_card]
+            parts = [tensor.detach().float().cpu().numpy()]
+        done_cards, outs = [], []
+        for tc, part in zip(cards, parts):
+            result = part.sum(axis=0) if part.shape[0] else \
+                np.zeros(tensor.shape[1:], dtype=np.float32)
+            if self.aggregate == 1:
+                done_cards.append(tc)
+                batched = isinstance(time_card, TimeCardList)
+                outs.append(int(result.argmax()) if part.shape[0] or not batched else -1)
+                continue
+            prev = self.results.get(tc.id)
+            total = result if prev is None else prev[0] + result
+            got = [tc] if prev is None else prev[1] + [tc]
+            if len(got) < self.aggregate:
+                self.results[tc.id] = (total, got)
+                continue
+            del self.results[tc.id]
+            done_cards.append(TimeCard.merge(got))
+            outs.append(int(total.argmax()))
+        if not done_cards:
             return None, None, None
-        total = prev[0] + result
-        cards = prev[1] + [time_card]
-        if len(cards) < self.aggregate:
-            self.results[time_card.id] = (total, cards)
-            return None, None, None
-        del self.results[time_card.id]
-        return None, int(total.argmax()), TimeCard.merge(cards)
+        if not isinstance(time_card, TimeCardList):
+            return None, outs[0], done_cards[0]
+        return None, outs, TimeCardList(done_cards)
 
     def input_shape(self):
         return ((DEFAULT_MAX_CLIPS, 400),)

@@ -11,8 +11,8 @@ bridges that with a *claim handshake* (SURVEY.md §7.4 item 3):
 2. the consumer that dequeues it posts ``(slot, my_rank)`` on the ring's claim
    queue and immediately posts ``recv`` from the producer's rank;
 3. the producer's sender thread pops claims in order and issues ``send`` of
-   the slot's valid rows to the claimer, waits for completion, then frees the
-   slot.
+   the slot's valid rows to the claimer (several claims per batched group),
+   waits for completion with a timeout, then frees the slot.
 
 Per (src, dst) pair the claims are served in the order the consumer posted
 them, so sends and receives match. All participating runners form one
@@ -53,6 +53,9 @@ def init_dist(info: Optional[DistInfo], device: torch.device) -> None:
         kwargs["device_id"] = device
     dist.init_process_group(info.backend, store=store, rank=info.rank,
                             world_size=info.world_size, **kwargs)
+    # one collective first: batched point-to-point groups may then involve
+    # only the two peers of an edge (torch.distributed.batch_isend_irecv)
+    dist.barrier()
     _state.update(rank=info.rank, world=info.world_size, backend=info.backend)
 
 
@@ -72,7 +75,32 @@ def my_rank() -> int:
     return _state["rank"]
 
 
+RCCL_TIMEOUT_ENV = "RNB_RCCL_TIMEOUT_S"
+MAX_CLAIMS_PER_BATCH = 16
+
+
+def _timeout():
+    from datetime import timedelta
+    return timedelta(seconds=float(os.environ.get(RCCL_TIMEOUT_ENV, "120")))
+
+
 class RcclRing(RingBase):
+    """Slots on the producer GPU, payload moved by RCCL point-to-point.
+
+    * The producer's slot write is ordered on the GPU: the copy (or the
+      model's direct write) is followed by a "written" event; the sender
+      thread's stream waits on that event, so the producer never blocks.
+    * The sender thread drains up to 16 claims at a time and issues their
+      sends as one ``batch_isend_irecv`` group (one NCCL group launch); each
+      completion is awaited with a timeout (``RNB_RCCL_TIMEOUT_S``, default
+      120 s) and the slot is freed only after its send completed.
+    * The consumer posts its claim and its ``irecv``s together and waits with
+      the same timeout: a dead or stuck sender makes the consumer raise (the
+      launcher's watchdog then aborts the job with CHILD_FAILED) instead of
+      hanging in ``recv``. A sender-side failure is reported on the producer's
+      next ``write`` and by ``raise_if_failed``.
+    """
+
     kind = "rccl"
 
     def __init__(self, ctx, shapes, dtypes, num_slots, name, producer_gpu):
@@ -80,6 +108,7 @@ class RcclRing(RingBase):
         self.claims = ctx.Queue()
         self.producer_rank = None          # assigned by the launcher
         self._slots = None
+        self._written = None
         self._thread = None
         self._stop = None
         self._error = None
@@ -87,6 +116,7 @@ class RcclRing(RingBase):
     def __getstate__(self):
         st = dict(self.__dict__)
         st["_slots"] = None
+        st["_written"] = None
         st["_thread"] = None
         st["_stop"] = None
         return st
@@ -97,6 +127,8 @@ class RcclRing(RingBase):
         self._slots = [tuple(torch.empty(s, dtype=d, device=device)
                              for s, d in zip(self.shapes, self.dtypes))
                        for _ in range(self.num_slots)]
+        if device.type == "cuda":
+            self._written = [torch.cuda.Event() for _ in range(self.num_slots)]
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._serve, name="rccl-send-" + self.name,
                                         daemon=True)
@@ -104,7 +136,10 @@ class RcclRing(RingBase):
 
     def _serve(self):
         import torch.distributed as dist
-        stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        cuda = self.device.type == "cuda"
+        if cuda:
+            torch.cuda.set_device(self.device)
+        stream = torch.cuda.Stream(self.device) if cuda else None
         ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
         with ctx:
             while not self._stop.is_set():
@@ -114,21 +149,41 @@ class RcclRing(RingBase):
                     continue
                 if claim is None:
                     break
-                idx, dst = claim
+                batch = [claim]
+                while len(batch) < MAX_CLAIMS_PER_BATCH:
+                    try:
+                        nxt = self.claims.get_nowait()
+                    except queue.Empty:
+                        break
+                    if nxt is None:
+                        self._stop.set()
+                        break
+                    batch.append(nxt)
                 try:
-                    for t, rows in zip(self._slots[idx], self.valid_rows(idx)):
-                        if rows:
-                            dist.send(t[:rows], dst)
+                    ops = []
+                    for idx, dst in batch:
+                        if cuda:
+                            stream.wait_event(self._written[idx])
+                        for t, rows in zip(self._slots[idx], self.valid_rows(idx)):
+                            if rows:
+                                ops.append(dist.P2POp(dist.isend, t[:rows], dst))
+                    works = dist.batch_isend_irecv(ops) if ops else []
+                    for w in works:
+                        w.wait(_timeout())
                     if stream is not None:
-                        stream.synchronize()
+                        stream.synchronize()     # send buffers free for reuse
                 except Exception as err:  # surfaced on the producer's next write
                     self._error = err
                     break
-                self.events[idx].set()
+                for idx, _ in batch:
+                    self.events[idx].set()
+
+    def raise_if_failed(self):
+        if self._error is not None:
+            raise RuntimeError("RCCL sender of ring %s failed: %s" % (self.name, self._error))
 
     def write(self, idx, tensors):
-        if self._error is not None:
-            raise RuntimeError("RCCL sender failed: %s" % self._error)
+        self.raise_if_failed()
         rows = []
         for dst, src in zip(self._slots[idx], tensors):
             b = src.shape[0]
@@ -138,8 +193,9 @@ class RcclRing(RingBase):
             if b:
                 dst[:b].copy_(src)
             rows.append(b)
-        if self.device.type == "cuda":
-            torch.cuda.current_stream(self.device).synchronize()
+        if self._written is not None:
+            # GPU-ordered: the sender's stream waits on this event
+            self._written[idx].record(torch.cuda.current_stream(self.device))
         self._set_valid(idx, rows)
         return self._publish(idx)
 
@@ -157,12 +213,15 @@ class RcclRing(RingBase):
     def read_into(self, idx, placeholders, descriptor=None):
         import torch.distributed as dist
         src = self.producer_rank if descriptor is None else descriptor
-        self.claims.put((idx, my_rank()))
-        out = []
+        ops, out = [], []
         for ph, rows in zip(placeholders, self.valid_rows(idx)):
             if rows:
-                dist.recv(ph[:rows], src)
+                ops.append(dist.P2POp(dist.irecv, ph[:rows], src))
             out.append(ph[:rows])
+        self.claims.put((idx, my_rank()))
+        works = dist.batch_isend_irecv(ops) if ops else []
+        for w in works:
+            w.wait(_timeout())
         if placeholders and placeholders[0].is_cuda:
             torch.cuda.current_stream(placeholders[0].device).synchronize()
         return out

@@ -357,6 +357,8 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                     r = rows_of(sig)
                     pull(sig, tuple(d[off:off + r] for d in dst))
                     off += r
+                    if not isinstance(tc, TimeCardList):
+                        tc.extra["rows"] = r     # where this item's rows end
                     cards.extend(cards_of(tc))
                     nts.append(nt)
                 tensor_inputs = tuple(d[:rows] for d in dst)

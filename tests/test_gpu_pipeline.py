@@ -83,10 +83,10 @@ def test_rnb_batcher_into_slot_gpu(tmp_path):
     assert res["ok"]
 
 
-def _ipc_producer(ring, q, n, delay_cycles):
+def _ipc_producer(ring, q, n, delay_cycles, dev_idx=0):
     import torch
-    torch.cuda.set_device(0)
-    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda:%d" % dev_idx)
     s = torch.cuda.Stream(dev)
     with torch.cuda.stream(s):
         ring.producer_attach(dev)

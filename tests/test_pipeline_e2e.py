@@ -282,3 +282,34 @@ def test_conv21_fits_checks_the_clip_count():
     assert k.conv21_fits(128, 8, 56, 56)
     assert not k.conv21_fits(700, 8, 56, 56)       # 32-bit offsets would overflow
     assert not k.conv21_fits(4, 8, 56, 57 + 64)    # too wide for the kernel
+
+
+def test_segments_through_batching_runner_rejoined_by_aggregator(tmp_path):
+    """Segment parallelism with consumer-side batching: segments of different
+    videos share a runner call; the aggregator splits the batch by the rows
+    each segment brought and re-joins a video's segments by id."""
+    cfg = {"video_path_iterator": IT, "defaults": SMALL, "pipeline": [
+        {"model": M + "R2P1DLoader", "num_segments": 2,
+         "queue_groups": [{"gpus": [-1], "out_queues": [0]}]},
+        {"model": M + "R2P1DRunner", "max_clips": 8, "max_batch_videos": 4,
+         "queue_groups": [{"gpus": [-1, -1], "in_queue": 0, "out_queues": [0]}]},
+        {"model": M + "R2P1DAggregator", "aggregate": 2,
+         "queue_groups": [{"gpus": [-1], "in_queue": 0}]}]}
+    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "6", "-mi", "0")
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert res["ok"] and res["videos_done"] == 6
+
+
+def test_bench_pipeline_configs_parse():
+    """Every bench.py topology is a valid benchmark.py pipeline config."""
+    import importlib.util
+    from rnb_amd.config import parse_pipeline
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    for pipe in ("global", "aggressive", "whole", "rnb", "two-stage", "segment"):
+        for n in (2, 8):
+            args = bench.parse_args(["--gpus", str(n), "--pipeline", pipe])
+            cfg = bench.pipeline_config(args, n)
+            sp = parse_pipeline(cfg)
+            assert sp.gpus_used() == list(range(n)), (pipe, n)

@@ -42,3 +42,49 @@ def test_rccl_rejects_same_gpu_edge(tmp_path):
     os.environ.pop("RNB_RCCL_BACKEND", None)
     with pytest.raises(ConfigError, match="different GPUs"):
         _assign_rccl_ranks(spec, QT(ring), "job")
+
+
+def _rccl_timeout_rank(rank, store_path, ring, out_q):
+    import os
+    os.environ["RNB_RCCL_TIMEOUT_S"] = "2"
+    import torch
+    from rnb_amd.parallel.rccl_channel import DistInfo, init_dist, shutdown_dist
+    init_dist(DistInfo(rank, 2, store_path, "gloo"), torch.device("cpu"))
+    try:
+        if rank == 0:
+            # producer publishes a slot but its sender never serves the claim
+            ring.producer_rank = 0
+            ring._set_valid(0, [1])
+            ring._publish(0)
+            import time
+            time.sleep(6)
+            out_q.put(("producer", "ok"))
+        else:
+            ring.producer_rank = 0
+            ph = [torch.zeros((1, 2))]
+            try:
+                ring.read_into(0, ph, 0)
+                out_q.put(("consumer", "returned"))
+            except Exception as err:          # the timeout, not a hang
+                out_q.put(("consumer", type(err).__name__))
+    finally:
+        shutdown_dist()
+
+
+def test_rccl_recv_times_out_instead_of_hanging(tmp_path):
+    """A consumer whose sender never sends raises after RNB_RCCL_TIMEOUT_S
+    (round 1's blocking dist.recv would hang the runner forever)."""
+    import multiprocessing as mp
+    import torch
+    from rnb_amd.parallel.rccl_channel import RcclRing
+    ctx = mp.get_context("spawn")
+    ring = RcclRing(ctx, ((1, 2),), (torch.float32,), 2, "to", -1)
+    q = ctx.Queue()
+    store = str(tmp_path / "store")
+    procs = [ctx.Process(target=_rccl_timeout_rank, args=(r, store, ring, q)) for r in (0, 1)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=60) for _ in range(2))
+    for p in procs:
+        p.join(30)
+    assert got["consumer"] != "returned", got
