@@ -65,12 +65,16 @@ def parse_args(argv=None):
     ap.add_argument("--segments", type=int, default=None,
                     help="(segment) segments per video (default min(4, GPUs), >= 2)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--bn", default="eval", choices=["eval", "batch"],
+                    help="eval: BatchNorm folded into the convs (inference numerics); "
+                         "batch: the reference's training-mode BN, statistics per video "
+                         "(fp32 only, eager: no HIP graphs)")
     ap.add_argument("--depth", type=int, default=34)
     ap.add_argument("--videos-per-step", type=int, default=256,
                     help="videos arriving per GPU per step")
-    ap.add_argument("--replicas", type=int, default=3,
+    ap.add_argument("--replicas", type=int, default=2,
                     help="R(2+1)D runner processes per GPU (the R of RnB)")
-    ap.add_argument("--loaders", type=int, default=3, help="loader processes per GPU")
+    ap.add_argument("--loaders", type=int, default=2, help="loader processes per GPU")
     ap.add_argument("--video-batch", type=int, default=64,
                     help="max videos per model invocation (consumer-side batching)")
     ap.add_argument("--clips-per-batch", type=int, default=128,
@@ -106,7 +110,7 @@ def pipeline_config(args, n_gpus: int) -> dict:
     loader_gpus = [g for g in gpus for _ in range(args.loaders)]
     runner_gpus = [g for g in gpus for _ in range(args.replicas)]
     defaults = {"depth": args.depth, "dtype": args.dtype,
-                "autotune": not args.no_autotune}
+                "autotune": not args.no_autotune, "bn_mode": args.bn}
     if args.pipeline == "global":
         steps = [{"model": LOADER, "queue_groups": [{"gpus": loader_gpus, "out_queues": [0]}]},
                  dict(runner, queue_groups=[{"gpus": runner_gpus, "in_queue": 0}])]
@@ -169,7 +173,7 @@ def run_pipeline(args, world: int) -> dict:
     root = os.path.dirname(os.path.abspath(__file__))
     out_dir = os.path.join(root, "logs", "bench")
     os.makedirs(out_dir, exist_ok=True)
-    name = "bench-%s-%s-%dgpu" % (args.pipeline, args.dtype, args.gpus)
+    name = "bench-%s-%s-%s-%dgpu" % (args.pipeline, args.dtype, args.bn, args.gpus)
     cfg_path = os.path.join(out_dir, name + ".json")
     with open(cfg_path, "w") as f:
         json.dump(pipeline_config(args, args.gpus), f, indent=1)
@@ -239,7 +243,10 @@ def main(argv=None) -> int:
                        "parallelism": "rnb pipeline: %d loader + %d runner processes per GPU"
                                       % (args.loaders, args.replicas),
                        "pipeline": args.pipeline, "launcher_config": res.get("config_path"),
-                       "bn": "eval (folded, fp64 fold)", "clip": "8x112x112",
+                       "bn": ("eval (folded into the convs in fp64)" if args.bn == "eval" else
+                              "batch (training-mode BN as the reference, per-video "
+                              "statistics)"),
+                       "clip": "8x112x112",
                        "clips_dist": "1 w.p. 10/11, 15 w.p. 1/11",
                        "max_batch_videos": args.video_batch,
                        "clips_per_batch": args.clips_per_batch,

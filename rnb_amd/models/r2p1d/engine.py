@@ -251,9 +251,13 @@ class R2P1DEngine:
 
     # -------------------------------------------------------------- forward
     def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
-                packed: bool = False) -> torch.Tensor:
-        """x: NDHWC bf16 boundary tensor (or NCDHW fp32 for backend=module);
-        with ``packed``, the stem's pair-packed input (``input_shape(n, True)``)."""
+                packed: bool = False, clip_offsets=None) -> torch.Tensor:
+        """x: NDHWC boundary tensor (or NCDHW fp32 for backend=module); with
+        ``packed``, the stem's pair-packed input (``input_shape(n, True)``).
+        ``clip_offsets`` (bn_mode='batch'): clip ranges of the videos in the
+        batch, [0, n1, n1+n2, ..., N]; every video's BatchNorms use that
+        video's own statistics, as the reference's one-video forwards do
+        (default: the whole batch is one video)."""
         if packed and not self.accepts_packed_input:
             raise ValueError("this engine's first op does not take a packed input")
         if self.backend == "module":
@@ -270,6 +274,14 @@ class R2P1DEngine:
                                device=x.device)
         hip = self.backend == "hip"
         bufs: Dict[str, torch.Tensor] = {"x": x}
+        coffs = None
+        if self.bn_mode == "batch" and clip_offsets is not None:
+            clip_offsets = [int(o) for o in clip_offsets]
+            if clip_offsets[0] != 0 or clip_offsets[-1] != x.shape[0]:
+                raise ValueError("clip_offsets must span [0, %d]" % x.shape[0])
+            if hip:
+                coffs = torch.tensor(clip_offsets, dtype=torch.int32).to(x.device,
+                                                                          non_blocking=True)
         skip = False
         free_after = self._free_after
         for i, op in enumerate(self.ops):
@@ -291,10 +303,18 @@ class R2P1DEngine:
             if op.bn is not None:
                 if hip:
                     y = op.layer.forward_hip(src, None)
-                    y = op.bn.forward_hip(y, res, op.bn_relu, out=y)
+                    seg = rows = None
+                    if coffs is not None:
+                        thw = y.shape[1] * y.shape[2] * y.shape[3]
+                        seg = coffs * thw
+                        rows = [(b - a) * thw for a, b in zip(clip_offsets[:-1],
+                                                              clip_offsets[1:])]
+                    y = op.bn.forward_hip(y, res, op.bn_relu, out=y, segments=seg,
+                                          seg_rows=rows)
                 else:
                     y = op.layer.forward_torch(src, None, out_dtype=self.dtype)
-                    y = op.bn.forward_torch(y, res, op.bn_relu, out_dtype=self.dtype)
+                    y = op.bn.forward_torch(y, res, op.bn_relu, out_dtype=self.dtype,
+                                            clip_offsets=clip_offsets)
             elif packed and i == 0:
                 y = (op.layer.forward_hip(src, res, prepacked=True) if hip
                      else op.layer.forward_torch(src, res, prepacked=True))

@@ -134,6 +134,7 @@ class R2P1DRunner(RunnerModel):
         self.start_index, self.end_index = start_index, end_index
         self.max_clips = int(max_clips)
         self.dtype = _dtype(dtype)
+        self.bn_mode = bn_mode
         self.max_batch_videos = int(max_batch_videos)
         self.batch_wait_s = float(batch_wait_ms) / 1000.0
         buckets = None
@@ -200,7 +201,19 @@ class R2P1DRunner(RunnerModel):
             y = self.engine.replay(x.shape[0])
         else:
             self._gather_ptr = None
-            y = self.engine(_to_boundary(x, self.start_index, self.dtype))
+            x = _to_boundary(x, self.start_index, self.dtype)
+            if self.bn_mode == "batch" and isinstance(time_card, TimeCardList) \
+                    and x.shape[0] > 0:
+                # a batch of several videos: each keeps its own BN statistics
+                offs = [0]
+                for tc in time_card.time_cards:
+                    n = tc.extra.get("rows")
+                    offs.append(offs[-1] + int(n if n is not None else (tc.num_clips or 0)))
+                if offs[-1] != x.shape[0]:
+                    offs = None
+                y = self.engine.forward(x, clip_offsets=offs)
+            else:
+                y = self.engine(x)
         return (y,), non_tensors, time_card
 
 

@@ -1,4 +1,4 @@
-"""Training-mode BatchNorm on NDHWC bf16 activations (reference BN numerics).
+"""Training-mode BatchNorm on NDHWC activations (reference BN numerics).
 
 The reference never calls ``.eval()``, so every BatchNorm3d
 normalises with the statistics of the batch it is given and updates its
@@ -43,8 +43,62 @@ class BatchNormBatch:
         self.running_mean.mul_(1 - m).add_(self.mean[:c], alpha=m)
         self.running_var.mul_(1 - m).add_(unbiased, alpha=m)
 
+    def _update_segments(self, mean: torch.Tensor, var: torch.Tensor, rows) -> None:
+        """Running statistics after one forward per segment, in order (what
+        the reference's per-video forwards leave behind)."""
+        if not self.update_running:
+            return
+        c, m = self.channels, self.momentum
+        for s in range(mean.shape[0]):
+            M = int(rows[s])
+            if M < 2:
+                continue
+            self.running_mean.mul_(1 - m).add_(mean[s, :c], alpha=m)
+            self.running_var.mul_(1 - m).add_(var[s, :c] * (M / (M - 1.0)), alpha=m)
+
+    def forward_hip_f32(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,
+                        out: Optional[torch.Tensor] = None,
+                        segments: Optional[torch.Tensor] = None,
+                        seg_rows=None) -> torch.Tensor:
+        """fp32 tensor; ``segments``: device int32 [nseg+1] ROW offsets (each
+        segment -- one video -- gets its own statistics); default one segment."""
+        from .native import kernels
+        k = kernels()
+        N, T, H, W, Cs = y.shape
+        M, C = N * T * H * W, self.channels_p
+        z = out if out is not None else torch.empty_like(y)
+        if M == 0:
+            return z
+        if segments is None:
+            segments = torch.tensor([0, M], dtype=torch.int32, device=y.device)
+            seg_rows = [M]
+        nseg = segments.numel() - 1
+        need = k.bn_seg_scratch_floats(nseg, C)
+        if self._scratch is None or self._scratch.numel() < need:
+            self._scratch = torch.empty(need, dtype=torch.float32, device=y.device)
+        mean = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
+        var = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
+        stream = torch.cuda.current_stream(y.device).cuda_stream
+        k.bn_seg_stats_f32(y.data_ptr(), segments.data_ptr(), nseg, C, Cs,
+                           self._scratch.data_ptr(), mean.data_ptr(), var.data_ptr(), stream)
+        k.bn_seg_apply_f32(y.data_ptr(), z.data_ptr(),
+                           residual.data_ptr() if residual is not None else None,
+                           segments.data_ptr(), nseg, mean.data_ptr(), var.data_ptr(),
+                           self.gamma.data_ptr(), self.beta.data_ptr(), self.eps,
+                           1 if relu else 0, M, C, Cs, z.shape[-1],
+                           residual.shape[-1] if residual is not None else 0, stream)
+        self.mean, self.var = mean[-1], var[-1]
+        if seg_rows is not None:
+            self._update_segments(mean, var, seg_rows)
+        return z
+
     def forward_hip(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,
-                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    out: Optional[torch.Tensor] = None, segments=None,
+                    seg_rows=None) -> torch.Tensor:
+        if y.dtype == torch.float32:
+            return self.forward_hip_f32(y, residual, relu, out, segments, seg_rows)
+        if segments is not None and segments.numel() > 2:
+            raise NotImplementedError("per-video BN statistics are fp32 only")
         from .native import kernels
         k = kernels()
         N, T, H, W, Cs = y.shape
@@ -67,21 +121,33 @@ class BatchNormBatch:
         return z
 
     def forward_torch(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,
-                      out_dtype=torch.bfloat16) -> torch.Tensor:
+                      out_dtype=torch.bfloat16, clip_offsets=None) -> torch.Tensor:
+        """``clip_offsets``: per-video clip ranges [0, n1, n1+n2, ...]: each
+        video is normalised with its own statistics (default: one video)."""
         c = self.channels
         x = y[..., :c].float()
-        M = x.numel() // c
-        mean = x.reshape(-1, c).mean(0)
-        var = x.reshape(-1, c).var(0, unbiased=False)
-        self.mean[:c].copy_(mean.to(self.mean.device))
-        self.var[:c].copy_(var.to(self.var.device))
+        N = x.shape[0]
+        offs = [0, N] if clip_offsets is None else [int(o) for o in clip_offsets]
         g, b = self.gamma[:c].to(x.device), self.beta[:c].to(x.device)
-        z = (x - mean) * torch.rsqrt(var + self.eps) * g + b
+        z = torch.zeros_like(x)
+        for a0, a1 in zip(offs[:-1], offs[1:]):
+            xs = x[a0:a1].reshape(-1, c)
+            if xs.shape[0] == 0:
+                continue
+            mean = xs.mean(0)
+            var = xs.var(0, unbiased=False)
+            z[a0:a1] = (x[a0:a1] - mean) * torch.rsqrt(var + self.eps) * g + b
+            self.mean[:c].copy_(mean.to(self.mean.device))
+            self.var[:c].copy_(var.to(self.var.device))
+            if len(offs) > 2:
+                self._update(xs.shape[0])
+        M = x.numel() // c
         if residual is not None:
             z = z + residual[..., :c].float()
         if relu:
             z = torch.relu(z)
         full = torch.zeros(y.shape[:-1] + (y.shape[-1],), dtype=torch.float32, device=y.device)
         full[..., :c] = z
-        self._update(M)
+        if len(offs) <= 2:
+            self._update(M)
         return full.to(out_dtype)

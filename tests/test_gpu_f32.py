@@ -203,3 +203,48 @@ def test_clipgen_video_args_kernel_matches_clipgen_u8():
                         torch.tensor(starts, dtype=torch.int32, device=DEV), 8, 112, 112)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (True, False)])
+def test_bn_per_video_stats_f32_kernel_matches_torch(res, relu):
+    """Training-mode BN with one set of statistics per video of the batch
+    (csrc/bn_ops.hip bn_seg_*_f32) vs the per-video torch reference."""
+    from rnb_amd.ops.bn import BatchNormBatch
+    bn = torch.nn.BatchNorm3d(88)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    op = BatchNormBatch(bn, 88, DEV)
+    ref_op = BatchNormBatch(bn, 88, torch.device("cpu"))
+    y = torch.randn((5, 4, 14, 14, 88), device=DEV) * 3 + 1
+    r = torch.randn_like(y) if res else None
+    offs = [0, 1, 3, 5]
+    thw = 4 * 14 * 14
+    seg = torch.tensor([o * thw for o in offs], dtype=torch.int32, device=DEV)
+    z = op.forward_hip(y, r, relu, segments=seg, seg_rows=[2 * thw, 2 * thw, 2 * thw])
+    ref = ref_op.forward_torch(y.cpu(), r.cpu() if res else None, relu,
+                               out_dtype=torch.float32, clip_offsets=offs)
+    torch.cuda.synchronize()
+    err = (z.cpu() - ref).abs().max().item()
+    assert err < 1e-4 * ref.abs().max().item(), err
+
+
+def test_r34_f32_batch_bn_two_videos_match_module_per_video():
+    """bn_mode='batch' (the reference's training-mode BN) at fp32: a batch of
+    two videos through the HIP engine equals the fp32 module run once per
+    video, the reference's one-video forwards (model.py:82-84)."""
+    from rnb_amd.models.r2p1d.model import build_network
+    from rnb_amd.models.r2p1d.engine import R2P1DEngine
+    from rnb_amd.models.r2p1d.decoder import SyntheticDecoder
+    eng = R2P1DEngine(build_network(1, 5, depth=34, seed=2), DEV, backend="hip",
+                      bn_mode="batch", dtype="fp32")
+    mod = R2P1DEngine(build_network(1, 5, depth=34, seed=2), DEV, backend="module",
+                      bn_mode="batch", dtype="fp32")
+    dec = SyntheticDecoder(DEV, dtype=torch.float32)
+    x = torch.cat([dec.decode(1, [0, 40, 80]), dec.decode(2, [10, 60])])
+    with torch.no_grad():
+        y = eng.forward(x, clip_offsets=[0, 3, 5])
+        ref = torch.cat([mod.forward(x[:3]), mod.forward(x[3:])])
+    torch.cuda.synchronize()
+    rel = (y - ref).abs().max().item() / ref.abs().max().item()
+    assert rel <= 1e-3, rel
