@@ -17,6 +17,7 @@ batch size.
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -52,6 +53,33 @@ def f32_geom(cin: int, cout: int, kernel, stride, padding) -> ConvGeom:
                     padding=tuple(padding), align=F32_ALIGN)
 
 
+# fused Winograd F(2x2,3x3) kernels (csrc/conv_wino_f32.hip) as extra
+# config ids next to the implicit-GEMM tiles: 16 * TC output channels per block
+WINO_BASE = 1000
+WINO_TC = {WINO_BASE + 2: 2, WINO_BASE + 3: 3}
+
+# Winograd F(2x2, 3x3) transforms: U = G g G^T (host, fp64), V = B^T d B and
+# Y = A^T M A in the kernel
+_WINO_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
+
+
+def winograd_weights(w: torch.Tensor, cout: int, tc: int) -> torch.Tensor:
+    """[Cout, Cin, 1, 3, 3] folded weights -> the kernel's U layout
+    [Cin/16][n_cblocks][16 (x = 4i + j)][CT = 16 tc][16 channels], fp32,
+    output rows past Cout zero."""
+    co, ci = w.shape[:2]
+    g = w.detach().double().reshape(co, ci, 3, 3)
+    G = torch.tensor(_WINO_G, dtype=torch.float64)
+    u = torch.einsum("ik,ockl,jl->oc ij".replace(" ", ""), G, g, G)      # [co, ci, 4, 4]
+    ct = 16 * tc
+    nb = (cout + ct - 1) // ct
+    full = torch.zeros(nb * ct, ci, 16, dtype=torch.float64)
+    full[:co] = u.reshape(co, ci, 16)
+    # [nb, ct, ci/16, 16ch, 16x] -> [ci/16, nb, 16x, ct, 16ch]
+    t = full.reshape(nb, ct, ci // 16, 16, 16).permute(2, 0, 4, 1, 3)
+    return t.contiguous().float()
+
+
 class ConvLayerF32:
     """One folded fp32 conv (+ optional residual add and ReLU) of the plan."""
 
@@ -81,6 +109,40 @@ class ConvLayerF32:
         self.b_ref = bias.detach().float().to(device)
         self._config: Dict[Tuple[int, int, int, int], int] = {}
         self._ktab: Dict[Tuple[int, int, int], torch.Tensor] = {}
+        # Winograd F(2x2,3x3) for stride-1 1x3x3 convs with Cin % 16 == 0
+        self.wino_ok = (geom.kernel == (1, 3, 3) and geom.stride == (1, 1, 1)
+                        and geom.padding == (0, 1, 1) and geom.cin_p % 16 == 0
+                        and geom.cin == geom.cin_p)
+        self._wino_u: Dict[int, torch.Tensor] = {}
+
+    def wino_u(self, tc: int) -> torch.Tensor:
+        u = self._wino_u.get(tc)
+        if u is None:
+            u = self._wino_u[tc] = winograd_weights(self.w_ref.cpu(), self.geom.cout_p,
+                                                    tc).to(self.device)
+        return u
+
+    def candidates(self):
+        from .native import kernels
+        c = list(range(len(kernels().f32_configs)))
+        if self.wino_ok:
+            c += sorted(WINO_TC)
+        return c
+
+    def _launch_wino(self, x, y, residual, cid, stream):
+        from .native import WinoParams, kernels
+        tc = WINO_TC[cid]
+        g = self.geom
+        N, T, H, W, C = x.shape
+        p = WinoParams()
+        p.x, p.u, p.bias = x.data_ptr(), self.wino_u(tc).data_ptr(), self.bias.data_ptr()
+        p.res = residual.data_ptr() if residual is not None else None
+        p.y = y.data_ptr()
+        p.F, p.H, p.W, p.Cin = N * T, H, W, C
+        p.Cout, p.y_stride = g.cout_p, y.shape[-1]
+        p.res_stride = residual.shape[-1] if residual is not None else 0
+        p.relu = 1 if self.relu else 0
+        kernels().wino_f32(p, tc, stream.cuda_stream)
 
     # ------------------------------------------------------------------
     def out_shape(self, x_shape) -> Tuple[int, int, int, int, int]:
@@ -183,10 +245,16 @@ class ConvLayerF32:
             if cid is None:
                 N, T, H, W, _ = x_shape
                 cid = tuning.nearest(tkey, N * T * H * W)
-            if cid is None or cid >= len(_configs()):
+            if cid is not None and cid in WINO_TC and not self.wino_ok:
+                cid = None
+            if cid is not None and cid not in WINO_TC and cid >= len(_configs()):
+                cid = None
+            if cid is None:
                 N, T, H, W, _ = x_shape
                 To, Ho, Wo = self.geom.out_thw(T, H, W)
                 cid = self.heuristic_config(N * To * Ho * Wo)
+                if self.wino_ok and os.environ.get("RNB_WINOGRAD", "1") != "0":
+                    cid = WINO_BASE + (3 if self.geom.cout_p % 48 == 0 else 2)
             self._config[key] = cid
         return cid
 
@@ -194,6 +262,15 @@ class ConvLayerF32:
         from .native import kernels
         k = kernels()
         N = x.shape[0]
+        if cid in WINO_TC:
+            step = self.chunk_clips(x.shape, y.shape,
+                                    residual.shape[-1] if residual is not None else 0)
+            for n0 in range(0, N, step):
+                n1 = min(N, n0 + step)
+                self._launch_wino(x[n0:n1], y[n0:n1],
+                                  residual[n0:n1] if residual is not None else None, cid,
+                                  stream)
+            return
         step = self.chunk_clips(x.shape, y.shape,
                                 residual.shape[-1] if residual is not None else 0)
         for n0 in range(0, N, step):
@@ -207,13 +284,14 @@ class ConvLayerF32:
         from .native import kernels
         tkey = self._tune_key(x.shape, x.device)
         cached = tuning.get(tkey)
-        if cached is not None and cached < len(kernels().f32_configs):
+        if cached is not None and (cached < len(kernels().f32_configs) or
+                                   (cached in WINO_TC and self.wino_ok)):
             self._config[tuple(x.shape[:4])] = cached
             return cached
         y = torch.empty(self.out_shape(x.shape), dtype=torch.float32, device=x.device)
         stream = torch.cuda.current_stream(x.device)
         best, best_t = None, None
-        for cid in range(len(kernels().f32_configs)):
+        for cid in self.candidates():
             self._launch_all(x, y, residual, cid, stream)       # warm
             start = torch.cuda.Event(enable_timing=True)
             end = torch.cuda.Event(enable_timing=True)

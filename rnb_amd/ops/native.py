@@ -142,6 +142,21 @@ class Conv21Params(ctypes.Structure):
     ]
 
 
+class WinoParams(ctypes.Structure):
+    """Mirror of ``struct WinoParams`` in csrc/conv_wino_f32.hip."""
+    _fields_ = [
+        ("x", ctypes.c_void_p), ("u", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+        ("res", ctypes.c_void_p), ("y", ctypes.c_void_p),
+        ("F", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int), ("Cin", ctypes.c_int),
+        ("Cout", ctypes.c_int), ("y_stride", ctypes.c_int), ("res_stride", ctypes.c_int),
+        ("relu", ctypes.c_int), ("tiles_h", ctypes.c_int), ("tiles_w", ctypes.c_int),
+        ("n_tiles", ctypes.c_int), ("n_tblocks", ctypes.c_int), ("n_cblocks", ctypes.c_int),
+        ("x_bytes", ctypes.c_uint32), ("u_bytes", ctypes.c_uint32),
+        ("m_tw", ctypes.c_uint32), ("s_tw", ctypes.c_uint32),
+        ("m_th", ctypes.c_uint32), ("s_th", ctypes.c_uint32),
+    ]
+
+
 class TemporalParams(ctypes.Structure):
     """Mirror of ``struct TemporalParams`` in csrc/conv_temporal.hip."""
     _fields_ = [
@@ -264,6 +279,11 @@ class Kernels:
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_void_p]
+        lib.rnb_wino_f32_launch.argtypes = [ctypes.POINTER(WinoParams), ctypes.c_int,
+                                            ctypes.c_void_p]
+        lib.rnb_wino_f32_launch.restype = ctypes.c_int
+        if lib.rnb_wino_params_size() != ctypes.sizeof(WinoParams):
+            raise NativeUnavailable("WinoParams layout mismatch: rebuild")
         if lib.rnb_conv_f32_params_size() != ctypes.sizeof(ConvParams):
             raise NativeUnavailable("ConvF32Params layout mismatch: rebuild")
         self.f32_configs = []      # (pixel tile, channel tile) per fp32 config id
@@ -287,6 +307,10 @@ class Kernels:
     def conv_f32(self, params: ConvParams, config_id: int, stream: int) -> None:
         _check(self.lib.rnb_conv_f32_launch(ctypes.byref(params), config_id, stream),
                "conv_f32 (config %d)" % config_id)
+
+    def wino_f32(self, params: "WinoParams", tc: int, stream: int) -> None:
+        _check(self.lib.rnb_wino_f32_launch(ctypes.byref(params), tc, stream),
+               "conv_wino_f32 (TC %d)" % tc)
 
     def preprocess_f32(self, in_ptr, out_ptr, npix, mean, std, stream):
         m = (ctypes.c_float * 3)(*mean)

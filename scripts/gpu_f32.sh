@@ -14,5 +14,5 @@ step() {
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-step f32_tests 600 python -u -m pytest tests/test_gpu_f32.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
+step f32_tests 600 python -u -m pytest tests/test_gpu_f32.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
 TAILN=60 step f32_layers 600 python scripts/profile_layers.py --depth 34 --clips ${CLIPS:-128} --autotune --dtype fp32

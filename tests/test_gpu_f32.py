@@ -248,3 +248,40 @@ def test_r34_f32_batch_bn_two_videos_match_module_per_video():
     torch.cuda.synchronize()
     rel = (y - ref).abs().max().item() / ref.abs().max().item()
     assert rel <= 1e-3, rel
+
+
+WINO_CASES = [  # (cin, cout, (T, H, W)): the stride-1 1x3x3 convs + odd frames
+    (64, 144, (8, 56, 56)), (128, 288, (4, 28, 28)), (256, 576, (2, 14, 14)),
+    (512, 1152, (1, 7, 7)), (32, 40, (3, 5, 9)),
+]
+
+
+@pytest.mark.parametrize("tc", [2, 3])
+@pytest.mark.parametrize("case", WINO_CASES, ids=lambda c: "%dx%d_%s" % (c[0], c[1], c[2]))
+def test_winograd_f32_matches_fp64(case, tc):
+    """Fused Winograd F(2x2,3x3) (csrc/conv_wino_f32.hip) vs an fp64 conv:
+    within 1e-5 of the output scale, like the direct fp32 kernel."""
+    from rnb_amd.ops.conv_f32 import WINO_BASE
+    cin, cout, thw = case
+    layer = _layer(cin, cout, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=True)
+    assert layer.wino_ok
+    x = _input(2, thw, layer.geom.cin_p, cin)
+    res = _input(2, thw, layer.geom.cout_p, cout, seed=5)
+    y = layer.forward_hip(x, res, config=WINO_BASE + tc)
+    torch.cuda.synchronize()
+    ref = _ref64(layer, x, res)
+    assert torch.all(y[..., cout:] == 0)
+    err = (y[..., :cout].double().cpu() - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item(), err
+
+
+def test_winograd_f32_exact_on_small_integers():
+    """Integer data whose transforms stay exact: bit-equal to the fp64 conv."""
+    from rnb_amd.ops.conv_f32 import WINO_BASE
+    layer = _layer(32, 48, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False, integer=True)
+    x = _input(2, (2, 9, 11), 32, 32, integer=True)
+    for tc in (2, 3):
+        y = layer.forward_hip(x, config=WINO_BASE + tc)
+        torch.cuda.synchronize()
+        ref = _ref64(layer, x).float()
+        assert torch.equal(y[..., :48].cpu(), ref), tc

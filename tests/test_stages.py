@@ -259,3 +259,34 @@ def test_nv12_mirror_equals_interpolate_of_planes():
     ref = rgb.clamp(0, 255) * scale + shift
     assert (got[..., :3] - ref).abs().max().item() < 1e-4
     assert got.shape == (2, 16, 24, 4)
+
+
+def test_winograd_weight_layout_reproduces_the_conv():
+    """CPU emulation of conv_wino_f32.hip's data flow on the packed U layout
+    (input transform per 4x4 patch, 16 GEMMs over channels, output
+    transform) equals the direct 1x3x3 conv: checks the host-side layout."""
+    import torch.nn.functional as F
+    from rnb_amd.ops.conv_f32 import winograd_weights
+    torch.manual_seed(0)
+    co, ci, H, W, tc = 40, 32, 6, 7, 2
+    w = torch.randn(co, ci, 1, 3, 3, dtype=torch.float64)
+    x = torch.randn(1, ci, H, W, dtype=torch.float64)
+    u = winograd_weights(w.float(), 40, tc).double()     # [ci/16, nb, 16, ct, 16]
+    ct = 16 * tc
+    BT = torch.tensor([[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]],
+                      dtype=torch.float64)
+    AT = torch.tensor([[1, 1, 1, 0], [0, 1, -1, -1]], dtype=torch.float64)
+    xp = F.pad(x, (1, 2, 1, 2))                          # pad 1 (+1 for odd tiles)
+    out = torch.zeros(co, (H + 1) // 2 * 2, (W + 1) // 2 * 2, dtype=torch.float64)
+    for ty in range((H + 1) // 2):
+        for tx in range((W + 1) // 2):
+            d = xp[0, :, 2 * ty:2 * ty + 4, 2 * tx:2 * tx + 4]          # [ci, 4, 4]
+            V = BT @ d @ BT.t()                                          # [ci, 4, 4]
+            for o in range(co):
+                cb, r = divmod(o, ct)
+                # U[chunk][cb][x][r][k] for channel c = 16 chunk + k
+                Uo = u[:, cb, :, r, :].permute(0, 2, 1).reshape(ci, 4, 4)
+                M = (Uo * V).sum(0)
+                out[o, 2 * ty:2 * ty + 2, 2 * tx:2 * tx + 2] = AT @ M @ AT.t()
+    ref = F.conv2d(x, w[:, :, 0], padding=1)[0]
+    assert (out[:, :H, :W] - ref).abs().max().item() < 1e-4
