@@ -345,6 +345,7 @@ def run_fused(args) -> int:
     red_dev = device if backend == "nccl" else torch.device("cpu")
 
     from rnb_amd.models.r2p1d.fused import FusedR2P1D
+    from rnb_amd.ops import video as vops
     from rnb_amd.timecard import percentile_stats
 
     vps, vb = args.videos_per_step, args.video_batch
@@ -431,6 +432,32 @@ def run_fused(args) -> int:
             t = start.elapsed_time(tev)
             lat_ms.extend([t] * nvid)
             preds += int((out >= 0).sum())
+    # correctness sample: the first timed step's batches, recomputed eagerly
+    # (decode -> engine -> per-video argmax) and compared with what the graph
+    # replays returned
+    checked = matched = 0
+    rep0 = eng.replicas[0]
+    for i, b in enumerate(step_batches[args.warmup][:4]):
+        vids = torch.tensor([vid for vid, st in b for _ in st], dtype=torch.int32,
+                            device=device)
+        starts = torch.tensor([s for _, st in b for s in st], dtype=torch.int32, device=device)
+        offs = [0]
+        for _, st in b:
+            offs.append(offs[-1] + len(st))
+
+        class _BG:
+            pass
+        bg = _BG()
+        bg.meta = torch.stack([vids, starts])
+        bg.frames = torch.empty(eng.engine.input_shape(len(starts), rep0.packed),
+                                dtype=rep0.dtype, device=device)
+        with torch.no_grad():
+            rep0._decode(bg)
+            logits = eng.engine.forward(bg.frames, packed=rep0.packed)
+            _, arg = vops.video_reduce(logits, torch.tensor(offs, device=device))
+        got = result_bufs[args.warmup][i][:len(b)]
+        checked += len(b)
+        matched += int((arg.cpu() == got).sum())
     n_videos = args.steps * vps
     clips = sum(len(st) for sb in step_batches[args.warmup:] for b in sb for _, st in b)
     stats = percentile_stats(np.asarray(lat_ms) / 1e3)
@@ -461,6 +488,7 @@ def run_fused(args) -> int:
             "clips_per_s": round(clips_all / elapsed, 1),
             "effective_tflops": round(flops / 1e12, 1),
             "videos_ok": int(preds_all),
+            "videos_checked": checked, "videos_match_eager": matched,
             "config": {"model": "R(2+1)D-%d" % args.depth,
                        "global_batch": vps * world, "seq_len": 8,
                        "parallelism": "dp%d (replicated runners)" % world,

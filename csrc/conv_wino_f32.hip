@@ -26,8 +26,11 @@
 // LDS. The transformed weights of the chunk (16 x CT x 16 fp32) are shared by
 // the 4 waves through LDS, staged by LDS-DMA one chunk ahead (2 buffers, one
 // barrier per chunk); their rows are 64 B with a 16-B-chunk XOR swizzle that
-// makes the ds_read_b128 fragment reads conflict free. The patch loads of the
-// next chunk are in flight during the current chunk's MFMAs. After the K loop
+// makes the ds_read_b128 fragment reads conflict free, and each GEMM step's
+// fragments are read while the previous step's MFMAs run. The patch loads of
+// the next chunk either run in flight during the current chunk's MFMAs (PF
+// variants, one block per CU) or behind a second block's MFMAs on the same CU
+// (2-3 blocks per CU at <= 256 / 168 VGPRs). After the K loop
 // each lane holds, for its tile and 4 output channels, all 16 M values per
 // channel group, so the output transform and the epilogue are lane-local.
 #include <hip/hip_runtime.h>
@@ -60,8 +63,12 @@ static __device__ __forceinline__ int w_swz(int q, int r) {
   return q ^ g;
 }
 
-template <int TC>
-__global__ __launch_bounds__(256, 1) void conv_wino_f32_kernel(const WinoParams p) {
+// PF = true: the next chunk's input patch is prefetched into a second register
+// set during the current chunk's MFMAs (one block per CU: ~300-400 VGPRs).
+// PF = false: no register prefetch (<= 256 VGPRs at TC = 2), so two blocks
+// share a CU and one block's loads hide behind the other's MFMAs.
+template <int TC, bool PF>
+__global__ __launch_bounds__(256, PF ? 1 : 2) void conv_wino_f32_kernel(const WinoParams p) {
   constexpr int CT = 16 * TC;
   constexpr int U_BYTES = 16 * CT * 64;                 // one chunk: 16 x CT rows of 64 B
   constexpr int U_INSTR = U_BYTES / 1024 / 4;           // DMA instructions per wave
@@ -139,23 +146,12 @@ __global__ __launch_bounds__(256, 1) void conv_wino_f32_kernel(const WinoParams 
     for (int c = 0; c < TC; ++c) acc[x][c] = (wf32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nchunks = p.Cin / 16;
-  wf32x4 d[16], dn[16];
-  issue_u(0, 0);
-  load_patch(0, d);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   const int frow = lane & 15;
-  for (int c = 0; c < nchunks; ++c) {
-    const int cur = c & 1;
-    if (c + 1 < nchunks) {
-      issue_u(c + 1, cur ^ 1);
-      load_patch(c + 1, dn);
-    }
-    // input transform V = B^T d B, 4 channels per lane (in place of d)
-    wf32x4 v[16];
+  // input transform V = B^T d B, 4 channels per lane, in place
+  auto transform = [&](wf32x4 (&v)[16]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const wf32x4 a0 = d[0 * 4 + j], a1 = d[1 * 4 + j], a2 = d[2 * 4 + j], a3 = d[3 * 4 + j];
+      const wf32x4 a0 = v[0 * 4 + j], a1 = v[1 * 4 + j], a2 = v[2 * 4 + j], a3 = v[3 * 4 + j];
       v[0 * 4 + j] = a0 - a2;
       v[1 * 4 + j] = a1 + a2;
       v[2 * 4 + j] = a2 - a1;
@@ -169,26 +165,76 @@ __global__ __launch_bounds__(256, 1) void conv_wino_f32_kernel(const WinoParams 
       v[i * 4 + 2] = b2 - b1;
       v[i * 4 + 3] = b1 - b3;
     }
-    const char* ub = lds + cur * U_BYTES;
+  };
+  // 16 GEMM steps of one chunk; the A fragments of step x+1 are read from LDS
+  // while step x's MFMAs run (one register set ahead)
+  auto gemm = [&](const char* ub, const wf32x4 (&v)[16]) {
+    wf32x4 af[2][TC];
+#pragma unroll
+    for (int tc = 0; tc < TC; ++tc) {
+      const int r = tc * 16 + frow;
+      af[0][tc] = *(const wf32x4*)(ub + r * 64 + (w_swz(q, r) << 4));
+    }
 #pragma unroll
     for (int x = 0; x < 16; ++x) {
-      wf32x4 af[TC];
+      if (x + 1 < 16) {
 #pragma unroll
-      for (int tc = 0; tc < TC; ++tc) {
-        const int r = tc * 16 + frow;
-        af[tc] = *(const wf32x4*)(ub + (x * CT + r) * 64 + (w_swz(q, r) << 4));
+        for (int tc = 0; tc < TC; ++tc) {
+          const int r = tc * 16 + frow;
+          af[(x + 1) & 1][tc] = *(const wf32x4*)(ub + ((x + 1) * CT + r) * 64 + (w_swz(q, r) << 4));
+        }
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int tc = 0; tc < TC; ++tc)
-          acc[x][tc] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[tc][j], v[x][j], acc[x][tc],
-                                                             0, 0, 0);
+          acc[x][tc] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[x & 1][tc][j], v[x][j],
+                                                             acc[x][tc], 0, 0, 0);
     }
+  };
+
+  wf32x4 d[16];
+  if constexpr (PF) {
+    wf32x4 dn[16];
+    issue_u(0, 0);
+    load_patch(0, d);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int c = 0; c < nchunks; ++c) {
+      const int cur = c & 1;
+      if (c + 1 < nchunks) {
+        issue_u(c + 1, cur ^ 1);
+        load_patch(c + 1, dn);
+      }
+      transform(d);
+      gemm(lds + cur * U_BYTES, d);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; ++k) d[k] = dn[k];
+      for (int k = 0; k < 16; ++k) d[k] = dn[k];
+    }
+  } else {
+    issue_u(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int c = 0; c < nchunks; ++c) {
+      const int cur = c & 1;
+      load_patch(c, d);
+      if (c + 1 < nchunks) {
+        issue_u(c + 1, cur ^ 1);
+        // the patch (older) must land; the next chunk's U DMA may stay in flight
+        if constexpr (U_INSTR == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if constexpr (U_INSTR == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if constexpr (U_INSTR == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      transform(d);
+      gemm(lds + cur * U_BYTES, d);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 
   // ---- output transform Y = A^T M A + epilogue (lane: tile tl, 4 channels) ----
@@ -245,11 +291,14 @@ extern "C" {
 
 int rnb_wino_params_size() { return (int)sizeof(WinoParams); }
 
-// TC: 2 or 3 (output channels per block = 16 * TC). Returns 0, a negative
-// contract code, or the hipError_t of the launch.
-int rnb_wino_f32_launch(const WinoParams* pp, int TC, hipStream_t stream) {
+// variant: 0 = TC 2 with register prefetch, 1 = TC 3 with prefetch,
+// 2 = TC 2 without prefetch (2 blocks per CU), 3 = TC 1 without prefetch.
+// Returns 0, a negative contract code, or the hipError_t of the launch.
+int rnb_wino_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) {
   WinoParams p = *pp;
-  if (TC != 2 && TC != 3) return -1;
+  static const int kTC[4] = {2, 3, 2, 1};
+  if (variant < 0 || variant > 3) return -1;
+  const int TC = kTC[variant];
   if (p.Cin % 16 != 0 || p.Cout % 4 != 0 || p.y_stride % 4 || (p.res && p.res_stride % 4))
     return -2;
   if (p.F <= 0 || p.H <= 0 || p.W <= 0) return 0;
@@ -271,10 +320,13 @@ int rnb_wino_f32_launch(const WinoParams* pp, int TC, hipStream_t stream) {
   w_magic((uint32_t)p.tiles_h, &p.m_th, &p.s_th);
   const long long blocks = (long long)p.n_tblocks * p.n_cblocks;
   if (blocks > 0x7FFFFFFF) return -8;
-  if (TC == 2)
-    hipLaunchKernelGGL(conv_wino_f32_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, stream, p);
-  else
-    hipLaunchKernelGGL(conv_wino_f32_kernel<3>, dim3((unsigned)blocks), dim3(256), 0, stream, p);
+  const dim3 grid((unsigned)blocks), block(256);
+  switch (variant) {
+    case 0: hipLaunchKernelGGL((conv_wino_f32_kernel<2, true>), grid, block, 0, stream, p); break;
+    case 1: hipLaunchKernelGGL((conv_wino_f32_kernel<3, true>), grid, block, 0, stream, p); break;
+    case 2: hipLaunchKernelGGL((conv_wino_f32_kernel<2, false>), grid, block, 0, stream, p); break;
+    default: hipLaunchKernelGGL((conv_wino_f32_kernel<1, false>), grid, block, 0, stream, p); break;
+  }
   return (int)hipGetLastError();
 }
 

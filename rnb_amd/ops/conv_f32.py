@@ -54,9 +54,12 @@ def f32_geom(cin: int, cout: int, kernel, stride, padding) -> ConvGeom:
 
 
 # fused Winograd F(2x2,3x3) kernels (csrc/conv_wino_f32.hip) as extra
-# config ids next to the implicit-GEMM tiles: 16 * TC output channels per block
-WINO_BASE = 1000
-WINO_TC = {WINO_BASE + 2: 2, WINO_BASE + 3: 3}
+# config ids next to the implicit-GEMM tiles: id WINO_BASE + variant ->
+# output channels per block / 16 (TC); variants 0-1 prefetch the next input
+# patch in registers (1 block per CU), 2-3 run 2-3 blocks per CU instead
+WINO_BASE = 1010
+WINO_TC = {WINO_BASE + 0: 2, WINO_BASE + 1: 3, WINO_BASE + 2: 2, WINO_BASE + 3: 1}
+WINO_DEFAULT = WINO_BASE + 2
 
 # Winograd F(2x2, 3x3) transforms: U = G g G^T (host, fp64), V = B^T d B and
 # Y = A^T M A in the kernel
@@ -132,6 +135,7 @@ class ConvLayerF32:
     def _launch_wino(self, x, y, residual, cid, stream):
         from .native import WinoParams, kernels
         tc = WINO_TC[cid]
+        variant = cid - WINO_BASE
         g = self.geom
         N, T, H, W, C = x.shape
         p = WinoParams()
@@ -142,7 +146,7 @@ class ConvLayerF32:
         p.Cout, p.y_stride = g.cout_p, y.shape[-1]
         p.res_stride = residual.shape[-1] if residual is not None else 0
         p.relu = 1 if self.relu else 0
-        kernels().wino_f32(p, tc, stream.cuda_stream)
+        kernels().wino_f32(p, variant, stream.cuda_stream)
 
     # ------------------------------------------------------------------
     def out_shape(self, x_shape) -> Tuple[int, int, int, int, int]:
@@ -254,7 +258,7 @@ class ConvLayerF32:
                 To, Ho, Wo = self.geom.out_thw(T, H, W)
                 cid = self.heuristic_config(N * To * Ho * Wo)
                 if self.wino_ok and os.environ.get("RNB_WINOGRAD", "1") != "0":
-                    cid = WINO_BASE + (3 if self.geom.cout_p % 48 == 0 else 2)
+                    cid = WINO_DEFAULT
             self._config[key] = cid
         return cid
 

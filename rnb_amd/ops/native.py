@@ -308,9 +308,9 @@ class Kernels:
         _check(self.lib.rnb_conv_f32_launch(ctypes.byref(params), config_id, stream),
                "conv_f32 (config %d)" % config_id)
 
-    def wino_f32(self, params: "WinoParams", tc: int, stream: int) -> None:
-        _check(self.lib.rnb_wino_f32_launch(ctypes.byref(params), tc, stream),
-               "conv_wino_f32 (TC %d)" % tc)
+    def wino_f32(self, params: "WinoParams", variant: int, stream: int) -> None:
+        _check(self.lib.rnb_wino_f32_launch(ctypes.byref(params), variant, stream),
+               "conv_wino_f32 (variant %d)" % variant)
 
     def preprocess_f32(self, in_ptr, out_ptr, npix, mean, std, stream):
         m = (ctypes.c_float * 3)(*mean)

@@ -23,6 +23,9 @@ def tile_name(cid, f32=False):
     from rnb_amd.ops.native import kernels
     k = kernels()
     if f32:
+        from rnb_amd.ops.conv_f32 import WINO_BASE, WINO_TC
+        if cid in WINO_TC:
+            return "wino%d%s" % (16 * WINO_TC[cid], "pf" if cid - WINO_BASE < 2 else "")
         return "%dx%d" % k.f32_configs[cid]
     if cid >= len(k.configs):
         from rnb_amd.ops.conv import SPECIAL_NAMES
@@ -110,7 +113,7 @@ def main():
                      "tflops": flops / ms / 1e9, "gflop": flops / 1e9})
         if args.compare:
             best = {}
-            cands = (list(range(len(kernels().f32_configs))) if f32 else
+            cands = (op.layer.candidates() if f32 else
                      list(range(len(cfgs))) + op.layer.special_candidates(src.shape))
             for c in cands:
                 s.record()

@@ -195,3 +195,37 @@ def test_batch_bn_mode_hip_matches_torch_and_module():
     assert e_hip <= 8e-2 * scale
     eng = build_engine(DEV, depth=18, bn_mode="batch", backend="hip")
     assert isinstance(eng, R2P1DEngine) and eng.bn_mode == "batch"
+
+
+def test_top1_agreement_512_clips_bf16_and_fp32_vs_fp32_module():
+    """Verdict round 1 item 8: over 512 synthetic clips, the argmax of the
+    bf16 and fp32 HIP engines must agree with the fp32 nn.Module on >= 99 %
+    of the clips (fp32: all of them up to exact near-ties)."""
+    from rnb_amd.models.r2p1d.model import build_network
+    from rnb_amd.models.r2p1d.engine import R2P1DEngine
+    from rnb_amd.models.r2p1d.decoder import SyntheticDecoder
+    dev = torch.device("cuda:0")
+    net = build_network(1, 5, depth=34, seed=3)
+    mod = R2P1DEngine(net, dev, backend="module", dtype="fp32")
+    e32 = R2P1DEngine(net, dev, backend="hip", dtype="fp32")
+    e16 = R2P1DEngine(net, dev, backend="hip", dtype="bf16")
+    dec = SyntheticDecoder(dev, dtype=torch.float32)
+    agree16 = agree32 = total = 0
+    with torch.no_grad():
+        for b in range(8):                              # 8 x 64 = 512 clips
+            x = torch.cat([dec.decode(1000 * b + v, [0, 20, 40, 60, 80, 100, 120, 140])
+                           for v in range(8)])
+            ref = mod.forward(x).argmax(1)
+            a32 = e32.forward(x).argmax(1)
+            x16 = torch.zeros(x.shape[:4] + (8,), dtype=torch.bfloat16, device=dev)
+            x16[..., :3] = x[..., :3].to(torch.bfloat16)
+            a16 = e16.forward(x16).argmax(1)
+            agree32 += int((a32 == ref).sum())
+            agree16 += int((a16 == ref).sum())
+            total += x.shape[0]
+    torch.cuda.synchronize()
+    print("top-1 agreement over %d clips: fp32 %.4f bf16 %.4f"
+          % (total, agree32 / total, agree16 / total))
+    assert total == 512
+    assert agree32 / total >= 0.99
+    assert agree16 / total >= 0.99

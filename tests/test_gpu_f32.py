@@ -256,9 +256,9 @@ WINO_CASES = [  # (cin, cout, (T, H, W)): the stride-1 1x3x3 convs + odd frames
 ]
 
 
-@pytest.mark.parametrize("tc", [2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("case", WINO_CASES, ids=lambda c: "%dx%d_%s" % (c[0], c[1], c[2]))
-def test_winograd_f32_matches_fp64(case, tc):
+def test_winograd_f32_matches_fp64(case, variant):
     """Fused Winograd F(2x2,3x3) (csrc/conv_wino_f32.hip) vs an fp64 conv:
     within 1e-5 of the output scale, like the direct fp32 kernel."""
     from rnb_amd.ops.conv_f32 import WINO_BASE
@@ -267,7 +267,7 @@ def test_winograd_f32_matches_fp64(case, tc):
     assert layer.wino_ok
     x = _input(2, thw, layer.geom.cin_p, cin)
     res = _input(2, thw, layer.geom.cout_p, cout, seed=5)
-    y = layer.forward_hip(x, res, config=WINO_BASE + tc)
+    y = layer.forward_hip(x, res, config=WINO_BASE + variant)
     torch.cuda.synchronize()
     ref = _ref64(layer, x, res)
     assert torch.all(y[..., cout:] == 0)
@@ -280,8 +280,8 @@ def test_winograd_f32_exact_on_small_integers():
     from rnb_amd.ops.conv_f32 import WINO_BASE
     layer = _layer(32, 48, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False, integer=True)
     x = _input(2, (2, 9, 11), 32, 32, integer=True)
-    for tc in (2, 3):
-        y = layer.forward_hip(x, config=WINO_BASE + tc)
+    for variant in range(4):
+        y = layer.forward_hip(x, config=WINO_BASE + variant)
         torch.cuda.synchronize()
         ref = _ref64(layer, x).float()
-        assert torch.equal(y[..., :48].cpu(), ref), tc
+        assert torch.equal(y[..., :48].cpu(), ref), variant

@@ -199,3 +199,28 @@ def test_engine_packed_input_matches_unpacked():
     assert not mod.accepts_packed_input
     with pytest.raises(ValueError):
         mod.input_shape(1, packed=True)
+
+
+def test_loader_with_npy_decoder(tmp_path):
+    """Round-1 advisor finding: NpyDecoder.decode ignored its video id and the
+    loader's warm-up crashed before any probe. Decoding is now keyed by the
+    probed id and the warm-up needs no file."""
+    import numpy as np
+    from rnb_amd.models.r2p1d.model import R2P1DLoader
+    from rnb_amd.ops import video as vops
+    rng = np.random.default_rng(0)
+    a = rng.integers(0, 256, (40, 112, 112, 3), dtype=np.uint8)
+    b = rng.integers(0, 256, (30, 112, 112, 3), dtype=np.uint8)
+    pa, pb = tmp_path / "a.npy", tmp_path / "b.npy"
+    np.save(pa, a)
+    np.save(pb, b)
+    loader = R2P1DLoader(CPU, decoder="npy", num_clips_population=[2],
+                         num_clips_weights=[1], seed=0, dtype="fp32")
+    dec = loader.decoder
+    va, _ = dec.probe(str(pa))
+    vb, _ = dec.probe(str(pb))
+    got = dec.decode(va, [0, 8])                      # a, probed before b
+    ref = vops.preprocess(torch.from_numpy(np.stack([a[0:8], a[8:16]])), dtype=torch.float32)
+    assert torch.equal(got, ref)
+    (frames,), _, tc = loader((None,), str(pb), TimeCard(1))
+    assert frames.shape == (2, 8, 112, 112, 4) and tc.num_clips == 2

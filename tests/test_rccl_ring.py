@@ -84,7 +84,7 @@ def test_rccl_recv_times_out_instead_of_hanging(tmp_path):
     procs = [ctx.Process(target=_rccl_timeout_rank, args=(r, store, ring, q)) for r in (0, 1)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=60) for _ in range(2))
+    got = dict(q.get(timeout=240) for _ in range(2))
     for p in procs:
         p.join(30)
     assert got["consumer"] != "returned", got
