@@ -36,6 +36,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 typedef float wf32x4 __attribute__((ext_vector_type(4)));
 
 struct WinoParams {
@@ -63,12 +65,15 @@ static __device__ __forceinline__ int w_swz(int q, int r) {
   return q ^ g;
 }
 
-// PF = true: the next chunk's input patch is prefetched into a second register
+// PF = 1: the next chunk's input patch is prefetched into a second register
 // set during the current chunk's MFMAs (one block per CU: ~300-400 VGPRs).
-// PF = false: no register prefetch (<= 256 VGPRs at TC = 2), so two blocks
-// share a CU and one block's loads hide behind the other's MFMAs.
-template <int TC, bool PF>
-__global__ __launch_bounds__(256, PF ? 1 : 2) void conv_wino_f32_kernel(const WinoParams p) {
+// PF = 0: no prefetch (<= 256 VGPRs at TC = 2), so two blocks share a CU and
+// one block's loads hide behind the other's MFMAs.
+// PF = 2: the patch registers are refilled element by element as the GEMM
+// steps consume them: prefetch at PF = 0's register count.
+template <int TC, int PF>
+__global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f32_kernel(
+    const WinoParams p) {
   constexpr int CT = 16 * TC;
   constexpr int U_BYTES = 16 * CT * 64;                 // one chunk: 16 x CT rows of 64 B
   constexpr int U_INSTR = U_BYTES / 1024 / 4;           // DMA instructions per wave
@@ -110,17 +115,18 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void conv_wino_f32_kernel(const Wi
   const __amdgpu_buffer_rsrc_t ur =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, p.u_bytes, 0x00020000);
 
+  // element e = 4 dy + dx of this lane's 4x4 patch, channels of chunk `chunk`
+  auto load_one = [&](int chunk, int e) -> wf32x4 {
+    const int dy = e >> 2, dx = e & 3;
+    const bool ok = ((rmask >> dy) & (cmask >> dx) & 1) != 0;
+    const uint32_t off =
+        ok ? (uint32_t)(pix0 * p.Cin * 4 + chunk * 64 + q * 16 + dy * row_bytes + dx * p.Cin * 4)
+           : WINO_INVALID;
+    return __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+  };
   auto load_patch = [&](int chunk, wf32x4 (&d)[16]) {
-    const int cbase = pix0 * p.Cin * 4 + chunk * 64 + q * 16;
 #pragma unroll
-    for (int dy = 0; dy < 4; ++dy)
-#pragma unroll
-      for (int dx = 0; dx < 4; ++dx) {
-        const bool ok = ((rmask >> dy) & (cmask >> dx) & 1) != 0;
-        const uint32_t off = ok ? (uint32_t)(cbase + dy * row_bytes + dx * p.Cin * 4)
-                                : WINO_INVALID;
-        d[dy * 4 + dx] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
-      }
+    for (int e = 0; e < 16; ++e) d[e] = load_one(chunk, e);
   };
 
   // ---- U staging: chunk c of this cout block, 16 x CT rows, swizzled ----
@@ -167,8 +173,10 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void conv_wino_f32_kernel(const Wi
     }
   };
   // 16 GEMM steps of one chunk; the A fragments of step x+1 are read from LDS
-  // while step x's MFMAs run (one register set ahead)
-  auto gemm = [&](const char* ub, const wf32x4 (&v)[16]) {
+  // while step x's MFMAs run (one register set ahead). With next >= 0, the
+  // register of V[x] is refilled with patch element x of chunk `next` as soon
+  // as step x's MFMAs have read it (prefetch without extra registers).
+  auto gemm = [&](const char* ub, wf32x4 (&v)[16], int next, auto refill) {
     wf32x4 af[2][TC];
 #pragma unroll
     for (int tc = 0; tc < TC; ++tc) {
@@ -190,11 +198,19 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void conv_wino_f32_kernel(const Wi
         for (int tc = 0; tc < TC; ++tc)
           acc[x][tc] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[x & 1][tc][j], v[x][j],
                                                              acc[x][tc], 0, 0, 0);
+      if constexpr (decltype(refill)::value) v[x] = load_one(next, x);
+      // keep the software pipeline: step x+1's fragment reads are issued
+      // before step x's MFMAs, then the refill load; nothing crosses steps
+      if (x + 1 < 16) __builtin_amdgcn_sched_group_barrier(0x0100, TC, 0);   // DS reads
+      __builtin_amdgcn_sched_group_barrier(0x0008, 4 * TC, 0);               // MFMA
+      if constexpr (decltype(refill)::value)
+        __builtin_amdgcn_sched_group_barrier(0x0020, 1, 0);                  // VMEM read
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
   wf32x4 d[16];
-  if constexpr (PF) {
+  if constexpr (PF == 1) {
     wf32x4 dn[16];
     issue_u(0, 0);
     load_patch(0, d);
@@ -207,13 +223,13 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void conv_wino_f32_kernel(const Wi
         load_patch(c + 1, dn);
       }
       transform(d);
-      gemm(lds + cur * U_BYTES, d);
+      gemm(lds + cur * U_BYTES, d, -1, std::false_type{});
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
 #pragma unroll
       for (int k = 0; k < 16; ++k) d[k] = dn[k];
     }
-  } else {
+  } else if constexpr (PF == 0) {
     issue_u(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -231,10 +247,29 @@ __global__ __launch_bounds__(256, PF ? 1 : 2) void conv_wino_f32_kernel(const Wi
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       transform(d);
-      gemm(lds + cur * U_BYTES, d);
+      gemm(lds + cur * U_BYTES, d, -1, std::false_type{});
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
+  } else {
+    // PF == 2: in-place prefetch through gemm(next)
+    issue_u(0, 0);
+    load_patch(0, d);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int c = 0; c + 1 < nchunks; ++c) {
+      const int cur = c & 1;
+      issue_u(c + 1, cur ^ 1);
+      // keep the U DMA ahead of the patch loads in issue order (vmcnt below)
+      asm volatile("" ::: "memory");
+      transform(d);
+      gemm(lds + cur * U_BYTES, d, c + 1, std::true_type{});
+      // U of chunk c+1 landed; the 16 younger patch loads may stay in flight
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      __syncthreads();
+    }
+    transform(d);
+    gemm(lds + ((nchunks - 1) & 1) * U_BYTES, d, -1, std::false_type{});
   }
 
   // ---- output transform Y = A^T M A + epilogue (lane: tile tl, 4 channels) ----
@@ -292,12 +327,13 @@ extern "C" {
 int rnb_wino_params_size() { return (int)sizeof(WinoParams); }
 
 // variant: 0 = TC 2 with register prefetch, 1 = TC 3 with prefetch,
-// 2 = TC 2 without prefetch (2 blocks per CU), 3 = TC 1 without prefetch.
+// 2 = TC 2 without prefetch (2 blocks per CU), 3 = TC 1 without prefetch,
+// 4 / 5 / 6 = TC 1 / 2 / 3 with in-place prefetch.
 // Returns 0, a negative contract code, or the hipError_t of the launch.
 int rnb_wino_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) {
   WinoParams p = *pp;
-  static const int kTC[4] = {2, 3, 2, 1};
-  if (variant < 0 || variant > 3) return -1;
+  static const int kTC[7] = {2, 3, 2, 1, 1, 2, 3};
+  if (variant < 0 || variant > 6) return -1;
   const int TC = kTC[variant];
   if (p.Cin % 16 != 0 || p.Cout % 4 != 0 || p.y_stride % 4 || (p.res && p.res_stride % 4))
     return -2;
@@ -322,10 +358,13 @@ int rnb_wino_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) {
   if (blocks > 0x7FFFFFFF) return -8;
   const dim3 grid((unsigned)blocks), block(256);
   switch (variant) {
-    case 0: hipLaunchKernelGGL((conv_wino_f32_kernel<2, true>), grid, block, 0, stream, p); break;
-    case 1: hipLaunchKernelGGL((conv_wino_f32_kernel<3, true>), grid, block, 0, stream, p); break;
-    case 2: hipLaunchKernelGGL((conv_wino_f32_kernel<2, false>), grid, block, 0, stream, p); break;
-    default: hipLaunchKernelGGL((conv_wino_f32_kernel<1, false>), grid, block, 0, stream, p); break;
+    case 0: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 1>), grid, block, 0, stream, p); break;
+    case 1: hipLaunchKernelGGL((conv_wino_f32_kernel<3, 1>), grid, block, 0, stream, p); break;
+    case 2: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 0>), grid, block, 0, stream, p); break;
+    case 3: hipLaunchKernelGGL((conv_wino_f32_kernel<1, 0>), grid, block, 0, stream, p); break;
+    case 4: hipLaunchKernelGGL((conv_wino_f32_kernel<1, 2>), grid, block, 0, stream, p); break;
+    case 5: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 2>), grid, block, 0, stream, p); break;
+    default: hipLaunchKernelGGL((conv_wino_f32_kernel<3, 2>), grid, block, 0, stream, p); break;
   }
   return (int)hipGetLastError();
 }

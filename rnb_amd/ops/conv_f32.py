@@ -56,10 +56,12 @@ def f32_geom(cin: int, cout: int, kernel, stride, padding) -> ConvGeom:
 # fused Winograd F(2x2,3x3) kernels (csrc/conv_wino_f32.hip) as extra
 # config ids next to the implicit-GEMM tiles: id WINO_BASE + variant ->
 # output channels per block / 16 (TC); variants 0-1 prefetch the next input
-# patch in registers (1 block per CU), 2-3 run 2-3 blocks per CU instead
+# patch into a second register set (1 block per CU), 2-3 do not prefetch (2-3
+# blocks per CU), 4-6 refill the patch registers in place as the GEMM steps
+# consume them (see rnb_wino_f32_launch)
 WINO_BASE = 1010
-WINO_TC = {WINO_BASE + 0: 2, WINO_BASE + 1: 3, WINO_BASE + 2: 2, WINO_BASE + 3: 1}
-WINO_DEFAULT = WINO_BASE + 2
+WINO_TC = {WINO_BASE + v: tc for v, tc in enumerate((2, 3, 2, 1, 1, 2, 3))}
+WINO_DEFAULT = WINO_BASE + 5
 
 # Winograd F(2x2, 3x3) transforms: U = G g G^T (host, fp64), V = B^T d B and
 # Y = A^T M A in the kernel

@@ -25,7 +25,7 @@ def tile_name(cid, f32=False):
     if f32:
         from rnb_amd.ops.conv_f32 import WINO_BASE, WINO_TC
         if cid in WINO_TC:
-            return "wino%d%s" % (16 * WINO_TC[cid], "pf" if cid - WINO_BASE < 2 else "")
+            return "wino%d%s" % (16 * WINO_TC[cid], ("pf", "pf", "", "", "ip", "ip", "ip")[cid - WINO_BASE])
         return "%dx%d" % k.f32_configs[cid]
     if cid >= len(k.configs):
         from rnb_amd.ops.conv import SPECIAL_NAMES

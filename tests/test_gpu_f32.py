@@ -256,7 +256,7 @@ WINO_CASES = [  # (cin, cout, (T, H, W)): the stride-1 1x3x3 convs + odd frames
 ]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", list(range(7)))
 @pytest.mark.parametrize("case", WINO_CASES, ids=lambda c: "%dx%d_%s" % (c[0], c[1], c[2]))
 def test_winograd_f32_matches_fp64(case, variant):
     """Fused Winograd F(2x2,3x3) (csrc/conv_wino_f32.hip) vs an fp64 conv:
@@ -280,7 +280,7 @@ def test_winograd_f32_exact_on_small_integers():
     from rnb_amd.ops.conv_f32 import WINO_BASE
     layer = _layer(32, 48, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False, integer=True)
     x = _input(2, (2, 9, 11), 32, 32, integer=True)
-    for variant in range(4):
+    for variant in range(7):
         y = layer.forward_hip(x, config=WINO_BASE + variant)
         torch.cuda.synchronize()
         ref = _ref64(layer, x).float()
