@@ -1,5 +1,9 @@
 // fp32 Winograd F(2x2, 3x3) convolution for the stride-1 1x3x3 spatial convs
-// of R(2+1)D (~70 % of R(2+1)D-34's FLOPs).
+// of R(2+1)D (~70 % of R(2+1)D-34's FLOPs),
+// and temporal F(4, 3) for the stride-1 3x1x1 convs (conv_winot_f32_kernel
+// below). A persistent-block variant whose chunk stream crosses work units,
+// an inline-asm LDS-DMA variant and a fused F(4x4, 3x3) were measured and
+// were slower (profiles/NOTES.md, round 2); this file keeps the winners.
 //
 // The reference runs these convs in fp32 through cuDNN with
 // cudnn.benchmark = True (reference runner.py:24-25), which picks Winograd
@@ -313,6 +317,179 @@ __global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f
   }
 }
 
+// ===========================================================================
+// Temporal F(4, 3): the stride-1 3x1x1 convs
+// over T = 8 / 4 frames. A tile = 4 output frames of one pixel; its patch is
+// the 6 input frames 4 tt - 1 .. 4 tt + 4 (zero outside [0, T)). 6 GEMM steps
+// per 16-channel chunk instead of the direct conv's 2.5-2.75 taps x 4 frames
+// = 10-11 (1.7-1.8x fewer MFMAs). The work split, U staging (64-B rows,
+// w_swz swizzle) and in-place patch refill follow conv_wino_f32_kernel; the
+// small accumulator set (6 x TC x 4) lets a block cover 64 output channels.
+// WinoParams reuse: F = clips, H = T, W = pixels per frame (H*W of the conv).
+template <int TC>
+__global__ __launch_bounds__(256, 2) void conv_winot_f32_kernel(const WinoParams p) {
+  constexpr int CT = 16 * TC;
+  constexpr int U_BYTES = 6 * CT * 64;
+  constexpr int U_TOTAL = U_BYTES / 1024;
+  constexpr int U_INSTR = (U_TOTAL + 3) / 4;
+  static_assert(U_BYTES % 1024 == 0, "U chunk in whole DMA instructions");
+  __shared__ __attribute__((aligned(16))) char lds[2 * U_BYTES];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int cb = wgid % p.n_cblocks;
+  const int tb = wgid / p.n_cblocks;
+
+  const int tl = lane & 15, q = lane >> 4;
+  const int t = tb * 64 + wave * 16 + tl;
+  int n = 0, tt = 0, hw = 0;
+  const bool tvalid = t < p.n_tiles;
+  if (tvalid) {
+    const int t1 = w_div(t, p.m_tw, p.s_tw);      // tiles_w = pixels per frame
+    hw = t - t1 * p.tiles_w;
+    n = w_div(t1, p.m_th, p.s_th);                // tiles_h = frame groups
+    tt = t1 - n * p.tiles_h;
+  }
+  const int T = p.H, HW = p.W;
+  const int fr0 = 4 * tt - 1;
+  int fmask = 0;
+#pragma unroll
+  for (int e = 0; e < 6; ++e) fmask |= (tvalid && fr0 + e >= 0 && fr0 + e < T) ? (1 << e) : 0;
+  const int pix0 = (n * T + fr0) * HW + hw;       // may be negative (padding)
+  const int frame_bytes = HW * p.Cin * 4;
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, p.u_bytes, 0x00020000);
+
+  auto load_one = [&](int chunk, int e) -> wf32x4 {
+    const bool ok = ((fmask >> e) & 1) != 0;
+    const uint32_t off =
+        ok ? (uint32_t)(pix0 * p.Cin * 4 + chunk * 64 + q * 16 + e * frame_bytes) : WINO_INVALID;
+    return __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+  };
+  const int urow = lane >> 2;
+  const int uq = (lane & 3) ^ ((0x1E >> (2 * ((urow >> 2) & 3))) & 3);
+  auto issue_u = [&](int chunk, int buf) {
+    const uint32_t base = ((uint32_t)chunk * (uint32_t)p.n_cblocks + (uint32_t)cb) * U_BYTES;
+#pragma unroll
+    for (int i = 0; i < U_INSTR; ++i) {
+      const int instr = wave * U_INSTR + i;                  // 16 rows each
+      if (U_TOTAL % 4 == 0 || instr < U_TOTAL)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            ur, (__attribute__((address_space(3))) void*)(lds + buf * U_BYTES + instr * 1024),
+            16, base + (uint32_t)((instr * 16 + urow) * 64 + uq * 16), 0, 0, 0);
+    }
+  };
+
+  wf32x4 acc[6][TC];
+#pragma unroll
+  for (int x = 0; x < 6; ++x)
+#pragma unroll
+    for (int c = 0; c < TC; ++c) acc[x][c] = (wf32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto transform = [](wf32x4 (&v)[6]) {
+    const wf32x4 d0 = v[0], d1 = v[1], d2 = v[2], d3 = v[3], d4 = v[4], d5 = v[5];
+    const wf32x4 t0 = d4 - 4.f * d2, t1 = d3 - 4.f * d1;
+    const wf32x4 t2 = d4 - d2, t3 = 2.f * (d3 - d1);
+    v[0] = 4.f * d0 - 5.f * d2 + d4;
+    v[1] = t0 + t1;
+    v[2] = t0 - t1;
+    v[3] = t2 + t3;
+    v[4] = t2 - t3;
+    v[5] = 4.f * d1 - 5.f * d3 + d5;
+  };
+  const int frow = lane & 15;
+  auto gemm = [&](const char* ub, wf32x4 (&v)[6], int next, auto refill) {
+    wf32x4 af[2][TC];
+#pragma unroll
+    for (int tc = 0; tc < TC; ++tc) {
+      const int r = tc * 16 + frow;
+      af[0][tc] = *(const wf32x4*)(ub + r * 64 + (w_swz(q, r) << 4));
+    }
+#pragma unroll
+    for (int x = 0; x < 6; ++x) {
+      if (x + 1 < 6) {
+#pragma unroll
+        for (int tc = 0; tc < TC; ++tc) {
+          const int r = tc * 16 + frow;
+          af[(x + 1) & 1][tc] =
+              *(const wf32x4*)(ub + ((x + 1) * CT + r) * 64 + (w_swz(q, r) << 4));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int tc = 0; tc < TC; ++tc)
+          acc[x][tc] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[x & 1][tc][j], v[x][j],
+                                                             acc[x][tc], 0, 0, 0);
+      if constexpr (decltype(refill)::value) v[x] = load_one(next, x);
+      if (x + 1 < 6) __builtin_amdgcn_sched_group_barrier(0x0100, TC, 0);    // DS reads
+      __builtin_amdgcn_sched_group_barrier(0x0008, 4 * TC, 0);               // MFMA
+      if constexpr (decltype(refill)::value)
+        __builtin_amdgcn_sched_group_barrier(0x0020, 1, 0);                  // VMEM read
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  const int nchunks = p.Cin / 16;
+  wf32x4 d[6];
+  issue_u(0, 0);
+#pragma unroll
+  for (int e = 0; e < 6; ++e) d[e] = load_one(0, e);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int c = 0; c + 1 < nchunks; ++c) {
+    const int cur = c & 1;
+    issue_u(c + 1, cur ^ 1);
+    asm volatile("" ::: "memory");
+    transform(d);
+    gemm(lds + cur * U_BYTES, d, c + 1, std::true_type{});
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");    // U landed; 6 refills may fly
+    __syncthreads();
+  }
+  transform(d);
+  gemm(lds + ((nchunks - 1) & 1) * U_BYTES, d, -1, std::false_type{});
+
+  // ---- Y = A^T M (4 frames) + epilogue (lane: tile tl, channels 4q..4q+3) ----
+  if (!tvalid) return;
+  const bool has_res = p.res != nullptr;
+#pragma unroll
+  for (int tc = 0; tc < TC; ++tc) {
+    const int co = cb * CT + tc * 16 + 4 * q;
+    if (co >= p.Cout) continue;
+    const float4 b4 = *(const float4*)(p.bias + co);
+    const wf32x4 bias = (wf32x4){b4.x, b4.y, b4.z, b4.w};
+    const wf32x4 m0 = acc[0][tc], m1 = acc[1][tc], m2 = acc[2][tc], m3 = acc[3][tc],
+                 m4 = acc[4][tc], m5 = acc[5][tc];
+    const wf32x4 s12 = m1 + m2, d12 = m1 - m2, s34 = m3 + m4, d34 = m3 - m4;
+    wf32x4 o[4];
+    o[0] = m0 + s12 + s34;
+    o[1] = d12 + 2.f * d34;
+    o[2] = s12 + 4.f * s34;
+    o[3] = d12 + 8.f * d34 + m5;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      if (4 * tt + a >= T) continue;
+      const long long pix = ((long long)n * T + 4 * tt + a) * HW + hw;
+      wf32x4 val = o[a] + bias;
+      if (has_res) {
+        const float4 r4 = *(const float4*)(p.res + pix * p.res_stride + co);
+        val += (wf32x4){r4.x, r4.y, r4.z, r4.w};
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) val[k] = fmaxf(val[k], 0.f);
+      }
+      *(float4*)(p.y + pix * p.y_stride + co) = make_float4(val[0], val[1], val[2], val[3]);
+    }
+  }
+}
+
 static void w_magic(uint32_t d, uint32_t* m, uint32_t* s) {
   if (d <= 1) { *m = 0; *s = 0; return; }
   uint32_t l = 0;
@@ -337,6 +514,7 @@ int rnb_wino_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) {
   const int TC = kTC[variant];
   if (p.Cin % 16 != 0 || p.Cout % 4 != 0 || p.y_stride % 4 || (p.res && p.res_stride % 4))
     return -2;
+  if (p.Cout > p.y_stride || (p.res && p.Cout > p.res_stride)) return -3;
   if (p.F <= 0 || p.H <= 0 || p.W <= 0) return 0;
   const long long xb = (long long)p.F * p.H * p.W * p.Cin * 4;
   if (xb > 0x7FFFFF00LL) return -5;
@@ -366,6 +544,43 @@ int rnb_wino_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) {
     case 5: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 2>), grid, block, 0, stream, p); break;
     default: hipLaunchKernelGGL((conv_wino_f32_kernel<3, 2>), grid, block, 0, stream, p); break;
   }
+  return (int)hipGetLastError();
+}
+
+// Temporal F(4, 3) for stride-1 3x1x1 convs: p.F = clips, p.H = T, p.W =
+// pixels per frame. variant 0 = TC 2 (32 output channels per block), 1 = TC 4.
+// U layout [Cin/16][n_cblocks][6][16 TC][16] fp32 (rows swizzled as w_swz).
+int rnb_winot_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) {
+  WinoParams p = *pp;
+  if (variant < 0 || variant > 1) return -1;
+  const int TC = variant ? 4 : 2;
+  if (p.Cin % 16 != 0 || p.Cout % 4 != 0 || p.y_stride % 4 || (p.res && p.res_stride % 4))
+    return -2;
+  if (p.Cout > p.y_stride || (p.res && p.Cout > p.res_stride)) return -3;
+  if (p.F <= 0 || p.H <= 0 || p.W <= 0) return 0;
+  const long long xb = (long long)p.F * p.H * p.W * p.Cin * 4;
+  if (xb > 0x7FFFFF00LL) return -5;
+  p.tiles_h = (p.H + 3) / 4;
+  p.tiles_w = p.W;
+  const long long nt = (long long)p.F * p.tiles_h * p.tiles_w;
+  if (nt > 0x7FFFFFFF) return -6;
+  p.n_tiles = (int)nt;
+  p.n_tblocks = (p.n_tiles + 63) / 64;
+  const int CT = 16 * TC;
+  p.n_cblocks = (p.Cout + CT - 1) / CT;
+  const long long ub = (long long)(p.Cin / 16) * p.n_cblocks * 6 * CT * 64;
+  if (ub > 0x7FFFFF00LL) return -7;
+  p.x_bytes = (uint32_t)xb;
+  p.u_bytes = (uint32_t)ub;
+  w_magic((uint32_t)p.tiles_w, &p.m_tw, &p.s_tw);
+  w_magic((uint32_t)p.tiles_h, &p.m_th, &p.s_th);
+  const long long blocks = (long long)p.n_tblocks * p.n_cblocks;
+  if (blocks > 0x7FFFFFFF) return -8;
+  const dim3 grid((unsigned)blocks), block(256);
+  if (TC == 2)
+    hipLaunchKernelGGL(conv_winot_f32_kernel<2>, grid, block, 0, stream, p);
+  else
+    hipLaunchKernelGGL(conv_winot_f32_kernel<4>, grid, block, 0, stream, p);
   return (int)hipGetLastError();
 }
 

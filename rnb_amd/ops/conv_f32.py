@@ -53,15 +53,22 @@ def f32_geom(cin: int, cout: int, kernel, stride, padding) -> ConvGeom:
                     padding=tuple(padding), align=F32_ALIGN)
 
 
-# fused Winograd F(2x2,3x3) kernels (csrc/conv_wino_f32.hip) as extra
-# config ids next to the implicit-GEMM tiles: id WINO_BASE + variant ->
-# output channels per block / 16 (TC); variants 0-1 prefetch the next input
-# patch into a second register set (1 block per CU), 2-3 do not prefetch (2-3
-# blocks per CU), 4-6 refill the patch registers in place as the GEMM steps
-# consume them (see rnb_wino_f32_launch)
+# fused Winograd kernels (csrc/conv_wino_f32.hip) as extra config ids next to
+# the implicit-GEMM tiles. Spatial F(2x2,3x3) for stride-1 1x3x3 convs:
+# id WINO_BASE + variant of rnb_wino_f32_launch; the tuned candidates are the
+# in-place-prefetch variants 4 / 5 / 6 = 16 / 32 / 48 output channels per
+# block (variants 0-3, register-prefetch and no-prefetch, always measured
+# slower: profiles/r2_layers_r34_128clips_f32_v2_wino_inplace.txt)
 WINO_BASE = 1010
-WINO_TC = {WINO_BASE + v: tc for v, tc in enumerate((2, 3, 2, 1, 1, 2, 3))}
+WINO_TC = {WINO_BASE + 4: 1, WINO_BASE + 5: 2, WINO_BASE + 6: 3}
 WINO_DEFAULT = WINO_BASE + 5
+# temporal F(4, 3) for stride-1 3x1x1 convs: 32 / 64 output channels per block
+WINOT_BASE = 1030
+WINOT_TC = {WINOT_BASE + 0: 2, WINOT_BASE + 1: 4}
+WINOT_DEFAULT = WINOT_BASE + 1
+WINO_ALL = set(WINO_TC) | set(WINOT_TC)
+# temporal F(4,3) pays off once most output frames see all 3 taps
+WINOT_MIN_T = 4
 
 # Winograd F(2x2, 3x3) transforms: U = G g G^T (host, fp64), V = B^T d B and
 # Y = A^T M A in the kernel
@@ -82,6 +89,26 @@ def winograd_weights(w: torch.Tensor, cout: int, tc: int) -> torch.Tensor:
     full[:co] = u.reshape(co, ci, 16)
     # [nb, ct, ci/16, 16ch, 16x] -> [ci/16, nb, 16x, ct, 16ch]
     t = full.reshape(nb, ct, ci // 16, 16, 16).permute(2, 0, 4, 1, 3)
+    return t.contiguous().float()
+
+
+# F(4, 3) (temporal): U = G g, interpolation points 0, +-1, +-2, inf
+_WINO_G43 = ((1 / 4, 0.0, 0.0), (-1 / 6, -1 / 6, -1 / 6), (-1 / 6, 1 / 6, -1 / 6),
+             (1 / 24, 1 / 12, 1 / 6), (1 / 24, -1 / 12, 1 / 6), (0.0, 0.0, 1.0))
+
+
+def winograd_t_weights(w: torch.Tensor, cout: int, tc: int) -> torch.Tensor:
+    """[Cout, Cin, 3, 1, 1] folded weights -> the temporal F(4, 3) kernel's U
+    layout [Cin/16][n_cblocks][6][CT = 16 tc][16 channels], fp32."""
+    co, ci = w.shape[:2]
+    g = w.detach().double().reshape(co, ci, 3)
+    G = torch.tensor(_WINO_G43, dtype=torch.float64)
+    u = torch.einsum("ik,ock->oci", G, g)                                # [co, ci, 6]
+    ct = 16 * tc
+    nb = (cout + ct - 1) // ct
+    full = torch.zeros(nb * ct, ci, 6, dtype=torch.float64)
+    full[:co] = u
+    t = full.reshape(nb, ct, ci // 16, 16, 6).permute(2, 0, 4, 1, 3)
     return t.contiguous().float()
 
 
@@ -118,37 +145,67 @@ class ConvLayerF32:
         self.wino_ok = (geom.kernel == (1, 3, 3) and geom.stride == (1, 1, 1)
                         and geom.padding == (0, 1, 1) and geom.cin_p % 16 == 0
                         and geom.cin == geom.cin_p)
-        self._wino_u: Dict[int, torch.Tensor] = {}
+        # temporal F(4,3) for stride-1 3x1x1 convs with Cin % 16 == 0
+        self.winot_ok = (geom.kernel == (3, 1, 1) and geom.stride == (1, 1, 1)
+                         and geom.padding == (1, 0, 0) and geom.cin_p % 16 == 0
+                         and geom.cin == geom.cin_p)
+        self.wino_ids = (set(WINO_TC) if self.wino_ok else
+                         set(WINOT_TC) if self.winot_ok else set())
+        self._wino_u: Dict[Tuple[int, int], torch.Tensor] = {}
 
-    def wino_u(self, tc: int) -> torch.Tensor:
-        u = self._wino_u.get(tc)
+    def wino_u(self, tc: int, m: int = 2) -> torch.Tensor:
+        """Transformed weights with 16 tc output channels per work unit: m = 2
+        spatial F(2x2, 3x3), m = -4 temporal F(4, 3) (built once per (m, tc))."""
+        u = self._wino_u.get((m, tc))
         if u is None:
-            u = self._wino_u[tc] = winograd_weights(self.w_ref.cpu(), self.geom.cout_p,
-                                                    tc).to(self.device)
+            fn = {2: winograd_weights, -4: winograd_t_weights}[m]
+            u = self._wino_u[(m, tc)] = fn(self.w_ref.cpu(), self.geom.cout_p, tc).to(self.device)
         return u
 
     def candidates(self):
         from .native import kernels
         c = list(range(len(kernels().f32_configs)))
-        if self.wino_ok:
-            c += sorted(WINO_TC)
-        return c
+        return c + sorted(self.wino_ids)
 
     def _launch_wino(self, x, y, residual, cid, stream):
         from .native import WinoParams, kernels
-        tc = WINO_TC[cid]
-        variant = cid - WINO_BASE
+        ft = cid in WINOT_TC
+        if ft:
+            tc, variant, m = WINOT_TC[cid], cid - WINOT_BASE, -4
+        else:
+            tc, variant, m = WINO_TC[cid], cid - WINO_BASE, 2
         g = self.geom
         N, T, H, W, C = x.shape
+        # the kernels index x / y / residual as dense NDHWC of the input's
+        # frame and pixel counts (stride 1, same padding): check before launch
+        if not (x.is_contiguous() and y.is_contiguous() and C == g.cin_p
+                and tuple(y.shape[:4]) == (N, T, H, W) and y.shape[-1] >= g.cout_p
+                and (residual is None or (residual.is_contiguous()
+                                          and tuple(residual.shape[:4]) == (N, T, H, W)
+                                          and residual.shape[-1] >= g.cout_p))):
+            raise ValueError("%s: Winograd operands do not match the conv geometry: x %s y %s "
+                             "res %s" % (self.name, tuple(x.shape), tuple(y.shape),
+                                         None if residual is None else tuple(residual.shape)))
+        u = self.wino_u(tc, m)
+        assert u.shape[0] * 16 == C and u.shape[1] * 16 * tc >= g.cout_p
         p = WinoParams()
-        p.x, p.u, p.bias = x.data_ptr(), self.wino_u(tc).data_ptr(), self.bias.data_ptr()
+        p.x, p.bias = x.data_ptr(), self.bias.data_ptr()
+        p.u = u.data_ptr()
         p.res = residual.data_ptr() if residual is not None else None
         p.y = y.data_ptr()
-        p.F, p.H, p.W, p.Cin = N * T, H, W, C
+        if ft:
+            p.F, p.H, p.W = N, T, H * W          # clips x frames x pixels per frame
+        else:
+            p.F, p.H, p.W = N * T, H, W
+        p.Cin = C
+        assert p.F * p.H * p.W * C == x.numel()
         p.Cout, p.y_stride = g.cout_p, y.shape[-1]
         p.res_stride = residual.shape[-1] if residual is not None else 0
         p.relu = 1 if self.relu else 0
-        kernels().wino_f32(p, variant, stream.cuda_stream)
+        if ft:
+            kernels().winot_f32(p, variant, stream.cuda_stream)
+        else:
+            kernels().wino_f32(p, variant, stream.cuda_stream)
 
     # ------------------------------------------------------------------
     def out_shape(self, x_shape) -> Tuple[int, int, int, int, int]:
@@ -251,16 +308,19 @@ class ConvLayerF32:
             if cid is None:
                 N, T, H, W, _ = x_shape
                 cid = tuning.nearest(tkey, N * T * H * W)
-            if cid is not None and cid in WINO_TC and not self.wino_ok:
+            if cid is not None and cid in WINO_ALL and cid not in self.wino_ids:
                 cid = None
-            if cid is not None and cid not in WINO_TC and cid >= len(_configs()):
+            if cid is not None and cid not in WINO_ALL and cid >= len(_configs()):
                 cid = None
             if cid is None:
                 N, T, H, W, _ = x_shape
                 To, Ho, Wo = self.geom.out_thw(T, H, W)
                 cid = self.heuristic_config(N * To * Ho * Wo)
-                if self.wino_ok and os.environ.get("RNB_WINOGRAD", "1") != "0":
-                    cid = WINO_DEFAULT
+                if os.environ.get("RNB_WINOGRAD", "1") != "0":
+                    if self.wino_ok:
+                        cid = WINO_DEFAULT
+                    elif self.winot_ok and T >= WINOT_MIN_T:
+                        cid = WINOT_DEFAULT
             self._config[key] = cid
         return cid
 
@@ -268,7 +328,7 @@ class ConvLayerF32:
         from .native import kernels
         k = kernels()
         N = x.shape[0]
-        if cid in WINO_TC:
+        if cid in WINO_ALL:
             step = self.chunk_clips(x.shape, y.shape,
                                     residual.shape[-1] if residual is not None else 0)
             for n0 in range(0, N, step):
@@ -291,7 +351,7 @@ class ConvLayerF32:
         tkey = self._tune_key(x.shape, x.device)
         cached = tuning.get(tkey)
         if cached is not None and (cached < len(kernels().f32_configs) or
-                                   (cached in WINO_TC and self.wino_ok)):
+                                   cached in self.wino_ids):
             self._config[tuple(x.shape[:4])] = cached
             return cached
         y = torch.empty(self.out_shape(x.shape), dtype=torch.float32, device=x.device)

@@ -282,6 +282,9 @@ class Kernels:
         lib.rnb_wino_f32_launch.argtypes = [ctypes.POINTER(WinoParams), ctypes.c_int,
                                             ctypes.c_void_p]
         lib.rnb_wino_f32_launch.restype = ctypes.c_int
+        lib.rnb_winot_f32_launch.argtypes = [ctypes.POINTER(WinoParams), ctypes.c_int,
+                                             ctypes.c_void_p]
+        lib.rnb_winot_f32_launch.restype = ctypes.c_int
         if lib.rnb_wino_params_size() != ctypes.sizeof(WinoParams):
             raise NativeUnavailable("WinoParams layout mismatch: rebuild")
         if lib.rnb_conv_f32_params_size() != ctypes.sizeof(ConvParams):
@@ -311,6 +314,10 @@ class Kernels:
     def wino_f32(self, params: "WinoParams", variant: int, stream: int) -> None:
         _check(self.lib.rnb_wino_f32_launch(ctypes.byref(params), variant, stream),
                "conv_wino_f32 (variant %d)" % variant)
+
+    def winot_f32(self, params: "WinoParams", variant: int, stream: int) -> None:
+        _check(self.lib.rnb_winot_f32_launch(ctypes.byref(params), variant, stream),
+               "conv_winot_f32 (variant %d)" % variant)
 
     def preprocess_f32(self, in_ptr, out_ptr, npix, mean, std, stream):
         m = (ctypes.c_float * 3)(*mean)

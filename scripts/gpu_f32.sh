@@ -15,4 +15,4 @@ step() {
   return 0
 }
 step f32_tests 600 python -u -m pytest tests/test_gpu_f32.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
-TAILN=60 step f32_layers 600 python scripts/profile_layers.py --depth 34 --clips ${CLIPS:-128} --autotune --dtype fp32
+TAILN=80 step f32_layers 600 python scripts/profile_layers.py --depth 34 --clips ${CLIPS:-128} --autotune --dtype fp32 ${PROFILE_ARGS:-}

@@ -23,9 +23,11 @@ def tile_name(cid, f32=False):
     from rnb_amd.ops.native import kernels
     k = kernels()
     if f32:
-        from rnb_amd.ops.conv_f32 import WINO_BASE, WINO_TC
+        from rnb_amd.ops.conv_f32 import WINO_TC, WINOT_TC
+        if cid in WINOT_TC:
+            return "wt4_%d" % (16 * WINOT_TC[cid])
         if cid in WINO_TC:
-            return "wino%d%s" % (16 * WINO_TC[cid], ("pf", "pf", "", "", "ip", "ip", "ip")[cid - WINO_BASE])
+            return "wino%d" % (16 * WINO_TC[cid])
         return "%dx%d" % k.f32_configs[cid]
     if cid >= len(k.configs):
         from rnb_amd.ops.conv import SPECIAL_NAMES
@@ -41,6 +43,8 @@ def main():
     ap.add_argument("--autotune", action="store_true")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--list-wino", action="store_true",
+                    help="fp32: time every Winograd variant once per layer shape")
     ap.add_argument("--compare", action="store_true",
                     help="time every tile config per layer; report best per family")
     ap.add_argument("--fuse", action="store_true",
@@ -62,6 +66,7 @@ def main():
     x[..., 3:] = 0
     bufs = {"x": x}
     rows = []
+    listed = set()
     from rnb_amd.ops.native import kernels
     cfgs = kernels().configs
     skip = False
@@ -111,6 +116,21 @@ def main():
                      "K": g.cin * g.kernel[0] * g.kernel[1] * g.kernel[2],
                      "tile": tile_name(cid, f32), "ms": ms,
                      "tflops": flops / ms / 1e9, "gflop": flops / 1e9})
+        if args.list_wino and f32 and getattr(op.layer, "wino_ids", None):
+            from rnb_amd.ops.conv_f32 import WINO_ALL
+            key = (tuple(src.shape), op.layer.geom.cout)
+            if key not in listed:
+                listed.add(key)
+                times = []
+                for c in [c for c in op.layer.candidates() if c in WINO_ALL]:
+                    op.layer.forward_hip(src, res, out=y, config=c)
+                    s.record()
+                    for _ in range(args.reps):
+                        op.layer.forward_hip(src, res, out=y, config=c)
+                    e.record()
+                    e.synchronize()
+                    times.append("%s %.3f" % (tile_name(c, f32), s.elapsed_time(e) / args.reps))
+                print("[wino] %s %s: %s" % (op.layer.name, tuple(src.shape), ", ".join(times)))
         if args.compare:
             best = {}
             cands = (op.layer.candidates() if f32 else

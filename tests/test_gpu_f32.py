@@ -256,32 +256,80 @@ WINO_CASES = [  # (cin, cout, (T, H, W)): the stride-1 1x3x3 convs + odd frames
 ]
 
 
-@pytest.mark.parametrize("variant", list(range(7)))
+def _wino_ids():
+    from rnb_amd.ops.conv_f32 import WINO_TC
+    return sorted(WINO_TC)
+
+
+@pytest.mark.parametrize("cid", _wino_ids())
 @pytest.mark.parametrize("case", WINO_CASES, ids=lambda c: "%dx%d_%s" % (c[0], c[1], c[2]))
-def test_winograd_f32_matches_fp64(case, variant):
+def test_winograd_f32_matches_fp64(case, cid):
     """Fused Winograd F(2x2,3x3) (csrc/conv_wino_f32.hip) vs an fp64 conv:
     within 1e-5 of the output scale, like the direct fp32 kernel."""
-    from rnb_amd.ops.conv_f32 import WINO_BASE
     cin, cout, thw = case
     layer = _layer(cin, cout, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=True)
     assert layer.wino_ok
     x = _input(2, thw, layer.geom.cin_p, cin)
     res = _input(2, thw, layer.geom.cout_p, cout, seed=5)
-    y = layer.forward_hip(x, res, config=WINO_BASE + variant)
+    y = layer.forward_hip(x, res, config=cid)
     torch.cuda.synchronize()
     ref = _ref64(layer, x, res)
     assert torch.all(y[..., cout:] == 0)
     err = (y[..., :cout].double().cpu() - ref).abs().max().item()
-    assert err <= 1e-5 * ref.abs().max().item(), err
+    rel = err / ref.abs().max().item()
+    print("wino cid %d %s rel err %.2e" % (cid, case, rel))
+    assert rel <= 1e-5, rel
 
 
 def test_winograd_f32_exact_on_small_integers():
     """Integer data whose transforms stay exact: bit-equal to the fp64 conv."""
-    from rnb_amd.ops.conv_f32 import WINO_BASE
     layer = _layer(32, 48, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False, integer=True)
     x = _input(2, (2, 9, 11), 32, 32, integer=True)
-    for variant in range(7):
-        y = layer.forward_hip(x, config=WINO_BASE + variant)
+    for cid in _wino_ids():
+        y = layer.forward_hip(x, config=cid)
         torch.cuda.synchronize()
         ref = _ref64(layer, x).float()
-        assert torch.equal(y[..., :48].cpu(), ref), variant
+        assert torch.equal(y[..., :48].cpu(), ref), cid
+
+
+WINOT_CASES = [  # (cin, cout, (T, H, W)): the stride-1 3x1x1 convs + odd frame counts
+    (144, 64, (8, 14, 14)), (288, 128, (4, 7, 7)), (576, 256, (2, 7, 7)),
+    (64, 40, (5, 3, 5)), (32, 36, (1, 4, 4)),
+]
+
+
+@pytest.mark.parametrize("case", WINOT_CASES, ids=lambda c: "%dx%d_%s" % (c[0], c[1], c[2]))
+def test_winograd_temporal_f32_matches_fp64(case):
+    """Temporal F(4, 3) (rnb_winot_f32_launch) vs an fp64 conv, every variant."""
+    from rnb_amd.ops.conv_f32 import WINOT_TC
+    cin, cout, thw = case
+    layer = _layer(cin, cout, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=True)
+    assert layer.winot_ok and layer.wino_ids == set(WINOT_TC)
+    x = _input(2, thw, layer.geom.cin_p, cin)
+    res = _input(2, thw, layer.geom.cout_p, cout, seed=5)
+    ref = _ref64(layer, x, res)
+    for cid in sorted(WINOT_TC):
+        y = layer.forward_hip(x, res, config=cid)
+        torch.cuda.synchronize()
+        assert torch.all(y[..., cout:] == 0)
+        rel = (y[..., :cout].double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+        print("winot cid %d %s rel err %.2e" % (cid, case, rel))
+        assert rel <= 2e-5, (cid, rel)
+
+
+def test_winograd_grid_sizes():
+    """A one-block launch and a many-wave launch (more blocks than the chip
+    holds at once) both equal the fp64 conv, spatial and temporal."""
+    from rnb_amd.ops.conv_f32 import WINO_TC, WINOT_TC
+    sp = _layer(32, 48, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False)
+    tp = _layer(48, 32, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=False)
+    for n, thw in ((1, (1, 6, 6)), (40, (4, 30, 30))):
+        for layer, ids in ((sp, WINO_TC), (tp, WINOT_TC)):
+            x = _input(n, thw, layer.geom.cin_p, layer.geom.cin)
+            ref = _ref64(layer, x)
+            for cid in sorted(ids):
+                y = layer.forward_hip(x, config=cid)
+                torch.cuda.synchronize()
+                rel = ((y[..., :layer.geom.cout].double().cpu() - ref).abs().max().item()
+                       / ref.abs().max().item())
+                assert rel <= 2e-5, (n, thw, cid, rel)

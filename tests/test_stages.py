@@ -290,3 +290,34 @@ def test_winograd_weight_layout_reproduces_the_conv():
                 out[o, 2 * ty:2 * ty + 2, 2 * tx:2 * tx + 2] = AT @ M @ AT.t()
     ref = F.conv2d(x, w[:, :, 0], padding=1)[0]
     assert (out[:, :H, :W] - ref).abs().max().item() < 1e-4
+
+
+def test_winograd_temporal_weight_layout_reproduces_the_conv():
+    """Emulation of the temporal F(4, 3) kernel on its packed U layout
+    [ci/16][nb][6][ct][16]: 6-frame patches at stride 4, zero padded."""
+    import torch.nn.functional as F
+    from rnb_amd.ops.conv_f32 import winograd_t_weights
+    torch.manual_seed(0)
+    co, ci, T, P, tc = 20, 16, 7, 3, 2
+    w = torch.randn(co, ci, 3, 1, 1, dtype=torch.float64)
+    x = torch.randn(1, ci, T, P, dtype=torch.float64)
+    u = winograd_t_weights(w.float(), 20, tc).double()   # [ci/16, nb, 6, ct, 16]
+    ct = 16 * tc
+    BT = torch.tensor([[4, 0, -5, 0, 1, 0], [0, -4, -4, 1, 1, 0], [0, 4, -4, -1, 1, 0],
+                       [0, -2, -1, 2, 1, 0], [0, 2, -1, -2, 1, 0], [0, 4, 0, -5, 0, 1]],
+                      dtype=torch.float64)
+    AT = torch.tensor([[1, 1, 1, 1, 1, 0], [0, 1, -1, 2, -2, 0], [0, 1, 1, 4, 4, 0],
+                       [0, 1, -1, 8, -8, 1]], dtype=torch.float64)
+    nt = (T + 3) // 4
+    xp = F.pad(x, (0, 0, 1, 4 * nt + 1 - T))
+    out = torch.zeros(co, 4 * nt, P, dtype=torch.float64)
+    for tt in range(nt):
+        d = xp[0, :, 4 * tt:4 * tt + 6, :]                                # [ci, 6, P]
+        V = torch.einsum("ik,ckp->cip", BT, d)
+        for o in range(co):
+            cb, r = divmod(o, ct)
+            Uo = u[:, cb, :, r, :].permute(0, 2, 1).reshape(ci, 6)
+            M = (Uo[:, :, None] * V).sum(0)                                # [6, P]
+            out[o, 4 * tt:4 * tt + 4] = AT @ M
+    ref = F.conv2d(x, w[:, :, :, 0], padding=(1, 0))[0]
+    assert (out[:, :T] - ref).abs().max().item() < 1e-4
