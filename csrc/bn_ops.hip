@@ -92,52 +92,92 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
 // runs one video per forward (training-mode BN, reference runner.py:45 and
 // model.py:82-84): segment s = rows [seg[s], seg[s+1]) of the [M][stride]
 // tensor. Rows outside every segment (graph-bucket padding) are ignored by
-// the statistics and left untouched by the apply. Grid of the partial
-// kernels: (BN_SEG_BLOCKS, nseg); block b of segment s sums an even share of
-// the segment's rows. Two passes (mean, then centred squares) as above.
+// the statistics and left untouched by the apply.
+//
+// One read of the tensor for the statistics: shifted sums S1 = sum(x - K),
+// S2 = sum((x - K)^2) with K = the segment's first row (a sample of the
+// channel, so |mean - K| is of the order of the spread and the cancellation in
+// var = S2/n - (S1/n)^2 stays at fp32 rounding of the spread, like a two-pass
+// variance). Grid (BN_SEG_BLOCKS, nseg); a block's 256 threads are
+// row lanes x channel quads (C = 64: 16 x 16), so every wave reads whole
+// contiguous rows; per-block partials are reduced in LDS and then by a
+// finalize kernel in a fixed order (deterministic).
 // ---------------------------------------------------------------------------
-#define BN_SEG_BLOCKS 64
+#define BN_SEG_BLOCKS 32
 
-__global__ __launch_bounds__(256) void bn_seg_partial_f32_kernel(
+__global__ __launch_bounds__(256) void bn_seg_sums_f32_kernel(
     const float* __restrict__ y, const int* __restrict__ seg, int C, int stride,
-    const float* __restrict__ mean, float* __restrict__ partial) {
+    float* __restrict__ partial) {
+  __shared__ float4 red1[256], red2[256];
   const int s = blockIdx.y;
   const int r0s = seg[s], r1s = seg[s + 1];
   const int rows = r1s - r0s;
   const int per = (rows + BN_SEG_BLOCKS - 1) / BN_SEG_BLOCKS;
   const int r0 = r0s + blockIdx.x * per;
   const int r1 = min(r1s, r0 + per);
-  float* out = partial + ((size_t)s * BN_SEG_BLOCKS + blockIdx.x) * C;
-  for (int c = threadIdx.x * 4; c < C; c += 1024) {
-    float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (mean) m = *(const float4*)(mean + (size_t)s * C + c);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int r = r0; r < r1; ++r) {
-      const float4 v = *(const float4*)(y + (size_t)r * stride + c);
-      if (mean) {
-        const float a = v.x - m.x, b = v.y - m.y, cc = v.z - m.z, d = v.w - m.w;
-        acc.x += a * a; acc.y += b * b; acc.z += cc * cc; acc.w += d * d;
-      } else {
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  const int CQ = C / 4;
+  const int QL = CQ < 256 ? CQ : 256;             // channel-quad lanes
+  const int RL = 256 / QL;                        // row lanes
+  const int tid = threadIdx.x, ql = tid % QL, rl = tid / QL;
+  float* out1 = partial + ((size_t)s * BN_SEG_BLOCKS + blockIdx.x) * 2 * C;
+  float* out2 = out1 + C;
+  for (int base = 0; base < CQ; base += QL) {     // uniform trip count (barriers)
+    const int qd = base + ql;
+    const bool act = qd < CQ && rl < RL;
+    float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f), a2 = a1;
+    if (act && rows > 0) {
+      const float4 k = *(const float4*)(y + (size_t)r0s * stride + 4 * qd);
+      for (int r = r0 + rl; r < r1; r += RL) {
+        const float4 v = *(const float4*)(y + (size_t)r * stride + 4 * qd);
+        const float x0 = v.x - k.x, x1 = v.y - k.y, x2 = v.z - k.z, x3 = v.w - k.w;
+        a1.x += x0; a1.y += x1; a1.z += x2; a1.w += x3;
+        a2.x += x0 * x0; a2.y += x1 * x1; a2.z += x2 * x2; a2.w += x3 * x3;
       }
     }
-    *(float4*)(out + c) = acc;
+    red1[tid] = a1;
+    red2[tid] = a2;
+    __syncthreads();
+    if (rl == 0 && qd < CQ) {
+      for (int l = 1; l < RL; ++l) {
+        const float4 b1 = red1[l * QL + ql], b2 = red2[l * QL + ql];
+        a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
+        a2.x += b2.x; a2.y += b2.y; a2.z += b2.z; a2.w += b2.w;
+      }
+      *(float4*)(out1 + 4 * qd) = a1;
+      *(float4*)(out2 + 4 * qd) = a2;
+    }
+    __syncthreads();
   }
 }
 
+// mean / biased variance per (segment, channel) from the shifted sums
 __global__ __launch_bounds__(256) void bn_seg_finalize_f32_kernel(
-    const float* __restrict__ partial, const int* __restrict__ seg, int C,
-    float* __restrict__ out) {
+    const float* __restrict__ y, const int* __restrict__ seg, int C, int stride,
+    const float* __restrict__ partial, float* __restrict__ mean, float* __restrict__ var) {
   const int s = blockIdx.y;
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
-  float acc = 0.f;
-  for (int b = 0; b < BN_SEG_BLOCKS; ++b) acc += partial[((size_t)s * BN_SEG_BLOCKS + b) * C + c];
   const int rows = seg[s + 1] - seg[s];
-  out[(size_t)s * C + c] = rows > 0 ? acc / (float)rows : 0.f;
+  if (rows <= 0) {
+    mean[(size_t)s * C + c] = 0.f;
+    var[(size_t)s * C + c] = 0.f;
+    return;
+  }
+  float s1 = 0.f, s2 = 0.f;
+  for (int b = 0; b < BN_SEG_BLOCKS; ++b) {
+    const float* p = partial + ((size_t)s * BN_SEG_BLOCKS + b) * 2 * C;
+    s1 += p[c];
+    s2 += p[C + c];
+  }
+  const float k = y[(size_t)seg[s] * stride + c];
+  const float m1 = s1 / (float)rows;
+  mean[(size_t)s * C + c] = k + m1;
+  var[(size_t)s * C + c] = fmaxf(s2 / (float)rows - m1 * m1, 0.f);
 }
 
-// one thread per (row, 4 channels); the row's segment by binary search
+// RPT consecutive rows x 4 channels per thread; the first row's segment by
+// binary search, later rows step forward across segment boundaries
+#define BN_APPLY_RPT 4
 __global__ __launch_bounds__(256) void bn_seg_apply_f32_kernel(
     const float* __restrict__ y, float* __restrict__ z, const float* __restrict__ res,
     const int* __restrict__ seg, int nseg, const float* __restrict__ mean,
@@ -146,39 +186,56 @@ __global__ __launch_bounds__(256) void bn_seg_apply_f32_kernel(
     int z_stride, int res_stride) {
   const int cq = C / 4;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= M * cq) return;
-  const int r = (int)(i / cq);
-  const int c = (int)(i - (long long)r * cq) * 4;
-  if (r < seg[0] || r >= seg[nseg]) return;
-  int lo = 0, hi = nseg - 1;                 // last s with seg[s] <= r
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (seg[mid] <= r) lo = mid; else hi = mid - 1;
-  }
-  const float4 v = *(const float4*)(y + (size_t)r * y_stride + c);
-  const float4 m = *(const float4*)(mean + (size_t)lo * C + c);
-  const float4 q = *(const float4*)(var + (size_t)lo * C + c);
-  const float4 g = *(const float4*)(gamma + c);
-  const float4 b = *(const float4*)(beta + c);
-  float o[4] = {(v.x - m.x) * rsqrtf(q.x + eps) * g.x + b.x,
-                (v.y - m.y) * rsqrtf(q.y + eps) * g.y + b.y,
-                (v.z - m.z) * rsqrtf(q.z + eps) * g.z + b.z,
-                (v.w - m.w) * rsqrtf(q.w + eps) * g.w + b.w};
-  if (res) {
-    const float4 rv = *(const float4*)(res + (size_t)r * res_stride + c);
-    o[0] += rv.x; o[1] += rv.y; o[2] += rv.z; o[3] += rv.w;
-  }
-  if (relu) {
+  const long long groups = (M + BN_APPLY_RPT - 1) / BN_APPLY_RPT;
+  if (i >= groups * cq) return;
+  const long long g = i / cq;
+  const int c = (int)(i - g * cq) * 4;
+  const int ra = (int)(g * BN_APPLY_RPT);
+  const int rb = (int)min((long long)ra + BN_APPLY_RPT, M);
+  const int lo_row = seg[0], hi_row = seg[nseg];
+  const float4 gm = *(const float4*)(gamma + c);
+  const float4 bt = *(const float4*)(beta + c);
+  int s = -1;
+  float4 sc = make_float4(0.f, 0.f, 0.f, 0.f), sh = sc;
+  for (int r = ra; r < rb; ++r) {
+    if (r < lo_row || r >= hi_row) continue;
+    if (s < 0 || r >= seg[s + 1]) {
+      if (s < 0) {
+        int lo = 0, hi = nseg - 1;                 // last s with seg[s] <= r
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (seg[mid] <= r) lo = mid; else hi = mid - 1;
+        }
+        s = lo;
+      } else {
+        while (r >= seg[s + 1]) ++s;
+      }
+      const float4 m = *(const float4*)(mean + (size_t)s * C + c);
+      const float4 q = *(const float4*)(var + (size_t)s * C + c);
+      sc = make_float4(gm.x * rsqrtf(q.x + eps), gm.y * rsqrtf(q.y + eps),
+                       gm.z * rsqrtf(q.z + eps), gm.w * rsqrtf(q.w + eps));
+      sh = make_float4(bt.x - m.x * sc.x, bt.y - m.y * sc.y, bt.z - m.z * sc.z,
+                       bt.w - m.w * sc.w);
+    }
+    const float4 v = *(const float4*)(y + (size_t)r * y_stride + c);
+    float o[4] = {fmaf(v.x, sc.x, sh.x), fmaf(v.y, sc.y, sh.y), fmaf(v.z, sc.z, sh.z),
+                  fmaf(v.w, sc.w, sh.w)};
+    if (res) {
+      const float4 rv = *(const float4*)(res + (size_t)r * res_stride + c);
+      o[0] += rv.x; o[1] += rv.y; o[2] += rv.z; o[3] += rv.w;
+    }
+    if (relu) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) o[k] = fmaxf(o[k], 0.f);
+      for (int k = 0; k < 4; ++k) o[k] = fmaxf(o[k], 0.f);
+    }
+    *(float4*)(z + (size_t)r * z_stride + c) = make_float4(o[0], o[1], o[2], o[3]);
   }
-  *(float4*)(z + (size_t)r * z_stride + c) = make_float4(o[0], o[1], o[2], o[3]);
 }
 
 extern "C" {
 
 long long rnb_bn_seg_scratch_floats(int nseg, int C) {
-  return (long long)nseg * BN_SEG_BLOCKS * C;
+  return (long long)nseg * BN_SEG_BLOCKS * 2 * C;
 }
 
 // seg: device [nseg+1] row offsets; mean/var: [nseg][C] (biased variance)
@@ -188,14 +245,10 @@ int rnb_bn_seg_stats_f32(const float* y, const int* seg, int nseg, int C, int st
   if (C % 4 != 0 || stride % 4 != 0 || stride < C) return -2;
   const dim3 grid(BN_SEG_BLOCKS, nseg);
   const dim3 fgrid((C + 255) / 256, nseg);
-  hipLaunchKernelGGL(bn_seg_partial_f32_kernel, grid, dim3(256), 0, stream, y, seg, C, stride,
-                     (const float*)nullptr, scratch);
-  hipLaunchKernelGGL(bn_seg_finalize_f32_kernel, fgrid, dim3(256), 0, stream, scratch, seg, C,
-                     mean);
-  hipLaunchKernelGGL(bn_seg_partial_f32_kernel, grid, dim3(256), 0, stream, y, seg, C, stride,
-                     (const float*)mean, scratch);
-  hipLaunchKernelGGL(bn_seg_finalize_f32_kernel, fgrid, dim3(256), 0, stream, scratch, seg, C,
-                     var);
+  hipLaunchKernelGGL(bn_seg_sums_f32_kernel, grid, dim3(256), 0, stream, y, seg, C, stride,
+                     scratch);
+  hipLaunchKernelGGL(bn_seg_finalize_f32_kernel, fgrid, dim3(256), 0, stream, y, seg, C, stride,
+                     (const float*)scratch, mean, var);
   return (int)hipGetLastError();
 }
 
@@ -205,7 +258,8 @@ int rnb_bn_seg_apply_f32(const float* y, float* z, const float* res, const int* 
                          int y_stride, int z_stride, int res_stride, hipStream_t stream) {
   if (M <= 0 || C <= 0 || nseg <= 0) return 0;
   if (C % 4 || y_stride % 4 || z_stride % 4 || (res && res_stride % 4)) return -2;
-  const long long n = M * (C / 4);
+  const long long n = (M + BN_APPLY_RPT - 1) / BN_APPLY_RPT * (C / 4);
+  if (M > 0x7FFFFFFFLL) return -3;
   hipLaunchKernelGGL(bn_seg_apply_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      stream, y, z, res, seg, nseg, mean, var, gamma, beta, eps, relu, M, C,
                      y_stride, z_stride, res_stride);

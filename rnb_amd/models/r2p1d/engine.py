@@ -251,13 +251,17 @@ class R2P1DEngine:
 
     # -------------------------------------------------------------- forward
     def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
-                packed: bool = False, clip_offsets=None) -> torch.Tensor:
+                packed: bool = False, clip_offsets=None,
+                clip_offsets_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
         """x: NDHWC boundary tensor (or NCDHW fp32 for backend=module); with
         ``packed``, the stem's pair-packed input (``input_shape(n, True)``).
         ``clip_offsets`` (bn_mode='batch'): clip ranges of the videos in the
         batch, [0, n1, n1+n2, ..., N]; every video's BatchNorms use that
         video's own statistics, as the reference's one-video forwards do
-        (default: the whole batch is one video)."""
+        (default: the whole batch is one video). ``clip_offsets_dev``: the same
+        as a device int32 tensor, possibly padded with trailing repeats of its
+        last offset (empty videos); nothing is read back to the host, so the
+        forward can be captured in a HIP graph."""
         if packed and not self.accepts_packed_input:
             raise ValueError("this engine's first op does not take a packed input")
         if self.backend == "module":
@@ -275,7 +279,10 @@ class R2P1DEngine:
         hip = self.backend == "hip"
         bufs: Dict[str, torch.Tensor] = {"x": x}
         coffs = None
-        if self.bn_mode == "batch" and clip_offsets is not None:
+        if self.bn_mode == "batch" and clip_offsets_dev is not None and hip:
+            coffs = clip_offsets_dev
+            clip_offsets = None
+        elif self.bn_mode == "batch" and clip_offsets is not None:
             clip_offsets = [int(o) for o in clip_offsets]
             if clip_offsets[0] != 0 or clip_offsets[-1] != x.shape[0]:
                 raise ValueError("clip_offsets must span [0, %d]" % x.shape[0])
@@ -307,8 +314,9 @@ class R2P1DEngine:
                     if coffs is not None:
                         thw = y.shape[1] * y.shape[2] * y.shape[3]
                         seg = coffs * thw
-                        rows = [(b - a) * thw for a, b in zip(clip_offsets[:-1],
-                                                              clip_offsets[1:])]
+                        if clip_offsets is not None:
+                            rows = [(b - a) * thw for a, b in zip(clip_offsets[:-1],
+                                                                  clip_offsets[1:])]
                     y = op.bn.forward_hip(y, res, op.bn_relu, out=y, segments=seg,
                                           seg_rows=rows)
                 else:
@@ -404,10 +412,19 @@ class GraphedEngine:
                  buckets: Sequence[int] = DEFAULT_BUCKETS, autotune: bool = True,
                  warmup: int = 2):
         assert engine.backend == "hip"
-        if engine.bn_mode != "eval":
-            # bucket padding rows would enter the batch statistics
-            raise ValueError("HIP graphs need bn_mode='eval'; run bn_mode='batch' eagerly")
+        if engine.bn_mode == "batch" and not engine.f32:
+            raise ValueError("graphed bn_mode='batch' (per-video statistics) is fp32 only")
         self.engine = engine
+        # bn_mode='batch': each bucket graph reads its videos' clip offsets
+        # from a static device tensor [b + 1] (padded with empty videos), so
+        # the bucket's padding rows stay outside every video's statistics
+        self.batch_bn = engine.bn_mode == "batch"
+        self.offsets: Dict[int, torch.Tensor] = {}
+        self._pinned = [torch.zeros(max_clips + 1, dtype=torch.int32).pin_memory()
+                        if self.batch_bn and torch.cuda.is_available() else None
+                        for _ in range(4)]
+        self._pinned_ev = [None] * 4
+        self._pinned_i = 0
         self.device = engine.device
         self.buckets = sorted({b for b in buckets if b < max_clips} | {max_clips})
         self.autotune = autotune
@@ -441,18 +458,24 @@ class GraphedEngine:
             with tuning.FileLock("autotune"):
                 eng.autotune(b)
         static_in = torch.zeros(eng.input_shape(b), dtype=eng.dtype, device=self.device)
+        kw = {}
+        if self.batch_bn:
+            offs = torch.full((b + 1,), b, dtype=torch.int32, device=self.device)
+            offs[0] = 0                              # one video until replay says otherwise
+            self.offsets[b] = offs
+            kw["clip_offsets_dev"] = offs
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             for _ in range(self.warmup):
-                eng.forward(static_in)
+                eng.forward(static_in, **kw)
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=self.pool):
-            static_out = eng.forward(static_in)
+            static_out = eng.forward(static_in, **kw)
         torch.cuda.synchronize(self.device)
         self.graphs[b] = (g, static_in, static_out)
         self.capture_s += time.time() - t0
@@ -470,21 +493,45 @@ class GraphedEngine:
             self._capture(b)
         return self.graphs[b][1], b
 
-    def replay(self, n: int) -> torch.Tensor:
-        """Replay the bucket graph whose input was filled via input_buffer."""
+    def _set_offsets(self, b: int, n: int, clip_offsets) -> None:
+        """Stage the videos' clip offsets (default: one video of n clips) into
+        bucket b's static offsets, padded with n (empty videos), through a
+        small ring of pinned buffers (stream-ordered, no host sync)."""
+        offs = [0, n] if clip_offsets is None else [int(o) for o in clip_offsets]
+        if offs[0] != 0 or offs[-1] != n or len(offs) > b + 1:
+            raise ValueError("clip offsets %s do not describe %d clips in bucket %d"
+                             % (offs, n, b))
+        i = self._pinned_i
+        self._pinned_i = (i + 1) % len(self._pinned)
+        if self._pinned_ev[i] is not None:
+            self._pinned_ev[i].synchronize()          # that copy has been consumed
+        host = self._pinned[i]
+        host[:len(offs)] = torch.tensor(offs, dtype=torch.int32)
+        host[len(offs):b + 1] = n
+        self.offsets[b].copy_(host[:b + 1], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._pinned_ev[i] = ev
+
+    def replay(self, n: int, clip_offsets=None) -> torch.Tensor:
+        """Replay the bucket graph whose input was filled via input_buffer;
+        ``clip_offsets`` (bn_mode='batch'): the videos' clip ranges."""
         b = self.bucket_for(n)
         g, static_in, static_out = self.graphs[b]
-        # rows >= n hold stale (finite) inputs; clip rows are independent in
-        # eval mode, so their outputs are simply not returned
+        if self.batch_bn:
+            self._set_offsets(b, n, clip_offsets)
+        # rows >= n hold stale (finite) inputs; in eval mode clip rows are
+        # independent, in batch mode they sit outside every video's segment:
+        # their outputs are simply not returned
         g.replay()
         return static_out[:n]
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, clip_offsets=None) -> torch.Tensor:
         n = x.shape[0]
         if n == 0:
             return self.engine.forward(x)
         static_in, b = self.input_buffer(n)
         static_in[:n].copy_(x)
-        return self.replay(n)
+        return self.replay(n, clip_offsets)
 
     __call__ = forward

@@ -96,8 +96,9 @@ def build_engine(device: torch.device, start_index=1, end_index=5, num_classes=4
                         ckpt_path)
     backend = _resolve_backend(backend, device)
     eng = R2P1DEngine(net, device, backend=backend, bn_mode=bn_mode, dtype=_dtype(dtype))
-    # batch-statistics BN runs eagerly: bucket graphs pad the clip batch
-    if backend == "hip" and use_graphs and bn_mode == "eval":
+    # batch-statistics BN is graphed for fp32 (per-video segments from a
+    # static offsets tensor); bf16 batch BN runs eagerly
+    if backend == "hip" and use_graphs and (bn_mode == "eval" or _dtype(dtype) == torch.float32):
         kw = {} if buckets is None else {"buckets": buckets}
         return GraphedEngine(eng, max_clips, autotune=autotune, **kw)
     return eng
@@ -192,25 +193,31 @@ class R2P1DRunner(RunnerModel):
     def output_dtypes_for(cls, end_index=5, dtype=None, **kwargs):
         return (torch.float32,) if end_index == 5 else (_dtype(dtype),)
 
+    @staticmethod
+    def _clip_offsets(time_card, n: int):
+        """Clip ranges of the videos batched into this call (bn_mode='batch':
+        each video keeps its own BN statistics); None = one video."""
+        if not isinstance(time_card, TimeCardList) or n == 0:
+            return None
+        offs = [0]
+        for tc in time_card.time_cards:
+            r = tc.extra.get("rows")
+            offs.append(offs[-1] + int(r if r is not None else (tc.num_clips or 0)))
+        return offs if offs[-1] == n else None
+
     def __call__(self, tensors, non_tensors, time_card):
         x = tensors[0]
+        offs = (self._clip_offsets(time_card, x.shape[0]) if self.bn_mode == "batch"
+                else None)
         if (self._gather_ptr is not None and x.data_ptr() == self._gather_ptr
                 and isinstance(self.engine, GraphedEngine) and x.shape[0] > 0):
             # rows already sit in the bucket graph's static input: replay only
             self._gather_ptr = None
-            y = self.engine.replay(x.shape[0])
+            y = self.engine.replay(x.shape[0], clip_offsets=offs)
         else:
             self._gather_ptr = None
             x = _to_boundary(x, self.start_index, self.dtype)
-            if self.bn_mode == "batch" and isinstance(time_card, TimeCardList) \
-                    and x.shape[0] > 0:
-                # a batch of several videos: each keeps its own BN statistics
-                offs = [0]
-                for tc in time_card.time_cards:
-                    n = tc.extra.get("rows")
-                    offs.append(offs[-1] + int(n if n is not None else (tc.num_clips or 0)))
-                if offs[-1] != x.shape[0]:
-                    offs = None
+            if self.bn_mode == "batch" and x.shape[0] > 0:
                 y = self.engine.forward(x, clip_offsets=offs)
             else:
                 y = self.engine(x)

@@ -9,6 +9,7 @@ reference of the same op and the CPU path.
 """
 from __future__ import annotations
 
+import math
 from typing import Optional
 
 import torch
@@ -34,6 +35,7 @@ class BatchNormBatch:
         self.mean = torch.zeros(channels_p, dtype=torch.float32, device=device)
         self.var = torch.zeros(channels_p, dtype=torch.float32, device=device)
         self._scratch = None
+        self._retired = []      # outgrown scratch buffers (graphs may reference them)
 
     def _update(self, M: int):
         if not self.update_running or M < 2:
@@ -56,6 +58,25 @@ class BatchNormBatch:
             self.running_mean.mul_(1 - m).add_(mean[s, :c], alpha=m)
             self.running_var.mul_(1 - m).add_(var[s, :c] * (M / (M - 1.0)), alpha=m)
 
+    def _update_segments_dev(self, mean: torch.Tensor, var: torch.Tensor,
+                             segments: torch.Tensor) -> None:
+        """``_update_segments`` on the device, without the host row counts (HIP
+        graph capture): the per-segment EMA steps in order collapse to
+        r = (1-m)^K r0 + sum_s m (1-m)^(valid segments after s) x_s over the K
+        segments with >= 2 rows (empty padding segments drop out)."""
+        if not self.update_running:
+            return
+        c, m = self.channels, self.momentum
+        rows = (segments[1:] - segments[:-1]).float()
+        valid = (rows >= 2).float()
+        k = valid.sum()
+        after = k - torch.cumsum(valid, 0)
+        w = valid * m * torch.exp(after * math.log1p(-m))
+        decay = torch.exp(k * math.log1p(-m))
+        unbiased = var[:, :c] * (rows / (rows - 1.0).clamp(min=1.0))[:, None]
+        self.running_mean.mul_(decay).add_(w @ mean[:, :c])
+        self.running_var.mul_(decay).add_(w @ unbiased)
+
     def forward_hip_f32(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,
                         out: Optional[torch.Tensor] = None,
                         segments: Optional[torch.Tensor] = None,
@@ -75,6 +96,9 @@ class BatchNormBatch:
         nseg = segments.numel() - 1
         need = k.bn_seg_scratch_floats(nseg, C)
         if self._scratch is None or self._scratch.numel() < need:
+            # a captured HIP graph may still point at the old scratch: keep it
+            if self._scratch is not None:
+                self._retired.append(self._scratch)
             self._scratch = torch.empty(need, dtype=torch.float32, device=y.device)
         mean = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
         var = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
@@ -88,8 +112,10 @@ class BatchNormBatch:
                            1 if relu else 0, M, C, Cs, z.shape[-1],
                            residual.shape[-1] if residual is not None else 0, stream)
         self.mean, self.var = mean[-1], var[-1]
-        if seg_rows is not None:
-            self._update_segments(mean, var, seg_rows)
+        # one closed-form update for all segments (equal to the per-segment EMA
+        # steps, _update_segments; tests/test_stages.py), a handful of kernels
+        # instead of ~4 per video
+        self._update_segments_dev(mean, var, segments)
         return z
 
     def forward_hip(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,
@@ -108,6 +134,8 @@ class BatchNormBatch:
             return z
         need = k.bn_scratch_floats(M, C)
         if self._scratch is None or self._scratch.numel() < need:
+            if self._scratch is not None:
+                self._retired.append(self._scratch)
             self._scratch = torch.empty(need, dtype=torch.float32, device=y.device)
         stream = torch.cuda.current_stream(y.device).cuda_stream
         k.bn_stats(y.data_ptr(), M, C, Cs, self._scratch.data_ptr(), self.mean.data_ptr(),

@@ -357,7 +357,12 @@ class ConvLayerF32:
         y = torch.empty(self.out_shape(x.shape), dtype=torch.float32, device=x.device)
         stream = torch.cuda.current_stream(x.device)
         best, best_t = None, None
+        verbose = os.environ.get("RNB_TUNE_VERBOSE") == "1"
         for cid in self.candidates():
+            if verbose:
+                print("[tune] %s x=%s res=%s cid=%d" % (
+                    self.name, tuple(x.shape), None if residual is None else
+                    tuple(residual.shape), cid), flush=True)
             self._launch_all(x, y, residual, cid, stream)       # warm
             start = torch.cuda.Event(enable_timing=True)
             end = torch.cuda.Event(enable_timing=True)

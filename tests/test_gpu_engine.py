@@ -193,7 +193,7 @@ def test_batch_bn_mode_hip_matches_torch_and_module():
     # statistics renormalise every layer, so bf16 rounding does not cancel)
     assert e_hip <= max(2.0 * e_tor, 3e-2 * scale)
     assert e_hip <= 8e-2 * scale
-    eng = build_engine(DEV, depth=18, bn_mode="batch", backend="hip")
+    eng = build_engine(DEV, depth=18, bn_mode="batch", backend="hip", dtype="bf16")
     assert isinstance(eng, R2P1DEngine) and eng.bn_mode == "batch"
 
 

@@ -321,3 +321,23 @@ def test_winograd_temporal_weight_layout_reproduces_the_conv():
             out[o, 4 * tt:4 * tt + 4] = AT @ M
     ref = F.conv2d(x, w[:, :, :, 0], padding=(1, 0))[0]
     assert (out[:, :T] - ref).abs().max().item() < 1e-4
+
+
+def test_bn_device_running_update_equals_sequential_segments():
+    """The graph-capturable running-statistics update (one closed form over
+    all segments, empty padding segments dropped) equals the per-segment EMA
+    steps the reference's one-video forwards perform."""
+    from rnb_amd.ops.bn import BatchNormBatch
+    torch.manual_seed(0)
+    bn = torch.nn.BatchNorm3d(12)
+    bn.running_mean.uniform_(-1, 1)
+    bn.running_var.uniform_(0.5, 2)
+    a = BatchNormBatch(bn, 12, torch.device("cpu"))
+    b = BatchNormBatch(bn, 12, torch.device("cpu"))
+    rows = [40, 1, 75, 0, 300, 0, 0]                  # a 1-row video and padding
+    seg = torch.tensor([0] + list(torch.tensor(rows).cumsum(0)), dtype=torch.int32)
+    mean, var = torch.randn(len(rows), 12), torch.rand(len(rows), 12) + 0.1
+    a._update_segments(mean, var, rows)
+    b._update_segments_dev(mean, var, seg)
+    assert torch.allclose(a.running_mean, b.running_mean, atol=1e-6)
+    assert torch.allclose(a.running_var, b.running_var, atol=1e-6)
