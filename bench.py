@@ -65,10 +65,12 @@ def parse_args(argv=None):
     ap.add_argument("--segments", type=int, default=None,
                     help="(segment) segments per video (default min(4, GPUs), >= 2)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
-    ap.add_argument("--bn", default="eval", choices=["eval", "batch"],
-                    help="eval: BatchNorm folded into the convs (inference numerics); "
-                         "batch: the reference's training-mode BN, statistics per video "
-                         "(fp32 only, eager: no HIP graphs)")
+    ap.add_argument("--bn", default="batch", choices=["eval", "batch"],
+                    help="batch (default): the reference's numerics -- it never calls "
+                         ".eval(), so every BatchNorm normalises with the statistics of "
+                         "the video being served (per-video segments when videos are "
+                         "batched; fp32, HIP-graphed); eval: BatchNorm folded into the "
+                         "convs (inference numerics, faster)")
     ap.add_argument("--depth", type=int, default=34)
     ap.add_argument("--videos-per-step", type=int, default=256,
                     help="videos arriving per GPU per step")
@@ -493,6 +495,8 @@ def run_fused(args) -> int:
                        "global_batch": vps * world, "seq_len": 8,
                        "parallelism": "dp%d (replicated runners)" % world,
                        "pipeline": "fused (single-process engine, not the RnB launcher)",
+                       "bn": "eval (folded into the convs; the fused engine has no batch-BN "
+                             "mode, so --bn does not apply)",
                        "video_batch": vb, "clips_per_batch": args.clips_per_batch,
                        "packing": args.packing, "bucket_step": bstep,
                        "replicas_per_gpu": args.fused_replicas,

@@ -175,6 +175,27 @@ __global__ __launch_bounds__(256) void bn_seg_finalize_f32_kernel(
   var[(size_t)s * C + c] = fmaxf(s2 / (float)rows - m1 * m1, 0.f);
 }
 
+// running statistics after one forward per segment, in segment order (what
+// the reference's one-video forwards leave behind): thread per channel,
+// segments with < 2 rows skipped (torch raises on them; empty = padding)
+__global__ __launch_bounds__(256) void bn_seg_running_f32_kernel(
+    const int* __restrict__ seg, int nseg, const float* __restrict__ mean,
+    const float* __restrict__ var, int C, int channels, float momentum,
+    float* __restrict__ running_mean, float* __restrict__ running_var) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= channels) return;
+  float rm = running_mean[c], rv = running_var[c];
+  for (int s = 0; s < nseg; ++s) {
+    const int rows = seg[s + 1] - seg[s];
+    if (rows < 2) continue;
+    rm = (1.f - momentum) * rm + momentum * mean[(size_t)s * C + c];
+    rv = (1.f - momentum) * rv +
+         momentum * var[(size_t)s * C + c] * ((float)rows / (float)(rows - 1));
+  }
+  running_mean[c] = rm;
+  running_var[c] = rv;
+}
+
 // RPT consecutive rows x 4 channels per thread; the first row's segment by
 // binary search, later rows step forward across segment boundaries
 #define BN_APPLY_RPT 4
@@ -249,6 +270,18 @@ int rnb_bn_seg_stats_f32(const float* y, const int* seg, int nseg, int C, int st
                      scratch);
   hipLaunchKernelGGL(bn_seg_finalize_f32_kernel, fgrid, dim3(256), 0, stream, y, seg, C, stride,
                      (const float*)scratch, mean, var);
+  return (int)hipGetLastError();
+}
+
+// running_mean / running_var: [channels] fp32, updated in place
+int rnb_bn_seg_running_f32(const int* seg, int nseg, const float* mean, const float* var, int C,
+                           int channels, float momentum, float* running_mean,
+                           float* running_var, hipStream_t stream) {
+  if (nseg <= 0 || channels <= 0) return 0;
+  if (channels > C) return -2;
+  hipLaunchKernelGGL(bn_seg_running_f32_kernel, dim3((channels + 255) / 256), dim3(256), 0,
+                     stream, seg, nseg, mean, var, C, channels, momentum, running_mean,
+                     running_var);
   return (int)hipGetLastError();
 }
 

@@ -112,10 +112,11 @@ class BatchNormBatch:
                            1 if relu else 0, M, C, Cs, z.shape[-1],
                            residual.shape[-1] if residual is not None else 0, stream)
         self.mean, self.var = mean[-1], var[-1]
-        # one closed-form update for all segments (equal to the per-segment EMA
-        # steps, _update_segments; tests/test_stages.py), a handful of kernels
-        # instead of ~4 per video
-        self._update_segments_dev(mean, var, segments)
+        if self.update_running:
+            # the per-segment EMA steps in order, one kernel (thread per channel)
+            k.bn_seg_running_f32(segments.data_ptr(), nseg, mean.data_ptr(), var.data_ptr(), C,
+                                 self.channels, self.momentum, self.running_mean.data_ptr(),
+                                 self.running_var.data_ptr(), stream)
         return z
 
     def forward_hip(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,

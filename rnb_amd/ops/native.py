@@ -232,6 +232,10 @@ class Kernels:
                                              ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_void_p]
+        lib.rnb_bn_seg_running_f32.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_float, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_void_p]
         lib.rnb_bn_seg_apply_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                              ctypes.c_void_p, ctypes.c_void_p,
@@ -379,6 +383,12 @@ class Kernels:
                          stream):
         _check(self.lib.rnb_bn_seg_stats_f32(y_ptr, seg_ptr, nseg, C, stride, scratch_ptr,
                                              mean_ptr, var_ptr, stream), "bn_seg_stats_f32")
+
+    def bn_seg_running_f32(self, seg_ptr, nseg, mean_ptr, var_ptr, C, channels, momentum,
+                           rmean_ptr, rvar_ptr, stream):
+        _check(self.lib.rnb_bn_seg_running_f32(seg_ptr, nseg, mean_ptr, var_ptr, C, channels,
+                                               momentum, rmean_ptr, rvar_ptr, stream),
+               "bn_seg_running_f32")
 
     def bn_seg_apply_f32(self, y_ptr, z_ptr, res_ptr, seg_ptr, nseg, mean_ptr, var_ptr,
                          gamma_ptr, beta_ptr, eps, relu, M, C, y_stride, z_stride, res_stride,

@@ -227,6 +227,10 @@ def test_bn_per_video_stats_f32_kernel_matches_torch(res, relu):
     torch.cuda.synchronize()
     err = (z.cpu() - ref).abs().max().item()
     assert err < 1e-4 * ref.abs().max().item(), err
+    # running statistics: the device kernel's in-order EMA over the videos vs
+    # the torch reference's per-video updates
+    assert torch.allclose(op.running_mean.cpu(), ref_op.running_mean, atol=1e-5)
+    assert torch.allclose(op.running_var.cpu(), ref_op.running_var, rtol=1e-4, atol=1e-5)
 
 
 def test_r34_f32_batch_bn_two_videos_match_module_per_video():
