@@ -56,6 +56,12 @@ struct WinoParams {
   int tiles_h, tiles_w, n_tiles, n_tblocks, n_cblocks;
   uint32_t x_bytes, u_bytes;
   uint32_t m_tw, s_tw, m_th, s_th;   // magic division by tiles_w, tiles_h
+  // temporal kernel only: training-mode BN + ReLU of the INPUT applied on load
+  // (the producer's BatchNorm deferred into this conv): x is the raw conv
+  // output; element = relu(x * scale + shift) with per-video scale / shift
+  // in_ss [nseg][2][Cin] and clip_seg [F] = video of each clip. Null = off.
+  const float* in_ss;
+  const int* clip_seg;
 };
 
 #define WINO_INVALID 0xFFFFFFF0u
@@ -361,6 +367,10 @@ __global__ __launch_bounds__(256, 2) void conv_winot_f32_kernel(const WinoParams
   for (int e = 0; e < 6; ++e) fmask |= (tvalid && fr0 + e >= 0 && fr0 + e < T) ? (1 << e) : 0;
   const int pix0 = (n * T + fr0) * HW + hw;       // may be negative (padding)
   const int frame_bytes = HW * p.Cin * 4;
+  // deferred input BN: this lane's video's scale / shift rows
+  const bool aff = p.in_ss != nullptr;            // uniform
+  const float* ssb = nullptr;
+  if (aff) ssb = p.in_ss + (size_t)(tvalid ? p.clip_seg[n] : 0) * 2 * p.Cin + 4 * q;
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ur =
@@ -437,21 +447,44 @@ __global__ __launch_bounds__(256, 2) void conv_winot_f32_kernel(const WinoParams
   };
 
   const int nchunks = p.Cin / 16;
+  // deferred BN + ReLU on the patch (padding frames stay zero: the reference
+  // pads the normalised tensor)
+  auto affine = [&](wf32x4 (&v)[6], const wf32x4& sc, const wf32x4& sh) {
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      const bool ok = ((fmask >> e) & 1) != 0;
+      wf32x4 t = v[e] * sc + sh;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t[k] = ok ? fmaxf(t[k], 0.f) : 0.f;
+      v[e] = t;
+    }
+  };
   wf32x4 d[6];
+  wf32x4 sc = (wf32x4){1.f, 1.f, 1.f, 1.f}, sh = (wf32x4){0.f, 0.f, 0.f, 0.f};
   issue_u(0, 0);
 #pragma unroll
   for (int e = 0; e < 6; ++e) d[e] = load_one(0, e);
+  if (aff) {
+    sc = *(const wf32x4*)ssb;
+    sh = *(const wf32x4*)(ssb + p.Cin);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int c = 0; c + 1 < nchunks; ++c) {
     const int cur = c & 1;
     issue_u(c + 1, cur ^ 1);
     asm volatile("" ::: "memory");
+    if (aff) affine(d, sc, sh);
     transform(d);
     gemm(lds + cur * U_BYTES, d, c + 1, std::true_type{});
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");    // U landed; 6 refills may fly
+    if (aff) {                                            // next chunk's scale / shift
+      sc = *(const wf32x4*)(ssb + (c + 1) * 16);
+      sh = *(const wf32x4*)(ssb + p.Cin + (c + 1) * 16);
+    }
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");    // U landed (6 younger loads may fly)
     __syncthreads();
   }
+  if (aff) affine(d, sc, sh);
   transform(d);
   gemm(lds + ((nchunks - 1) & 1) * U_BYTES, d, -1, std::false_type{});
 

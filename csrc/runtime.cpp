@@ -82,6 +82,8 @@ int rnb_stream_wait_event(void* stream, void* ev) {
 
 int rnb_event_synchronize(void* ev) { return (int)hipEventSynchronize((hipEvent_t)ev); }
 
+int rnb_event_query(void* ev) { return (int)hipEventQuery((hipEvent_t)ev); }
+
 int rnb_event_destroy(void* ev) { return (int)hipEventDestroy((hipEvent_t)ev); }
 
 int rnb_memcpy_async(void* dst, const void* src, size_t bytes, void* stream) {

@@ -201,6 +201,20 @@ class R2P1DEngine:
         for name, i in last.items():
             if name not in ("x", self.out_name):
                 self._free_after[i].append(name)
+        # bn_mode='batch': a BN + ReLU whose output feeds only the next conv
+        # (the spatial->temporal intermediate) may be applied by that conv on
+        # load (temporal Winograd kernel) instead of a separate pass
+        uses = {}
+        for op in self.ops:
+            uses[op.src] = uses.get(op.src, 0) + 1
+            if op.res is not None:
+                uses[op.res] = uses.get(op.res, 0) + 1
+        self._defer_ok = [
+            i + 1 < len(self.ops) and op.bn is not None and op.bn_relu and op.res is None
+            and self.f32 and uses.get(op.dst, 0) == 1 and self.ops[i + 1].src == op.dst
+            and self.ops[i + 1].bn is not None
+            and getattr(self.ops[i + 1].layer, "winot_ok", False)
+            for i, op in enumerate(self.ops)]
 
     # ------------------------------------------------------------- metadata
     @property
@@ -279,6 +293,8 @@ class R2P1DEngine:
         hip = self.backend == "hip"
         bufs: Dict[str, torch.Tensor] = {"x": x}
         coffs = None
+        defer = os.environ.get("RNB_BN_DEFER", "1") != "0"
+        clip_seg = None              # video index of each clip (deferred BN)
         if self.bn_mode == "batch" and clip_offsets_dev is not None and hip:
             coffs = clip_offsets_dev
             clip_offsets = None
@@ -290,6 +306,7 @@ class R2P1DEngine:
                 coffs = torch.tensor(clip_offsets, dtype=torch.int32).to(x.device,
                                                                           non_blocking=True)
         skip = False
+        pending = None               # deferred (scale_shift, clip_seg) for the next conv
         free_after = self._free_after
         for i, op in enumerate(self.ops):
             if skip:                      # temporal half of a fused pair
@@ -309,16 +326,30 @@ class R2P1DEngine:
             res = bufs[op.res] if op.res is not None else None
             if op.bn is not None:
                 if hip:
-                    y = op.layer.forward_hip(src, None)
+                    if pending is not None:
+                        y = op.layer.forward_hip(src, None, in_affine=pending)
+                        pending = None
+                    else:
+                        y = op.layer.forward_hip(src, None)
                     seg = rows = None
+                    thw = y.shape[1] * y.shape[2] * y.shape[3]
                     if coffs is not None:
-                        thw = y.shape[1] * y.shape[2] * y.shape[3]
                         seg = coffs * thw
                         if clip_offsets is not None:
                             rows = [(b - a) * thw for a, b in zip(clip_offsets[:-1],
                                                                   clip_offsets[1:])]
-                    y = op.bn.forward_hip(y, res, op.bn_relu, out=y, segments=seg,
-                                          seg_rows=rows)
+                    if (defer and self._defer_ok[i] and self.f32
+                            and self.ops[i + 1].layer.accepts_input_affine(y.shape)):
+                        # statistics now; normalise + ReLU inside the next conv
+                        if seg is None:
+                            seg = torch.tensor([0, y.shape[0] * thw], dtype=torch.int32,
+                                               device=y.device)
+                        if clip_seg is None:
+                            clip_seg = self._clip_segments(coffs, x.shape[0], x.device)
+                        pending = (op.bn.scale_shift_f32(y, seg), clip_seg)
+                    else:
+                        y = op.bn.forward_hip(y, res, op.bn_relu, out=y, segments=seg,
+                                              seg_rows=rows)
                 else:
                     y = op.layer.forward_torch(src, None, out_dtype=self.dtype)
                     y = op.bn.forward_torch(y, res, op.bn_relu, out_dtype=self.dtype,
@@ -343,6 +374,18 @@ class R2P1DEngine:
         return y
 
     __call__ = forward
+
+    @staticmethod
+    def _clip_segments(coffs: Optional[torch.Tensor], n: int, device) -> torch.Tensor:
+        """int32 [n]: the video (segment) of each clip, from the clip offsets
+        (device tensor, may carry trailing empty videos; None = one video)."""
+        if coffs is None:
+            return torch.zeros(n, dtype=torch.int32, device=device)
+        idx = torch.arange(n, dtype=coffs.dtype, device=device)
+        # bucket padding clips (>= the last offset) land past the last video:
+        # clamp them onto it (their rows are never returned)
+        seg = torch.searchsorted(coffs[1:].contiguous(), idx, right=True)
+        return seg.clamp_(max=coffs.numel() - 2).to(torch.int32).contiguous()
 
     def autotune(self, n: int, reps: int = 3) -> Dict[str, int]:
         """Pick the fastest tile per conv for ``n`` clips (GPU only)."""

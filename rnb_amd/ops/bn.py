@@ -119,6 +119,34 @@ class BatchNormBatch:
                                  self.running_var.data_ptr(), stream)
         return z
 
+    def scale_shift_f32(self, y: torch.Tensor, segments: torch.Tensor) -> torch.Tensor:
+        """Statistics only (plus the running update), for a BN whose apply is
+        deferred into the consuming conv: [nseg, 2, Cp] fp32 rows (scale =
+        gamma * rsqrt(var + eps), shift = beta - mean * scale) per segment."""
+        from .native import kernels
+        k = kernels()
+        N, T, H, W, Cs = y.shape
+        C = self.channels_p
+        nseg = segments.numel() - 1
+        need = k.bn_seg_scratch_floats(nseg, C)
+        if self._scratch is None or self._scratch.numel() < need:
+            if self._scratch is not None:
+                self._retired.append(self._scratch)
+            self._scratch = torch.empty(need, dtype=torch.float32, device=y.device)
+        mean = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
+        var = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
+        stream = torch.cuda.current_stream(y.device).cuda_stream
+        k.bn_seg_stats_f32(y.data_ptr(), segments.data_ptr(), nseg, C, Cs,
+                           self._scratch.data_ptr(), mean.data_ptr(), var.data_ptr(), stream)
+        if self.update_running:
+            k.bn_seg_running_f32(segments.data_ptr(), nseg, mean.data_ptr(), var.data_ptr(), C,
+                                 self.channels, self.momentum, self.running_mean.data_ptr(),
+                                 self.running_var.data_ptr(), stream)
+        scale = self.gamma * torch.rsqrt(var + self.eps)
+        shift = self.beta - mean * scale
+        self.mean, self.var = mean[-1], var[-1]
+        return torch.stack([scale, shift], dim=1).contiguous()
+
     def forward_hip(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,
                     out: Optional[torch.Tensor] = None, segments=None,
                     seg_rows=None) -> torch.Tensor:

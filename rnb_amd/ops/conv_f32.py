@@ -167,7 +167,7 @@ class ConvLayerF32:
         c = list(range(len(kernels().f32_configs)))
         return c + sorted(self.wino_ids)
 
-    def _launch_wino(self, x, y, residual, cid, stream):
+    def _launch_wino(self, x, y, residual, cid, stream, in_affine=None):
         from .native import WinoParams, kernels
         ft = cid in WINOT_TC
         if ft:
@@ -202,6 +202,18 @@ class ConvLayerF32:
         p.Cout, p.y_stride = g.cout_p, y.shape[-1]
         p.res_stride = residual.shape[-1] if residual is not None else 0
         p.relu = 1 if self.relu else 0
+        if in_affine is not None:
+            ss, clip_seg = in_affine
+            if not ft:
+                raise ValueError("%s: deferred input BN needs the temporal Winograd kernel"
+                                 % self.name)
+            if (ss.dim() != 3 or ss.shape[1:] != (2, C) or ss.dtype != torch.float32
+                    or not ss.is_contiguous() or clip_seg.dtype != torch.int32
+                    or clip_seg.numel() != N):
+                raise ValueError("%s: input BN scale/shift %s / clip_seg %s do not match x %s"
+                                 % (self.name, tuple(ss.shape), tuple(clip_seg.shape),
+                                    tuple(x.shape)))
+            p.in_ss, p.clip_seg = ss.data_ptr(), clip_seg.data_ptr()
         if ft:
             kernels().winot_f32(p, variant, stream.cuda_stream)
         else:
@@ -324,7 +336,7 @@ class ConvLayerF32:
             self._config[key] = cid
         return cid
 
-    def _launch_all(self, x, y, residual, cid, stream):
+    def _launch_all(self, x, y, residual, cid, stream, in_affine=None):
         from .native import kernels
         k = kernels()
         N = x.shape[0]
@@ -333,10 +345,13 @@ class ConvLayerF32:
                                     residual.shape[-1] if residual is not None else 0)
             for n0 in range(0, N, step):
                 n1 = min(N, n0 + step)
+                aff = None if in_affine is None else (in_affine[0], in_affine[1][n0:n1])
                 self._launch_wino(x[n0:n1], y[n0:n1],
                                   residual[n0:n1] if residual is not None else None, cid,
-                                  stream)
+                                  stream, aff)
             return
+        if in_affine is not None:
+            raise ValueError("%s: deferred input BN needs a Winograd config" % self.name)
         step = self.chunk_clips(x.shape, y.shape,
                                 residual.shape[-1] if residual is not None else 0)
         for n0 in range(0, N, step):
@@ -379,8 +394,17 @@ class ConvLayerF32:
         return best
 
     # ------------------------------------------------------------------
+    def accepts_input_affine(self, x_shape) -> bool:
+        """True when this conv's kernel for ``x_shape`` can apply its input's
+        BatchNorm + ReLU on load (``forward_hip(in_affine=...)``)."""
+        return self.config_for(x_shape) in WINOT_TC
+
     def forward_hip(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                    out: Optional[torch.Tensor] = None, config: Optional[int] = None):
+                    out: Optional[torch.Tensor] = None, config: Optional[int] = None,
+                    in_affine=None):
+        """``in_affine`` = (scale_shift [nseg, 2, Cin], clip_seg int32 [N]): x is
+        the raw output of a conv whose BatchNorm + ReLU (per video) is applied
+        here on load (temporal Winograd configs only)."""
         if x.dtype != torch.float32 or not x.is_contiguous():
             raise ValueError("%s: expected contiguous fp32 NDHWC input" % self.name)
         y = out if out is not None else torch.empty(self.out_shape(x.shape),
@@ -395,7 +419,7 @@ class ConvLayerF32:
         if x.shape[0] == 0:
             return y
         cid = self.config_for(x.shape) if config is None else config
-        self._launch_all(x, y, residual, cid, torch.cuda.current_stream(x.device))
+        self._launch_all(x, y, residual, cid, torch.cuda.current_stream(x.device), in_affine)
         return y
 
     def forward_torch(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,

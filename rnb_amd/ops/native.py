@@ -154,6 +154,7 @@ class WinoParams(ctypes.Structure):
         ("x_bytes", ctypes.c_uint32), ("u_bytes", ctypes.c_uint32),
         ("m_tw", ctypes.c_uint32), ("s_tw", ctypes.c_uint32),
         ("m_th", ctypes.c_uint32), ("s_th", ctypes.c_uint32),
+        ("in_ss", ctypes.c_void_p), ("clip_seg", ctypes.c_void_p),
     ]
 
 
@@ -471,6 +472,7 @@ class Runtime:
         lib.rnb_event_record.argtypes = [vp, vp]
         lib.rnb_stream_wait_event.argtypes = [vp, vp]
         lib.rnb_event_synchronize.argtypes = [vp]
+        lib.rnb_event_query.argtypes = [vp]
         lib.rnb_event_destroy.argtypes = [vp]
         lib.rnb_can_access_peer.argtypes = [ctypes.c_int, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_int)]
@@ -526,6 +528,16 @@ class Runtime:
 
     def stream_wait_event(self, stream: int, ev: int) -> None:
         _check(self.lib.rnb_stream_wait_event(stream, ev), "hipStreamWaitEvent")
+
+    def try_stream_wait_event(self, stream: int, ev: int) -> int:
+        """hipStreamWaitEvent's error code (0 = ok) instead of raising."""
+        return int(self.lib.rnb_stream_wait_event(stream, ev))
+
+    def event_synchronize(self, ev: int) -> None:
+        _check(self.lib.rnb_event_synchronize(ev), "hipEventSynchronize")
+
+    def event_query(self, ev: int) -> int:
+        return int(self.lib.rnb_event_query(ev))
 
     def memcpy_async(self, dst: int, src: int, nbytes: int, stream: int) -> None:
         _check(self.lib.rnb_memcpy_async(dst, src, nbytes, stream), "hipMemcpyAsync")

@@ -217,6 +217,9 @@ def device_view(ptr: int, shape, dtype, device) -> torch.Tensor:
     return torch.as_tensor(_CudaArray(ptr, shape, dtype), device=device)
 
 
+HIP_ERROR_NOT_READY = 600
+
+
 class IpcRing(RingBase):
     """Producer-owned HBM slots exported through HIP IPC (native runtime).
 
@@ -263,6 +266,7 @@ class IpcRing(RingBase):
         self._cid = None           # consumer id of this process
         self._rev = None           # consumer: own release events [slot]
         self._wopen: Dict[Tuple, List[int]] = {}              # consumer: opened written events
+        self.stale_event_waits = 0      # stream waits ROCm refused on completed events
         self._dev = None
         self._views = None
         self._token = None
@@ -362,7 +366,27 @@ class IpcRing(RingBase):
             return
         from ..ops import native
         stream = stream or torch.cuda.current_stream(self._dev)
-        native.runtime().stream_wait_event(stream.cuda_stream, self._release_event(cid, idx))
+        self._wait_ipc_event(stream, self._release_event(cid, idx), idx)
+
+    def _wait_ipc_event(self, stream, ev: int, idx: int) -> None:
+        """Order ``stream`` after an interprocess event. ROCm's IPC events can
+        refuse a stream wait on a record that has already completed (seen at
+        high slot-reuse rates: hipErrorInvalidValue while hipEventQuery says
+        hipSuccess). Complete means the ordered work is done: go on; still
+        pending: wait on the host; any other state: fail."""
+        from ..ops import native
+        rt = native.runtime()
+        rc = rt.try_stream_wait_event(stream.cuda_stream, ev)
+        if rc == 0:
+            return
+        q = rt.event_query(ev)
+        if q == HIP_ERROR_NOT_READY:
+            rt.event_synchronize(ev)
+            q = rt.event_query(ev)
+        if q != 0:
+            raise RuntimeError("ring %s: hipStreamWaitEvent on slot %d failed (%d), "
+                               "hipEventQuery %d" % (self.name, idx, rc, q))
+        self.stale_event_waits += 1
 
     def commit(self, idx: int, rows: Sequence[int], stream=None) -> int:
         """Publish slot ``idx`` holding ``rows`` valid rows per tensor (its data
@@ -453,7 +477,7 @@ class IpcRing(RingBase):
         if gpu:
             stream = torch.cuda.current_stream(dev)
             if self.gpu_ordered:
-                rt.stream_wait_event(stream.cuda_stream, self._wopen[tuple(descriptor[:2])][idx])
+                self._wait_ipc_event(stream, self._wopen[tuple(descriptor[:2])][idx], idx)
         for t, (ph, b) in enumerate(zip(placeholders, self.valid_rows(idx))):
             if b:
                 if b > ph.shape[0] or not ph.is_contiguous():

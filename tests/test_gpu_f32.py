@@ -373,3 +373,30 @@ def test_graphed_batch_bn_per_video_matches_eager_and_module():
     # vs replaying the same per-segment EMA steps on the host
     bns = [op.bn for op in g.engine.ops if op.bn is not None]
     assert any((b.running_mean - r).abs().max().item() > 0 for b, r in zip(bns, r0))
+
+
+def test_deferred_batch_bn_into_temporal_winograd_matches_separate_apply(monkeypatch):
+    """bn_mode='batch': the spatial conv's BatchNorm + ReLU applied on load by
+    the temporal Winograd kernel (per-video scale/shift, padding frames kept
+    at zero) equals the separate BN apply pass, and the fp32 module per video."""
+    from rnb_amd.models.r2p1d.model import build_network
+    from rnb_amd.models.r2p1d.engine import R2P1DEngine
+    from rnb_amd.models.r2p1d.decoder import SyntheticDecoder
+    eng = R2P1DEngine(build_network(1, 5, depth=18, seed=6), DEV, backend="hip",
+                      bn_mode="batch", dtype="fp32")
+    mod = R2P1DEngine(build_network(1, 5, depth=18, seed=6), DEV, backend="module",
+                      bn_mode="batch", dtype="fp32")
+    assert any(eng._defer_ok)
+    dec = SyntheticDecoder(DEV, dtype=torch.float32)
+    x = torch.cat([dec.decode(1, [0, 40, 80]), dec.decode(2, [10, 60]), dec.decode(5, [7])])
+    offs = [0, 3, 5, 6]
+    with torch.no_grad():
+        monkeypatch.setenv("RNB_BN_DEFER", "1")
+        a = eng.forward(x, clip_offsets=offs).clone()
+        monkeypatch.setenv("RNB_BN_DEFER", "0")
+        b = eng.forward(x, clip_offsets=offs).clone()
+        ref = torch.cat([mod.forward(x[p:q]) for p, q in zip(offs[:-1], offs[1:])])
+    torch.cuda.synchronize()
+    scale = ref.abs().max().item()
+    assert (a - b).abs().max().item() <= 2e-5 * scale
+    assert (a - ref).abs().max().item() <= 1e-3 * scale
