@@ -84,6 +84,10 @@ int rnb_event_synchronize(void* ev) { return (int)hipEventSynchronize((hipEvent_
 
 int rnb_event_query(void* ev) { return (int)hipEventQuery((hipEvent_t)ev); }
 
+// returns and clears the thread's last HIP error (a tolerated failure must not
+// surface later through a kernel wrapper's hipGetLastError)
+int rnb_clear_last_error() { return (int)hipGetLastError(); }
+
 int rnb_event_destroy(void* ev) { return (int)hipEventDestroy((hipEvent_t)ev); }
 
 int rnb_memcpy_async(void* dst, const void* src, size_t bytes, void* stream) {

@@ -473,6 +473,7 @@ class Runtime:
         lib.rnb_stream_wait_event.argtypes = [vp, vp]
         lib.rnb_event_synchronize.argtypes = [vp]
         lib.rnb_event_query.argtypes = [vp]
+        lib.rnb_clear_last_error.argtypes = []
         lib.rnb_event_destroy.argtypes = [vp]
         lib.rnb_can_access_peer.argtypes = [ctypes.c_int, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_int)]
@@ -535,6 +536,9 @@ class Runtime:
 
     def event_synchronize(self, ev: int) -> None:
         _check(self.lib.rnb_event_synchronize(ev), "hipEventSynchronize")
+
+    def clear_last_error(self) -> int:
+        return int(self.lib.rnb_clear_last_error())
 
     def event_query(self, ev: int) -> int:
         return int(self.lib.rnb_event_query(ev))

@@ -379,6 +379,7 @@ class IpcRing(RingBase):
         rc = rt.try_stream_wait_event(stream.cuda_stream, ev)
         if rc == 0:
             return
+        rt.clear_last_error()        # else the next kernel launch check reports it
         q = rt.event_query(ev)
         if q == HIP_ERROR_NOT_READY:
             rt.event_synchronize(ev)
