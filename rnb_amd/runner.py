@@ -28,6 +28,9 @@ from queue import Empty, Full
 NUM_EXIT_MARKERS = 10
 NUM_SUMMARY_SKIPS = 10
 QUEUE_POLL_S = 0.1
+# with RNB_ADAPTIVE_GATHER=1, consumer-side batching keeps gathering at most this
+# long while the replica's previous batch still runs on the GPU
+INFLIGHT_GATHER_S = 0.05
 
 
 def _set_flag(flag, value, only_if_unset=True):
@@ -133,6 +136,9 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         # buffer their rows are pulled into (RunnerModel.gather_limits)
         gather = getattr(model, "gather_limits", None)
         gather = gather() if callable(gather) else None
+        # measured neutral on throughput at 1 GPU (profiles/NOTES.md): opt-in
+        adaptive_gather = os.environ.get("RNB_ADAPTIVE_GATHER", "0") == "1"
+        inflight = None             # completion event of this replica's last batch
         # producer writes straight into its output slot (no staging copy)
         direct_out = (shared_output_ring is not None and num_segments == 1
                       and callable(getattr(model, "call_into", None))
@@ -325,13 +331,24 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 # every item's rows straight into the model's input buffer
                 max_items, max_rows, max_wait_s = gather
                 items, rows = [tpl], rows_of(signal)
-                deadline = time.time() + max_wait_s
+                t0 = time.time()
+                deadline = t0 + max_wait_s
                 while len(items) < max_items and rows < max_rows:
+                    # while this replica's previous batch is still running on
+                    # the GPU, a launch now would only queue behind it: keep
+                    # gathering (bounded), so batches grow with the load
+                    busy = (inflight is not None and not inflight.query()
+                            and time.time() - t0 < INFLIGHT_GATHER_S)
                     try:
                         wait = deadline - time.time()
-                        nxt = input_queue.get_nowait() if wait <= 0 else \
-                            input_queue.get(timeout=wait)
+                        if busy:
+                            nxt = input_queue.get(timeout=max(wait, 0.0005))
+                        else:
+                            nxt = input_queue.get_nowait() if wait <= 0 else \
+                                input_queue.get(timeout=wait)
                     except Empty:
+                        if busy:
+                            continue
                         break
                     if nxt is None:
                         continue            # end-of-stream wake-up marker
@@ -384,6 +401,9 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 tick("model")
                 if not emit(outputs, gslot):
                     break
+                if stream is not None and adaptive_gather:
+                    inflight = torch.cuda.Event()
+                    inflight.record(stream)
                 tick("emit")
                 continue
             if direct_out:
@@ -424,6 +444,21 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                   % (step_idx, group_idx, instance_idx, g_idx, gstats["calls"],
                      gstats["items"] / gstats["calls"], gstats["rows"] / gstats["calls"]),
                   flush=True)
+        def _rings(x):
+            if isinstance(x, dict):
+                x = list(x.values())
+            if isinstance(x, (list, tuple)):
+                for y in x:
+                    yield from _rings(y)
+            elif x is not None:
+                yield x
+        stale = sum(getattr(r, "stale_event_waits", 0) for r in _rings(shared_input_rings))
+        stale_out = getattr(shared_output_ring, "stale_event_waits", 0) \
+            if shared_output_ring is not None else 0
+        if stale or stale_out:
+            print("[runner %d/%d/%d gpu %d] IPC stream waits refused by ROCm on completed "
+                  "events: %d on input rings, %d on the output ring"
+                  % (step_idx, group_idx, instance_idx, g_idx, stale, stale_out), flush=True)
         # ---- shutdown
         if not is_final_step:
             try:
