@@ -59,9 +59,13 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pipeline", default="global",
+    ap.add_argument("--pipeline", default="aggressive",
                     choices=["global", "aggressive", "whole", "rnb", "two-stage", "segment",
-                             "fused"])
+                             "fused"],
+                    help="aggressive (default, BASELINE config #5): loaders and runner "
+                         "replicas per GPU with a queue per GPU -- at 1 GPU the same "
+                         "topology as global (one shared queue), at N GPUs no slot "
+                         "crosses xGMI; global shares one queue across all GPUs")
     ap.add_argument("--segments", type=int, default=None,
                     help="(segment) segments per video (default min(4, GPUs), >= 2)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])

@@ -176,6 +176,13 @@ def run(args) -> dict:
         spec = spec.on_cpu()
     if args.overrides:
         spec = spec.override_kwargs(_parse_overrides(args.overrides))
+    fold = int(os.environ.get("RNB_FOLD_GPUS", "0") or 0)
+    if fold > 0:
+        # rehearsal: logical GPU g runs on device g % fold (e.g. an 8-GPU
+        # topology on a 1-GPU box); every process, ring and queue is as at N
+        spec = spec.remap_gpus({g: g % fold for g in spec.gpus_used()})
+        print("[launcher] RNB_FOLD_GPUS=%d: logical GPUs folded onto %d device(s)"
+              % (fold, fold), flush=True)
     check_gpus(spec)
     _apply_batch_default(spec, args.batch_size)
     # slot rings sized from the consumers' batching and free HBM (amdsmi: no

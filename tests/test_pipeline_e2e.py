@@ -313,3 +313,25 @@ def test_bench_pipeline_configs_parse():
             cfg = bench.pipeline_config(args, n)
             sp = parse_pipeline(cfg)
             assert sp.gpus_used() == list(range(n)), (pipe, n)
+
+
+def test_bench_default_topology_is_per_gpu():
+    """bench.py's default pipeline (aggressive): at 1 GPU the same topology as
+    global, at N GPUs every runner queue is fed only by loaders on its own GPU
+    (no slot crosses xGMI in the driver's scaling runs)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    a1 = bench.pipeline_config(bench.parse_args([]), 1)
+    g1 = bench.pipeline_config(bench.parse_args(["--pipeline", "global"]), 1)
+    assert bench.parse_args([]).pipeline == "aggressive"
+    assert a1 == g1
+    cfg = bench.pipeline_config(bench.parse_args(["--gpus", "8"]), 8)
+    loader, runner = cfg["pipeline"]
+    feeds = {}
+    for grp in loader["queue_groups"]:
+        for q in grp["out_queues"]:
+            feeds.setdefault(q, set()).update(grp["gpus"])
+    for grp in runner["queue_groups"]:
+        assert feeds[grp["in_queue"]] == set(grp["gpus"]), grp
