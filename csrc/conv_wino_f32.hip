@@ -62,7 +62,42 @@ struct WinoParams {
   // in_ss [nseg][2][Cin] and clip_seg [F] = video of each clip. Null = off.
   const float* in_ss;
   const int* clip_seg;
+  // training-mode BN statistics of the OUTPUT, accumulated in the epilogue:
+  // out_stats [nseg][2][stats_c] fp64 (sum, sum of squares per video and
+  // channel; zeroed by the caller), video of clip n = clip_seg[n]; spatial
+  // frames map to clips as n = frame / clip_frames. Null = off.
+  double* out_stats;
+  int clip_frames, stats_c;
 };
+
+// Adds this lane's per-channel sums (4 output channels co..co+3, fp64) into
+// out_stats[seg]. When every valid tile of the wave belongs to one video (the
+// common case) the 16 tiles of each lane group are reduced with cross-lane
+// shuffles first and one lane per group commits: 8 fp64 atomics per group.
+static __device__ __forceinline__ void w_commit_stats(const WinoParams& p, int lane, bool valid,
+                                                      int seg, int co, double (&s1)[4],
+                                                      double (&s2)[4]) {
+  const int s0 = __builtin_amdgcn_readfirstlane(seg);     // lane 0's tile is valid if any is
+  const bool mixed = __ballot(valid && seg != s0) != 0;
+  if (!mixed) {
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s1[k] += __shfl_xor(s1[k], m);
+        s2[k] += __shfl_xor(s2[k], m);
+      }
+    if ((lane & 15) != 0 || !valid || co >= p.Cout) return;
+  } else if (!valid || co >= p.Cout) {
+    return;
+  }
+  double* d = p.out_stats + ((size_t)(mixed ? seg : s0) * 2) * p.stats_c + co;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    atomicAdd(d + k, s1[k]);
+    atomicAdd(d + p.stats_c + k, s2[k]);
+  }
+}
 
 #define WINO_INVALID 0xFFFFFFF0u
 
@@ -283,13 +318,19 @@ __global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f
   }
 
   // ---- output transform Y = A^T M A + epilogue (lane: tile tl, 4 channels) ----
-  if (!tvalid) return;
+  const bool stats = p.out_stats != nullptr;        // uniform
+  if (!tvalid && !stats) return;
   const int oy = 2 * ty, ox = 2 * tx;
   const bool has_res = p.res != nullptr;
+  const int seg = (stats && tvalid) ? p.clip_seg[f / p.clip_frames] : 0;
 #pragma unroll
   for (int tc = 0; tc < TC; ++tc) {
     const int co = cb * CT + tc * 16 + 4 * q;
-    if (co >= p.Cout) continue;
+    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+    if (co >= p.Cout || !tvalid) {
+      if (stats) w_commit_stats(p, lane, false, seg, co, s1, s2);
+      continue;
+    }
     wf32x4 t0[4], t1[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -319,7 +360,15 @@ __global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f
           for (int k = 0; k < 4; ++k) val[k] = fmaxf(val[k], 0.f);
         }
         *(float4*)(p.y + pix * p.y_stride + co) = make_float4(val[0], val[1], val[2], val[3]);
+        if (stats) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            s1[k] += (double)val[k];
+            s2[k] += (double)val[k] * (double)val[k];
+          }
+        }
       }
+    if (stats) w_commit_stats(p, lane, true, seg, co, s1, s2);
   }
 }
 
@@ -489,12 +538,18 @@ __global__ __launch_bounds__(256, 2) void conv_winot_f32_kernel(const WinoParams
   gemm(lds + ((nchunks - 1) & 1) * U_BYTES, d, -1, std::false_type{});
 
   // ---- Y = A^T M (4 frames) + epilogue (lane: tile tl, channels 4q..4q+3) ----
-  if (!tvalid) return;
+  const bool stats = p.out_stats != nullptr;        // uniform
+  if (!tvalid && !stats) return;
   const bool has_res = p.res != nullptr;
+  const int seg = (stats && tvalid) ? p.clip_seg[n] : 0;
 #pragma unroll
   for (int tc = 0; tc < TC; ++tc) {
     const int co = cb * CT + tc * 16 + 4 * q;
-    if (co >= p.Cout) continue;
+    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+    if (co >= p.Cout || !tvalid) {
+      if (stats) w_commit_stats(p, lane, false, seg, co, s1, s2);
+      continue;
+    }
     const float4 b4 = *(const float4*)(p.bias + co);
     const wf32x4 bias = (wf32x4){b4.x, b4.y, b4.z, b4.w};
     const wf32x4 m0 = acc[0][tc], m1 = acc[1][tc], m2 = acc[2][tc], m3 = acc[3][tc],
@@ -519,7 +574,15 @@ __global__ __launch_bounds__(256, 2) void conv_winot_f32_kernel(const WinoParams
         for (int k = 0; k < 4; ++k) val[k] = fmaxf(val[k], 0.f);
       }
       *(float4*)(p.y + pix * p.y_stride + co) = make_float4(val[0], val[1], val[2], val[3]);
+      if (stats) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          s1[k] += (double)val[k];
+          s2[k] += (double)val[k] * (double)val[k];
+        }
+      }
     }
+    if (stats) w_commit_stats(p, lane, true, seg, co, s1, s2);
   }
 }
 

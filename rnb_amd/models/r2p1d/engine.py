@@ -294,6 +294,10 @@ class R2P1DEngine:
         bufs: Dict[str, torch.Tensor] = {"x": x}
         coffs = None
         defer = os.environ.get("RNB_BN_DEFER", "1") != "0"
+        # BN statistics from the Winograd epilogues (fp64 atomics): measured
+        # slower than the separate one-read pass (61.9 -> 64.6 ms per 128
+        # clips; 324 -> 259 videos/s one video per call), so opt-in
+        stats_fuse = os.environ.get("RNB_BN_EPILOGUE_STATS", "0") == "1"
         clip_seg = None              # video index of each clip (deferred BN)
         if self.bn_mode == "batch" and clip_offsets_dev is not None and hip:
             coffs = clip_offsets_dev
@@ -326,11 +330,21 @@ class R2P1DEngine:
             res = bufs[op.res] if op.res is not None else None
             if op.bn is not None:
                 if hip:
+                    kw = {}
                     if pending is not None:
-                        y = op.layer.forward_hip(src, None, in_affine=pending)
+                        kw["in_affine"] = pending
                         pending = None
-                    else:
-                        y = op.layer.forward_hip(src, None)
+                    sums = None
+                    if (self.f32 and stats_fuse
+                            and op.layer.emits_output_stats(src.shape)):
+                        # the producer's epilogue accumulates this BN's statistics
+                        if clip_seg is None:
+                            clip_seg = self._clip_segments(coffs, x.shape[0], x.device)
+                        nvid = 1 if coffs is None else coffs.numel() - 1
+                        sums = torch.zeros((nvid, 2, op.layer.geom.cout_p),
+                                           dtype=torch.float64, device=x.device)
+                        kw["out_stats"] = (sums, clip_seg)
+                    y = op.layer.forward_hip(src, None, **kw)
                     seg = rows = None
                     thw = y.shape[1] * y.shape[2] * y.shape[3]
                     if coffs is not None:
@@ -346,10 +360,13 @@ class R2P1DEngine:
                                                device=y.device)
                         if clip_seg is None:
                             clip_seg = self._clip_segments(coffs, x.shape[0], x.device)
-                        pending = (op.bn.scale_shift_f32(y, seg), clip_seg)
+                        pending = (op.bn.scale_shift_f32(y, seg, sums), clip_seg)
                     else:
+                        if sums is not None and seg is None:
+                            seg = torch.tensor([0, y.shape[0] * thw], dtype=torch.int32,
+                                               device=y.device)
                         y = op.bn.forward_hip(y, res, op.bn_relu, out=y, segments=seg,
-                                              seg_rows=rows)
+                                              seg_rows=rows, sums=sums)
                 else:
                     y = op.layer.forward_torch(src, None, out_dtype=self.dtype)
                     y = op.bn.forward_torch(y, res, op.bn_relu, out_dtype=self.dtype,

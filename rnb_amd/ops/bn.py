@@ -80,7 +80,7 @@ class BatchNormBatch:
     def forward_hip_f32(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,
                         out: Optional[torch.Tensor] = None,
                         segments: Optional[torch.Tensor] = None,
-                        seg_rows=None) -> torch.Tensor:
+                        seg_rows=None, sums=None) -> torch.Tensor:
         """fp32 tensor; ``segments``: device int32 [nseg+1] ROW offsets (each
         segment -- one video -- gets its own statistics); default one segment."""
         from .native import kernels
@@ -94,64 +94,71 @@ class BatchNormBatch:
             segments = torch.tensor([0, M], dtype=torch.int32, device=y.device)
             seg_rows = [M]
         nseg = segments.numel() - 1
-        need = k.bn_seg_scratch_floats(nseg, C)
-        if self._scratch is None or self._scratch.numel() < need:
-            # a captured HIP graph may still point at the old scratch: keep it
-            if self._scratch is not None:
-                self._retired.append(self._scratch)
-            self._scratch = torch.empty(need, dtype=torch.float32, device=y.device)
-        mean = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
-        var = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
+        # statistics (one read of y, or the producer epilogue's sums) and the
+        # in-order running update (one kernel, thread per channel)
+        mean, var = self._stats(y, segments, sums)
         stream = torch.cuda.current_stream(y.device).cuda_stream
-        k.bn_seg_stats_f32(y.data_ptr(), segments.data_ptr(), nseg, C, Cs,
-                           self._scratch.data_ptr(), mean.data_ptr(), var.data_ptr(), stream)
         k.bn_seg_apply_f32(y.data_ptr(), z.data_ptr(),
                            residual.data_ptr() if residual is not None else None,
                            segments.data_ptr(), nseg, mean.data_ptr(), var.data_ptr(),
                            self.gamma.data_ptr(), self.beta.data_ptr(), self.eps,
                            1 if relu else 0, M, C, Cs, z.shape[-1],
                            residual.shape[-1] if residual is not None else 0, stream)
-        self.mean, self.var = mean[-1], var[-1]
-        if self.update_running:
-            # the per-segment EMA steps in order, one kernel (thread per channel)
-            k.bn_seg_running_f32(segments.data_ptr(), nseg, mean.data_ptr(), var.data_ptr(), C,
-                                 self.channels, self.momentum, self.running_mean.data_ptr(),
-                                 self.running_var.data_ptr(), stream)
         return z
 
-    def scale_shift_f32(self, y: torch.Tensor, segments: torch.Tensor) -> torch.Tensor:
-        """Statistics only (plus the running update), for a BN whose apply is
-        deferred into the consuming conv: [nseg, 2, Cp] fp32 rows (scale =
-        gamma * rsqrt(var + eps), shift = beta - mean * scale) per segment."""
+    @staticmethod
+    def moments_from_sums(sums: torch.Tensor, segments: torch.Tensor):
+        """fp32 mean / biased variance [nseg, C] from a producer epilogue's fp64
+        per-video sums [nseg, 2, C] (empty videos: 0, 0)."""
+        n = (segments[1:] - segments[:-1]).to(torch.float64).clamp(min=1.0)[:, None]
+        mean = sums[:, 0] / n
+        var = (sums[:, 1] / n - mean * mean).clamp(min=0.0)
+        return mean.float().contiguous(), var.float().contiguous()
+
+    def _stats(self, y: torch.Tensor, segments: torch.Tensor, sums=None):
+        """(mean, var) [nseg, Cp] fp32 of the segments: from the producer's
+        epilogue sums when given, else one read of y; running update applied."""
         from .native import kernels
         k = kernels()
         N, T, H, W, Cs = y.shape
         C = self.channels_p
         nseg = segments.numel() - 1
-        need = k.bn_seg_scratch_floats(nseg, C)
-        if self._scratch is None or self._scratch.numel() < need:
-            if self._scratch is not None:
-                self._retired.append(self._scratch)
-            self._scratch = torch.empty(need, dtype=torch.float32, device=y.device)
-        mean = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
-        var = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
         stream = torch.cuda.current_stream(y.device).cuda_stream
-        k.bn_seg_stats_f32(y.data_ptr(), segments.data_ptr(), nseg, C, Cs,
-                           self._scratch.data_ptr(), mean.data_ptr(), var.data_ptr(), stream)
+        if sums is not None:
+            mean, var = self.moments_from_sums(sums[:, :, :C], segments)
+        else:
+            need = k.bn_seg_scratch_floats(nseg, C)
+            if self._scratch is None or self._scratch.numel() < need:
+                if self._scratch is not None:
+                    self._retired.append(self._scratch)
+                self._scratch = torch.empty(need, dtype=torch.float32, device=y.device)
+            mean = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
+            var = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
+            k.bn_seg_stats_f32(y.data_ptr(), segments.data_ptr(), nseg, C, Cs,
+                               self._scratch.data_ptr(), mean.data_ptr(), var.data_ptr(),
+                               stream)
         if self.update_running:
             k.bn_seg_running_f32(segments.data_ptr(), nseg, mean.data_ptr(), var.data_ptr(), C,
                                  self.channels, self.momentum, self.running_mean.data_ptr(),
                                  self.running_var.data_ptr(), stream)
+        self.mean, self.var = mean[-1], var[-1]
+        return mean, var
+
+    def scale_shift_f32(self, y: torch.Tensor, segments: torch.Tensor,
+                        sums=None) -> torch.Tensor:
+        """Statistics only (plus the running update), for a BN whose apply is
+        deferred into the consuming conv: [nseg, 2, Cp] fp32 rows (scale =
+        gamma * rsqrt(var + eps), shift = beta - mean * scale) per segment."""
+        mean, var = self._stats(y, segments, sums)
         scale = self.gamma * torch.rsqrt(var + self.eps)
         shift = self.beta - mean * scale
-        self.mean, self.var = mean[-1], var[-1]
         return torch.stack([scale, shift], dim=1).contiguous()
 
     def forward_hip(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,
                     out: Optional[torch.Tensor] = None, segments=None,
-                    seg_rows=None) -> torch.Tensor:
+                    seg_rows=None, sums=None) -> torch.Tensor:
         if y.dtype == torch.float32:
-            return self.forward_hip_f32(y, residual, relu, out, segments, seg_rows)
+            return self.forward_hip_f32(y, residual, relu, out, segments, seg_rows, sums)
         if segments is not None and segments.numel() > 2:
             raise NotImplementedError("per-video BN statistics are fp32 only")
         from .native import kernels

@@ -167,7 +167,7 @@ class ConvLayerF32:
         c = list(range(len(kernels().f32_configs)))
         return c + sorted(self.wino_ids)
 
-    def _launch_wino(self, x, y, residual, cid, stream, in_affine=None):
+    def _launch_wino(self, x, y, residual, cid, stream, in_affine=None, out_stats=None):
         from .native import WinoParams, kernels
         ft = cid in WINOT_TC
         if ft:
@@ -214,6 +214,17 @@ class ConvLayerF32:
                                  % (self.name, tuple(ss.shape), tuple(clip_seg.shape),
                                     tuple(x.shape)))
             p.in_ss, p.clip_seg = ss.data_ptr(), clip_seg.data_ptr()
+        if out_stats is not None:
+            sums, clip_seg = out_stats
+            if (sums.dim() != 3 or sums.shape[1] != 2 or sums.shape[2] < g.cout_p
+                    or sums.dtype != torch.float64 or not sums.is_contiguous()
+                    or clip_seg.dtype != torch.int32 or clip_seg.numel() != N
+                    or (in_affine is not None and in_affine[1].data_ptr() != clip_seg.data_ptr())):
+                raise ValueError("%s: output BN sums %s / clip_seg %s do not match y %s"
+                                 % (self.name, tuple(sums.shape), tuple(clip_seg.shape),
+                                    tuple(y.shape)))
+            p.out_stats, p.clip_seg = sums.data_ptr(), clip_seg.data_ptr()
+            p.clip_frames, p.stats_c = T, sums.shape[2]
         if ft:
             kernels().winot_f32(p, variant, stream.cuda_stream)
         else:
@@ -336,7 +347,7 @@ class ConvLayerF32:
             self._config[key] = cid
         return cid
 
-    def _launch_all(self, x, y, residual, cid, stream, in_affine=None):
+    def _launch_all(self, x, y, residual, cid, stream, in_affine=None, out_stats=None):
         from .native import kernels
         k = kernels()
         N = x.shape[0]
@@ -346,12 +357,13 @@ class ConvLayerF32:
             for n0 in range(0, N, step):
                 n1 = min(N, n0 + step)
                 aff = None if in_affine is None else (in_affine[0], in_affine[1][n0:n1])
+                ost = None if out_stats is None else (out_stats[0], out_stats[1][n0:n1])
                 self._launch_wino(x[n0:n1], y[n0:n1],
                                   residual[n0:n1] if residual is not None else None, cid,
-                                  stream, aff)
+                                  stream, aff, ost)
             return
-        if in_affine is not None:
-            raise ValueError("%s: deferred input BN needs a Winograd config" % self.name)
+        if in_affine is not None or out_stats is not None:
+            raise ValueError("%s: fused input/output BN needs a Winograd config" % self.name)
         step = self.chunk_clips(x.shape, y.shape,
                                 residual.shape[-1] if residual is not None else 0)
         for n0 in range(0, N, step):
@@ -394,6 +406,11 @@ class ConvLayerF32:
         return best
 
     # ------------------------------------------------------------------
+    def emits_output_stats(self, x_shape) -> bool:
+        """True when this conv's kernel for ``x_shape`` accumulates its output's
+        per-video BN sums in the epilogue (``forward_hip(out_stats=...)``)."""
+        return self.config_for(x_shape) in WINO_ALL
+
     def accepts_input_affine(self, x_shape) -> bool:
         """True when this conv's kernel for ``x_shape`` can apply its input's
         BatchNorm + ReLU on load (``forward_hip(in_affine=...)``)."""
@@ -401,10 +418,13 @@ class ConvLayerF32:
 
     def forward_hip(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                     out: Optional[torch.Tensor] = None, config: Optional[int] = None,
-                    in_affine=None):
+                    in_affine=None, out_stats=None):
         """``in_affine`` = (scale_shift [nseg, 2, Cin], clip_seg int32 [N]): x is
         the raw output of a conv whose BatchNorm + ReLU (per video) is applied
-        here on load (temporal Winograd configs only)."""
+        here on load (temporal Winograd configs only). ``out_stats`` = (sums
+        fp64 [nseg, 2, >=Cout_p] zeroed, clip_seg): the epilogue adds each
+        video's per-channel sum and sum of squares of the output (Winograd
+        configs only)."""
         if x.dtype != torch.float32 or not x.is_contiguous():
             raise ValueError("%s: expected contiguous fp32 NDHWC input" % self.name)
         y = out if out is not None else torch.empty(self.out_shape(x.shape),
@@ -419,7 +439,8 @@ class ConvLayerF32:
         if x.shape[0] == 0:
             return y
         cid = self.config_for(x.shape) if config is None else config
-        self._launch_all(x, y, residual, cid, torch.cuda.current_stream(x.device), in_affine)
+        self._launch_all(x, y, residual, cid, torch.cuda.current_stream(x.device), in_affine,
+                         out_stats)
         return y
 
     def forward_torch(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,

@@ -155,6 +155,7 @@ class WinoParams(ctypes.Structure):
         ("m_tw", ctypes.c_uint32), ("s_tw", ctypes.c_uint32),
         ("m_th", ctypes.c_uint32), ("s_th", ctypes.c_uint32),
         ("in_ss", ctypes.c_void_p), ("clip_seg", ctypes.c_void_p),
+        ("out_stats", ctypes.c_void_p), ("clip_frames", ctypes.c_int), ("stats_c", ctypes.c_int),
     ]
 
 

@@ -378,7 +378,9 @@ def test_graphed_batch_bn_per_video_matches_eager_and_module():
 def test_deferred_batch_bn_into_temporal_winograd_matches_separate_apply(monkeypatch):
     """bn_mode='batch': the spatial conv's BatchNorm + ReLU applied on load by
     the temporal Winograd kernel (per-video scale/shift, padding frames kept
-    at zero) equals the separate BN apply pass, and the fp32 module per video."""
+    at zero) equals the separate BN apply pass; BN statistics accumulated in
+    the Winograd epilogues (fp64 per-video sums) equal the separate stats pass;
+    both match the fp32 module run per video."""
     from rnb_amd.models.r2p1d.model import build_network
     from rnb_amd.models.r2p1d.engine import R2P1DEngine
     from rnb_amd.models.r2p1d.decoder import SyntheticDecoder
@@ -395,8 +397,12 @@ def test_deferred_batch_bn_into_temporal_winograd_matches_separate_apply(monkeyp
         a = eng.forward(x, clip_offsets=offs).clone()
         monkeypatch.setenv("RNB_BN_DEFER", "0")
         b = eng.forward(x, clip_offsets=offs).clone()
+        # BN statistics from the Winograd epilogues instead of a separate pass
+        monkeypatch.setenv("RNB_BN_EPILOGUE_STATS", "1")
+        c = eng.forward(x, clip_offsets=offs).clone()
         ref = torch.cat([mod.forward(x[p:q]) for p, q in zip(offs[:-1], offs[1:])])
     torch.cuda.synchronize()
     scale = ref.abs().max().item()
     assert (a - b).abs().max().item() <= 2e-5 * scale
+    assert (b - c).abs().max().item() <= 2e-5 * scale
     assert (a - ref).abs().max().item() <= 1e-3 * scale
