@@ -100,6 +100,9 @@ static __device__ __forceinline__ void w_commit_stats(const WinoParams& p, int l
 }
 
 #define WINO_INVALID 0xFFFFFFF0u
+#ifndef WINO_AD
+#define WINO_AD 1
+#endif
 
 static __device__ __forceinline__ int w_div(int n, uint32_t m, uint32_t s) {
   return m ? (int)(__umulhi((uint32_t)n, m) >> s) : n;
@@ -116,7 +119,7 @@ static __device__ __forceinline__ int w_swz(int q, int r) {
 // one block's loads hide behind the other's MFMAs.
 // PF = 2: the patch registers are refilled element by element as the GEMM
 // steps consume them: prefetch at PF = 0's register count.
-template <int TC, int PF>
+template <int TC, int PF, bool ST = false>
 __global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f32_kernel(
     const WinoParams p) {
   constexpr int CT = 16 * TC;
@@ -221,32 +224,38 @@ __global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f
   // while step x's MFMAs run (one register set ahead). With next >= 0, the
   // register of V[x] is refilled with patch element x of chunk `next` as soon
   // as step x's MFMAs have read it (prefetch without extra registers).
+  // fragment prefetch distance: step x+AD's A fragments are read from LDS
+  // while step x's MFMAs issue (AD = 1 leaves ~64 issue cycles for the read)
+  constexpr int AD = WINO_AD;
   auto gemm = [&](const char* ub, wf32x4 (&v)[16], int next, auto refill) {
-    wf32x4 af[2][TC];
+    wf32x4 af[AD + 1][TC];
 #pragma unroll
-    for (int tc = 0; tc < TC; ++tc) {
-      const int r = tc * 16 + frow;
-      af[0][tc] = *(const wf32x4*)(ub + r * 64 + (w_swz(q, r) << 4));
-    }
+    for (int s0 = 0; s0 < AD; ++s0)
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc) {
+        const int r = tc * 16 + frow;
+        af[s0][tc] = *(const wf32x4*)(ub + (s0 * CT + r) * 64 + (w_swz(q, r) << 4));
+      }
 #pragma unroll
     for (int x = 0; x < 16; ++x) {
-      if (x + 1 < 16) {
+      if (x + AD < 16) {
 #pragma unroll
         for (int tc = 0; tc < TC; ++tc) {
           const int r = tc * 16 + frow;
-          af[(x + 1) & 1][tc] = *(const wf32x4*)(ub + ((x + 1) * CT + r) * 64 + (w_swz(q, r) << 4));
+          af[(x + AD) % (AD + 1)][tc] =
+              *(const wf32x4*)(ub + ((x + AD) * CT + r) * 64 + (w_swz(q, r) << 4));
         }
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int tc = 0; tc < TC; ++tc)
-          acc[x][tc] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[x & 1][tc][j], v[x][j],
+          acc[x][tc] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[x % (AD + 1)][tc][j], v[x][j],
                                                              acc[x][tc], 0, 0, 0);
       if constexpr (decltype(refill)::value) v[x] = load_one(next, x);
-      // keep the software pipeline: step x+1's fragment reads are issued
+      // keep the software pipeline: step x+AD's fragment reads are issued
       // before step x's MFMAs, then the refill load; nothing crosses steps
-      if (x + 1 < 16) __builtin_amdgcn_sched_group_barrier(0x0100, TC, 0);   // DS reads
+      if (x + AD < 16) __builtin_amdgcn_sched_group_barrier(0x0100, TC, 0);  // DS reads
       __builtin_amdgcn_sched_group_barrier(0x0008, 4 * TC, 0);               // MFMA
       if constexpr (decltype(refill)::value)
         __builtin_amdgcn_sched_group_barrier(0x0020, 1, 0);                  // VMEM read
@@ -318,7 +327,7 @@ __global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f
   }
 
   // ---- output transform Y = A^T M A + epilogue (lane: tile tl, 4 channels) ----
-  const bool stats = p.out_stats != nullptr;        // uniform
+  constexpr bool stats = ST;                        // launcher: ST <=> p.out_stats
   if (!tvalid && !stats) return;
   const int oy = 2 * ty, ox = 2 * tx;
   const bool has_res = p.res != nullptr;
@@ -381,7 +390,7 @@ __global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f
 // w_swz swizzle) and in-place patch refill follow conv_wino_f32_kernel; the
 // small accumulator set (6 x TC x 4) lets a block cover 64 output channels.
 // WinoParams reuse: F = clips, H = T, W = pixels per frame (H*W of the conv).
-template <int TC>
+template <int TC, bool ST = false>
 __global__ __launch_bounds__(256, 2) void conv_winot_f32_kernel(const WinoParams p) {
   constexpr int CT = 16 * TC;
   constexpr int U_BYTES = 6 * CT * 64;
@@ -538,7 +547,7 @@ __global__ __launch_bounds__(256, 2) void conv_winot_f32_kernel(const WinoParams
   gemm(lds + ((nchunks - 1) & 1) * U_BYTES, d, -1, std::false_type{});
 
   // ---- Y = A^T M (4 frames) + epilogue (lane: tile tl, channels 4q..4q+3) ----
-  const bool stats = p.out_stats != nullptr;        // uniform
+  constexpr bool stats = ST;                        // launcher: ST <=> p.out_stats
   if (!tvalid && !stats) return;
   const bool has_res = p.res != nullptr;
   const int seg = (stats && tvalid) ? p.clip_seg[n] : 0;
@@ -631,14 +640,25 @@ int rnb_wino_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) {
   const long long blocks = (long long)p.n_tblocks * p.n_cblocks;
   if (blocks > 0x7FFFFFFF) return -8;
   const dim3 grid((unsigned)blocks), block(256);
+  const bool st = p.out_stats != nullptr;
+  if (st && variant < 4) return -9;             // epilogue statistics: variants 4-6 only
   switch (variant) {
     case 0: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 1>), grid, block, 0, stream, p); break;
     case 1: hipLaunchKernelGGL((conv_wino_f32_kernel<3, 1>), grid, block, 0, stream, p); break;
     case 2: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 0>), grid, block, 0, stream, p); break;
     case 3: hipLaunchKernelGGL((conv_wino_f32_kernel<1, 0>), grid, block, 0, stream, p); break;
-    case 4: hipLaunchKernelGGL((conv_wino_f32_kernel<1, 2>), grid, block, 0, stream, p); break;
-    case 5: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 2>), grid, block, 0, stream, p); break;
-    default: hipLaunchKernelGGL((conv_wino_f32_kernel<3, 2>), grid, block, 0, stream, p); break;
+    case 4:
+      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<1, 2, true>), grid, block, 0, stream, p);
+      else hipLaunchKernelGGL((conv_wino_f32_kernel<1, 2>), grid, block, 0, stream, p);
+      break;
+    case 5:
+      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<2, 2, true>), grid, block, 0, stream, p);
+      else hipLaunchKernelGGL((conv_wino_f32_kernel<2, 2>), grid, block, 0, stream, p);
+      break;
+    default:
+      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<3, 2, true>), grid, block, 0, stream, p);
+      else hipLaunchKernelGGL((conv_wino_f32_kernel<3, 2>), grid, block, 0, stream, p);
+      break;
   }
   return (int)hipGetLastError();
 }
@@ -673,10 +693,13 @@ int rnb_winot_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) 
   const long long blocks = (long long)p.n_tblocks * p.n_cblocks;
   if (blocks > 0x7FFFFFFF) return -8;
   const dim3 grid((unsigned)blocks), block(256);
+  const bool st = p.out_stats != nullptr;
   if (TC == 2)
-    hipLaunchKernelGGL(conv_winot_f32_kernel<2>, grid, block, 0, stream, p);
+    if (st) hipLaunchKernelGGL((conv_winot_f32_kernel<2, true>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((conv_winot_f32_kernel<2>), grid, block, 0, stream, p);
   else
-    hipLaunchKernelGGL(conv_winot_f32_kernel<4>, grid, block, 0, stream, p);
+    if (st) hipLaunchKernelGGL((conv_winot_f32_kernel<4, true>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((conv_winot_f32_kernel<4>), grid, block, 0, stream, p);
   return (int)hipGetLastError();
 }
 
