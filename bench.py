@@ -102,6 +102,11 @@ def parse_args(argv=None):
     # fused (in-process) engine options
     ap.add_argument("--packing", choices=["first-fit", "arrival"], default="first-fit")
     ap.add_argument("--fused-replicas", type=int, default=3)
+    ap.add_argument("--no-cross-gpu-extras", dest="cross_gpu_extras", action="store_false",
+                    help="at --gpus > 1, skip the short global (xGMI IPC) and two-stage "
+                         "(RCCL) runs reported under cross_gpu")
+    ap.add_argument("--cross-gpu-steps", type=int, default=4)
+    ap.add_argument("--cross-gpu-timeout", type=float, default=420.0)
     ap.add_argument("--trace", type=str, default=None,
                     help="(fused) write a per-kernel time table of the timed steps")
     return ap.parse_args(argv)
@@ -259,6 +264,8 @@ def main(argv=None) -> int:
                        "bucket_step": args.bucket_step,
                        "job_wall_s": round(res.get("wall_s", 0.0), 1)},
         }
+        if args.gpus > 1 and args.cross_gpu_extras and args.pipeline == "aggressive":
+            rec["cross_gpu"] = run_cross_gpu_extras(args)
         line = json.dumps(rec)
     if world > 1:
         dist.barrier()
@@ -269,6 +276,44 @@ def main(argv=None) -> int:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     return rc
+
+
+def run_cross_gpu_extras(args) -> dict:
+    """After the headline (per-GPU queues, no slot crosses GPUs), measure the
+    two cross-GPU data planes briefly, each in its own process (a failure
+    there cannot take the headline down): ``global`` (one queue shared by all
+    GPUs: runners pull other GPUs' slots over xGMI via HIP IPC) and
+    ``two-stage`` (loader GPU -> model GPU pairs over RCCL send/recv). Their
+    videos/s and Poisson p50/p99 are reported under ``cross_gpu``."""
+    import subprocess
+    root = os.path.dirname(os.path.abspath(__file__))
+    out = {}
+    topologies = ["global"] + (["two-stage"] if args.gpus % 2 == 0 else [])
+    for topo in topologies:
+        path = os.path.join(root, "logs", "bench", "cross-%s-%dgpu.json" % (topo, args.gpus))
+        cmd = [sys.executable, os.path.join(root, "bench.py"), "--pipeline", topo,
+               "--gpus", str(args.gpus), "--steps", str(args.cross_gpu_steps),
+               "--warmup", "1", "--dtype", args.dtype, "--bn", args.bn,
+               "--depth", str(args.depth), "--latency-seconds", "2",
+               "--no-cross-gpu-extras", "--json-out", path]
+        env = {k: v for k, v in os.environ.items()
+               if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+                            "MASTER_ADDR", "MASTER_PORT", "GROUP_RANK", "ROLE_RANK",
+                            "TORCHELASTIC_RUN_ID")}
+        t0 = time.time()
+        try:
+            r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                               timeout=args.cross_gpu_timeout)
+            with open(path) as f:
+                sub = json.loads(f.read())
+            out[topo] = {"videos_per_s": sub.get("value"), "p50_ms": sub.get("p50_ms"),
+                         "p99_ms": sub.get("p99_ms"), "steps": args.cross_gpu_steps,
+                         "rc": r.returncode, "wall_s": round(time.time() - t0, 1)}
+        except Exception as e:          # reported, never fatal for the headline
+            out[topo] = {"error": "%s: %s" % (type(e).__name__, str(e)[:200]),
+                         "wall_s": round(time.time() - t0, 1)}
+        print("[bench] cross-GPU %s: %s" % (topo, out[topo]), file=sys.stderr, flush=True)
+    return out
 
 
 def pack_step(videos, clip_cap: int, video_cap: int, mode: str = "first-fit"):
