@@ -301,6 +301,7 @@ def run_cross_gpu_extras(args) -> dict:
                             "MASTER_ADDR", "MASTER_PORT", "GROUP_RANK", "ROLE_RANK",
                             "TORCHELASTIC_RUN_ID")}
         t0 = time.time()
+        r = None
         try:
             r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
                                timeout=args.cross_gpu_timeout)
@@ -310,8 +311,11 @@ def run_cross_gpu_extras(args) -> dict:
                          "p99_ms": sub.get("p99_ms"), "steps": args.cross_gpu_steps,
                          "rc": r.returncode, "wall_s": round(time.time() - t0, 1)}
         except Exception as e:          # reported, never fatal for the headline
+            tail = ""
+            if r is not None and r.stderr:
+                tail = r.stderr.decode(errors="replace").strip().splitlines()[-3:]
             out[topo] = {"error": "%s: %s" % (type(e).__name__, str(e)[:200]),
-                         "wall_s": round(time.time() - t0, 1)}
+                         "stderr_tail": tail, "wall_s": round(time.time() - t0, 1)}
         print("[bench] cross-GPU %s: %s" % (topo, out[topo]), file=sys.stderr, flush=True)
     return out
 

@@ -341,3 +341,37 @@ def test_bn_device_running_update_equals_sequential_segments():
     b._update_segments_dev(mean, var, seg)
     assert torch.allclose(a.running_mean, b.running_mean, atol=1e-6)
     assert torch.allclose(a.running_var, b.running_var, atol=1e-6)
+
+
+def test_clip_segments_from_padded_offsets():
+    """Video index of every clip from the graph's padded clip offsets; bucket
+    padding clips land on the trailing empty video (never a real one)."""
+    from rnb_amd.models.r2p1d.engine import R2P1DEngine
+    offs = torch.tensor([0, 3, 5, 6, 6, 6, 6, 6, 6], dtype=torch.int32)   # 6 clips, bucket 8
+    seg = R2P1DEngine._clip_segments(offs, 8, torch.device("cpu"))
+    assert seg.dtype == torch.int32
+    assert seg.tolist() == [0, 0, 0, 1, 1, 2, 7, 7]
+    assert R2P1DEngine._clip_segments(None, 4, torch.device("cpu")).tolist() == [0, 0, 0, 0]
+
+
+def test_bn_moments_from_epilogue_sums():
+    """fp32 mean / biased variance from fp64 per-video sums (the Winograd
+    epilogue statistics) equal torch's per-video moments; empty videos 0."""
+    from rnb_amd.ops.bn import BatchNormBatch
+    torch.manual_seed(0)
+    rows = [50, 0, 120]
+    seg = torch.tensor([0, 50, 50, 170], dtype=torch.int32)
+    x = torch.randn(170, 8, dtype=torch.float64) * 3 + 5
+    sums = torch.zeros(3, 2, 8, dtype=torch.float64)
+    for s in range(3):
+        xs = x[seg[s]:seg[s + 1]]
+        sums[s, 0] = xs.sum(0)
+        sums[s, 1] = (xs * xs).sum(0)
+    mean, var = BatchNormBatch.moments_from_sums(sums, seg)
+    for s, n in enumerate(rows):
+        xs = x[seg[s]:seg[s + 1]]
+        if n == 0:
+            assert mean[s].abs().max() == 0 and var[s].abs().max() == 0
+            continue
+        assert torch.allclose(mean[s].double(), xs.mean(0), atol=1e-5)
+        assert torch.allclose(var[s].double(), xs.var(0, unbiased=False), rtol=1e-5)
