@@ -85,7 +85,7 @@ def parse_args(argv=None):
                     help="max videos per model invocation (consumer-side batching)")
     ap.add_argument("--clips-per-batch", type=int, default=128,
                     help="clip capacity of one model invocation (largest graph bucket)")
-    ap.add_argument("--bucket-step", type=int, default=8,
+    ap.add_argument("--bucket-step", type=int, default=4,
                     help="HIP-graph clip buckets every this many clips")
     ap.add_argument("--batch-wait-ms", type=float, default=0.0,
                     help="how long a runner waits for more queued videos to batch")
