@@ -263,6 +263,75 @@ __global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f
     }
   };
 
+  // PF == 3: the input transform is split so a chunk can start before its
+  // whole patch has landed. V row 0 = e0 - e2 (e = d B per patch row) needs
+  // only patch rows 0 and 2; rows 1-3 of V need row 1 (and 2, 3). The GEMM
+  // steps run in V-row order 0, 2, 1, 3, so the refill loads for the next
+  // chunk go out as rows 0, 2 (early in the chunk) and rows 1, 3 (late); the
+  // next chunk transforms rows 0 / 2 and runs V row 0's 4 steps while rows
+  // 1 / 3 are still in flight, then finishes the transform in place.
+  auto row_t = [](wf32x4 (&v)[16], int r) {
+    const wf32x4 b0 = v[r * 4 + 0], b1 = v[r * 4 + 1], b2 = v[r * 4 + 2], b3 = v[r * 4 + 3];
+    v[r * 4 + 0] = b0 - b2;
+    v[r * 4 + 1] = b1 + b2;
+    v[r * 4 + 2] = b2 - b1;
+    v[r * 4 + 3] = b1 - b3;
+  };
+  auto transform_a = [&](wf32x4 (&v)[16]) {          // V row 0 (+ e2 kept in row 2)
+    row_t(v, 0);
+    row_t(v, 2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = v[j] - v[8 + j];
+  };
+  auto transform_b = [&](wf32x4 (&v)[16]) {          // V rows 1-3, in place
+    row_t(v, 1);
+    row_t(v, 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[12 + j] = v[4 + j] - v[12 + j];               // V3 = e1 - e3
+      const wf32x4 e1 = v[4 + j];
+      v[4 + j] = e1 + v[8 + j];                       // V1 = e1 + e2
+      v[8 + j] = v[8 + j] - e1;                       // V2 = e2 - e1
+    }
+  };
+  auto gemm_split = [&](const char* ub, wf32x4 (&v)[16], int next, auto refill) {
+    constexpr int perm[16] = {0, 1, 2, 3, 8, 9, 10, 11, 4, 5, 6, 7, 12, 13, 14, 15};
+    wf32x4 af[2][TC];
+#pragma unroll
+    for (int tc = 0; tc < TC; ++tc) {
+      const int r = tc * 16 + frow;
+      af[0][tc] = *(const wf32x4*)(ub + r * 64 + (w_swz(q, r) << 4));
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int x = perm[k];
+      if (k == 4) {
+        transform_b(v);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (k + 1 < 16) {
+        const int xn = perm[k + 1];
+#pragma unroll
+        for (int tc = 0; tc < TC; ++tc) {
+          const int r = tc * 16 + frow;
+          af[(k + 1) & 1][tc] = *(const wf32x4*)(ub + (xn * CT + r) * 64 + (w_swz(q, r) << 4));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int tc = 0; tc < TC; ++tc)
+          acc[x][tc] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[k & 1][tc][j], v[x][j],
+                                                             acc[x][tc], 0, 0, 0);
+      if constexpr (decltype(refill)::value) v[x] = load_one(next, x);
+      if (k + 1 < 16) __builtin_amdgcn_sched_group_barrier(0x0100, TC, 0);   // DS reads
+      __builtin_amdgcn_sched_group_barrier(0x0008, 4 * TC, 0);               // MFMA
+      if constexpr (decltype(refill)::value)
+        __builtin_amdgcn_sched_group_barrier(0x0020, 1, 0);                  // VMEM read
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
   wf32x4 d[16];
   if constexpr (PF == 1) {
     wf32x4 dn[16];
@@ -305,6 +374,22 @@ __global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
+  } else if constexpr (PF == 3) {
+    issue_u(0, 0);
+    load_patch(0, d);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int c = 0; c + 1 < nchunks; ++c) {
+      const int cur = c & 1;
+      issue_u(c + 1, cur ^ 1);
+      asm volatile("" ::: "memory");
+      transform_a(d);
+      gemm_split(lds + cur * U_BYTES, d, c + 1, std::true_type{});
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      __syncthreads();
+    }
+    transform_a(d);
+    gemm_split(lds + ((nchunks - 1) & 1) * U_BYTES, d, -1, std::false_type{});
   } else {
     // PF == 2: in-place prefetch through gemm(next)
     issue_u(0, 0);
@@ -614,8 +699,8 @@ int rnb_wino_params_size() { return (int)sizeof(WinoParams); }
 // Returns 0, a negative contract code, or the hipError_t of the launch.
 int rnb_wino_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) {
   WinoParams p = *pp;
-  static const int kTC[7] = {2, 3, 2, 1, 1, 2, 3};
-  if (variant < 0 || variant > 6) return -1;
+  static const int kTC[10] = {2, 3, 2, 1, 1, 2, 3, 1, 2, 3};
+  if (variant < 0 || variant > 9) return -1;
   const int TC = kTC[variant];
   if (p.Cin % 16 != 0 || p.Cout % 4 != 0 || p.y_stride % 4 || (p.res && p.res_stride % 4))
     return -2;
@@ -641,7 +726,7 @@ int rnb_wino_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) {
   if (blocks > 0x7FFFFFFF) return -8;
   const dim3 grid((unsigned)blocks), block(256);
   const bool st = p.out_stats != nullptr;
-  if (st && variant < 4) return -9;             // epilogue statistics: variants 4-6 only
+  if (st && (variant < 4 || variant > 6)) return -9;   // epilogue statistics: variants 4-6
   switch (variant) {
     case 0: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 1>), grid, block, 0, stream, p); break;
     case 1: hipLaunchKernelGGL((conv_wino_f32_kernel<3, 1>), grid, block, 0, stream, p); break;
@@ -655,10 +740,13 @@ int rnb_wino_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) {
       if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<2, 2, true>), grid, block, 0, stream, p);
       else hipLaunchKernelGGL((conv_wino_f32_kernel<2, 2>), grid, block, 0, stream, p);
       break;
-    default:
+    case 6:
       if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<3, 2, true>), grid, block, 0, stream, p);
       else hipLaunchKernelGGL((conv_wino_f32_kernel<3, 2>), grid, block, 0, stream, p);
       break;
+    case 7: hipLaunchKernelGGL((conv_wino_f32_kernel<1, 3>), grid, block, 0, stream, p); break;
+    case 8: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 3>), grid, block, 0, stream, p); break;
+    default: hipLaunchKernelGGL((conv_wino_f32_kernel<3, 3>), grid, block, 0, stream, p); break;
   }
   return (int)hipGetLastError();
 }

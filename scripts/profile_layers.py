@@ -23,11 +23,11 @@ def tile_name(cid, f32=False):
     from rnb_amd.ops.native import kernels
     k = kernels()
     if f32:
-        from rnb_amd.ops.conv_f32 import WINO_TC, WINOT_TC
+        from rnb_amd.ops.conv_f32 import WINO_SPLIT, WINO_TC, WINOT_TC
         if cid in WINOT_TC:
             return "wt4_%d" % (16 * WINOT_TC[cid])
         if cid in WINO_TC:
-            return "wino%d" % (16 * WINO_TC[cid])
+            return "wino%d%s" % (16 * WINO_TC[cid], "s" if cid in WINO_SPLIT else "")
         return "%dx%d" % k.f32_configs[cid]
     if cid >= len(k.configs):
         from rnb_amd.ops.conv import SPECIAL_NAMES

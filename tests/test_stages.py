@@ -292,6 +292,34 @@ def test_winograd_weight_layout_reproduces_the_conv():
     assert (out[:, :H, :W] - ref).abs().max().item() < 1e-4
 
 
+def test_winograd_split_input_transform_matches_bt_d_b():
+    """The split input transform of the variant-7..9 kernels, replayed in the
+    kernel's order on the 16 register slots (x = 4 row + col): rows 0 / 2 and
+    V row 0 first, rows 1 / 3 and V rows 1-3 in place later, equals B^T d B."""
+    torch.manual_seed(0)
+    d = torch.randn(4, 4, dtype=torch.float64)
+    v = [d[x // 4, x % 4].clone() for x in range(16)]
+
+    def row_t(r):
+        b0, b1, b2, b3 = v[4 * r:4 * r + 4]
+        v[4 * r:4 * r + 4] = [b0 - b2, b1 + b2, b2 - b1, b1 - b3]
+
+    row_t(0)
+    row_t(2)
+    for j in range(4):
+        v[j] = v[j] - v[8 + j]
+    row_t(1)
+    row_t(3)
+    for j in range(4):
+        v[12 + j] = v[4 + j] - v[12 + j]
+        e1 = v[4 + j]
+        v[4 + j] = e1 + v[8 + j]
+        v[8 + j] = v[8 + j] - e1
+    BT = torch.tensor([[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]],
+                      dtype=torch.float64)
+    assert torch.allclose(torch.stack(v).reshape(4, 4), BT @ d @ BT.t(), atol=1e-12)
+
+
 def test_winograd_temporal_weight_layout_reproduces_the_conv():
     """Emulation of the temporal F(4, 3) kernel on its packed U layout
     [ci/16][nb][6][ct][16]: 6-frame patches at stride 4, zero padded."""
