@@ -90,45 +90,94 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
 // fp32, per-segment statistics. A batch of several videos is normalised with
 // each video's OWN statistics, which is what the reference computes when it
 // runs one video per forward (training-mode BN, reference runner.py:45 and
-// model.py:82-84): segment s = rows [seg[s], seg[s+1]) of the [M][stride]
-// tensor. Rows outside every segment (graph-bucket padding) are ignored by
-// the statistics and left untouched by the apply.
+// model.py:82-84). Segment s = clips [coffs[s], coffs[s+1]) = rows
+// [coffs[s] rpc, coffs[s+1] rpc) of the [M][stride] tensor (rpc = rows per
+// clip, T*H*W of the layer), so one device clip-offset tensor serves every
+// layer of a forward. Rows past the last segment (graph-bucket padding) are
+// ignored by the statistics and left untouched by the apply.
 //
-// One read of the tensor for the statistics: shifted sums S1 = sum(x - K),
-// S2 = sum((x - K)^2) with K = the segment's first row (a sample of the
-// channel, so |mean - K| is of the order of the spread and the cancellation in
-// var = S2/n - (S1/n)^2 stays at fp32 rounding of the spread, like a two-pass
-// variance). Grid (BN_SEG_BLOCKS, nseg); a block's 256 threads are
-// row lanes x channel quads (C = 64: 16 x 16), so every wave reads whole
-// contiguous rows; per-block partials are reduced in LDS and then by a
-// finalize kernel in a fixed order (deterministic).
+// rnb_bn_seg_stats_f32 = three small dispatches per BatchNorm (it was sums +
+// finalize + running update + a multiply for the row offsets and five torch
+// ops for the scale / shift):
+//  1. bn_seg_sums: blocks (32 per segment) reduce
+//     shifted sums S1 = sum(x - K), S2 = sum((x - K)^2) of their rows, K = the
+//     segment's first row (a sample of the channel: var = S2/n - (S1/n)^2
+//     then cancels only at the spread's fp32 rounding, like a two-pass
+//     variance); partials reduced in LDS, written to scratch;
+//  2. bn_seg_finalize: thread per (segment, channel) reduces the partials in
+//     a fixed order (deterministic), writes mean / biased var and the apply's
+//     scale / shift [s][2][C], and adds the segment's term of the running-
+//     statistics update into an fp64 accumulator (device-scope atomics);
+//  3. bn_seg_running: r = decay r + acc, and re-arms acc for the next launch.
+// Cross-block hand-off happens only at kernel boundaries: a last-block
+// ticket inside one kernel needs agent-scope fences, which on this part write
+// back and invalidate the XCD's L2 and measured 10x slower.
+//
+// Running statistics: the reference's one-video forwards apply, in video
+// order, r <- (1-m) r + m x_s for every segment with >= 2 rows (torch rejects
+// 1-row training BN; empty segments are padding). In closed form
+// r = (1-m)^K r0 + sum_s m (1-m)^(valid segments after s) x_s, so segments
+// contribute independently (x_s = mean, or var * n/(n-1) for running_var).
 // ---------------------------------------------------------------------------
-#define BN_SEG_BLOCKS 32
+#define BN_SEG_MAX_BPS 256
 
-__global__ __launch_bounds__(256) void bn_seg_sums_f32_kernel(
-    const float* __restrict__ y, const int* __restrict__ seg, int C, int stride,
-    float* __restrict__ partial) {
+static __device__ __forceinline__ void bn_f4_add(float4& a, const float4 b) {
+  a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+}
+
+struct BnSegParams {
+  const float* y;
+  const int* coffs;          // [nseg + 1] clip offsets
+  int nseg, rpc, C, stride, bps;
+  float* partial;            // [nseg][bps][2][C]
+  double* run_acc;           // [2][channels], zero between launches (re-armed)
+  const float* gamma;
+  const float* beta;
+  float eps, momentum;
+  int channels;              // real channels (<= C) of the running statistics
+  float* running_mean;       // null: no running update
+  float* running_var;
+  float* mean;               // [nseg][C]
+  float* var;                // [nseg][C]
+  float* ss;                 // [nseg][2][C]: scale, shift
+};
+
+__global__ __launch_bounds__(256) void bn_seg_sums_f32_kernel(BnSegParams p) {
   __shared__ float4 red1[256], red2[256];
-  const int s = blockIdx.y;
-  const int r0s = seg[s], r1s = seg[s + 1];
+  const int s = blockIdx.y, C = p.C;
+  const int r0s = p.coffs[s] * p.rpc, r1s = p.coffs[s + 1] * p.rpc;
   const int rows = r1s - r0s;
-  const int per = (rows + BN_SEG_BLOCKS - 1) / BN_SEG_BLOCKS;
+  const int per = (rows + p.bps - 1) / p.bps;
   const int r0 = r0s + blockIdx.x * per;
   const int r1 = min(r1s, r0 + per);
   const int CQ = C / 4;
   const int QL = CQ < 256 ? CQ : 256;             // channel-quad lanes
   const int RL = 256 / QL;                        // row lanes
   const int tid = threadIdx.x, ql = tid % QL, rl = tid / QL;
-  float* out1 = partial + ((size_t)s * BN_SEG_BLOCKS + blockIdx.x) * 2 * C;
+  const float* y = p.y;
+  float* out1 = p.partial + ((size_t)s * p.bps + blockIdx.x) * 2 * C;
   float* out2 = out1 + C;
+  // shifted sums of this block's rows (4 independent rows in flight)
   for (int base = 0; base < CQ; base += QL) {     // uniform trip count (barriers)
     const int qd = base + ql;
     const bool act = qd < CQ && rl < RL;
     float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f), a2 = a1;
     if (act && rows > 0) {
-      const float4 k = *(const float4*)(y + (size_t)r0s * stride + 4 * qd);
-      for (int r = r0 + rl; r < r1; r += RL) {
-        const float4 v = *(const float4*)(y + (size_t)r * stride + 4 * qd);
+      const float4 k = *(const float4*)(y + (size_t)r0s * p.stride + 4 * qd);
+      int r = r0 + rl;
+      for (; r + 3 * RL < r1; r += 4 * RL) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *(const float4*)(y + (size_t)(r + u * RL) * p.stride + 4 * qd);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float x0 = v[u].x - k.x, x1 = v[u].y - k.y, x2 = v[u].z - k.z, x3 = v[u].w - k.w;
+          a1.x += x0; a1.y += x1; a1.z += x2; a1.w += x3;
+          a2.x += x0 * x0; a2.y += x1 * x1; a2.z += x2 * x2; a2.w += x3 * x3;
+        }
+      }
+      for (; r < r1; r += RL) {
+        const float4 v = *(const float4*)(y + (size_t)r * p.stride + 4 * qd);
         const float x0 = v.x - k.x, x1 = v.y - k.y, x2 = v.z - k.z, x3 = v.w - k.w;
         a1.x += x0; a1.y += x1; a1.z += x2; a1.w += x3;
         a2.x += x0 * x0; a2.y += x1 * x1; a2.z += x2 * x2; a2.w += x3 * x3;
@@ -139,9 +188,8 @@ __global__ __launch_bounds__(256) void bn_seg_sums_f32_kernel(
     __syncthreads();
     if (rl == 0 && qd < CQ) {
       for (int l = 1; l < RL; ++l) {
-        const float4 b1 = red1[l * QL + ql], b2 = red2[l * QL + ql];
-        a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
-        a2.x += b2.x; a2.y += b2.y; a2.z += b2.z; a2.w += b2.w;
+        bn_f4_add(a1, red1[l * QL + ql]);
+        bn_f4_add(a2, red2[l * QL + ql]);
       }
       *(float4*)(out1 + 4 * qd) = a1;
       *(float4*)(out2 + 4 * qd) = a2;
@@ -150,61 +198,72 @@ __global__ __launch_bounds__(256) void bn_seg_sums_f32_kernel(
   }
 }
 
-// mean / biased variance per (segment, channel) from the shifted sums
-__global__ __launch_bounds__(256) void bn_seg_finalize_f32_kernel(
-    const float* __restrict__ y, const int* __restrict__ seg, int C, int stride,
-    const float* __restrict__ partial, float* __restrict__ mean, float* __restrict__ var) {
-  const int s = blockIdx.y;
+// one thread per (segment, channel): fixed-order reduction of the bps
+// partials, moments, scale / shift, and the segment's running-update term
+__global__ __launch_bounds__(256) void bn_seg_finalize_f32_kernel(BnSegParams p) {
+  const int s = blockIdx.y, C = p.C;
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
-  const int rows = seg[s + 1] - seg[s];
-  if (rows <= 0) {
-    mean[(size_t)s * C + c] = 0.f;
-    var[(size_t)s * C + c] = 0.f;
-    return;
-  }
+  const int r0s = p.coffs[s] * p.rpc, rows = p.coffs[s + 1] * p.rpc - r0s;
+  const float* base = p.partial + (size_t)s * p.bps * 2 * C;
   float s1 = 0.f, s2 = 0.f;
-  for (int b = 0; b < BN_SEG_BLOCKS; ++b) {
-    const float* p = partial + ((size_t)s * BN_SEG_BLOCKS + b) * 2 * C;
-    s1 += p[c];
-    s2 += p[C + c];
+  int b = 0;
+  for (; b + 4 <= p.bps; b += 4) {
+    float t1[4], t2[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      t1[u] = base[(size_t)(b + u) * 2 * C + c];
+      t2[u] = base[(size_t)(b + u) * 2 * C + C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { s1 += t1[u]; s2 += t2[u]; }
   }
-  const float k = y[(size_t)seg[s] * stride + c];
-  const float m1 = s1 / (float)rows;
-  mean[(size_t)s * C + c] = k + m1;
-  var[(size_t)s * C + c] = fmaxf(s2 / (float)rows - m1 * m1, 0.f);
+  for (; b < p.bps; ++b) {
+    s1 += base[(size_t)b * 2 * C + c];
+    s2 += base[(size_t)b * 2 * C + C + c];
+  }
+  float mu = 0.f, va = 0.f;
+  if (rows > 0) {
+    const float k = p.y[(size_t)r0s * p.stride + c];
+    const float m1 = s1 / (float)rows;
+    mu = k + m1;
+    va = fmaxf(s2 / (float)rows - m1 * m1, 0.f);
+  }
+  p.mean[(size_t)s * C + c] = mu;
+  p.var[(size_t)s * C + c] = va;
+  const float sc = p.gamma[c] * rsqrtf(va + p.eps);
+  p.ss[(size_t)s * 2 * C + c] = sc;
+  p.ss[(size_t)s * 2 * C + C + c] = p.beta[c] - mu * sc;
+  if (p.running_mean != nullptr && rows >= 2 && c < p.channels) {
+    int after = 0;                                 // segments with >= 2 rows after s
+    for (int t = s + 1; t < p.nseg; ++t) after += (p.coffs[t + 1] - p.coffs[t]) * p.rpc >= 2;
+    const double w = (double)p.momentum * pow(1.0 - (double)p.momentum, (double)after);
+    atomicAdd(p.run_acc + c, w * (double)mu);
+    atomicAdd(p.run_acc + p.channels + c, w * (double)va * ((double)rows / (double)(rows - 1)));
+  }
 }
 
-// running statistics after one forward per segment, in segment order (what
-// the reference's one-video forwards leave behind): thread per channel,
-// segments with < 2 rows skipped (torch raises on them; empty = padding)
-__global__ __launch_bounds__(256) void bn_seg_running_f32_kernel(
-    const int* __restrict__ seg, int nseg, const float* __restrict__ mean,
-    const float* __restrict__ var, int C, int channels, float momentum,
-    float* __restrict__ running_mean, float* __restrict__ running_var) {
+// r = (1-m)^K r + acc over the K segments with >= 2 rows; re-arms acc
+__global__ __launch_bounds__(256) void bn_seg_running_f32_kernel(BnSegParams p) {
   const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= channels) return;
-  float rm = running_mean[c], rv = running_var[c];
-  for (int s = 0; s < nseg; ++s) {
-    const int rows = seg[s + 1] - seg[s];
-    if (rows < 2) continue;
-    rm = (1.f - momentum) * rm + momentum * mean[(size_t)s * C + c];
-    rv = (1.f - momentum) * rv +
-         momentum * var[(size_t)s * C + c] * ((float)rows / (float)(rows - 1));
-  }
-  running_mean[c] = rm;
-  running_var[c] = rv;
+  if (c >= p.channels) return;
+  int valid = 0;
+  for (int t = 0; t < p.nseg; ++t) valid += (p.coffs[t + 1] - p.coffs[t]) * p.rpc >= 2;
+  const double decay = pow(1.0 - (double)p.momentum, (double)valid);
+  p.running_mean[c] = (float)(decay * (double)p.running_mean[c] + p.run_acc[c]);
+  p.running_var[c] = (float)(decay * (double)p.running_var[c] + p.run_acc[p.channels + c]);
+  p.run_acc[c] = 0.0;
+  p.run_acc[p.channels + c] = 0.0;
 }
 
-// RPT consecutive rows x 4 channels per thread; the first row's segment by
-// binary search, later rows step forward across segment boundaries
+// RPT consecutive rows x 4 channels per thread: z = y * scale + shift of the
+// row's segment (+ residual) (+ ReLU); the first row's segment by binary
+// search, later rows step forward across segment boundaries
 #define BN_APPLY_RPT 4
 __global__ __launch_bounds__(256) void bn_seg_apply_f32_kernel(
     const float* __restrict__ y, float* __restrict__ z, const float* __restrict__ res,
-    const int* __restrict__ seg, int nseg, const float* __restrict__ mean,
-    const float* __restrict__ var, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float eps, int relu, long long M, int C, int y_stride,
-    int z_stride, int res_stride) {
+    const int* __restrict__ coffs, int nseg, int rpc, const float* __restrict__ ss, int relu,
+    long long M, int C, int y_stride, int z_stride, int res_stride) {
   const int cq = C / 4;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   const long long groups = (M + BN_APPLY_RPT - 1) / BN_APPLY_RPT;
@@ -213,30 +272,24 @@ __global__ __launch_bounds__(256) void bn_seg_apply_f32_kernel(
   const int c = (int)(i - g * cq) * 4;
   const int ra = (int)(g * BN_APPLY_RPT);
   const int rb = (int)min((long long)ra + BN_APPLY_RPT, M);
-  const int lo_row = seg[0], hi_row = seg[nseg];
-  const float4 gm = *(const float4*)(gamma + c);
-  const float4 bt = *(const float4*)(beta + c);
-  int s = -1;
+  const int lo_row = coffs[0] * rpc, hi_row = coffs[nseg] * rpc;
+  int s = -1, s_end = 0;
   float4 sc = make_float4(0.f, 0.f, 0.f, 0.f), sh = sc;
   for (int r = ra; r < rb; ++r) {
     if (r < lo_row || r >= hi_row) continue;
-    if (s < 0 || r >= seg[s + 1]) {
+    if (s < 0 || r >= s_end) {
       if (s < 0) {
-        int lo = 0, hi = nseg - 1;                 // last s with seg[s] <= r
+        int lo = 0, hi = nseg - 1;                 // last s with start(s) <= r
         while (lo < hi) {
           const int mid = (lo + hi + 1) >> 1;
-          if (seg[mid] <= r) lo = mid; else hi = mid - 1;
+          if (coffs[mid] * rpc <= r) lo = mid; else hi = mid - 1;
         }
         s = lo;
-      } else {
-        while (r >= seg[s + 1]) ++s;
       }
-      const float4 m = *(const float4*)(mean + (size_t)s * C + c);
-      const float4 q = *(const float4*)(var + (size_t)s * C + c);
-      sc = make_float4(gm.x * rsqrtf(q.x + eps), gm.y * rsqrtf(q.y + eps),
-                       gm.z * rsqrtf(q.z + eps), gm.w * rsqrtf(q.w + eps));
-      sh = make_float4(bt.x - m.x * sc.x, bt.y - m.y * sc.y, bt.z - m.z * sc.z,
-                       bt.w - m.w * sc.w);
+      while (r >= coffs[s + 1] * rpc) ++s;
+      s_end = coffs[s + 1] * rpc;
+      sc = *(const float4*)(ss + (size_t)s * 2 * C + c);
+      sh = *(const float4*)(ss + (size_t)s * 2 * C + C + c);
     }
     const float4 v = *(const float4*)(y + (size_t)r * y_stride + c);
     float o[4] = {fmaf(v.x, sc.x, sh.x), fmaf(v.y, sc.y, sh.y), fmaf(v.z, sc.z, sh.z),
@@ -255,47 +308,64 @@ __global__ __launch_bounds__(256) void bn_seg_apply_f32_kernel(
 
 extern "C" {
 
-long long rnb_bn_seg_scratch_floats(int nseg, int C) {
-  return (long long)nseg * BN_SEG_BLOCKS * 2 * C;
+// Blocks per segment: a fixed 32, so the split of a video's rows -- and with
+// it the fp32 rounding of its statistics -- does not depend on the batch the
+// video is in (per-video results are batch-invariant, like the reference's
+// one-video forwards). A split sized to fill the chip from (nseg, C, M)
+// measured the same (13.4 ms per 24-clip forward, 60.2 ms per 128).
+static int g_bn_fixed_bps = 0;     // > 0: override (experiments)
+void rnb_bn_seg_set_bps(int bps) { g_bn_fixed_bps = bps > BN_SEG_MAX_BPS ? BN_SEG_MAX_BPS : bps; }
+
+int rnb_bn_seg_bps(int nseg, int C, long long M) {
+  (void)nseg; (void)C; (void)M;
+  return g_bn_fixed_bps > 0 ? g_bn_fixed_bps : 32;
 }
 
-// seg: device [nseg+1] row offsets; mean/var: [nseg][C] (biased variance)
-int rnb_bn_seg_stats_f32(const float* y, const int* seg, int nseg, int C, int stride,
-                         float* scratch, float* mean, float* var, hipStream_t stream) {
+long long rnb_bn_seg_scratch_floats(int nseg, int C, long long M) {
+  return (long long)nseg * rnb_bn_seg_bps(nseg, C, M) * 2 * C;
+}
+
+// coffs: device [nseg+1] clip offsets; rows of segment s = [coffs[s] rpc,
+// coffs[s+1] rpc) of the [M][stride] tensor. Outputs mean / var [nseg][C]
+// (biased), ss [nseg][2][C] (scale, shift); running_* [channels] updated in
+// place (null: no update). run_acc fp64 [2][channels] must be zero before the
+// first launch; the running kernel re-arms it.
+int rnb_bn_seg_stats_f32(const float* y, const int* coffs, int nseg, int rpc, long long M,
+                         int C, int stride, float* scratch, long long scratch_floats,
+                         double* run_acc, const float* gamma, const float* beta,
+                         float eps, float momentum, int channels, float* running_mean,
+                         float* running_var, float* mean, float* var, float* ss,
+                         hipStream_t stream) {
   if (nseg <= 0 || C <= 0) return 0;
-  if (C % 4 != 0 || stride % 4 != 0 || stride < C) return -2;
-  const dim3 grid(BN_SEG_BLOCKS, nseg);
-  const dim3 fgrid((C + 255) / 256, nseg);
-  hipLaunchKernelGGL(bn_seg_sums_f32_kernel, grid, dim3(256), 0, stream, y, seg, C, stride,
-                     scratch);
-  hipLaunchKernelGGL(bn_seg_finalize_f32_kernel, fgrid, dim3(256), 0, stream, y, seg, C, stride,
-                     (const float*)scratch, mean, var);
+  if (C % 4 != 0 || stride % 4 != 0 || stride < C || channels > C || rpc <= 0) return -2;
+  if (M * (long long)stride > 0x7FFFFFFFLL * 4) return -3;
+  BnSegParams p;
+  p.y = y; p.coffs = coffs; p.nseg = nseg; p.rpc = rpc; p.C = C; p.stride = stride;
+  p.bps = rnb_bn_seg_bps(nseg, C, M);
+  if ((long long)nseg * p.bps * 2 * C > scratch_floats) return -4;
+  p.partial = scratch; p.run_acc = run_acc;
+  p.gamma = gamma; p.beta = beta; p.eps = eps; p.momentum = momentum;
+  p.channels = channels; p.running_mean = running_mean; p.running_var = running_var;
+  p.mean = mean; p.var = var; p.ss = ss;
+  hipLaunchKernelGGL(bn_seg_sums_f32_kernel, dim3(p.bps, nseg), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL(bn_seg_finalize_f32_kernel, dim3((C + 255) / 256, nseg), dim3(256), 0,
+                     stream, p);
+  if (running_mean != nullptr)
+    hipLaunchKernelGGL(bn_seg_running_f32_kernel, dim3((channels + 255) / 256), dim3(256), 0,
+                       stream, p);
   return (int)hipGetLastError();
 }
 
-// running_mean / running_var: [channels] fp32, updated in place
-int rnb_bn_seg_running_f32(const int* seg, int nseg, const float* mean, const float* var, int C,
-                           int channels, float momentum, float* running_mean,
-                           float* running_var, hipStream_t stream) {
-  if (nseg <= 0 || channels <= 0) return 0;
-  if (channels > C) return -2;
-  hipLaunchKernelGGL(bn_seg_running_f32_kernel, dim3((channels + 255) / 256), dim3(256), 0,
-                     stream, seg, nseg, mean, var, C, channels, momentum, running_mean,
-                     running_var);
-  return (int)hipGetLastError();
-}
-
-int rnb_bn_seg_apply_f32(const float* y, float* z, const float* res, const int* seg, int nseg,
-                         const float* mean, const float* var, const float* gamma,
-                         const float* beta, float eps, int relu, long long M, int C,
-                         int y_stride, int z_stride, int res_stride, hipStream_t stream) {
+int rnb_bn_seg_apply_f32(const float* y, float* z, const float* res, const int* coffs, int nseg,
+                         int rpc, const float* ss, int relu, long long M, int C, int y_stride,
+                         int z_stride, int res_stride, hipStream_t stream) {
   if (M <= 0 || C <= 0 || nseg <= 0) return 0;
-  if (C % 4 || y_stride % 4 || z_stride % 4 || (res && res_stride % 4)) return -2;
+  if (C % 4 || y_stride % 4 || z_stride % 4 || (res && res_stride % 4) || rpc <= 0) return -2;
   const long long n = (M + BN_APPLY_RPT - 1) / BN_APPLY_RPT * (C / 4);
   if (M > 0x7FFFFFFFLL) return -3;
   hipLaunchKernelGGL(bn_seg_apply_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     stream, y, z, res, seg, nseg, mean, var, gamma, beta, eps, relu, M, C,
-                     y_stride, z_stride, res_stride);
+                     stream, y, z, res, coffs, nseg, rpc, ss, relu, M, C, y_stride, z_stride,
+                     res_stride);
   return (int)hipGetLastError();
 }
 

@@ -345,28 +345,21 @@ class R2P1DEngine:
                                            dtype=torch.float64, device=x.device)
                         kw["out_stats"] = (sums, clip_seg)
                     y = op.layer.forward_hip(src, None, **kw)
-                    seg = rows = None
+                    # segments in clip units: the BN kernels scale the clip
+                    # offsets by the layer's rows per clip (T*H*W)
                     thw = y.shape[1] * y.shape[2] * y.shape[3]
-                    if coffs is not None:
-                        seg = coffs * thw
-                        if clip_offsets is not None:
-                            rows = [(b - a) * thw for a, b in zip(clip_offsets[:-1],
-                                                                  clip_offsets[1:])]
+                    if coffs is None and self.f32:
+                        coffs = torch.tensor([0, x.shape[0]], dtype=torch.int32,
+                                             device=x.device)
                     if (defer and self._defer_ok[i] and self.f32
                             and self.ops[i + 1].layer.accepts_input_affine(y.shape)):
                         # statistics now; normalise + ReLU inside the next conv
-                        if seg is None:
-                            seg = torch.tensor([0, y.shape[0] * thw], dtype=torch.int32,
-                                               device=y.device)
                         if clip_seg is None:
                             clip_seg = self._clip_segments(coffs, x.shape[0], x.device)
-                        pending = (op.bn.scale_shift_f32(y, seg, sums), clip_seg)
+                        pending = (op.bn.scale_shift_f32(y, coffs, sums, rpc=thw), clip_seg)
                     else:
-                        if sums is not None and seg is None:
-                            seg = torch.tensor([0, y.shape[0] * thw], dtype=torch.int32,
-                                               device=y.device)
-                        y = op.bn.forward_hip(y, res, op.bn_relu, out=y, segments=seg,
-                                              seg_rows=rows, sums=sums)
+                        y = op.bn.forward_hip(y, res, op.bn_relu, out=y, segments=coffs,
+                                              sums=sums, rpc=thw)
                 else:
                     y = op.layer.forward_torch(src, None, out_dtype=self.dtype)
                     y = op.bn.forward_torch(y, res, op.bn_relu, out_dtype=self.dtype,

@@ -80,9 +80,11 @@ class BatchNormBatch:
     def forward_hip_f32(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,
                         out: Optional[torch.Tensor] = None,
                         segments: Optional[torch.Tensor] = None,
-                        seg_rows=None, sums=None) -> torch.Tensor:
-        """fp32 tensor; ``segments``: device int32 [nseg+1] ROW offsets (each
-        segment -- one video -- gets its own statistics); default one segment."""
+                        seg_rows=None, sums=None, rpc: int = 1) -> torch.Tensor:
+        """fp32 tensor; ``segments``: device int32 [nseg+1] offsets in units of
+        ``rpc`` rows (clip offsets with rpc = T*H*W, or row offsets with rpc =
+        1): each segment -- one video -- gets its own statistics; default one
+        segment."""
         from .native import kernels
         k = kernels()
         N, T, H, W, Cs = y.shape
@@ -91,74 +93,98 @@ class BatchNormBatch:
         if M == 0:
             return z
         if segments is None:
-            segments = torch.tensor([0, M], dtype=torch.int32, device=y.device)
-            seg_rows = [M]
+            segments, rpc = self._whole(M, y.device), 1
         nseg = segments.numel() - 1
-        # statistics (one read of y, or the producer epilogue's sums) and the
-        # in-order running update (one kernel, thread per channel)
-        mean, var = self._stats(y, segments, sums)
+        # statistics, scale / shift and the running update (three small
+        # kernels, or the producer epilogue's sums), then the apply
+        ss = self.scale_shift_f32(y, segments, sums, rpc)
         stream = torch.cuda.current_stream(y.device).cuda_stream
         k.bn_seg_apply_f32(y.data_ptr(), z.data_ptr(),
                            residual.data_ptr() if residual is not None else None,
-                           segments.data_ptr(), nseg, mean.data_ptr(), var.data_ptr(),
-                           self.gamma.data_ptr(), self.beta.data_ptr(), self.eps,
-                           1 if relu else 0, M, C, Cs, z.shape[-1],
+                           segments.data_ptr(), nseg, rpc, ss.data_ptr(), 1 if relu else 0,
+                           M, C, Cs, z.shape[-1],
                            residual.shape[-1] if residual is not None else 0, stream)
         return z
 
+    def _whole(self, M: int, device) -> torch.Tensor:
+        t = getattr(self, "_whole_seg", None)
+        if t is None or int(t[1]) != M or t.device != device:
+            t = self._whole_seg = torch.tensor([0, M], dtype=torch.int32, device=device)
+        return t
+
     @staticmethod
-    def moments_from_sums(sums: torch.Tensor, segments: torch.Tensor):
+    def moments_from_sums(sums: torch.Tensor, segments: torch.Tensor, rpc: int = 1):
         """fp32 mean / biased variance [nseg, C] from a producer epilogue's fp64
         per-video sums [nseg, 2, C] (empty videos: 0, 0)."""
-        n = (segments[1:] - segments[:-1]).to(torch.float64).clamp(min=1.0)[:, None]
+        n = ((segments[1:] - segments[:-1]).to(torch.float64) * rpc).clamp(min=1.0)[:, None]
         mean = sums[:, 0] / n
         var = (sums[:, 1] / n - mean * mean).clamp(min=0.0)
         return mean.float().contiguous(), var.float().contiguous()
 
-    def _stats(self, y: torch.Tensor, segments: torch.Tensor, sums=None):
-        """(mean, var) [nseg, Cp] fp32 of the segments: from the producer's
-        epilogue sums when given, else one read of y; running update applied."""
+    def _buffers(self, nseg: int, C: int, M: int, device):
+        """Scratch partials and the fp64 running-update accumulators (zero
+        between launches: the running kernel re-arms them); outgrown buffers
+        are retired, not freed (captured graphs use them)."""
+        from .native import kernels
+        need = kernels().bn_seg_scratch_floats(nseg, C, M)
+        if self._scratch is None or self._scratch.numel() < need:
+            if self._scratch is not None:
+                self._retired.append(self._scratch)
+            self._scratch = torch.empty(need, dtype=torch.float32, device=device)
+        acc = getattr(self, "_run_acc", None)
+        if acc is None:
+            acc = self._run_acc = torch.zeros(2 * self.channels, dtype=torch.float64,
+                                              device=device)
+        return self._scratch, acc
+
+    def _stats_ss(self, y: torch.Tensor, segments: torch.Tensor, sums=None, rpc: int = 1):
+        """(mean, var [nseg, Cp], scale/shift [nseg, 2, Cp]) fp32 of the
+        segments, running update applied: one kernel reading y, or (opt-in)
+        from the producer's epilogue sums."""
         from .native import kernels
         k = kernels()
         N, T, H, W, Cs = y.shape
-        C = self.channels_p
+        M, C = N * T * H * W, self.channels_p
         nseg = segments.numel() - 1
-        stream = torch.cuda.current_stream(y.device).cuda_stream
         if sums is not None:
-            mean, var = self.moments_from_sums(sums[:, :, :C], segments)
+            mean, var = self.moments_from_sums(sums[:, :, :C], segments, rpc)
+            if self.update_running:
+                self._update_segments_dev(mean, var, segments * rpc)
+            scale = self.gamma * torch.rsqrt(var + self.eps)
+            ss = torch.stack([scale, self.beta - mean * scale], dim=1).contiguous()
         else:
-            need = k.bn_seg_scratch_floats(nseg, C)
-            if self._scratch is None or self._scratch.numel() < need:
-                if self._scratch is not None:
-                    self._retired.append(self._scratch)
-                self._scratch = torch.empty(need, dtype=torch.float32, device=y.device)
+            scratch, acc = self._buffers(nseg, C, M, y.device)
             mean = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
             var = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
-            k.bn_seg_stats_f32(y.data_ptr(), segments.data_ptr(), nseg, C, Cs,
-                               self._scratch.data_ptr(), mean.data_ptr(), var.data_ptr(),
-                               stream)
-        if self.update_running:
-            k.bn_seg_running_f32(segments.data_ptr(), nseg, mean.data_ptr(), var.data_ptr(), C,
-                                 self.channels, self.momentum, self.running_mean.data_ptr(),
-                                 self.running_var.data_ptr(), stream)
+            ss = torch.empty((nseg, 2, C), dtype=torch.float32, device=y.device)
+            run = self.update_running
+            k.bn_seg_stats_f32(y.data_ptr(), segments.data_ptr(), nseg, rpc, M, C, Cs,
+                               scratch.data_ptr(), scratch.numel(), acc.data_ptr(), self.gamma.data_ptr(), self.beta.data_ptr(),
+                               self.eps, self.momentum, self.channels,
+                               self.running_mean.data_ptr() if run else None,
+                               self.running_var.data_ptr() if run else None,
+                               mean.data_ptr(), var.data_ptr(), ss.data_ptr(),
+                               torch.cuda.current_stream(y.device).cuda_stream)
         self.mean, self.var = mean[-1], var[-1]
+        return mean, var, ss
+
+    def _stats(self, y: torch.Tensor, segments: torch.Tensor, sums=None, rpc: int = 1):
+        """(mean, var) [nseg, Cp] fp32 of the segments; running update applied."""
+        mean, var, _ = self._stats_ss(y, segments, sums, rpc)
         return mean, var
 
     def scale_shift_f32(self, y: torch.Tensor, segments: torch.Tensor,
-                        sums=None) -> torch.Tensor:
-        """Statistics only (plus the running update), for a BN whose apply is
-        deferred into the consuming conv: [nseg, 2, Cp] fp32 rows (scale =
-        gamma * rsqrt(var + eps), shift = beta - mean * scale) per segment."""
-        mean, var = self._stats(y, segments, sums)
-        scale = self.gamma * torch.rsqrt(var + self.eps)
-        shift = self.beta - mean * scale
-        return torch.stack([scale, shift], dim=1).contiguous()
+                        sums=None, rpc: int = 1) -> torch.Tensor:
+        """Statistics (plus the running update) as [nseg, 2, Cp] fp32 rows
+        (scale = gamma * rsqrt(var + eps), shift = beta - mean * scale) per
+        segment: the apply's operand, or a BN deferred into the next conv."""
+        return self._stats_ss(y, segments, sums, rpc)[2]
 
     def forward_hip(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,
                     out: Optional[torch.Tensor] = None, segments=None,
-                    seg_rows=None, sums=None) -> torch.Tensor:
+                    seg_rows=None, sums=None, rpc: int = 1) -> torch.Tensor:
         if y.dtype == torch.float32:
-            return self.forward_hip_f32(y, residual, relu, out, segments, seg_rows, sums)
+            return self.forward_hip_f32(y, residual, relu, out, segments, seg_rows, sums, rpc)
         if segments is not None and segments.numel() > 2:
             raise NotImplementedError("per-video BN statistics are fp32 only")
         from .native import kernels

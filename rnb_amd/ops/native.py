@@ -228,23 +228,23 @@ class Kernels:
                                      ctypes.c_void_p, ctypes.c_float, ctypes.c_int,
                                      ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
-        lib.rnb_bn_seg_scratch_floats.argtypes = [ctypes.c_int, ctypes.c_int]
+        lib.rnb_bn_seg_bps.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_longlong]
+        lib.rnb_bn_seg_set_bps.argtypes = [ctypes.c_int]
+        if os.environ.get("RNB_BN_BPS"):
+            # fixed BN statistics blocks per segment (batch-invariant split)
+            lib.rnb_bn_seg_set_bps(int(os.environ["RNB_BN_BPS"]))
+        lib.rnb_bn_seg_scratch_floats.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_longlong]
         lib.rnb_bn_seg_scratch_floats.restype = ctypes.c_longlong
-        lib.rnb_bn_seg_stats_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
-                                             ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
-                                             ctypes.c_void_p, ctypes.c_void_p,
-                                             ctypes.c_void_p]
-        lib.rnb_bn_seg_running_f32.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
-                                               ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                                               ctypes.c_float, ctypes.c_void_p,
-                                               ctypes.c_void_p, ctypes.c_void_p]
-        lib.rnb_bn_seg_apply_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
-                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
-                                             ctypes.c_void_p, ctypes.c_void_p,
-                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
-                                             ctypes.c_int, ctypes.c_longlong, ctypes.c_int,
-                                             ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                             ctypes.c_void_p]
+        lib.rnb_bn_seg_stats_f32.argtypes = [
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_longlong,
+            ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_float,
+            ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p]
+        lib.rnb_bn_seg_apply_f32.argtypes = [
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+            ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_int,
+            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         lib.rnb_video_reduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_void_p]
@@ -378,27 +378,25 @@ class Kernels:
                                      beta_ptr, eps, relu, M, C, y_stride, z_stride, res_stride,
                                      stream), "bn_apply")
 
-    def bn_seg_scratch_floats(self, nseg: int, C: int) -> int:
-        return self.lib.rnb_bn_seg_scratch_floats(nseg, C)
+    def bn_seg_bps(self, nseg: int, C: int, M: int) -> int:
+        return self.lib.rnb_bn_seg_bps(nseg, C, M)
 
-    def bn_seg_stats_f32(self, y_ptr, seg_ptr, nseg, C, stride, scratch_ptr, mean_ptr, var_ptr,
-                         stream):
-        _check(self.lib.rnb_bn_seg_stats_f32(y_ptr, seg_ptr, nseg, C, stride, scratch_ptr,
-                                             mean_ptr, var_ptr, stream), "bn_seg_stats_f32")
+    def bn_seg_scratch_floats(self, nseg: int, C: int, M: int) -> int:
+        return self.lib.rnb_bn_seg_scratch_floats(nseg, C, M)
 
-    def bn_seg_running_f32(self, seg_ptr, nseg, mean_ptr, var_ptr, C, channels, momentum,
-                           rmean_ptr, rvar_ptr, stream):
-        _check(self.lib.rnb_bn_seg_running_f32(seg_ptr, nseg, mean_ptr, var_ptr, C, channels,
-                                               momentum, rmean_ptr, rvar_ptr, stream),
-               "bn_seg_running_f32")
+    def bn_seg_stats_f32(self, y_ptr, coffs_ptr, nseg, rpc, M, C, stride, scratch_ptr,
+                         scratch_floats, run_acc_ptr, gamma_ptr, beta_ptr, eps, momentum,
+                         channels, rmean_ptr, rvar_ptr, mean_ptr, var_ptr, ss_ptr, stream):
+        _check(self.lib.rnb_bn_seg_stats_f32(y_ptr, coffs_ptr, nseg, rpc, M, C, stride,
+                                             scratch_ptr, scratch_floats, run_acc_ptr, gamma_ptr, beta_ptr, eps, momentum,
+                                             channels, rmean_ptr, rvar_ptr, mean_ptr, var_ptr,
+                                             ss_ptr, stream), "bn_seg_stats_f32")
 
-    def bn_seg_apply_f32(self, y_ptr, z_ptr, res_ptr, seg_ptr, nseg, mean_ptr, var_ptr,
-                         gamma_ptr, beta_ptr, eps, relu, M, C, y_stride, z_stride, res_stride,
-                         stream):
-        _check(self.lib.rnb_bn_seg_apply_f32(y_ptr, z_ptr, res_ptr, seg_ptr, nseg, mean_ptr,
-                                             var_ptr, gamma_ptr, beta_ptr, eps, relu, M, C,
-                                             y_stride, z_stride, res_stride, stream),
-               "bn_seg_apply_f32")
+    def bn_seg_apply_f32(self, y_ptr, z_ptr, res_ptr, coffs_ptr, nseg, rpc, ss_ptr, relu, M, C,
+                         y_stride, z_stride, res_stride, stream):
+        _check(self.lib.rnb_bn_seg_apply_f32(y_ptr, z_ptr, res_ptr, coffs_ptr, nseg, rpc,
+                                             ss_ptr, relu, M, C, y_stride, z_stride, res_stride,
+                                             stream), "bn_seg_apply_f32")
 
     def clipgen_u8(self, out_ptr, vids_ptr, starts_ptr, nclips, F, H, W, stream):
         _check(self.lib.rnb_clipgen_u8(out_ptr, vids_ptr, starts_ptr, nclips, F, H, W,

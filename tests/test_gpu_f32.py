@@ -205,10 +205,14 @@ def test_clipgen_video_args_kernel_matches_clipgen_u8():
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("units", ["rows", "clips"])
 @pytest.mark.parametrize("res,relu", [(False, True), (True, True), (True, False)])
-def test_bn_per_video_stats_f32_kernel_matches_torch(res, relu):
+def test_bn_per_video_stats_f32_kernel_matches_torch(res, relu, units):
     """Training-mode BN with one set of statistics per video of the batch
-    (csrc/bn_ops.hip bn_seg_*_f32) vs the per-video torch reference."""
+    (csrc/bn_ops.hip: one stats dispatch + apply) vs the per-video torch
+    reference, segments given as row offsets or as clip offsets x rows per
+    clip, with a trailing empty (graph padding) video; launched twice so the
+    running-update accumulators must re-arm."""
     from rnb_amd.ops.bn import BatchNormBatch
     bn = torch.nn.BatchNorm3d(88)
     with torch.no_grad():
@@ -218,19 +222,24 @@ def test_bn_per_video_stats_f32_kernel_matches_torch(res, relu):
     ref_op = BatchNormBatch(bn, 88, torch.device("cpu"))
     y = torch.randn((5, 4, 14, 14, 88), device=DEV) * 3 + 1
     r = torch.randn_like(y) if res else None
-    offs = [0, 1, 3, 5]
+    offs = [0, 1, 3, 5, 5]
     thw = 4 * 14 * 14
-    seg = torch.tensor([o * thw for o in offs], dtype=torch.int32, device=DEV)
-    z = op.forward_hip(y, r, relu, segments=seg, seg_rows=[2 * thw, 2 * thw, 2 * thw])
-    ref = ref_op.forward_torch(y.cpu(), r.cpu() if res else None, relu,
-                               out_dtype=torch.float32, clip_offsets=offs)
-    torch.cuda.synchronize()
-    err = (z.cpu() - ref).abs().max().item()
-    assert err < 1e-4 * ref.abs().max().item(), err
-    # running statistics: the device kernel's in-order EMA over the videos vs
-    # the torch reference's per-video updates
+    if units == "rows":
+        seg, rpc = torch.tensor([o * thw for o in offs], dtype=torch.int32, device=DEV), 1
+    else:
+        seg, rpc = torch.tensor(offs, dtype=torch.int32, device=DEV), thw
+    for _ in range(2):
+        z = op.forward_hip(y, r, relu, segments=seg, rpc=rpc)
+        ref = ref_op.forward_torch(y.cpu(), r.cpu() if res else None, relu,
+                                   out_dtype=torch.float32, clip_offsets=offs)
+        torch.cuda.synchronize()
+        err = (z.cpu() - ref).abs().max().item()
+        assert err < 1e-4 * ref.abs().max().item(), err
+    # running statistics: the device kernel's closed-form update over the
+    # videos (fp64) vs the torch reference's in-order per-video updates
     assert torch.allclose(op.running_mean.cpu(), ref_op.running_mean, atol=1e-5)
     assert torch.allclose(op.running_var.cpu(), ref_op.running_var, rtol=1e-4, atol=1e-5)
+    assert float(op._run_acc.abs().sum()) == 0.0
 
 
 def test_r34_f32_batch_bn_two_videos_match_module_per_video():
