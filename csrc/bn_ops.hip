@@ -243,6 +243,41 @@ __global__ __launch_bounds__(256) void bn_seg_finalize_f32_kernel(BnSegParams p)
   }
 }
 
+// The same from a producer epilogue's fp64 per-segment sums [nseg][2][sums_c]
+// (sum, sum of squares of the conv output; fp64, so E[x^2] - mean^2 keeps
+// fp32 accuracy without a shift): moments, scale / shift, running term; the
+// sums are zeroed after use (re-armed for the producer's next launch).
+__global__ __launch_bounds__(256) void bn_seg_finalize_sums_f32_kernel(BnSegParams p,
+                                                                       double* sums,
+                                                                       int sums_c) {
+  const int s = blockIdx.y, C = p.C;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const int rows = (p.coffs[s + 1] - p.coffs[s]) * p.rpc;
+  double* sp = sums + (size_t)s * 2 * sums_c;
+  const double s1 = sp[c], s2 = sp[sums_c + c];
+  sp[c] = 0.0;
+  sp[sums_c + c] = 0.0;
+  float mu = 0.f, va = 0.f;
+  if (rows > 0) {
+    const double m = s1 / (double)rows;
+    mu = (float)m;
+    va = (float)fmax(s2 / (double)rows - m * m, 0.0);
+  }
+  p.mean[(size_t)s * C + c] = mu;
+  p.var[(size_t)s * C + c] = va;
+  const float sc = p.gamma[c] * rsqrtf(va + p.eps);
+  p.ss[(size_t)s * 2 * C + c] = sc;
+  p.ss[(size_t)s * 2 * C + C + c] = p.beta[c] - mu * sc;
+  if (p.running_mean != nullptr && rows >= 2 && c < p.channels) {
+    int after = 0;
+    for (int t = s + 1; t < p.nseg; ++t) after += (p.coffs[t + 1] - p.coffs[t]) * p.rpc >= 2;
+    const double w = (double)p.momentum * pow(1.0 - (double)p.momentum, (double)after);
+    atomicAdd(p.run_acc + c, w * (double)mu);
+    atomicAdd(p.run_acc + p.channels + c, w * (double)va * ((double)rows / (double)(rows - 1)));
+  }
+}
+
 // r = (1-m)^K r + acc over the K segments with >= 2 rows; re-arms acc
 __global__ __launch_bounds__(256) void bn_seg_running_f32_kernel(BnSegParams p) {
   const int c = blockIdx.x * 256 + threadIdx.x;
@@ -350,6 +385,28 @@ int rnb_bn_seg_stats_f32(const float* y, const int* coffs, int nseg, int rpc, lo
   hipLaunchKernelGGL(bn_seg_sums_f32_kernel, dim3(p.bps, nseg), dim3(256), 0, stream, p);
   hipLaunchKernelGGL(bn_seg_finalize_f32_kernel, dim3((C + 255) / 256, nseg), dim3(256), 0,
                      stream, p);
+  if (running_mean != nullptr)
+    hipLaunchKernelGGL(bn_seg_running_f32_kernel, dim3((channels + 255) / 256), dim3(256), 0,
+                       stream, p);
+  return (int)hipGetLastError();
+}
+
+// As rnb_bn_seg_stats_f32, from a producer epilogue's fp64 sums [nseg][2][sums_c]
+// (zeroed on the way out) instead of a read of the tensor.
+int rnb_bn_seg_stats_from_sums_f32(double* sums, int sums_c, const int* coffs, int nseg, int rpc,
+                                   int C, double* run_acc, const float* gamma, const float* beta,
+                                   float eps, float momentum, int channels, float* running_mean,
+                                   float* running_var, float* mean, float* var, float* ss,
+                                   hipStream_t stream) {
+  if (nseg <= 0 || C <= 0) return 0;
+  if (sums_c < C || channels > C || rpc <= 0) return -2;
+  BnSegParams p = {};
+  p.coffs = coffs; p.nseg = nseg; p.rpc = rpc; p.C = C; p.stride = C; p.bps = 1;
+  p.run_acc = run_acc; p.gamma = gamma; p.beta = beta; p.eps = eps; p.momentum = momentum;
+  p.channels = channels; p.running_mean = running_mean; p.running_var = running_var;
+  p.mean = mean; p.var = var; p.ss = ss;
+  hipLaunchKernelGGL(bn_seg_finalize_sums_f32_kernel, dim3((C + 255) / 256, nseg), dim3(256), 0,
+                     stream, p, sums, sums_c);
   if (running_mean != nullptr)
     hipLaunchKernelGGL(bn_seg_running_f32_kernel, dim3((channels + 255) / 256), dim3(256), 0,
                        stream, p);

@@ -726,7 +726,7 @@ int rnb_wino_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) {
   if (blocks > 0x7FFFFFFF) return -8;
   const dim3 grid((unsigned)blocks), block(256);
   const bool st = p.out_stats != nullptr;
-  if (st && (variant < 4 || variant > 6)) return -9;   // epilogue statistics: variants 4-6
+  if (st && variant < 4) return -9;             // epilogue statistics: variants 4-9
   switch (variant) {
     case 0: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 1>), grid, block, 0, stream, p); break;
     case 1: hipLaunchKernelGGL((conv_wino_f32_kernel<3, 1>), grid, block, 0, stream, p); break;
@@ -744,9 +744,18 @@ int rnb_wino_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) {
       if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<3, 2, true>), grid, block, 0, stream, p);
       else hipLaunchKernelGGL((conv_wino_f32_kernel<3, 2>), grid, block, 0, stream, p);
       break;
-    case 7: hipLaunchKernelGGL((conv_wino_f32_kernel<1, 3>), grid, block, 0, stream, p); break;
-    case 8: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 3>), grid, block, 0, stream, p); break;
-    default: hipLaunchKernelGGL((conv_wino_f32_kernel<3, 3>), grid, block, 0, stream, p); break;
+    case 7:
+      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<1, 3, true>), grid, block, 0, stream, p);
+      else hipLaunchKernelGGL((conv_wino_f32_kernel<1, 3>), grid, block, 0, stream, p);
+      break;
+    case 8:
+      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<2, 3, true>), grid, block, 0, stream, p);
+      else hipLaunchKernelGGL((conv_wino_f32_kernel<2, 3>), grid, block, 0, stream, p);
+      break;
+    default:
+      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<3, 3, true>), grid, block, 0, stream, p);
+      else hipLaunchKernelGGL((conv_wino_f32_kernel<3, 3>), grid, block, 0, stream, p);
+      break;
   }
   return (int)hipGetLastError();
 }

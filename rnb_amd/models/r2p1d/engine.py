@@ -294,9 +294,10 @@ class R2P1DEngine:
         bufs: Dict[str, torch.Tensor] = {"x": x}
         coffs = None
         defer = os.environ.get("RNB_BN_DEFER", "1") != "0"
-        # BN statistics from the Winograd epilogues (fp64 atomics): measured
-        # slower than the separate one-read pass (61.9 -> 64.6 ms per 128
-        # clips; 324 -> 259 videos/s one video per call), so opt-in
+        # BN statistics from the Winograd epilogues (fp64 per-wave sums and
+        # atomics, finalized by one kernel): saves the 4.8 ms statistics pass
+        # per 128-clip forward but the epilogues cost 5.1 ms more (60.3 vs
+        # 61.3 ms; 13.4 ms either way at 24 clips), so opt-in
         stats_fuse = os.environ.get("RNB_BN_EPILOGUE_STATS", "0") == "1"
         clip_seg = None              # video index of each clip (deferred BN)
         if self.bn_mode == "batch" and clip_offsets_dev is not None and hip:
@@ -341,8 +342,7 @@ class R2P1DEngine:
                         if clip_seg is None:
                             clip_seg = self._clip_segments(coffs, x.shape[0], x.device)
                         nvid = 1 if coffs is None else coffs.numel() - 1
-                        sums = torch.zeros((nvid, 2, op.layer.geom.cout_p),
-                                           dtype=torch.float64, device=x.device)
+                        sums = op.bn.epilogue_sums(nvid, x.device)
                         kw["out_stats"] = (sums, clip_seg)
                     y = op.layer.forward_hip(src, None, **kw)
                     # segments in clip units: the BN kernels scale the clip

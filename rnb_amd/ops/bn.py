@@ -146,27 +146,46 @@ class BatchNormBatch:
         N, T, H, W, Cs = y.shape
         M, C = N * T * H * W, self.channels_p
         nseg = segments.numel() - 1
+        scratch, acc = self._buffers(nseg, C, M, y.device)
+        mean = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
+        var = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
+        ss = torch.empty((nseg, 2, C), dtype=torch.float32, device=y.device)
+        run = self.update_running
+        stream = torch.cuda.current_stream(y.device).cuda_stream
         if sums is not None:
-            mean, var = self.moments_from_sums(sums[:, :, :C], segments, rpc)
-            if self.update_running:
-                self._update_segments_dev(mean, var, segments * rpc)
-            scale = self.gamma * torch.rsqrt(var + self.eps)
-            ss = torch.stack([scale, self.beta - mean * scale], dim=1).contiguous()
+            if (sums.dtype != torch.float64 or not sums.is_contiguous() or sums.dim() != 3
+                    or sums.shape[0] < nseg or sums.shape[1] != 2 or sums.shape[2] < C):
+                raise ValueError("epilogue sums %s do not match %d segments x %d channels"
+                                 % (tuple(sums.shape), nseg, C))
+            k.bn_seg_stats_from_sums_f32(sums.data_ptr(), sums.shape[2], segments.data_ptr(),
+                                         nseg, rpc, C, acc.data_ptr(), self.gamma.data_ptr(),
+                                         self.beta.data_ptr(), self.eps, self.momentum,
+                                         self.channels,
+                                         self.running_mean.data_ptr() if run else None,
+                                         self.running_var.data_ptr() if run else None,
+                                         mean.data_ptr(), var.data_ptr(), ss.data_ptr(), stream)
         else:
-            scratch, acc = self._buffers(nseg, C, M, y.device)
-            mean = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
-            var = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
-            ss = torch.empty((nseg, 2, C), dtype=torch.float32, device=y.device)
-            run = self.update_running
             k.bn_seg_stats_f32(y.data_ptr(), segments.data_ptr(), nseg, rpc, M, C, Cs,
                                scratch.data_ptr(), scratch.numel(), acc.data_ptr(), self.gamma.data_ptr(), self.beta.data_ptr(),
                                self.eps, self.momentum, self.channels,
                                self.running_mean.data_ptr() if run else None,
                                self.running_var.data_ptr() if run else None,
-                               mean.data_ptr(), var.data_ptr(), ss.data_ptr(),
-                               torch.cuda.current_stream(y.device).cuda_stream)
+                               mean.data_ptr(), var.data_ptr(), ss.data_ptr(), stream)
         self.mean, self.var = mean[-1], var[-1]
         return mean, var, ss
+
+    def epilogue_sums(self, nseg: int, device) -> torch.Tensor:
+        """fp64 [nseg, 2, Cp] per-segment (sum, sum of squares) for a producer
+        conv's epilogue to accumulate into: zero on return, and zeroed again
+        by the finalize kernel that consumes it (persistent; outgrown buffers
+        are retired, captured graphs may use them)."""
+        buf = getattr(self, "_esums", None)
+        if buf is None or buf.shape[0] < nseg:
+            if buf is not None:
+                self._retired.append(buf)
+            buf = self._esums = torch.zeros((max(nseg, 72), 2, self.channels_p),
+                                            dtype=torch.float64, device=device)
+        return buf[:nseg]
 
     def _stats(self, y: torch.Tensor, segments: torch.Tensor, sums=None, rpc: int = 1):
         """(mean, var) [nseg, Cp] fp32 of the segments; running update applied."""

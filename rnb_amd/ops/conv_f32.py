@@ -63,8 +63,7 @@ WINO_BASE = 1010
 WINO_TC = {WINO_BASE + 4: 1, WINO_BASE + 5: 2, WINO_BASE + 6: 3,
            WINO_BASE + 7: 1, WINO_BASE + 8: 2, WINO_BASE + 9: 3}
 # variants 7 / 8 / 9: split input transform with the refill issued in patch-row
-# order 0, 2, 1, 3 (the next chunk starts on V row 0 while rows 1 / 3 land);
-# no epilogue-statistics build, so those launches fall back to 4 / 5 / 6
+# order 0, 2, 1, 3 (the next chunk starts on V row 0 while rows 1 / 3 land)
 WINO_SPLIT = {WINO_BASE + 7, WINO_BASE + 8, WINO_BASE + 9}
 WINO_DEFAULT = WINO_BASE + 8
 # temporal F(4, 3) for stride-1 3x1x1 convs: 32 / 64 output channels per block
@@ -179,8 +178,6 @@ class ConvLayerF32:
             tc, variant, m = WINOT_TC[cid], cid - WINOT_BASE, -4
         else:
             tc, variant, m = WINO_TC[cid], cid - WINO_BASE, 2
-            if out_stats is not None and cid in WINO_SPLIT:
-                variant -= 3
         g = self.geom
         N, T, H, W, C = x.shape
         # the kernels index x / y / residual as dense NDHWC of the input's

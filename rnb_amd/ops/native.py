@@ -241,6 +241,11 @@ class Kernels:
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_float,
             ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_void_p, ctypes.c_void_p]
+        lib.rnb_bn_seg_stats_from_sums_f32.argtypes = [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+            ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+            ctypes.c_float, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         lib.rnb_bn_seg_apply_f32.argtypes = [
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
             ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_int,
@@ -391,6 +396,14 @@ class Kernels:
                                              scratch_ptr, scratch_floats, run_acc_ptr, gamma_ptr, beta_ptr, eps, momentum,
                                              channels, rmean_ptr, rvar_ptr, mean_ptr, var_ptr,
                                              ss_ptr, stream), "bn_seg_stats_f32")
+
+    def bn_seg_stats_from_sums_f32(self, sums_ptr, sums_c, coffs_ptr, nseg, rpc, C, run_acc_ptr,
+                                   gamma_ptr, beta_ptr, eps, momentum, channels, rmean_ptr,
+                                   rvar_ptr, mean_ptr, var_ptr, ss_ptr, stream):
+        _check(self.lib.rnb_bn_seg_stats_from_sums_f32(
+            sums_ptr, sums_c, coffs_ptr, nseg, rpc, C, run_acc_ptr, gamma_ptr, beta_ptr, eps,
+            momentum, channels, rmean_ptr, rvar_ptr, mean_ptr, var_ptr, ss_ptr, stream),
+            "bn_seg_stats_from_sums_f32")
 
     def bn_seg_apply_f32(self, y_ptr, z_ptr, res_ptr, coffs_ptr, nseg, rpc, ss_ptr, relu, M, C,
                          y_stride, z_stride, res_stride, stream):
