@@ -99,6 +99,48 @@ static __device__ __forceinline__ void w_commit_stats(const WinoParams& p, int l
   }
 }
 
+// Block-level variant for a block whose 64 tiles all belong to one video:
+// the lanes' sums (tile tl of wave w, channels tc*16 + 4q + k) are reduced
+// through LDS in two passes (sum, then sum of squares): tile-major rows of
+// CT+1 doubles (odd stride: the 16 tiles of a lane group hit different
+// banks), PARTS threads per channel, then one fp64 atomic per channel and
+// statistic per block -- instead of per-wave cross-lane shuffles and 8
+// atomics per lane group. Needs 64 (CT+1) * 8 + 2048 bytes of LDS, free
+// (the caller's barrier: every wave is done with its staged weights).
+template <int TC>
+static __device__ __forceinline__ void w_block_stats(const WinoParams& p, char* lds, int wave,
+                                                     int tl, int q, int cb, int seg,
+                                                     const double (&s1)[TC][4],
+                                                     const double (&s2)[TC][4]) {
+  constexpr int CT = 16 * TC, CTP = CT + 1, PARTS = 256 / CT;
+  double* red = (double*)lds;
+  double* red2 = red + 64 * CTP;
+  const int tid = threadIdx.x, row = wave * 16 + tl;
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    __syncthreads();
+#pragma unroll
+    for (int tc = 0; tc < TC; ++tc)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) red[row * CTP + tc * 16 + 4 * q + k] = st ? s2[tc][k] : s1[tc][k];
+    __syncthreads();
+    if (tid < PARTS * CT) {
+      const int ch = tid % CT, part = tid / CT;
+      double v = 0.0;
+      for (int i = part; i < 64; i += PARTS) v += red[i * CTP + ch];
+      red2[part * CT + ch] = v;
+    }
+    __syncthreads();
+    if (tid < CT) {
+      double v = 0.0;
+#pragma unroll
+      for (int part = 0; part < PARTS; ++part) v += red2[part * CT + tid];
+      const int co = cb * CT + tid;
+      if (co < p.Cout) atomicAdd(p.out_stats + ((size_t)seg * 2 + st) * p.stats_c + co, v);
+    }
+  }
+}
+
 #define WINO_INVALID 0xFFFFFFF0u
 #ifndef WINO_AD
 #define WINO_AD 1
@@ -417,12 +459,25 @@ __global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f
   const int oy = 2 * ty, ox = 2 * tx;
   const bool has_res = p.res != nullptr;
   const int seg = (stats && tvalid) ? p.clip_seg[f / p.clip_frames] : 0;
+  // statistics: block-level LDS reduction when the block's tiles are all in
+  // one video (the first and last valid tile: clips are in video order)
+  bool buni = false;
+  int bseg = 0;
+  if constexpr (stats) {
+    const int ta = tb * 64, tz = min(tb * 64 + 63, p.n_tiles - 1);
+    const int fa = w_div(w_div(ta, p.m_tw, p.s_tw), p.m_th, p.s_th);
+    const int fz = w_div(w_div(tz, p.m_tw, p.s_tw), p.m_th, p.s_th);
+    bseg = p.clip_seg[fa / p.clip_frames];
+    buni = bseg == p.clip_seg[fz / p.clip_frames];
+  }
+  double s1[TC][4], s2[TC][4];
 #pragma unroll
   for (int tc = 0; tc < TC; ++tc) {
     const int co = cb * CT + tc * 16 + 4 * q;
-    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s1[tc][k] = s2[tc][k] = 0.0;
     if (co >= p.Cout || !tvalid) {
-      if (stats) w_commit_stats(p, lane, false, seg, co, s1, s2);
+      if (stats && !buni) w_commit_stats(p, lane, false, seg, co, s1[tc], s2[tc]);
       continue;
     }
     wf32x4 t0[4], t1[4];
@@ -457,12 +512,15 @@ __global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f
         if (stats) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            s1[k] += (double)val[k];
-            s2[k] += (double)val[k] * (double)val[k];
+            s1[tc][k] += (double)val[k];
+            s2[tc][k] += (double)val[k] * (double)val[k];
           }
         }
       }
-    if (stats) w_commit_stats(p, lane, true, seg, co, s1, s2);
+    if (stats && !buni) w_commit_stats(p, lane, true, seg, co, s1[tc], s2[tc]);
+  }
+  if constexpr (stats) {
+    if (buni) w_block_stats<TC>(p, lds, wave, tl, q, cb, bseg, s1, s2);
   }
 }
 
@@ -636,12 +694,21 @@ __global__ __launch_bounds__(256, 2) void conv_winot_f32_kernel(const WinoParams
   if (!tvalid && !stats) return;
   const bool has_res = p.res != nullptr;
   const int seg = (stats && tvalid) ? p.clip_seg[n] : 0;
+  bool buni = false;                                // see the spatial kernel
+  int bseg = 0;
+  if constexpr (stats) {
+    const int ta = tb * 64, tz = min(tb * 64 + 63, p.n_tiles - 1);
+    bseg = p.clip_seg[w_div(w_div(ta, p.m_tw, p.s_tw), p.m_th, p.s_th)];
+    buni = bseg == p.clip_seg[w_div(w_div(tz, p.m_tw, p.s_tw), p.m_th, p.s_th)];
+  }
+  double s1[TC][4], s2[TC][4];
 #pragma unroll
   for (int tc = 0; tc < TC; ++tc) {
     const int co = cb * CT + tc * 16 + 4 * q;
-    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s1[tc][k] = s2[tc][k] = 0.0;
     if (co >= p.Cout || !tvalid) {
-      if (stats) w_commit_stats(p, lane, false, seg, co, s1, s2);
+      if (stats && !buni) w_commit_stats(p, lane, false, seg, co, s1[tc], s2[tc]);
       continue;
     }
     const float4 b4 = *(const float4*)(p.bias + co);
@@ -671,12 +738,15 @@ __global__ __launch_bounds__(256, 2) void conv_winot_f32_kernel(const WinoParams
       if (stats) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          s1[k] += (double)val[k];
-          s2[k] += (double)val[k] * (double)val[k];
+          s1[tc][k] += (double)val[k];
+          s2[tc][k] += (double)val[k] * (double)val[k];
         }
       }
     }
-    if (stats) w_commit_stats(p, lane, true, seg, co, s1, s2);
+    if (stats && !buni) w_commit_stats(p, lane, true, seg, co, s1[tc], s2[tc]);
+  }
+  if constexpr (stats) {
+    if (buni) w_block_stats<TC>(p, lds, wave, tl, q, cb, bseg, s1, s2);
   }
 }
 

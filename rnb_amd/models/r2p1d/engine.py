@@ -294,11 +294,12 @@ class R2P1DEngine:
         bufs: Dict[str, torch.Tensor] = {"x": x}
         coffs = None
         defer = os.environ.get("RNB_BN_DEFER", "1") != "0"
-        # BN statistics from the Winograd epilogues (fp64 per-wave sums and
-        # atomics, finalized by one kernel): saves the 4.8 ms statistics pass
-        # per 128-clip forward but the epilogues cost 5.1 ms more (60.3 vs
-        # 61.3 ms; 13.4 ms either way at 24 clips), so opt-in
-        stats_fuse = os.environ.get("RNB_BN_EPILOGUE_STATS", "0") == "1"
+        # BN statistics from the Winograd epilogues (fp64 sums, block-level
+        # LDS reduction, one atomic per channel per block; finalized by one
+        # kernel) instead of a statistics pass over the output: 60.3 -> 58.5
+        # ms per 128-clip forward, 13.4 -> 13.2 ms at 24 clips
+        # (profiles/r2_bn_kernel_breakdown.txt); RNB_BN_EPILOGUE_STATS=0: pass
+        stats_fuse = os.environ.get("RNB_BN_EPILOGUE_STATS", "1") == "1"
         clip_seg = None              # video index of each clip (deferred BN)
         if self.bn_mode == "batch" and clip_offsets_dev is not None and hip:
             coffs = clip_offsets_dev

@@ -57,7 +57,7 @@ def main():
             cid = WINO_BASE + variant
             res.append("wino%s %.3f" % ("s" if variant == 8 else "", timeit(
                 lambda: layer.forward_hip(x, out=y, config=cid))))
-        cid = WINO_BASE + 5
+        cid = WINO_BASE + 8
         for name, seg, nseg in (("st/video", vseg, videos), ("st/clip", cseg, n)):
             sums = torch.zeros((nseg, 2, layer.geom.cout_p), dtype=torch.float64, device=DEV)
 

@@ -384,6 +384,34 @@ def test_graphed_batch_bn_per_video_matches_eager_and_module():
     assert any((b.running_mean - r).abs().max().item() > 0 for b, r in zip(bns, r0))
 
 
+@pytest.mark.parametrize("kind", ["spatial", "temporal"])
+def test_winograd_epilogue_stats_match_fp64_sums(kind):
+    """Per-video BN sums accumulated in the Winograd epilogues (block-level
+    LDS reduction for blocks inside one video, per-wave atomics for blocks
+    that straddle videos) equal fp64 sums of the conv output, for every
+    statistics-capable variant, with zero-clip videos in the offsets."""
+    from rnb_amd.ops.conv_f32 import WINO_TC, WINOT_TC, WINO_BASE
+    if kind == "spatial":
+        layer = _layer(64, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False)
+        shape, ids = (7, 4, 20, 28), [c for c in sorted(WINO_TC) if c - WINO_BASE >= 4]
+    else:
+        layer = _layer(64, 80, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=False)
+        shape, ids = (7, 8, 14, 14), sorted(WINOT_TC)
+    offs = [0, 2, 2, 3, 7]                    # video 1 has no clips
+    clip_seg = torch.tensor([0, 0, 2, 3, 3, 3, 3], dtype=torch.int32, device=DEV)
+    x = _input(shape[0], shape[1:], 64, 64)
+    for cid in ids:
+        sums = torch.zeros((4, 2, layer.geom.cout_p), dtype=torch.float64, device=DEV)
+        y = layer.forward_hip(x, config=cid, out_stats=(sums, clip_seg))
+        torch.cuda.synchronize()
+        yd = y[..., :layer.geom.cout].double().cpu()
+        for v in range(4):
+            seg = yd[offs[v]:offs[v + 1]].reshape(-1, layer.geom.cout)
+            got = sums[v, :, :layer.geom.cout].cpu()
+            assert torch.allclose(got[0], seg.sum(0), rtol=1e-9, atol=1e-6), (cid, v)
+            assert torch.allclose(got[1], (seg * seg).sum(0), rtol=1e-9, atol=1e-6), (cid, v)
+
+
 def test_deferred_batch_bn_into_temporal_winograd_matches_separate_apply(monkeypatch):
     """bn_mode='batch': the spatial conv's BatchNorm + ReLU applied on load by
     the temporal Winograd kernel (per-video scale/shift, padding frames kept
