@@ -157,14 +157,33 @@ class ConvLayerF32:
                          set(WINOT_TC) if self.winot_ok else set())
         self._wino_u: Dict[Tuple[int, int], torch.Tensor] = {}
 
-    def wino_u(self, tc: int, m: int = 2) -> torch.Tensor:
-        """Transformed weights with 16 tc output channels per work unit: m = 2
-        spatial F(2x2, 3x3), m = -4 temporal F(4, 3) (built once per (m, tc))."""
-        u = self._wino_u.get((m, tc))
+    def wino_u(self, tc: int, m: int = 2, co0: int = 0, nco: Optional[int] = None) -> torch.Tensor:
+        """Transformed weights of output channels [co0, co0 + nco) (default: all
+        cout_p) with 16 tc channels per work unit: m = 2 spatial F(2x2, 3x3),
+        m = -4 temporal F(4, 3) (built once per (m, tc, co0, nco))."""
+        nco = self.geom.cout_p - co0 if nco is None else nco
+        key = (m, tc, co0, nco)
+        u = self._wino_u.get(key)
         if u is None:
             fn = {2: winograd_weights, -4: winograd_t_weights}[m]
-            u = self._wino_u[(m, tc)] = fn(self.w_ref.cpu(), self.geom.cout_p, tc).to(self.device)
+            w = self.w_ref[co0:co0 + nco].cpu()
+            u = self._wino_u[key] = fn(w, nco, tc).to(self.device)
         return u
+
+    def wino_parts(self, cid: int):
+        """[(co0, nco, tc, variant)] launches of Winograd config ``cid``: the
+        split-transform spatial variants cover a cout_p that is not a multiple
+        of their 16 tc channels with a main launch plus a narrower tail launch
+        (conv2's 144 = 128 + 16 instead of 160 channels of MFMA work)."""
+        if cid in WINOT_TC:
+            return [(0, self.geom.cout_p, WINOT_TC[cid], cid - WINOT_BASE)]
+        tc, variant = WINO_TC[cid], cid - WINO_BASE
+        cp, ct = self.geom.cout_p, 16 * tc
+        main, rem = cp // ct * ct, cp % ct
+        if cid in WINO_SPLIT and main > 0 and rem > 0 and rem % 16 == 0:
+            # tail: split variant 7 (TC 1) or 8 (TC 2)
+            return [(0, main, tc, variant), (main, rem, rem // 16, 6 + rem // 16)]
+        return [(0, cp, tc, variant)]
 
     def candidates(self):
         from .native import kernels
@@ -174,10 +193,7 @@ class ConvLayerF32:
     def _launch_wino(self, x, y, residual, cid, stream, in_affine=None, out_stats=None):
         from .native import WinoParams, kernels
         ft = cid in WINOT_TC
-        if ft:
-            tc, variant, m = WINOT_TC[cid], cid - WINOT_BASE, -4
-        else:
-            tc, variant, m = WINO_TC[cid], cid - WINO_BASE, 2
+        m = -4 if ft else 2
         g = self.geom
         N, T, H, W, C = x.shape
         # the kernels index x / y / residual as dense NDHWC of the input's
@@ -190,20 +206,15 @@ class ConvLayerF32:
             raise ValueError("%s: Winograd operands do not match the conv geometry: x %s y %s "
                              "res %s" % (self.name, tuple(x.shape), tuple(y.shape),
                                          None if residual is None else tuple(residual.shape)))
-        u = self.wino_u(tc, m)
-        assert u.shape[0] * 16 == C and u.shape[1] * 16 * tc >= g.cout_p
         p = WinoParams()
-        p.x, p.bias = x.data_ptr(), self.bias.data_ptr()
-        p.u = u.data_ptr()
-        p.res = residual.data_ptr() if residual is not None else None
-        p.y = y.data_ptr()
+        p.x = x.data_ptr()
         if ft:
             p.F, p.H, p.W = N, T, H * W          # clips x frames x pixels per frame
         else:
             p.F, p.H, p.W = N * T, H, W
         p.Cin = C
         assert p.F * p.H * p.W * C == x.numel()
-        p.Cout, p.y_stride = g.cout_p, y.shape[-1]
+        p.y_stride = y.shape[-1]
         p.res_stride = residual.shape[-1] if residual is not None else 0
         p.relu = 1 if self.relu else 0
         if in_affine is not None:
@@ -218,6 +229,7 @@ class ConvLayerF32:
                                  % (self.name, tuple(ss.shape), tuple(clip_seg.shape),
                                     tuple(x.shape)))
             p.in_ss, p.clip_seg = ss.data_ptr(), clip_seg.data_ptr()
+        sums = None
         if out_stats is not None:
             sums, clip_seg = out_stats
             if (sums.dim() != 3 or sums.shape[1] != 2 or sums.shape[2] < g.cout_p
@@ -227,12 +239,20 @@ class ConvLayerF32:
                 raise ValueError("%s: output BN sums %s / clip_seg %s do not match y %s"
                                  % (self.name, tuple(sums.shape), tuple(clip_seg.shape),
                                     tuple(y.shape)))
-            p.out_stats, p.clip_seg = sums.data_ptr(), clip_seg.data_ptr()
+            p.clip_seg = clip_seg.data_ptr()
             p.clip_frames, p.stats_c = T, sums.shape[2]
-        if ft:
-            kernels().winot_f32(p, variant, stream.cuda_stream)
-        else:
-            kernels().wino_f32(p, variant, stream.cuda_stream)
+        launch = kernels().winot_f32 if ft else kernels().wino_f32
+        for co0, nco, tc, variant in self.wino_parts(cid):
+            u = self.wino_u(tc, m, co0, nco)
+            assert u.shape[0] * 16 == C and u.shape[1] * 16 * tc >= nco
+            p.u = u.data_ptr()
+            p.bias = self.bias.data_ptr() + 4 * co0
+            p.res = residual.data_ptr() + 4 * co0 if residual is not None else None
+            p.y = y.data_ptr() + 4 * co0
+            p.Cout = nco
+            if sums is not None:
+                p.out_stats = sums.data_ptr() + 8 * co0
+            launch(p, variant, stream.cuda_stream)
 
     # ------------------------------------------------------------------
     def out_shape(self, x_shape) -> Tuple[int, int, int, int, int]:

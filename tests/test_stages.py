@@ -320,6 +320,22 @@ def test_winograd_split_input_transform_matches_bt_d_b():
     assert torch.allclose(torch.stack(v).reshape(4, 4), BT @ d @ BT.t(), atol=1e-12)
 
 
+def test_winograd_channel_split_launches():
+    """Split-transform spatial configs cover cout_p = 144 with a 128-channel
+    TC 2 launch and a 16-channel TC 1 tail (no 160-channel padding); the
+    parts' transformed weights are the full transform's channel slices."""
+    from rnb_amd.ops.conv_f32 import (ConvLayerF32, WINO_BASE, f32_geom, winograd_weights)
+    w = torch.randn(144, 64, 1, 3, 3)
+    layer = ConvLayerF32(w, torch.zeros(144), f32_geom(64, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1)),
+                         False, torch.device("cpu"))
+    assert layer.wino_parts(WINO_BASE + 8) == [(0, 128, 2, 8), (128, 16, 1, 7)]
+    assert layer.wino_parts(WINO_BASE + 9) == [(0, 144, 3, 9)]          # 3 x 48: exact
+    assert layer.wino_parts(WINO_BASE + 5) == [(0, 144, 2, 5)]          # unsplit family
+    full = winograd_weights(w, 144, 1)                                   # [4, 9, 16, 16, 16]
+    tail = layer.wino_u(1, 2, 128, 16)
+    assert torch.equal(tail[:, 0], full[:, 8])
+
+
 def test_winograd_temporal_weight_layout_reproduces_the_conv():
     """Emulation of the temporal F(4, 3) kernel on its packed U layout
     [ci/16][nb][6][ct][16]: 6-frame patches at stride 4, zero padded."""
