@@ -37,7 +37,7 @@ import torch
 from ...ops.bn import BatchNormBatch
 from ...ops.conv import ConvGeom, ConvLayer, StemConv, fold_bn, pad_to, CH_ALIGN
 from ...ops.conv21 import FusedSTConv
-from ...ops.conv_f32 import F32_ALIGN, ConvLayerF32
+from ...ops.conv_f32 import F32_ALIGN, WINOT_MIN_T, ConvLayerF32
 from ...ops.video import (Head, IN_CHANNELS_P, ndhwc_to_ncdhw, ncdhw_to_ndhwc,
                           packed_input_shape)
 from .network import (LAYER_CHANNELS, LAYER_INPUT_CTHW, LAYER_OUTPUT_CTHW,
@@ -115,12 +115,13 @@ class R2P1DEngine:
         return "t%d" % self._n
 
     def _conv(self, conv: torch.nn.Conv3d, bn, relu: bool, name: str,
-              src: str, dst: str) -> ConvLayer:
+              src: str, dst: str, cin_pad: int = 0, cout_pad: int = 0) -> ConvLayer:
         w, b = fold_bn(conv.weight, conv.bias, bn)
         geom = ConvGeom(cin=conv.in_channels, cout=conv.out_channels,
                         kernel=tuple(conv.kernel_size), stride=tuple(conv.stride),
                         padding=tuple(conv.padding),
-                        align=F32_ALIGN if self.f32 else CH_ALIGN)
+                        align=F32_ALIGN if self.f32 else CH_ALIGN,
+                        cin_pad=cin_pad, cout_pad=cout_pad)
         T, H, W = self._thw[src]
         self._thw[dst] = geom.out_thw(T, H, W)
         nominal = geom
@@ -133,7 +134,7 @@ class R2P1DEngine:
             w = w[:, :, pt:pt + 1].contiguous()
             geom = ConvGeom(cin=geom.cin, cout=geom.cout, kernel=(1,) + geom.kernel[1:],
                             stride=geom.stride, padding=(0,) + geom.padding[1:],
-                            align=geom.align)
+                            align=geom.align, cin_pad=cin_pad, cout_pad=cout_pad)
         if self.f32:
             layer = ConvLayerF32(w, b, geom, relu, self.device, name)
         elif self.pack_stem and StemConv.eligible(geom):
@@ -146,9 +147,22 @@ class R2P1DEngine:
     def _stconv(self, st: SpatioTemporalConv, src: str, post_bn, relu: bool,
                 res: Optional[str], name: str) -> str:
         mid = self._name()
-        self._append(st.spatial_conv, st.bn, True, None, name + ".spatial", src, mid)
+        # fp32: a stride-1 3x1x1 temporal conv over >= 4 frames runs as the
+        # temporal Winograd kernel, which takes 16-channel chunks -- store the
+        # mid activation padded to 16 channels (the stem's 83 -> 96; the pad
+        # channels are exact zeros: zero weights and bias, BN gamma/beta 0)
+        tc = st.temporal_conv
+        T = self._thw[src][0]
+        pad = 0
+        if (self.f32 and tuple(tc.kernel_size) == (3, 1, 1) and tuple(tc.stride) == (1, 1, 1)
+                and tuple(tc.padding) == (1, 0, 0) and tc.in_channels % 16
+                and T >= WINOT_MIN_T and os.environ.get("RNB_PAD_MID16", "1") != "0"):
+            pad = (tc.in_channels + 15) // 16 * 16
+        self._append(st.spatial_conv, st.bn, True, None, name + ".spatial", src, mid,
+                     cout_pad=pad)
         dst = self._name()
-        self._append(st.temporal_conv, post_bn, relu, res, name + ".temporal", mid, dst)
+        self._append(st.temporal_conv, post_bn, relu, res, name + ".temporal", mid, dst,
+                     cin_pad=pad)
         sp, tp = self.ops[-2], self.ops[-1]
         if (not self.f32 and sp.bn is None and tp.bn is None
                 and FusedSTConv.eligible(sp.layer, tp.layer)):
@@ -156,16 +170,17 @@ class R2P1DEngine:
             sp.fuse = FusedSTConv(sp.layer, tp.layer)
         return dst
 
-    def _append(self, conv, bn, relu: bool, res: Optional[str], name: str, src: str, dst: str):
+    def _append(self, conv, bn, relu: bool, res: Optional[str], name: str, src: str, dst: str,
+                cin_pad: int = 0, cout_pad: int = 0):
         if self.bn_mode == "batch" and bn is not None:
             # reference numerics: conv (unfolded) -> BN with batch statistics
             # -> (+ residual) -> ReLU
-            layer = self._conv(conv, None, False, name, src, dst)
+            layer = self._conv(conv, None, False, name, src, dst, cin_pad, cout_pad)
             bnop = BatchNormBatch(bn, layer.geom.cout_p, self.device)
             self.ops.append(PlanOp("conv", layer, src, dst, res, bn=bnop, bn_relu=relu))
         else:
-            self.ops.append(PlanOp("conv", self._conv(conv, bn, relu, name, src, dst),
-                                   src, dst, res))
+            self.ops.append(PlanOp("conv", self._conv(conv, bn, relu, name, src, dst, cin_pad,
+                                                      cout_pad), src, dst, res))
 
     def _block(self, blk, src: str, name: str) -> str:
         if blk.downsample:
@@ -212,7 +227,6 @@ class R2P1DEngine:
         self._defer_ok = [
             i + 1 < len(self.ops) and op.bn is not None and op.bn_relu and op.res is None
             and self.f32 and uses.get(op.dst, 0) == 1 and self.ops[i + 1].src == op.dst
-            and self.ops[i + 1].bn is not None
             and getattr(self.ops[i + 1].layer, "winot_ok", False)
             for i, op in enumerate(self.ops)]
 
@@ -369,7 +383,11 @@ class R2P1DEngine:
                 y = (op.layer.forward_hip(src, res, prepacked=True) if hip
                      else op.layer.forward_torch(src, res, prepacked=True))
             elif hip:
-                y = op.layer.forward_hip(src, res)
+                if pending is not None:           # the producer's deferred BN + ReLU
+                    y = op.layer.forward_hip(src, res, in_affine=pending)
+                    pending = None
+                else:
+                    y = op.layer.forward_hip(src, res)
             else:
                 y = op.layer.forward_torch(src, res, out_dtype=self.dtype)
             bufs[op.dst] = y

@@ -76,14 +76,18 @@ class ConvGeom:
     stride: Tuple[int, int, int]
     padding: Tuple[int, int, int]
     align: int = CH_ALIGN      # channel padding (8 for bf16, 4 for fp32)
+    # wider padding of one activation (0 = align): e.g. the fp32 stem's 83
+    # mid channels stored as 96 so the temporal conv can run as Winograd
+    cin_pad: int = 0
+    cout_pad: int = 0
 
     @property
     def cin_p(self) -> int:
-        return pad_to(self.cin, self.align)
+        return max(pad_to(self.cin, self.align), self.cin_pad)
 
     @property
     def cout_p(self) -> int:
-        return pad_to(self.cout, self.align)
+        return max(pad_to(self.cout, self.align), self.cout_pad)
 
     @property
     def k_total(self) -> int:

@@ -145,14 +145,13 @@ class ConvLayerF32:
         self.b_ref = bias.detach().float().to(device)
         self._config: Dict[Tuple[int, int, int, int], int] = {}
         self._ktab: Dict[Tuple[int, int, int], torch.Tensor] = {}
-        # Winograd F(2x2,3x3) for stride-1 1x3x3 convs with Cin % 16 == 0
+        # Winograd F(2x2,3x3) for stride-1 1x3x3 convs with Cin_p % 16 == 0
+        # (padded input channels are zeros and get zero weights)
         self.wino_ok = (geom.kernel == (1, 3, 3) and geom.stride == (1, 1, 1)
-                        and geom.padding == (0, 1, 1) and geom.cin_p % 16 == 0
-                        and geom.cin == geom.cin_p)
-        # temporal F(4,3) for stride-1 3x1x1 convs with Cin % 16 == 0
+                        and geom.padding == (0, 1, 1) and geom.cin_p % 16 == 0)
+        # temporal F(4,3) for stride-1 3x1x1 convs with Cin_p % 16 == 0
         self.winot_ok = (geom.kernel == (3, 1, 1) and geom.stride == (1, 1, 1)
-                         and geom.padding == (1, 0, 0) and geom.cin_p % 16 == 0
-                         and geom.cin == geom.cin_p)
+                         and geom.padding == (1, 0, 0) and geom.cin_p % 16 == 0)
         self.wino_ids = (set(WINO_TC) if self.wino_ok else
                          set(WINOT_TC) if self.winot_ok else set())
         self._wino_u: Dict[Tuple[int, int], torch.Tensor] = {}
@@ -167,6 +166,9 @@ class ConvLayerF32:
         if u is None:
             fn = {2: winograd_weights, -4: winograd_t_weights}[m]
             w = self.w_ref[co0:co0 + nco].cpu()
+            if w.shape[1] < self.geom.cin_p:            # zero weights for pad channels
+                w = torch.cat([w, w.new_zeros((w.shape[0], self.geom.cin_p - w.shape[1])
+                                              + tuple(w.shape[2:]))], dim=1)
             u = self._wino_u[key] = fn(w, nco, tc).to(self.device)
         return u
 
