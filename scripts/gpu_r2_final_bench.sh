@@ -16,7 +16,7 @@ step() {
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-step fb_global_batch 600 python bench.py --steps 10 --warmup 2 --json-out gpurun_out/fb_global_batch.json
-step fb_global_eval 600 python bench.py --bn eval --steps 10 --warmup 2 --json-out gpurun_out/fb_global_eval.json
+step fb_global_batch 600 python bench.py --steps ${STEPS:-10} --warmup 2 --json-out gpurun_out/fb_global_batch.json
+step fb_global_eval 600 python bench.py --bn eval --steps ${STEPS:-10} --warmup 2 --json-out gpurun_out/fb_global_eval.json
 step fb_whole_batch 600 python bench.py --pipeline whole --steps 4 --warmup 1 --json-out gpurun_out/fb_whole_batch.json
 step fb_fused_eval 600 python bench.py --pipeline fused --steps 10 --warmup 2 --json-out gpurun_out/fb_fused_eval.json
