@@ -44,6 +44,7 @@ import argparse
 import json
 import os
 import sys
+import signal
 import time
 
 BASELINE_VIDEOS_PER_S = 11.30
@@ -106,7 +107,9 @@ def parse_args(argv=None):
                     help="at --gpus > 1, skip the short global (xGMI IPC) and two-stage "
                          "(RCCL) runs reported under cross_gpu")
     ap.add_argument("--cross-gpu-steps", type=int, default=4)
-    ap.add_argument("--cross-gpu-timeout", type=float, default=420.0)
+    ap.add_argument("--cross-gpu-timeout", type=float, default=240.0,
+                    help="total seconds for the cross-GPU extras (both topologies); the "
+                         "headline line is printed after them, so keep this bounded")
     ap.add_argument("--trace", type=str, default=None,
                     help="(fused) write a per-kernel time table of the timed steps")
     return ap.parse_args(argv)
@@ -289,8 +292,15 @@ def run_cross_gpu_extras(args) -> dict:
     root = os.path.dirname(os.path.abspath(__file__))
     out = {}
     topologies = ["global"] + (["two-stage"] if args.gpus % 2 == 0 else [])
+    deadline = time.time() + args.cross_gpu_timeout
     for topo in topologies:
+        budget = deadline - time.time()
+        if budget < 45:
+            out[topo] = {"skipped": "cross-GPU time budget spent (%.0f s left)" % budget}
+            continue
         path = os.path.join(root, "logs", "bench", "cross-%s-%dgpu.json" % (topo, args.gpus))
+        if os.path.exists(path):
+            os.remove(path)                     # never report a previous run's record
         cmd = [sys.executable, os.path.join(root, "bench.py"), "--pipeline", topo,
                "--gpus", str(args.gpus), "--steps", str(args.cross_gpu_steps),
                "--warmup", "1", "--dtype", args.dtype, "--bn", args.bn,
@@ -303,8 +313,18 @@ def run_cross_gpu_extras(args) -> dict:
         t0 = time.time()
         r = None
         try:
-            r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
-                               timeout=args.cross_gpu_timeout)
+            # own process group: on timeout the whole launcher tree (its loader
+            # and runner processes) is killed, not just the bench child
+            proc = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL,
+                                    stderr=subprocess.PIPE, start_new_session=True)
+            try:
+                _, err = proc.communicate(timeout=budget)
+            except subprocess.TimeoutExpired:
+                os.killpg(proc.pid, signal.SIGKILL)
+                _, err = proc.communicate()
+                r = subprocess.CompletedProcess(cmd, proc.returncode, None, err)
+                raise
+            r = subprocess.CompletedProcess(cmd, proc.returncode, None, err)
             with open(path) as f:
                 sub = json.loads(f.read())
             out[topo] = {"videos_per_s": sub.get("value"), "p50_ms": sub.get("p50_ms"),
