@@ -32,6 +32,7 @@
 // conv (rows pair-permuted, k = tap * 64 + c); the temporal matrix is the
 // temporal ConvLayer's rows (pair-permuted) repacked to k = dt * 160 + c.
 #include <hip/hip_runtime.h>
+#include "lds_attr.h"
 #include <stdint.h>
 
 #include <type_traits>
@@ -797,15 +798,7 @@ int rnb_conv21_launch(const Conv21Params* pp, hipStream_t stream) {
   p.x_bytes = (uint32_t)(M * 64 * 2);
   c21_magic((uint32_t)p.bands, &p.mB, &p.sB);
   c21_magic((uint32_t)p.W, &p.mW, &p.sW);
-  // the LDS limit is a per-device function attribute: set it once per device
-  static bool attr_set[64] = {false};
-  int adev = 0;
-  if (hipGetDevice(&adev) != hipSuccess || adev < 0 || adev >= 64) adev = 0;
-  if (!attr_set[adev]) {
-    (void)hipFuncSetAttribute((const void*)conv21_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    attr_set[adev] = true;
-  }
+  rnb_ensure_max_lds((const void*)conv21_kernel);
   int grid = c21_num_cus();
   if (grid > p.n_units) grid = p.n_units;
   hipLaunchKernelGGL(conv21_kernel, dim3((unsigned)grid), dim3(256), C21_LDS, stream, p);
@@ -827,15 +820,7 @@ int rnb_conv21s_launch(const Conv21Params* pp, hipStream_t stream) {
   p.x_bytes = (uint32_t)(M * 64 * 2);
   c21_magic((uint32_t)p.bands, &p.mB, &p.sB);
   c21_magic((uint32_t)p.W, &p.mW, &p.sW);
-  // the LDS limit is a per-device function attribute: set it once per device
-  static bool attr_set[64] = {false};
-  int adev = 0;
-  if (hipGetDevice(&adev) != hipSuccess || adev < 0 || adev >= 64) adev = 0;
-  if (!attr_set[adev]) {
-    (void)hipFuncSetAttribute((const void*)conv21s_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    attr_set[adev] = true;
-  }
+  rnb_ensure_max_lds((const void*)conv21s_kernel);
   int grid = c21_num_cus();
   if (grid > p.n_units) grid = p.n_units;
   hipLaunchKernelGGL(conv21s_kernel, dim3((unsigned)grid), dim3(512), C21S_LDS, stream, p);

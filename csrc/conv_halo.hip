@@ -22,6 +22,7 @@
 // LDS rows are 128 B (64 bf16 channels) with the chunk XOR swizzle
 // (chunk ^ (row & 7)) applied on the DMA source side.
 #include <hip/hip_runtime.h>
+#include "lds_attr.h"
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
@@ -307,13 +308,7 @@ int rnb_halo_launch_v(const HaloParams* pp, int v, hipStream_t stream) {
   if (p.y_stride < p.Cout_p || (p.res && p.res_stride < p.Cout_p)) return -9;
   if ((long long)p.M * p.y_stride * 2 > 0xFFFFFF00LL ||
       (long long)p.M * (p.res ? p.res_stride : 0) * 2 > 0xFFFFFF00LL) return -11;
-  static bool attr_set[3] = {false, false, false};
-  const int vi = (int)(hv - kHalo);
-  if (!attr_set[vi]) {
-    hipFuncSetAttribute((const void*)hv->kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    attr_set[vi] = true;
-  }
+  rnb_ensure_max_lds((const void*)hv->kernel);
   hipLaunchKernelGGL(hv->kernel, dim3((unsigned)(p.n_ptiles * p.n_ctiles)), dim3(64 * waves),
                      lds, stream, p);
   return (int)hipGetLastError();

@@ -34,6 +34,7 @@
 // B = activations, v_mfma_f32_16x16x32_bf16, bias folded into the initial
 // accumulator, + residual, ReLU, 16-byte paired stores).
 #include <hip/hip_runtime.h>
+#include "lds_attr.h"
 #include <stdint.h>
 
 #include "conv_epilogue.h"
@@ -293,12 +294,7 @@ int rnb_halo_ws_launch(const HaloParams* pp, hipStream_t stream) {
   const bool has8 = p.Cout_p > 128;
   void (*kern)(const HaloParams) =
       has8 ? conv_halo_ws_kernel<true> : conv_halo_ws_kernel<false>;
-  static bool attr_set[2] = {false, false};
-  if (!attr_set[has8]) {
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    attr_set[has8] = true;
-  }
+  rnb_ensure_max_lds((const void*)kern);
   int grid = ws_num_cus();
   if (grid > p.n_ptiles) grid = p.n_ptiles;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WS_WAVES * 64), lds, stream, p);

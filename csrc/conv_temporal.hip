@@ -28,6 +28,7 @@
 // with 4 consecutive output channels of one pixel -> bias + residual + ReLU
 // fused epilogue with one 8-byte store.
 #include <hip/hip_runtime.h>
+#include "lds_attr.h"
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
@@ -323,12 +324,7 @@ int rnb_temporal_launch(const TemporalParams* pp, int num_cus, int blocks_per_cu
   temporal_magic((uint32_t)p.gpc, &p.mG, &p.sG);
   const int lds = temporal_lds(v);
   if (lds > 160 * 1024) return -6;
-  static bool attr_set[16] = {false};
-  if (!attr_set[vi]) {
-    hipFuncSetAttribute((const void*)v.kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    attr_set[vi] = true;
-  }
+  rnb_ensure_max_lds((const void*)v.kernel);
   if (blocks_per_cu <= 0) {
     blocks_per_cu = (160 * 1024) / lds;
     if (blocks_per_cu > 8 / v.waves) blocks_per_cu = 8 / v.waves;
