@@ -242,6 +242,41 @@ def test_bn_per_video_stats_f32_kernel_matches_torch(res, relu, units):
     assert float(op._run_acc.abs().sum()) == 0.0
 
 
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (True, False), (False, False)])
+def test_bn_segment_apply_strides_and_untouched_rows(res, relu):
+    """The segment apply kernel vs a torch reference: padded y / z / residual
+    strides, segments that start after row 0 and end before M (rows outside
+    them must stay untouched), an empty segment, a partial tail."""
+    from rnb_amd.ops.native import kernels
+    k = kernels()
+    M, C = 3 * 1000 + 17, 88
+    ys, zs, rs = 96, 92, 100
+    y = torch.randn((M, ys), device=DEV)
+    resid = torch.randn((M, rs), device=DEV) if res else None
+    rpc = 7
+    coffs = [5, 60, 60, 201, 333, 420]                  # rows 35 .. 2940 of 3017
+    seg = torch.tensor(coffs, dtype=torch.int32, device=DEV)
+    nseg = len(coffs) - 1
+    ss = torch.randn((nseg, 2, C), device=DEV)
+    stream = torch.cuda.current_stream(DEV).cuda_stream
+    z = torch.full((M, zs), 7.0, device=DEV)
+    k.bn_seg_apply_f32(y.data_ptr(), z.data_ptr(), resid.data_ptr() if res else None,
+                       seg.data_ptr(), nseg, rpc, ss.data_ptr(), 1 if relu else 0, M, C, ys, zs,
+                       rs if res else 0, stream)
+    torch.cuda.synchronize()
+    ref = torch.full((M, zs), 7.0)
+    yc, sc = y.cpu(), ss.cpu()
+    for s in range(nseg):
+        a, b = coffs[s] * rpc, coffs[s + 1] * rpc
+        o = yc[a:b, :C] * sc[s, 0] + sc[s, 1]
+        if res:
+            o = o + resid.cpu()[a:b, :C]
+        if relu:
+            o = o.clamp_min(0)
+        ref[a:b, :C] = o
+    assert torch.allclose(z.cpu(), ref, atol=1e-5, rtol=1e-5)
+
+
 def test_r34_f32_batch_bn_two_videos_match_module_per_video():
     """bn_mode='batch' (the reference's training-mode BN) at fp32: a batch of
     two videos through the HIP engine equals the fp32 module run once per
