@@ -61,6 +61,21 @@ def _dtype(d):
     return _as_dtype(d if d is not None else DEFAULT_DTYPE)
 
 
+def default_bn_mode(bn_mode, dtype) -> str:
+    """BatchNorm numerics of the runner plugins when a config does not say.
+    The reference never calls ``.eval()`` (its runner only wraps the forward
+    in ``torch.no_grad()``, reference runner.py:45), so every BatchNorm
+    normalises with the statistics of the video being served: 'batch'
+    (per-video segments, graphed at fp32). bf16 batch BN runs eagerly, so
+    bf16 defaults to the folded 'eval' numerics. Configs choose either with
+    ``"bn_mode"`` (per step or in ``defaults``)."""
+    if bn_mode is None:
+        return "batch" if _dtype(dtype) == torch.float32 else "eval"
+    if bn_mode not in ("eval", "batch"):
+        raise ValueError("bn_mode must be 'eval' or 'batch', got %r" % (bn_mode,))
+    return bn_mode
+
+
 def clip_channels(dtype) -> int:
     """Channels of a decoded NDHWC clip pixel (RGB padded to 16 bytes)."""
     from ...ops.video import IN_CHANNELS_P, IN_CHANNELS_P_F32
@@ -122,7 +137,7 @@ class R2P1DRunner(RunnerModel):
 
     def __init__(self, device, start_index=1, end_index=5, num_classes=400,
                  layer_sizes=None, depth=None, block_type=None, backend="auto",
-                 bn_mode="eval", seed=0, ckpt_path=None, max_clips=DEFAULT_MAX_CLIPS,
+                 bn_mode=None, seed=0, ckpt_path=None, max_clips=DEFAULT_MAX_CLIPS,
                  warmup=3, use_graphs=True, autotune=True, dtype=None,
                  max_batch_videos=1, batch_wait_ms=0.0, bucket_step=None, **unused):
         super().__init__(device)
@@ -135,7 +150,7 @@ class R2P1DRunner(RunnerModel):
         self.start_index, self.end_index = start_index, end_index
         self.max_clips = int(max_clips)
         self.dtype = _dtype(dtype)
-        self.bn_mode = bn_mode
+        self.bn_mode = bn_mode = default_bn_mode(bn_mode, self.dtype)
         self.max_batch_videos = int(max_batch_videos)
         self.batch_wait_s = float(batch_wait_ms) / 1000.0
         buckets = None
@@ -302,7 +317,7 @@ class R2P1DSingleStep(RunnerModel):
     def __init__(self, device, num_classes=400, layer_sizes=None, depth=None,
                  block_type=None, num_clips_population=(1, 15), num_clips_weights=(10, 1),
                  decoder="synthetic", seed=None, model_seed=0, backend="auto",
-                 bn_mode="eval", ckpt_path=None, max_clips=DEFAULT_MAX_CLIPS, warmup=3,
+                 bn_mode=None, ckpt_path=None, max_clips=DEFAULT_MAX_CLIPS, warmup=3,
                  use_graphs=True, autotune=True, dtype=None, **unused):
         super().__init__(device)
         self.loader = R2P1DLoader(device, num_clips_population, num_clips_weights,

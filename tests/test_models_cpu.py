@@ -224,3 +224,18 @@ def test_loader_with_npy_decoder(tmp_path):
     assert torch.equal(got, ref)
     (frames,), _, tc = loader((None,), str(pb), TimeCard(1))
     assert frames.shape == (2, 8, 112, 112, 4) and tc.num_clips == 2
+
+
+def test_runner_default_bn_numerics_follow_the_reference():
+    """The reference never calls .eval(): runner plugins default to per-video
+    batch statistics at fp32 (the reference precision), folded BN at bf16
+    (batch BN is eager-only there); configs can choose either."""
+    from rnb_amd.models.r2p1d.model import default_bn_mode
+    assert default_bn_mode(None, "fp32") == "batch"
+    assert default_bn_mode(None, None) == "batch"
+    assert default_bn_mode(None, "bf16") == "eval"
+    assert default_bn_mode("eval", "fp32") == "eval"
+    with pytest.raises(ValueError):
+        default_bn_mode("train", "fp32")
+    r = R2P1DRunner(CPU, 5, 5, depth=10, warmup=0)
+    assert r.bn_mode == "batch"
