@@ -1,0 +1,94 @@
+"""Per-dispatch MFMA counters of one graphed R(2+1)D-34 fp32 forward.
+
+    rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES \\
+        --kernel-trace --output-format csv -d gpurun_out/pmcf -o run -- \\
+        python scripts/bn_breakdown.py run --mode batch --clips 128 --reps 1
+    python scripts/pmc_forward.py gpurun_out/pmcf
+
+For every dispatch after the spin-kernel marker (one graph replay): duration
+(kernel trace), fp32 MFMA instructions, MFMA busy per SIMD and the achieved
+MFMA rate. ``SQ_VALU_MFMA_BUSY_CYCLES`` is summed over the 1024 SIMDs and
+``GRBM_GUI_ACTIVE`` over the 8 XCDs, so busy = BUSY / (GRBM/8 * 1024). One
+``v_mfma_f32_16x16x4_f32`` is 2048 FLOP; the chip's dense fp32 MFMA peak is
+~157 TFLOP/s (256 CUs x 4 SIMDs x 64 FLOP/clk x 2.4 GHz). For the Winograd
+kernels the *effective* rate (direct-conv FLOPs / time) is higher than the
+MFMA rate: they do 2.25x (spatial) / ~1.8x (temporal) fewer multiplies.
+"""
+import collections
+import csv
+import glob
+import os
+import re
+import sys
+
+PEAK_TF = 157.3
+FLOP_PER_MFMA = 2048
+
+FAMILIES = (
+    ("wino spatial", r"conv_wino_f32_kernel"),
+    ("wino temporal", r"conv_winot_f32_kernel"),
+    ("conv direct", r"conv_f32_kernel"),
+    ("bn", r"bn_seg"),
+)
+
+
+def _find(root, name):
+    hits = glob.glob(os.path.join(root, "**", name), recursive=True)
+    if not hits:
+        raise SystemExit("no %s under %s" % (name, root))
+    return hits[-1]
+
+
+def main(root):
+    trace = {}
+    rows = []
+    with open(_find(root, "run_kernel_trace.csv")) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                         r["Kernel_Name"], r["Dispatch_Id"]))
+    rows.sort()
+    marks = [i for i, r in enumerate(rows) if "spin" in r[2]]
+    rows = rows[marks[-1] + 1:] if marks else rows
+    for s, e, name, did in rows:
+        trace[did] = (s, e, name)
+    ctr = collections.defaultdict(dict)
+    with open(_find(root, "run_counter_collection.csv")) as f:
+        for r in csv.DictReader(f):
+            did = r["Dispatch_Id"]
+            if did in trace:
+                ctr[did][r["Counter_Name"]] = ctr[did].get(r["Counter_Name"], 0.0) + \
+                    float(r["Counter_Value"])
+    fam = collections.defaultdict(lambda: [0, 0.0, 0.0, 0.0, 0.0])
+    print("%-4s %-44s %9s %10s %8s %8s" % ("#", "kernel", "us", "MFMA(M)", "busy%", "TF/s"))
+    for i, (s, e, name, did) in enumerate(rows):
+        c = ctr.get(did, {})
+        us = (e - s) / 1e3
+        mf = c.get("SQ_INSTS_MFMA", 0.0)
+        clk = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0 * 1024
+        busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / clk if clk else 0.0
+        tf = mf * FLOP_PER_MFMA / (us * 1e-6) / 1e12 if us > 0 else 0.0
+        short = re.sub(r"\(.*\)$", "", name)[:44]
+        print("%-4d %-44s %9.1f %10.2f %7.1f%% %8.1f" % (i, short, us, mf / 1e6, 100 * busy, tf))
+        key = next((k for k, p in FAMILIES if re.search(p, name)), "other")
+        a = fam[key]
+        a[0] += 1
+        a[1] += us
+        a[2] += mf
+        a[3] += c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        a[4] += clk
+    tot_us = sum(a[1] for a in fam.values())
+    print("\n%-16s %5s %10s %6s %10s %8s %8s" % ("family", "n", "ms", "share", "MFMA busy",
+                                                  "TF/s", "% peak"))
+    for k, (n, us, mf, b, clk) in sorted(fam.items(), key=lambda kv: -kv[1][1]):
+        tf = mf * FLOP_PER_MFMA / (us * 1e-6) / 1e12 if us else 0.0
+        print("%-16s %5d %10.3f %5.1f%% %9.1f%% %8.1f %7.1f%%"
+              % (k, n, us / 1e3, 100 * us / tot_us, 100 * b / clk if clk else 0.0, tf,
+                 100 * tf / PEAK_TF))
+    mf_all = sum(a[2] for a in fam.values())
+    print("\nwhole forward: %.3f ms, %.1f TF/s fp32 MFMA (%.1f%% of %.0f)"
+          % (tot_us / 1e3, mf_all * FLOP_PER_MFMA / (tot_us * 1e-6) / 1e12,
+             100 * mf_all * FLOP_PER_MFMA / (tot_us * 1e-6) / 1e12 / PEAK_TF, PEAK_TF))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmcf")
