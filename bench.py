@@ -79,8 +79,11 @@ def parse_args(argv=None):
     ap.add_argument("--depth", type=int, default=34)
     ap.add_argument("--videos-per-step", type=int, default=256,
                     help="videos arriving per GPU per step")
-    ap.add_argument("--replicas", type=int, default=2,
-                    help="R(2+1)D runner processes per GPU (the R of RnB)")
+    ap.add_argument("--replicas", type=int, default=None,
+                    help="R(2+1)D runner processes per GPU (the R of RnB); default 2, and 4 "
+                         "for --pipeline whole: one-video model calls are launch-latency "
+                         "bound, so more concurrent graphs fill the GPU (2/3/4/5/6 replicas: "
+                         "386/483/572/463/511 videos/s, profiles/r2_whole_replicas_sweep.txt)")
     ap.add_argument("--loaders", type=int, default=2, help="loader processes per GPU")
     ap.add_argument("--video-batch", type=int, default=64,
                     help="max videos per model invocation (consumer-side batching)")
@@ -112,7 +115,10 @@ def parse_args(argv=None):
                          "headline line is printed after them, so keep this bounded")
     ap.add_argument("--trace", type=str, default=None,
                     help="(fused) write a per-kernel time table of the timed steps")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.replicas is None:
+        args.replicas = 4 if args.pipeline == "whole" else 2
+    return args
 
 
 def pipeline_config(args, n_gpus: int) -> dict:
