@@ -81,6 +81,16 @@ class PipelineSpec:
         return sorted({g for s in self.steps for grp in s.groups
                        for g in grp.gpus if g >= 0})
 
+    def processes_per_gpu(self) -> Dict[int, int]:
+        """Runner processes placed on each GPU (CPU replicas excluded)."""
+        out: Dict[int, int] = {}
+        for s in self.steps:
+            for grp in s.groups:
+                for g in grp.gpus:
+                    if g >= 0:
+                        out[g] = out.get(g, 0) + 1
+        return out
+
     def max_gpu(self) -> int:
         used = self.gpus_used()
         return max(used) if used else -1

@@ -23,6 +23,7 @@ import sys
 import threading
 import time
 from datetime import datetime
+from typing import Dict
 
 from .utils.arg_utils import nonnegative_int, positive_int
 
@@ -79,6 +80,26 @@ def _parse_overrides(items):
         except json.JSONDecodeError:
             out[k] = v
     return out
+
+
+# Runner processes one device serves well. Measured on one MI355X: 4 (2
+# loaders + 2 runners) run the headline at ~940 videos/s, 8 run but lose
+# throughput to contention, 9 collapsed to 47-121 videos/s with 0.5-s stalls
+# per model call (profiles/NOTES.md, "Pipeline"): the device's hardware
+# scheduler then time-slices whole processes. One process per stage replica is
+# the RnB design, so this is a warning, not an error.
+CROWDED_GPU_PROCESSES = 8
+
+
+def warn_crowded_gpus(spec, limit: int = CROWDED_GPU_PROCESSES) -> Dict[int, int]:
+    """Print a warning for every GPU with more than ``limit`` processes;
+    returns those GPUs and their process counts."""
+    crowded = {g: n for g, n in sorted(spec.processes_per_gpu().items()) if n > limit}
+    for g, n in crowded.items():
+        print("[launcher] warning: %d GPU processes on gpu %d (> %d): one device time-slices "
+              "that many processes and throughput can collapse; fewer replicas or more GPUs "
+              "serve better" % (n, g, limit), flush=True)
+    return crowded
 
 
 def _apply_batch_default(spec, batch_size: int) -> None:
@@ -184,6 +205,7 @@ def run(args) -> dict:
         print("[launcher] RNB_FOLD_GPUS=%d: logical GPUs folded onto %d device(s)"
               % (fold, fold), flush=True)
     check_gpus(spec)
+    warn_crowded_gpus(spec)
     _apply_batch_default(spec, args.batch_size)
     # slot rings sized from the consumers' batching and free HBM (amdsmi: no
     # HIP context in this process)

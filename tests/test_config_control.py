@@ -210,3 +210,21 @@ def test_runner_slot_shape_follows_layer_range():
     spec = parse_pipeline(cfg)
     shapes, dtypes = step_output_spec(spec.steps[1], spec.steps[1].groups[0])
     assert shapes == ((15, 8, 56, 56, 64),) and dtypes == (torch.bfloat16,)
+
+
+def test_crowded_gpu_warning(capsys):
+    """The launcher warns when one GPU would host more runner processes than
+    one device serves well (measured: 9 on one MI355X collapse)."""
+    from rnb_amd.config import parse_pipeline
+    from rnb_amd.launcher import warn_crowded_gpus
+    it = "rnb_amd.models.r2p1d.model.R2P1DVideoPathIterator"
+    loader = "rnb_amd.models.r2p1d.model.R2P1DLoader"
+    runner = "rnb_amd.models.r2p1d.model.R2P1DRunner"
+    cfg = {"video_path_iterator": it, "pipeline": [
+        {"model": loader, "queue_groups": [{"gpus": [0, 0, 0, 1], "out_queues": [0]}]},
+        {"model": runner, "queue_groups": [{"gpus": [0] * 6 + [1, -1], "in_queue": 0}]}]}
+    spec = parse_pipeline(cfg)
+    assert spec.processes_per_gpu() == {0: 9, 1: 2}
+    assert warn_crowded_gpus(spec) == {0: 9}
+    assert "9 GPU processes on gpu 0" in capsys.readouterr().out
+    assert warn_crowded_gpus(spec, limit=9) == {}
