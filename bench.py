@@ -80,10 +80,13 @@ def parse_args(argv=None):
     ap.add_argument("--videos-per-step", type=int, default=256,
                     help="videos arriving per GPU per step")
     ap.add_argument("--replicas", type=int, default=None,
-                    help="R(2+1)D runner processes per GPU (the R of RnB); default 2, and 4 "
-                         "for --pipeline whole: one-video model calls are launch-latency "
-                         "bound, so more concurrent graphs fill the GPU (2/3/4/5/6 replicas: "
-                         "386/483/572/463/511 videos/s, profiles/r2_whole_replicas_sweep.txt)")
+                    help="R(2+1)D runner processes per GPU (the R of RnB); default 3 (a third "
+                         "concurrent graph fills the small-kernel phases of the others: "
+                         "967 vs 936 videos/s mean over interleaved runs, "
+                         "profiles/r2_headline_process_sweep.txt), and 4 for --pipeline "
+                         "whole: one-video model calls are launch-latency bound (2/3/4/5/6 "
+                         "replicas: 386/483/572/463/511 videos/s, "
+                         "profiles/r2_whole_replicas_sweep.txt)")
     ap.add_argument("--loaders", type=int, default=2, help="loader processes per GPU")
     ap.add_argument("--video-batch", type=int, default=64,
                     help="max videos per model invocation (consumer-side batching)")
@@ -117,7 +120,7 @@ def parse_args(argv=None):
                     help="(fused) write a per-kernel time table of the timed steps")
     args = ap.parse_args(argv)
     if args.replicas is None:
-        args.replicas = 4 if args.pipeline == "whole" else 2
+        args.replicas = 4 if args.pipeline == "whole" else 3
     return args
 
 
