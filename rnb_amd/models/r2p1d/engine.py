@@ -554,9 +554,17 @@ class GraphedEngine:
         return self.graphs[b]
 
     def prepare(self, sizes: Optional[Sequence[int]] = None):
-        for b in (self.buckets if sizes is None else sorted({self.bucket_for(s) for s in sizes})):
+        """Capture the bucket graphs, largest first: the buckets share one
+        graph memory pool (replays are serialised on the runner's stream), and
+        blocks freed by a larger capture serve every smaller one, where an
+        ascending order grows the pool at each step. Then the eager warm-up's
+        cached blocks go back to the device."""
+        todo = self.buckets if sizes is None else sorted({self.bucket_for(s) for s in sizes})
+        for b in sorted(todo, reverse=True):
             if b not in self.graphs:
                 self._capture(b)
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
 
     def input_buffer(self, n: int) -> Tuple[torch.Tensor, int]:
         """Static input of the bucket for n clips (write rows [:n] in place)."""

@@ -162,6 +162,13 @@ class R2P1DRunner(RunnerModel):
                                    self.max_clips, use_graphs, autotune, self.dtype, buckets)
         if isinstance(self.engine, GraphedEngine):
             self.engine.prepare()
+            if device.type == "cuda" and os.environ.get("RNB_REPORT_MEMORY") == "1":
+                print("[runner gpu %d] %d graph buckets, capture %.1f s, %.1f GB allocated, "
+                      "%.1f GB reserved" % (device.index or 0, len(self.engine.graphs),
+                                            self.engine.capture_s,
+                                            torch.cuda.memory_allocated(device) / 2 ** 30,
+                                            torch.cuda.memory_reserved(device) / 2 ** 30),
+                      flush=True)
         n = min(10, self.max_clips)
         tmp = torch.randn(boundary_shape(start_index, n, self.dtype)).to(self.dtype).to(device)
         for _ in range(warmup):
