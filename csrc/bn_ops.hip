@@ -334,6 +334,94 @@ __global__ __launch_bounds__(64) void bn_seg_sums_walk_f32_kernel(BnSegParams p,
   }
 }
 
+// Statistics-pass finalize + running update in ONE dispatch, for graph
+// buckets of <= 32 clips (a bucket's segment list is padded with empty videos
+// to one per clip; at 128 the split kernels are faster: one block per 64
+// channels then walks too many segments). A block owns 64 channels; its 16
+// waves take segments s = wave, wave + 16 (a wave reads 64 consecutive
+// channels; empty segments skip the partials). Per (segment, channel): moments and scale / shift as
+// bn_seg_finalize_f32_kernel; the running update's closed-form terms
+// m (1-m)^(valid segments after s) x_s (weights computed once per segment in
+// LDS) are reduced across the waves in LDS in a fixed order, and wave 0
+// writes r = (1-m)^K r + sum: no fp64 atomics, no re-arm, one dispatch
+// instead of two.
+#define BN_FR_CH 64
+#define BN_FR_SL 16
+#define BN_FR_MAX_SEG 32
+__global__ __launch_bounds__(1024) void bn_seg_finalize_running_f32_kernel(BnSegParams p) {
+  __shared__ int srow[BN_FR_MAX_SEG + 1];          // segment start rows
+  __shared__ double wts[BN_FR_MAX_SEG];            // running-update weight per segment
+  __shared__ double decay;
+  __shared__ double red[2][BN_FR_SL][BN_FR_CH];
+  const int C = p.C, nseg = p.nseg;
+  const int cl = threadIdx.x & (BN_FR_CH - 1), w = threadIdx.x / BN_FR_CH;
+  const int c = blockIdx.x * BN_FR_CH + cl;
+  if (threadIdx.x <= nseg) srow[threadIdx.x] = p.coffs[threadIdx.x] * p.rpc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double keep = 1.0 - (double)p.momentum;
+    double dk = 1.0;                               // (1-m)^(valid segments after s)
+    for (int s = nseg - 1; s >= 0; --s) {
+      const bool valid = srow[s + 1] - srow[s] >= 2;
+      wts[s] = valid ? (double)p.momentum * dk : 0.0;
+      if (valid) dk *= keep;
+    }
+    decay = dk;                                    // (1-m)^(valid segments)
+  }
+  __syncthreads();
+  const bool upd = p.running_mean != nullptr && c < p.channels;
+  double t1 = 0.0, t2 = 0.0;
+  for (int s = w; c < C && s < nseg; s += BN_FR_SL) {
+    const int r0s = srow[s], rows = srow[s + 1] - r0s;
+    const float* base = p.partial + (size_t)s * p.bps * 2 * C;
+    float s1 = 0.f, s2 = 0.f;
+    int k = rows > 0 ? 0 : p.bps;                  // empty (padding) video: no partials
+    for (; k + 4 <= p.bps; k += 4) {               // fixed order (deterministic)
+      float u1[4], u2[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        u1[u] = base[(size_t)(k + u) * 2 * C + c];
+        u2[u] = base[(size_t)(k + u) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { s1 += u1[u]; s2 += u2[u]; }
+    }
+    for (; k < p.bps; ++k) {
+      s1 += base[(size_t)k * 2 * C + c];
+      s2 += base[(size_t)k * 2 * C + C + c];
+    }
+    float mu = 0.f, va = 0.f;
+    if (rows > 0) {
+      const float kf = p.y[(size_t)r0s * p.stride + c];
+      const float m1 = s1 / (float)rows;
+      mu = kf + m1;
+      va = fmaxf(s2 / (float)rows - m1 * m1, 0.f);
+    }
+    p.mean[(size_t)s * C + c] = mu;
+    p.var[(size_t)s * C + c] = va;
+    const float sc = p.gamma[c] * rsqrtf(va + p.eps);
+    p.ss[(size_t)s * 2 * C + c] = sc;
+    p.ss[(size_t)s * 2 * C + C + c] = p.beta[c] - mu * sc;
+    if (upd && rows >= 2) {
+      t1 += wts[s] * (double)mu;
+      t2 += wts[s] * (double)va * ((double)rows / (double)(rows - 1));
+    }
+  }
+  red[0][w][cl] = t1;
+  red[1][w][cl] = t2;
+  __syncthreads();
+  if (w == 0 && upd) {
+    double a1 = 0.0, a2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < BN_FR_SL; ++i) {
+      a1 += red[0][i][cl];
+      a2 += red[1][i][cl];
+    }
+    p.running_mean[c] = (float)(decay * (double)p.running_mean[c] + a1);
+    p.running_var[c] = (float)(decay * (double)p.running_var[c] + a2);
+  }
+}
+
 // r = (1-m)^K r + acc over the K segments with >= 2 rows; re-arms acc
 __global__ __launch_bounds__(256) void bn_seg_running_f32_kernel(BnSegParams p) {
   const int c = blockIdx.x * 256 + threadIdx.x;
@@ -405,6 +493,8 @@ extern "C" {
 // one-video forwards). A split sized to fill the chip from (nseg, C, M)
 // measured the same (13.4 ms per 24-clip forward, 60.2 ms per 128).
 static int g_bn_fixed_bps = 0;     // > 0: override (experiments)
+static int g_bn_fused_finalize = 1;  // 0: separate finalize + running kernels (A/B)
+void rnb_bn_seg_set_fused_finalize(int on) { g_bn_fused_finalize = on; }
 void rnb_bn_seg_set_bps(int bps) { g_bn_fixed_bps = bps > BN_SEG_MAX_BPS ? BN_SEG_MAX_BPS : bps; }
 
 int rnb_bn_seg_bps(int nseg, int C, long long M) {
@@ -439,6 +529,11 @@ int rnb_bn_seg_stats_f32(const float* y, const int* coffs, int nseg, int rpc, lo
   p.channels = channels; p.running_mean = running_mean; p.running_var = running_var;
   p.mean = mean; p.var = var; p.ss = ss;
   hipLaunchKernelGGL(bn_seg_sums_f32_kernel, dim3(p.bps, nseg), dim3(256), 0, stream, p);
+  if (g_bn_fused_finalize && nseg <= BN_FR_MAX_SEG) {
+    hipLaunchKernelGGL(bn_seg_finalize_running_f32_kernel, dim3((C + BN_FR_CH - 1) / BN_FR_CH),
+                       dim3(BN_FR_CH * BN_FR_SL), 0, stream, p);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(bn_seg_finalize_f32_kernel, dim3((C + 255) / 256, nseg), dim3(256), 0,
                      stream, p);
   if (running_mean != nullptr)

@@ -233,6 +233,10 @@ class Kernels:
         if os.environ.get("RNB_BN_BPS"):
             # fixed BN statistics blocks per segment (batch-invariant split)
             lib.rnb_bn_seg_set_bps(int(os.environ["RNB_BN_BPS"]))
+        lib.rnb_bn_seg_set_fused_finalize.argtypes = [ctypes.c_int]
+        if os.environ.get("RNB_BN_FUSED_FINALIZE"):
+            # 0: separate finalize + running-update kernels (A/B)
+            lib.rnb_bn_seg_set_fused_finalize(int(os.environ["RNB_BN_FUSED_FINALIZE"]))
         lib.rnb_bn_seg_scratch_floats.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_longlong]
         lib.rnb_bn_seg_scratch_floats.restype = ctypes.c_longlong
         lib.rnb_bn_seg_stats_f32.argtypes = [

@@ -478,3 +478,69 @@ def test_deferred_batch_bn_into_temporal_winograd_matches_separate_apply(monkeyp
     assert (a - b).abs().max().item() <= 2e-5 * scale
     assert (b - c).abs().max().item() <= 2e-5 * scale
     assert (a - ref).abs().max().item() <= 1e-3 * scale
+
+
+@pytest.mark.parametrize("source,nseg", [("pass", 14), ("pass", 28), ("pass", 41),
+                                         ("sums", 14), ("sums", 41)])
+def test_bn_fused_finalize_running_matches_split_kernels_and_torch(source, nseg):
+    """BN statistics per video, every finalize path against the others and an
+    fp64 torch reference: statistics pass with <= 32 segments (the fused
+    finalize + running-update kernel, 16 segment waves, vs the separate
+    kernels), > 32 segments (separate kernels), epilogue sums (in-order walk <= 16, separate kernels
+    above). Per-segment mean / var / scale / shift, the running statistics
+    (segments with < 2 rows skipped), 88 channels (a partial 64-channel
+    block), empty and one-row segments; epilogue sums re-armed to zero."""
+    from rnb_amd.ops.bn import BatchNormBatch
+    from rnb_amd.ops.native import kernels
+    k = kernels()
+    C = 88
+    bn = torch.nn.BatchNorm3d(C)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-1, 1)
+        bn.running_var.uniform_(0.5, 2)
+    g = torch.Generator().manual_seed(5)
+    rows = [int(r) for r in torch.randint(0, 40, (nseg,), generator=g)]
+    rows[3], rows[7], rows[nseg - 1] = 0, 1, 0
+    offs = [0]
+    for r in rows:
+        offs.append(offs[-1] + r)
+    M = offs[-1]
+    y = (torch.randn((M, C), generator=g) * 2 + 0.5).to(DEV)
+    seg = torch.tensor(offs, dtype=torch.int32, device=DEV)
+    outs = []
+    for fused in (1, 0):
+        op = BatchNormBatch(bn, C, DEV)
+        sums = None
+        if source == "sums":
+            yd = y.double()
+            sums = torch.zeros((len(rows), 2, C), dtype=torch.float64, device=DEV)
+            for s in range(len(rows)):
+                a, b = offs[s], offs[s + 1]
+                sums[s, 0] = yd[a:b].sum(0)
+                sums[s, 1] = (yd[a:b] * yd[a:b]).sum(0)
+        k.lib.rnb_bn_seg_set_fused_finalize(fused)
+        try:
+            mean, var, ss = op._stats_ss(y.view(M, 1, 1, 1, C), seg, sums, 1)
+        finally:
+            k.lib.rnb_bn_seg_set_fused_finalize(1)
+        torch.cuda.synchronize()
+        if sums is not None:
+            assert float(sums.abs().sum()) == 0.0, "epilogue sums must be re-armed"
+        outs.append([t.cpu() for t in (mean, var, ss, op.running_mean, op.running_var)])
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.allclose(a, b, rtol=1e-6, atol=1e-6)
+    yc = y.double().cpu()
+    rm, rv = bn.running_mean.double().clone(), bn.running_var.double().clone()
+    for s, r in enumerate(rows):
+        part = yc[offs[s]:offs[s + 1]]
+        if r > 0:
+            mu, va = part.mean(0), part.var(0, unbiased=False)
+            assert torch.allclose(outs[0][0][s].double(), mu, atol=1e-5)
+            assert torch.allclose(outs[0][1][s].double(), va, rtol=1e-4, atol=1e-5)
+        if r >= 2:
+            rm = (1 - bn.momentum) * rm + bn.momentum * part.mean(0)
+            rv = (1 - bn.momentum) * rv + bn.momentum * part.var(0, unbiased=True)
+    assert torch.allclose(outs[0][3].double(), rm, atol=1e-5)
+    assert torch.allclose(outs[0][4].double(), rv, rtol=1e-4, atol=1e-5)
