@@ -339,8 +339,9 @@ __global__ __launch_bounds__(64) void bn_seg_sums_walk_f32_kernel(BnSegParams p,
 // to one per clip; at 128 the split kernels are faster: one block per 64
 // channels then walks too many segments). A block owns 64 channels; its 16
 // waves take segments s = wave, wave + 16 (a wave reads 64 consecutive
-// channels; empty segments skip the partials). Per (segment, channel): moments and scale / shift as
-// bn_seg_finalize_f32_kernel; the running update's closed-form terms
+// channels; empty segments skip the partials). Per (segment, channel):
+// moments and scale / shift as bn_seg_finalize_f32_kernel; the running
+// update's closed-form terms
 // m (1-m)^(valid segments after s) x_s (weights computed once per segment in
 // LDS) are reduced across the waves in LDS in a fixed order, and wave 0
 // writes r = (1-m)^K r + sum: no fp64 atomics, no re-arm, one dispatch
