@@ -334,8 +334,9 @@ __global__ __launch_bounds__(64) void bn_seg_sums_walk_f32_kernel(BnSegParams p,
   }
 }
 
-// Statistics-pass finalize + running update in ONE dispatch, for graph
-// buckets of <= 32 clips (a bucket's segment list is padded with empty videos
+// Finalize + running update in ONE dispatch (statistics pass, or epilogue
+// sums above the in-order walk's 16 segments), for graph buckets of <= 32
+// clips (a bucket's segment list is padded with empty videos
 // to one per clip; at 128 the split kernels are faster: one block per 64
 // channels then walks too many segments). A block owns 64 channels; its 16
 // waves take segments s = wave, wave + 16 (a wave reads 64 consecutive
@@ -349,7 +350,12 @@ __global__ __launch_bounds__(64) void bn_seg_sums_walk_f32_kernel(BnSegParams p,
 #define BN_FR_CH 64
 #define BN_FR_SL 16
 #define BN_FR_MAX_SEG 32
-__global__ __launch_bounds__(1024) void bn_seg_finalize_running_f32_kernel(BnSegParams p) {
+// FROM_SUMS: moments from a producer epilogue's fp64 sums [nseg][2][sums_c]
+// (re-armed to zero here), as bn_seg_finalize_sums_f32_kernel.
+template <bool FROM_SUMS>
+__global__ __launch_bounds__(1024) void bn_seg_finalize_running_f32_kernel(BnSegParams p,
+                                                                           double* sums,
+                                                                           int sums_c) {
   __shared__ int srow[BN_FR_MAX_SEG + 1];          // segment start rows
   __shared__ double wts[BN_FR_MAX_SEG];            // running-update weight per segment
   __shared__ double decay;
@@ -374,29 +380,41 @@ __global__ __launch_bounds__(1024) void bn_seg_finalize_running_f32_kernel(BnSeg
   double t1 = 0.0, t2 = 0.0;
   for (int s = w; c < C && s < nseg; s += BN_FR_SL) {
     const int r0s = srow[s], rows = srow[s + 1] - r0s;
-    const float* base = p.partial + (size_t)s * p.bps * 2 * C;
-    float s1 = 0.f, s2 = 0.f;
-    int k = rows > 0 ? 0 : p.bps;                  // empty (padding) video: no partials
-    for (; k + 4 <= p.bps; k += 4) {               // fixed order (deterministic)
-      float u1[4], u2[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        u1[u] = base[(size_t)(k + u) * 2 * C + c];
-        u2[u] = base[(size_t)(k + u) * 2 * C + C + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) { s1 += u1[u]; s2 += u2[u]; }
-    }
-    for (; k < p.bps; ++k) {
-      s1 += base[(size_t)k * 2 * C + c];
-      s2 += base[(size_t)k * 2 * C + C + c];
-    }
     float mu = 0.f, va = 0.f;
-    if (rows > 0) {
-      const float kf = p.y[(size_t)r0s * p.stride + c];
-      const float m1 = s1 / (float)rows;
-      mu = kf + m1;
-      va = fmaxf(s2 / (float)rows - m1 * m1, 0.f);
+    if constexpr (FROM_SUMS) {
+      double* sp = sums + (size_t)s * 2 * sums_c;
+      const double d1 = sp[c], d2 = sp[sums_c + c];
+      sp[c] = 0.0;                                 // re-armed for the producer
+      sp[sums_c + c] = 0.0;
+      if (rows > 0) {
+        const double m = d1 / (double)rows;
+        mu = (float)m;
+        va = (float)fmax(d2 / (double)rows - m * m, 0.0);
+      }
+    } else {
+      const float* base = p.partial + (size_t)s * p.bps * 2 * C;
+      float s1 = 0.f, s2 = 0.f;
+      int k = rows > 0 ? 0 : p.bps;                // empty (padding) video: no partials
+      for (; k + 4 <= p.bps; k += 4) {             // fixed order (deterministic)
+        float u1[4], u2[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          u1[u] = base[(size_t)(k + u) * 2 * C + c];
+          u2[u] = base[(size_t)(k + u) * 2 * C + C + c];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { s1 += u1[u]; s2 += u2[u]; }
+      }
+      for (; k < p.bps; ++k) {
+        s1 += base[(size_t)k * 2 * C + c];
+        s2 += base[(size_t)k * 2 * C + C + c];
+      }
+      if (rows > 0) {
+        const float kf = p.y[(size_t)r0s * p.stride + c];
+        const float m1 = s1 / (float)rows;
+        mu = kf + m1;
+        va = fmaxf(s2 / (float)rows - m1 * m1, 0.f);
+      }
     }
     p.mean[(size_t)s * C + c] = mu;
     p.var[(size_t)s * C + c] = va;
@@ -531,8 +549,9 @@ int rnb_bn_seg_stats_f32(const float* y, const int* coffs, int nseg, int rpc, lo
   p.mean = mean; p.var = var; p.ss = ss;
   hipLaunchKernelGGL(bn_seg_sums_f32_kernel, dim3(p.bps, nseg), dim3(256), 0, stream, p);
   if (g_bn_fused_finalize && nseg <= BN_FR_MAX_SEG) {
-    hipLaunchKernelGGL(bn_seg_finalize_running_f32_kernel, dim3((C + BN_FR_CH - 1) / BN_FR_CH),
-                       dim3(BN_FR_CH * BN_FR_SL), 0, stream, p);
+    hipLaunchKernelGGL(bn_seg_finalize_running_f32_kernel<false>,
+                       dim3((C + BN_FR_CH - 1) / BN_FR_CH), dim3(BN_FR_CH * BN_FR_SL), 0, stream,
+                       p, (double*)nullptr, 0);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(bn_seg_finalize_f32_kernel, dim3((C + 255) / 256, nseg), dim3(256), 0,
@@ -557,6 +576,12 @@ int rnb_bn_seg_stats_from_sums_f32(double* sums, int sums_c, const int* coffs, i
   p.run_acc = run_acc; p.gamma = gamma; p.beta = beta; p.eps = eps; p.momentum = momentum;
   p.channels = channels; p.running_mean = running_mean; p.running_var = running_var;
   p.mean = mean; p.var = var; p.ss = ss;
+  if (g_bn_fused_finalize && nseg > BN_WALK_MAX_SEG && nseg <= BN_FR_MAX_SEG) {
+    hipLaunchKernelGGL(bn_seg_finalize_running_f32_kernel<true>,
+                       dim3((C + BN_FR_CH - 1) / BN_FR_CH), dim3(BN_FR_CH * BN_FR_SL), 0, stream,
+                       p, sums, sums_c);
+    return (int)hipGetLastError();
+  }
   if (nseg <= BN_WALK_MAX_SEG) {
     hipLaunchKernelGGL(bn_seg_sums_walk_f32_kernel, dim3((C + 63) / 64), dim3(64), 0, stream, p,
                        sums, sums_c);

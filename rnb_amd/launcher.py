@@ -82,13 +82,13 @@ def _parse_overrides(items):
     return out
 
 
-# Runner processes one device serves well. Measured on one MI355X: 4 (2
-# loaders + 2 runners) run the headline at ~940 videos/s, 8 run but lose
-# throughput to contention, 9 collapsed to 47-121 videos/s with 0.5-s stalls
-# per model call (profiles/NOTES.md, "Pipeline"): the device's hardware
-# scheduler then time-slices whole processes. One process per stage replica is
-# the RnB design, so this is a warning, not an error.
-CROWDED_GPU_PROCESSES = 8
+# Runner processes one device serves well. Measured on one MI355X: an early
+# round-2 build collapsed to 47-121 videos/s with 9 processes (6 loaders + 3
+# runners) while each runner held ~60 GB of graph pools; with largest-first
+# graph capture (~9.5 GB per runner) 10 processes (a --gpus 2 topology folded
+# onto one card) ran at 907 videos/s, the 1-GPU rate (profiles/NOTES.md).
+# One process per stage replica is the RnB design, so this is a warning.
+CROWDED_GPU_PROCESSES = 12
 
 
 def warn_crowded_gpus(spec, limit: int = CROWDED_GPU_PROCESSES) -> Dict[int, int]:
@@ -96,9 +96,9 @@ def warn_crowded_gpus(spec, limit: int = CROWDED_GPU_PROCESSES) -> Dict[int, int
     returns those GPUs and their process counts."""
     crowded = {g: n for g, n in sorted(spec.processes_per_gpu().items()) if n > limit}
     for g, n in crowded.items():
-        print("[launcher] warning: %d GPU processes on gpu %d (> %d): one device time-slices "
-              "that many processes and throughput can collapse; fewer replicas or more GPUs "
-              "serve better" % (n, g, limit), flush=True)
+        print("[launcher] warning: %d GPU processes on gpu %d (> %d measured): the device "
+              "time-slices its processes; fewer replicas or more GPUs may serve better"
+              % (n, g, limit), flush=True)
     return crowded
 
 

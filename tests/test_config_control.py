@@ -213,8 +213,8 @@ def test_runner_slot_shape_follows_layer_range():
 
 
 def test_crowded_gpu_warning(capsys):
-    """The launcher warns when one GPU would host more runner processes than
-    one device serves well (measured: 9 on one MI355X collapse)."""
+    """The launcher counts runner processes per GPU and warns above the
+    measured range (launcher.CROWDED_GPU_PROCESSES)."""
     from rnb_amd.config import parse_pipeline
     from rnb_amd.launcher import warn_crowded_gpus
     it = "rnb_amd.models.r2p1d.model.R2P1DVideoPathIterator"
@@ -225,6 +225,7 @@ def test_crowded_gpu_warning(capsys):
         {"model": runner, "queue_groups": [{"gpus": [0] * 6 + [1, -1], "in_queue": 0}]}]}
     spec = parse_pipeline(cfg)
     assert spec.processes_per_gpu() == {0: 9, 1: 2}
-    assert warn_crowded_gpus(spec) == {0: 9}
+    assert warn_crowded_gpus(spec, limit=8) == {0: 9}
     assert "9 GPU processes on gpu 0" in capsys.readouterr().out
     assert warn_crowded_gpus(spec, limit=9) == {}
+    assert warn_crowded_gpus(spec) == {}            # default limit 12

@@ -481,13 +481,13 @@ def test_deferred_batch_bn_into_temporal_winograd_matches_separate_apply(monkeyp
 
 
 @pytest.mark.parametrize("source,nseg", [("pass", 14), ("pass", 28), ("pass", 41),
-                                         ("sums", 14), ("sums", 41)])
+                                         ("sums", 14), ("sums", 28), ("sums", 41)])
 def test_bn_fused_finalize_running_matches_split_kernels_and_torch(source, nseg):
     """BN statistics per video, every finalize path against the others and an
     fp64 torch reference: statistics pass with <= 32 segments (the fused
     finalize + running-update kernel, 16 segment waves, vs the separate
-    kernels), > 32 segments (separate kernels), epilogue sums (in-order walk <= 16, separate kernels
-    above). Per-segment mean / var / scale / shift, the running statistics
+    kernels), > 32 segments (separate kernels), epilogue sums (in-order walk
+    <= 16, fused kernel 17..32, separate kernels above). Per-segment mean / var / scale / shift, the running statistics
     (segments with < 2 rows skipped), 88 channels (a partial 64-channel
     block), empty and one-row segments; epilogue sums re-armed to zero."""
     from rnb_amd.ops.bn import BatchNormBatch
