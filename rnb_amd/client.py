@@ -56,46 +56,84 @@ def _push_exit_markers(q):
         pass
 
 
+# phase_start layout (shared doubles): [0] start of the timed bulk phase, then
+# per latency phase p at PHASE_BASE + PHASE_FIELDS * p: start time, offered
+# videos/s, first request id, last request id
+PHASE_BASE, PHASE_FIELDS, MAX_LATENCY_PHASES = 3, 4, 4
+
+
+def phase_array_len() -> int:
+    return PHASE_BASE + PHASE_FIELDS * MAX_LATENCY_PHASES
+
+
+def parse_latency_phases(load: float, mean_interval_ms=None):
+    """Latency phases after the bulk phase, in order: an absolute Poisson
+    phase at ``mean_interval_ms`` (the reference client's ``-mi``, e.g. BASELINE
+    config #5's 10 ms) when given, then ``load`` x the measured throughput."""
+    phases = []
+    if mean_interval_ms:
+        phases.append(("mi", float(mean_interval_ms)))
+    if load:
+        phases.append(("load", float(load)))
+    return phases[:MAX_LATENCY_PHASES]
+
+
 def _latency_phase(video_iter, filename_queue, count, bulk_videos, counter, termination_flag,
-                   phase_start, seconds, load, target, seed):
+                   phase_start, seconds, load, target, seed, phases=None):
     """After a timed bulk phase: wait until it completed, then offer Poisson
-    arrivals at ``load`` x the bulk phase's measured throughput for about
-    ``seconds`` seconds (request latency below saturation). ``target`` (shared)
-    is raised to cover the new requests before the first is enqueued;
-    ``phase_start[1]``/``[2]`` get the phase start and the offered rate."""
+    arrivals for about ``seconds`` seconds per phase (request latency below
+    saturation): ``("load", f)`` at f x the bulk phase's measured throughput,
+    ``("mi", ms)`` at a fixed mean interval. Each phase starts once the
+    previous one has completed. ``target`` (shared) is raised to cover a
+    phase's requests before its first is enqueued. Returns the last id."""
     import numpy as np
     from queue import Full
     from .control import TerminationFlag
     from .timecard import TimeCard
+    phases = phases if phases is not None else [("load", load)]
+    rng = np.random.default_rng(None if seed is None else seed + 1)
     while counter.value < count:
         if termination_flag.value != TerminationFlag.UNSET:
-            return
+            return count
         time.sleep(WARMUP_POLL_S)
     t_bulk = time.time() - phase_start[0]
-    rate = load * bulk_videos / max(t_bulk, 1e-6)           # videos/s offered
-    n = max(1, int(round(seconds * rate)))
+    plan = []
+    for kind, val in phases:
+        rate = (val * bulk_videos / max(t_bulk, 1e-6) if kind == "load"
+                else 1000.0 / max(val, 1e-3))               # videos/s offered
+        plan.append((rate, max(1, int(round(seconds * rate)))))
+    # the final step stops the job at the target: cover every phase up front
     with target.get_lock():
-        target.value = count + n
-    phase_start[1] = time.time()
-    phase_start[2] = rate
-    rng = np.random.default_rng(None if seed is None else seed + 1)
-    next_t = time.perf_counter()
-    for i in range(n):
-        if termination_flag.value != TerminationFlag.UNSET:
-            return
-        tc = TimeCard(count + i + 1)
-        tc.record("enqueue_filename")
-        try:
-            filename_queue.put_nowait((None, next(video_iter), tc))
-        except Full:
-            with termination_flag.get_lock():
-                if termination_flag.value == TerminationFlag.UNSET:
-                    termination_flag.value = TerminationFlag.FILENAME_QUEUE_FULL
-            return
-        next_t += rng.exponential(1.0 / rate)
-        delay = next_t - time.perf_counter()
-        if delay > 0:
-            time.sleep(delay)
+        target.value = count + sum(n for _, n in plan)
+    for p, (rate, n) in enumerate(plan):
+        while counter.value < count:                  # previous phase completed
+            if termination_flag.value != TerminationFlag.UNSET:
+                return count
+            time.sleep(WARMUP_POLL_S)
+        base = PHASE_BASE + PHASE_FIELDS * p
+        phase_start[base] = time.time()
+        phase_start[base + 1] = rate
+        phase_start[base + 2] = count + 1
+        phase_start[base + 3] = count + n
+        next_t = time.perf_counter()
+        for i in range(n):
+            if termination_flag.value != TerminationFlag.UNSET:
+                return count
+            tc = TimeCard(count + i + 1)
+            tc.record("enqueue_filename")
+            try:
+                filename_queue.put_nowait((None, next(video_iter), tc))
+            except Full:
+                with termination_flag.get_lock():
+                    if termination_flag.value == TerminationFlag.UNSET:
+                        termination_flag.value = TerminationFlag.FILENAME_QUEUE_FULL
+                return count
+            next_t += rng.exponential(1.0 / rate)
+            delay = next_t - time.perf_counter()
+            if delay > 0:
+                time.sleep(delay)
+        count += n
+    return count
 
 
 def poisson_client(video_path_iterator, filename_queue, beta, termination_flag,
@@ -143,7 +181,7 @@ def poisson_client(video_path_iterator, filename_queue, beta, termination_flag,
 def bulk_client(video_path_iterator, filename_queue, num_videos, termination_flag,
                 sta_bar, fin_bar, seed=None, barrier_timeout=None, iterator_kwargs=None,
                 done_counter=None, warmup_videos=0, counter=None, phase_start=None,
-                latency_seconds=0.0, latency_load=0.5, target=None):
+                latency_seconds=0.0, latency_load=0.5, target=None, latency_phases=None):
     from queue import Full
     from .control import TerminationFlag
     from .timecard import TimeCard
@@ -176,7 +214,7 @@ def bulk_client(video_path_iterator, filename_queue, num_videos, termination_fla
             termination_flag.value == TerminationFlag.UNSET:
         _latency_phase(it, filename_queue, count, num_videos - warmup_videos, counter,
                        termination_flag, phase_start, latency_seconds, latency_load,
-                       target, seed)
+                       target, seed, latency_phases)
     _push_exit_markers(filename_queue)
     if done_counter is not None and termination_flag.value == TerminationFlag.UNSET:
         filename_queue.close()

@@ -62,6 +62,10 @@ def build_parser() -> argparse.ArgumentParser:
                         "Poisson arrivals for about this long at --latency-load x the "
                         "measured throughput and report their request latency")
     p.add_argument("--latency-load", type=float, default=0.5)
+    p.add_argument("--latency-mi", type=float, default=None,
+                   help="(with --latency-seconds) first run a Poisson phase at this fixed "
+                        "mean interval in ms (reference client.py:44 semantics, e.g. 10 for "
+                        "config r2p1d-aggressive), then the --latency-load phase")
     p.add_argument("--set", dest="overrides", action="append", default=[],
                    metavar="KEY=JSON",
                    help="Override a model kwarg in every step, e.g. --set depth=18")
@@ -226,7 +230,10 @@ def run(args) -> dict:
     fin_bar = ctx.Barrier(num_runners + 2)
     counter = ctx.Value("i", 0)
     flag = ctx.Value("i", TerminationFlag.UNSET)
-    phase_start = ctx.Array("d", 3)     # timed start, latency-phase start, offered rate
+    from .client import phase_array_len, parse_latency_phases, PHASE_BASE, PHASE_FIELDS
+    phase_start = ctx.Array("d", phase_array_len())   # timed start + latency phases
+    lat_phases = parse_latency_phases(getattr(args, "latency_load", 0.5),
+                                      getattr(args, "latency_mi", None))
     warm = int(getattr(args, "warmup_videos", 0) or 0)
     total_videos = args.videos + warm
     lat_s = float(getattr(args, "latency_seconds", 0.0) or 0.0)
@@ -267,7 +274,7 @@ def run(args) -> dict:
                                          warmup_videos=warm, counter=counter,
                                          phase_start=phase_start, latency_seconds=lat_s,
                                          latency_load=getattr(args, "latency_load", 0.5),
-                                         target=target))
+                                         target=target, latency_phases=lat_phases))
     procs = [("client", client)]
     last = len(spec.steps) - 1
     dist_infos = _assign_rccl_ranks(spec, qt, job_id)
@@ -354,14 +361,26 @@ def run(args) -> dict:
         # window from the start of the timed phase to the completion of its
         # last request (the barrier-based time also covers the shutdown)
         window = float(fin.max() - time_start) if fin.size else total
-        if lat_s and phase_start[1] > 0:
-            result["latency_phase"] = dict(
-                summaries.latency_stats(min_id=last + 1),
-                offered_videos_per_s=phase_start[2], seconds=lat_s)
-            print("Latency phase: %.1f videos/s offered (Poisson), p50 %.2f ms p99 %.2f ms "
-                  "(%d requests)" % (phase_start[2], result["latency_phase"]["p50_ms"],
-                                     result["latency_phase"]["p99_ms"],
-                                     result["latency_phase"]["count"]), flush=True)
+        phases = []
+        for i, (kind, val) in enumerate(lat_phases if lat_s else []):
+            base = PHASE_BASE + PHASE_FIELDS * i
+            if phase_start[base] <= 0:
+                continue
+            ph = dict(summaries.latency_stats(min_id=int(phase_start[base + 2]),
+                                              max_id=int(phase_start[base + 3])),
+                      offered_videos_per_s=phase_start[base + 1], seconds=lat_s,
+                      kind=kind, **({"mean_interval_ms": val} if kind == "mi" else
+                                    {"load": val}))
+            phases.append(ph)
+            print("Latency phase (%s %g): %.1f videos/s offered (Poisson), p50 %.2f ms "
+                  "p99 %.2f ms (%d requests)" % (kind, val, ph["offered_videos_per_s"],
+                                                 ph["p50_ms"], ph["p99_ms"], ph["count"]),
+                  flush=True)
+        if phases:
+            result["latency_phases"] = phases
+            # the relative-load phase (the bench's headline latency), else the first
+            result["latency_phase"] = next((ph for ph in phases if ph["kind"] == "load"),
+                                           phases[0])
         if lat_s:
             total = window      # the barrier also waits for the latency phase
         result.update({"time_s": total, "videos_per_s": done / total if total > 0 else 0.0,

@@ -217,14 +217,19 @@ class R2P1DRunner(RunnerModel):
 
     @staticmethod
     def _clip_offsets(time_card, n: int):
-        """Clip ranges of the videos batched into this call (bn_mode='batch':
-        each video keeps its own BN statistics); None = one video."""
+        """Clip ranges of the BN segments of this call (bn_mode='batch'); None =
+        one segment. A segment is one queued item as the reference would run
+        it: a single video keeps its own statistics, while a Batcher batch
+        (reference batcher.py:28 + runner.py:125-126: one forward over the
+        concatenated videos) is normalised with its joint statistics."""
         if not isinstance(time_card, TimeCardList) or n == 0:
             return None
+        rows = getattr(time_card, "item_rows", None)
+        if not rows or len(rows) < 2:
+            return None
         offs = [0]
-        for tc in time_card.time_cards:
-            r = tc.extra.get("rows")
-            offs.append(offs[-1] + int(r if r is not None else (tc.num_clips or 0)))
+        for r in rows:
+            offs.append(offs[-1] + int(r))
         return offs if offs[-1] == n else None
 
     def __call__(self, tensors, non_tensors, time_card):

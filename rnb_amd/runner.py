@@ -369,7 +369,7 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                     dst = tuple(shared_output_ring.slot_views(gslot))
                 else:
                     dst = model.gather_buffers(rows)
-                off, cards, nts = 0, [], []
+                off, cards, nts, item_rows = 0, [], [], []
                 for sig, nt, tc in items:
                     r = rows_of(sig)
                     pull(sig, tuple(d[off:off + r] for d in dst))
@@ -378,8 +378,9 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                         tc.extra["rows"] = r     # where this item's rows end
                     cards.extend(cards_of(tc))
                     nts.append(nt)
+                    item_rows.append(r)
                 tensor_inputs = tuple(d[:rows] for d in dst)
-                time_card = TimeCardList(cards)
+                time_card = TimeCardList(cards, item_rows)
                 gstats["calls"] += 1
                 gstats["items"] += len(items)
                 gstats["rows"] += rows
@@ -480,6 +481,19 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 for ring in rings:
                     if ring is not None:
                         ring.release_all()
+        # GPU-ordered rings leave pulls (and IPC stream waits) queued on this
+        # stream: drain them before fin_bar, after which producers free their
+        # slots, then close the handles this consumer opened on input rings
+        if stream is not None:
+            stream.synchronize()
+        for ring in _rings(shared_input_rings):
+            if hasattr(ring, "close"):
+                try:
+                    ring.close()
+                except Exception as err:
+                    print("[runner %d/%d/%d] closing input ring %s: %s"
+                          % (step_idx, group_idx, instance_idx, ring.name, err),
+                          file=sys.stderr, flush=True)
 
     fin_bar.wait(barrier_timeout)
     if output_queues is not None:

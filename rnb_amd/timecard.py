@@ -143,8 +143,12 @@ class TimeCard:
 class TimeCardList:
     """A batch of TimeCards that travel together (output of the Batcher)."""
 
-    def __init__(self, time_cards: List[TimeCard]):
+    def __init__(self, time_cards: List[TimeCard], item_rows: Optional[List[int]] = None):
         self.time_cards = time_cards
+        # rows of each queued item this list was gathered from (set by a
+        # gathering runner): one item is one forward in the reference -- a
+        # single video, or a whole Batcher batch -- and so one BN segment
+        self.item_rows = item_rows
 
     def record(self, key: str) -> None:
         ts = time.time()

@@ -239,3 +239,26 @@ def test_runner_default_bn_numerics_follow_the_reference():
         default_bn_mode("train", "fp32")
     r = R2P1DRunner(CPU, 5, 5, depth=10, warmup=0)
     assert r.bn_mode == "batch"
+
+
+def test_batch_bn_segments_follow_queued_items():
+    """bn_mode='batch': one BN segment per queued item, as the reference runs
+    one forward per item -- a gathered single video keeps its own statistics,
+    while a Batcher batch (reference batcher.py:28, one forward over the
+    concatenated videos) is normalised with its joint statistics."""
+    from rnb_amd.timecard import TimeCardList
+    r = R2P1DRunner(CPU, 4, 5, depth=10, warmup=0, bn_mode="batch", dtype="fp32")
+    x = torch.randn(3, 4, 28, 28, 128, generator=torch.Generator().manual_seed(3))
+    a, b = TimeCard(1), TimeCard(2)
+    a.num_clips, b.num_clips = 1, 2
+    with torch.no_grad():
+        joint = r((x,), None, TimeCard(9))[0][0]
+        per_video = torch.cat([r((x[:1],), None, TimeCard(7))[0][0],
+                               r((x[1:],), None, TimeCard(8))[0][0]])
+        batcher_out = r((x,), None, TimeCardList([a, b]))[0][0]
+        gathered = r((x,), None, TimeCardList([a, b], item_rows=[1, 2]))[0][0]
+        gathered_batch = r((x,), None, TimeCardList([a, b], item_rows=[3]))[0][0]
+    assert (joint - per_video).abs().max().item() > 1e-3     # the two numerics differ
+    assert torch.allclose(batcher_out, joint, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(gathered_batch, joint, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(gathered, per_video, atol=1e-5, rtol=1e-5)

@@ -202,17 +202,24 @@ def test_consumer_side_batching_warmup_and_latency_phase(tmp_path):
         {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [-1], "in_queue": 0}],
          "max_clips": 8, "max_batch_videos": 4}]}
     proc, res, _ = run_cfg(tmp_path, cfg, "-v", "6", "-mi", "0", "--warmup-videos", "2",
-                           "--latency-seconds", "1", "--latency-load", "0.5")
+                           "--latency-seconds", "1", "--latency-load", "0.5",
+                           "--latency-mi", "250")
     assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
     assert res["ok"] and res["warmup_videos"] == 2
     assert res["latency"]["count"] == 6              # timed ids 3..8 only
-    assert res["latency_phase"]["count"] >= 1
+    # two Poisson phases: the fixed 250 ms interval (reference -mi semantics)
+    # first, then half the measured rate; their request ids do not overlap
+    fixed, rel = res["latency_phases"]
+    assert fixed["kind"] == "mi" and fixed["mean_interval_ms"] == 250
+    assert abs(fixed["offered_videos_per_s"] - 4.0) < 1e-6
+    assert rel["kind"] == "load" and res["latency_phase"] == rel
+    assert fixed["count"] >= 1 and rel["count"] >= 1
     assert res["window_s"] > 0 and res["videos_per_s_window"] > 0
-    # the runner log holds every request: warm-up + timed + latency phase
+    # the runner log holds every request: warm-up + timed + both latency phases
     logs = [f for f in os.listdir(tmp_path / "logs" / res["job_id"]) if f.startswith("g")]
     rows = sum(len(open(tmp_path / "logs" / res["job_id"] / f).read().splitlines()) - 1
                for f in logs)
-    assert rows == 8 + res["latency_phase"]["count"]
+    assert rows == 8 + fixed["count"] + rel["count"]
 
 
 def test_batcher_gathers_without_staging_copies(tmp_path):
