@@ -16,9 +16,10 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 
 // kind: 0 = v_mfma_f32_16x16x4_f32, 1 = v_mfma_f32_16x16x16_bf16,
-//       2 = v_mfma_f32_16x16x32_bf16, 3 = v_mfma_f32_32x32x8_bf16
-template <int KIND>
-__global__ __launch_bounds__(256) void rate_kernel(float* out, long long* cyc, int iters) {
+//       2 = v_mfma_f32_16x16x32_bf16, 3 = v_mfma_f32_32x32x8_bf16,
+//       4 / 5 = 16x16x16_bf16 with 2 / 1 dependent accumulator chains
+template <int KIND, int NACC = 4>
+__global__ __launch_bounds__(512) void rate_kernel(float* out, long long* cyc, int iters) {
   const int lane = threadIdx.x & 63;
   float fa = 1.0f + 1e-3f * lane, fb = 0.5f - 1e-3f * lane;
   s16x4 a4 = (s16x4){(short)(0x3f80 + lane), 0x3f00, 0x3e80, (short)(0x3f00 + lane)};
@@ -38,10 +39,21 @@ __global__ __launch_bounds__(256) void rate_kernel(float* out, long long* cyc, i
         c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(fa, fb, c2, 0, 0, 0);
         c3 = __builtin_amdgcn_mfma_f32_16x16x4f32(fa, fb, c3, 0, 0, 0);
       } else if constexpr (KIND == 1) {
+        // NACC independent accumulator chains (1: every MFMA depends on the last)
         c0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c1, 0, 0, 0);
-        c2 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c2, 0, 0, 0);
-        c3 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c3, 0, 0, 0);
+        if constexpr (NACC == 1) {
+          c0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c0, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c0, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c0, 0, 0, 0);
+        } else if constexpr (NACC == 2) {
+          c1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c1, 0, 0, 0);
+          c0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c1, 0, 0, 0);
+        } else {
+          c1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c1, 0, 0, 0);
+          c2 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c2, 0, 0, 0);
+          c3 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c3, 0, 0, 0);
+        }
       } else if constexpr (KIND == 2) {
         c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, b8, c0, 0, 0, 0);
         c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, b8, c1, 0, 0, 0);
@@ -74,8 +86,21 @@ static __device__ __forceinline__ void split3(float v, short& h, short& m, short
   l = (short)(__float_as_uint(r2) >> 16);
 }
 
+// the same split with round-to-nearest-even parts (v_cvt_pk_bf16_f32)
+static __device__ __forceinline__ void split3_rne(float v, short& h, short& m, short& l) {
+  const __bf16 hb = (__bf16)v;
+  const float hf = (float)hb;
+  const float r = v - hf;
+  const __bf16 mb = (__bf16)r;
+  const float r2 = r - (float)mb;
+  const __bf16 lb = (__bf16)r2;
+  h = __builtin_bit_cast(short, hb);
+  m = __builtin_bit_cast(short, mb);
+  l = __builtin_bit_cast(short, lb);
+}
+
 // One wave: C[16][16] = A[16][K] * B[K][16] (row-major fp32), K % 16 == 0.
-// mode 0 = fp32 MFMA, 1 = bf16x6, 2 = bf16x3.
+// mode 0 = fp32 MFMA, 1 = bf16x6, 2 = bf16x3, 3 = bf16x6 with RNE parts.
 __global__ __launch_bounds__(64) void tile_kernel(const float* A, const float* B, float* C, int K,
                                                   int mode) {
   const int lane = threadIdx.x, r = lane & 15, q = lane >> 4;
@@ -93,13 +118,15 @@ __global__ __launch_bounds__(64) void tile_kernel(const float* A, const float* B
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         short h, m, l;
-        split3(A[r * K + k0 + 4 * q + j], h, m, l);
+        if (mode == 3) split3_rne(A[r * K + k0 + 4 * q + j], h, m, l);
+        else split3(A[r * K + k0 + 4 * q + j], h, m, l);
         ah[j] = h; am[j] = m; al[j] = l;
-        split3(B[(k0 + 4 * q + j) * 16 + r], h, m, l);
+        if (mode == 3) split3_rne(B[(k0 + 4 * q + j) * 16 + r], h, m, l);
+        else split3(B[(k0 + 4 * q + j) * 16 + r], h, m, l);
         bh[j] = h; bm[j] = m; bl[j] = l;
       }
       // small terms first
-      if (mode == 1) {
+      if (mode == 1 || mode == 3) {
         acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(am, bm, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bl, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, bh, acc, 0, 0, 0);
@@ -124,6 +151,8 @@ int rnb_mfma_rate(int kind, float* out, long long* cyc, int blocks, int threads,
     case 1: hipLaunchKernelGGL(rate_kernel<1>, g, b, 0, s, out, cyc, iters); break;
     case 2: hipLaunchKernelGGL(rate_kernel<2>, g, b, 0, s, out, cyc, iters); break;
     case 3: hipLaunchKernelGGL(rate_kernel<3>, g, b, 0, s, out, cyc, iters); break;
+    case 4: hipLaunchKernelGGL((rate_kernel<1, 2>), g, b, 0, s, out, cyc, iters); break;
+    case 5: hipLaunchKernelGGL((rate_kernel<1, 1>), g, b, 0, s, out, cyc, iters); break;
     default: return -1;
   }
   return (int)hipGetLastError();

@@ -1,0 +1,523 @@
+// fp32 Winograd convolutions on the bf16 matrix cores ("x6": six bf16
+// products per fp32 product). Same math and work split as conv_wino_f32.hip
+// (F(2x2, 3x3) spatial, F(4, 3) temporal; SURVEY.md §2.4 K3/K7/K13/K19 and
+// K4/K8/K14), but every GEMM step runs on v_mfma_f32_16x16x16_bf16 instead
+// of v_mfma_f32_16x16x4_f32, which on gfx950 does 16x the FLOPs per cycle.
+//
+// Each fp32 operand is split EXACTLY into three bf16 parts, a = ah + am + al
+// (8 significant bits each, round-to-nearest: |am| <= 2^-8 |a|, |al| <=
+// 2^-16 |a|). The fp32 product a*b is then
+//   ah bh + ah bm + am bh + ah bl + al bh + am bm   (+ am bl + al bm + al bl)
+// and the three dropped terms are <= ~2^-24 |ab|, i.e. at the rounding level
+// of one fp32 multiply; each bf16 x bf16 product is exact in the fp32
+// accumulator. The six products pair up along K into three
+// v_mfma_f32_16x16x32_bf16 (16 cycles each, measured:
+// profiles/r3_mfma_split.txt) per 16-channel GEMM step, which replace four
+// v_mfma_f32_16x16x4_f32 (32 cycles each): 2.6x less matrix-core time for the
+// same fp32-accurate result (tests: within 1e-5 of an fp64 conv, like the
+// fp32-MFMA kernels; the 16x16x16 bf16 form takes the same 16 cycles for
+// half the K, so it would gain only 1.3x).
+//
+// Weights (U = G g G^T, fp64 on the host) are split on the host into
+// [chunk][cout block][x][row][8 x 16-B chunks (Ah|Am), (Ah|Al) per channel
+// quad]: 128-B rows whose chunks are permuted per row (x6_chunk) so the
+// ds_read_b128 fragment reads are conflict free; the LDS image is a linear
+// DMA copy of that layout. The input patch is transformed in fp32 (V = B^T d B, exact
+// +-1 arithmetic as before) and each GEMM step's V fragment (4 channels of
+// one tile per lane) is split in registers right before its MFMAs
+// (v_cvt_pk_bf16_f32, RNE) -- the transformed tensor still never leaves
+// the CU.
+//
+// A block is WAVES waves x 16 tiles x 16 TC output channels. With TC = 2 and
+// WAVES = 8 the two U buffers take 128 KB of LDS (one block = 2 waves per
+// SIMD per CU) and every staged U chunk serves 128 tiles.
+#include <type_traits>
+
+#include "wino_common.h"
+
+// 1: software-pipelined GEMM steps (split / fragment reads one step ahead,
+// interleaved with the MFMAs); 0: in-order steps; 2: pipelined where the
+// registers allow (TC 1: the TC 2 spatial kernel spills at 256 VGPRs)
+#ifndef X6_PIPE
+#define X6_PIPE 2
+#endif
+// the ~30 VALU ops of a step's split spread over its 3 TC MFMAs
+#define X6_VALU_PER_MFMA(TC) ((30 + 3 * (TC) - 1) / (3 * (TC)))
+
+typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 wbf16x2 __attribute__((ext_vector_type(2)));
+typedef float wf32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int wu32x4 __attribute__((ext_vector_type(4)));
+
+// v_mfma_f32_16x16x32_bf16 sums 32 products per output; lane (col n, quad
+// q) supplies k = 8q .. 8q+7 of B and lane (row m, q) the same k of A. Each
+// lane keeps 4 channels (4q .. 4q+3 of the 16-channel chunk), so its 8 k
+// slots carry two bf16 parts of those 4 channels, and the six products
+// pair up into three MFMAs:
+//   (Ah | Am) x (Bh ; Bh) = Ah Bh + Am Bh
+//   (Ah | Al) x (Bm ; Bh) = Ah Bm + Al Bh
+//   (Ah | Am) x (Bl ; Bm) = Ah Bl + Am Bm
+struct X6B {                  // B fragments of one GEMM step
+  wu32x4 hh, mh, lm;
+};
+struct X6A {                  // A fragments of one GEMM step and channel group
+  wu32x4 hm, hl;
+};
+
+static __device__ __forceinline__ uint32_t x6_pk(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((wf32x2){a, b}, wbf16x2));
+}
+
+// exact 3-way split of 4 fp32 values (channels j = 0..3 of a B fragment)
+static __device__ __forceinline__ X6B x6_split(const wf32x4& v) {
+  uint32_t h[2], m[2], l[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float a = v[2 * k], b = v[2 * k + 1];
+    const uint32_t hh = x6_pk(a, b);
+    const float ra = a - __uint_as_float(hh << 16), rb = b - __uint_as_float(hh & 0xFFFF0000u);
+    const uint32_t mm = x6_pk(ra, rb);
+    const float la = ra - __uint_as_float(mm << 16), lb = rb - __uint_as_float(mm & 0xFFFF0000u);
+    h[k] = hh;
+    m[k] = mm;
+    l[k] = x6_pk(la, lb);
+  }
+  X6B f;
+  f.hh = (wu32x4){h[0], h[1], h[0], h[1]};
+  f.mh = (wu32x4){m[0], m[1], h[0], h[1]};
+  f.lm = (wu32x4){l[0], l[1], m[0], m[1]};
+  return f;
+}
+
+static __device__ __forceinline__ wf32x4 x6_mma(const wu32x4& a, const wu32x4& b, const wf32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(wbf16x8, a),
+                                                 __builtin_bit_cast(wbf16x8, b), c, 0, 0, 0);
+}
+
+// the six products of one GEMM step into acc[tc] (3 MFMAs per channel
+// group, TC chains interleaved, small terms first)
+template <int TC>
+static __device__ __forceinline__ void x6_step(wf32x4 (&acc)[TC], const X6A (&a)[TC],
+                                               const X6B& b) {
+#pragma unroll
+  for (int tc = 0; tc < TC; ++tc) acc[tc] = x6_mma(a[tc].hm, b.lm, acc[tc]);
+#pragma unroll
+  for (int tc = 0; tc < TC; ++tc) acc[tc] = x6_mma(a[tc].hl, b.mh, acc[tc]);
+#pragma unroll
+  for (int tc = 0; tc < TC; ++tc) acc[tc] = x6_mma(a[tc].hm, b.hh, acc[tc]);
+}
+
+// 16-B chunk permutation of a 128-B U row: logical chunk c = 2 q + half
+// (q = channel quad, half 0 = (Ah | Am), 1 = (Ah | Al)) lives at physical
+// chunk c ^ s(row >> 1 & 7), s = [0, 1, 0, 1, 6, 7, 6, 7], which makes the
+// ds_read_b128 fragment reads of every 16-lane group conflict free
+// (rows alternate between the two 128-B halves of the 64 banks)
+static __device__ __forceinline__ int x6_chunk(int c, int row) {
+  return c ^ ((0x76761010 >> (4 * ((row >> 1) & 7))) & 7);
+}
+
+// A fragments (weights) of GEMM step x for the lane's row frow / quad q
+template <int TC>
+static __device__ __forceinline__ void x6_read_a(X6A (&a)[TC], const char* ub, int x, int frow,
+                                                 int q) {
+  constexpr int CT = 16 * TC;
+  const int c0 = x6_chunk(2 * q, frow) << 4, c1 = x6_chunk(2 * q + 1, frow) << 4;
+#pragma unroll
+  for (int tc = 0; tc < TC; ++tc) {
+    const char* row = ub + (x * CT + tc * 16 + frow) * 128;
+    a[tc].hm = *(const wu32x4*)(row + c0);
+    a[tc].hl = *(const wu32x4*)(row + c1);
+  }
+}
+
+// U chunk staging: a linear LDS-DMA copy of NBYTES (a multiple of 1 KB),
+// 16 B per lane per instruction, spread over the block's waves
+template <int NBYTES, int WAVES>
+static __device__ __forceinline__ void x6_issue_u(const __amdgpu_buffer_rsrc_t& ur, uint32_t base,
+                                                  char* dst, int wave, int lane) {
+  constexpr int TOTAL = NBYTES / 1024;
+  constexpr int PER = (TOTAL + WAVES - 1) / WAVES;
+  static_assert(NBYTES % 1024 == 0, "U chunk in whole DMA instructions");
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int instr = wave * PER + i;
+    if (TOTAL % WAVES == 0 || instr < TOTAL)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          ur, (__attribute__((address_space(3))) void*)(dst + instr * 1024), 16,
+          base + (uint32_t)(instr * 1024 + lane * 16), 0, 0, 0);
+  }
+}
+
+// ===========================================================================
+// Spatial F(2x2, 3x3), stride 1, pad 1
+template <int TC, int WAVES, bool ST = false>
+__global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoParams p) {
+  constexpr int CT = 16 * TC, NT = 16 * WAVES;
+  constexpr int U_BYTES = 16 * CT * 128;                // one chunk: 16 x CT rows of 128 B
+  __shared__ __attribute__((aligned(16))) char lds[2 * U_BYTES];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wgid = w_xcd_remap();
+  const int cb = wgid % p.n_cblocks;
+  const int tb = wgid / p.n_cblocks;
+
+  const int tl = lane & 15, q = lane >> 4;
+  const int t = tb * NT + wave * 16 + tl;
+  int f = 0, ty = 0, tx = 0;
+  const bool tvalid = t < p.n_tiles;
+  if (tvalid) {
+    const int t1 = w_div(t, p.m_tw, p.s_tw);
+    tx = t - t1 * p.tiles_w;
+    f = w_div(t1, p.m_th, p.s_th);
+    ty = t1 - f * p.tiles_h;
+  }
+  const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
+  int rmask = 0, cmask = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    rmask |= (tvalid && y0 + d >= 0 && y0 + d < p.H) ? (1 << d) : 0;
+    cmask |= (x0 + d >= 0 && x0 + d < p.W) ? (1 << d) : 0;
+  }
+  const int pix0 = (f * p.H + y0) * p.W + x0;           // may be negative (padding)
+  const int row_bytes = p.W * p.Cin * 4;
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, p.u_bytes, 0x00020000);
+
+  auto load_one = [&](int chunk, int e) -> wf32x4 {
+    const int dy = e >> 2, dx = e & 3;
+    const bool ok = ((rmask >> dy) & (cmask >> dx) & 1) != 0;
+    const uint32_t off =
+        ok ? (uint32_t)(pix0 * p.Cin * 4 + chunk * 64 + q * 16 + dy * row_bytes + dx * p.Cin * 4)
+           : WINO_INVALID;
+    return __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+  };
+  auto issue_u = [&](int chunk, int buf) {
+    const uint32_t base = ((uint32_t)chunk * (uint32_t)p.n_cblocks + (uint32_t)cb) * U_BYTES;
+    x6_issue_u<U_BYTES, WAVES>(ur, base, lds + buf * U_BYTES, wave, lane);
+  };
+
+  wf32x4 acc[16][TC];
+#pragma unroll
+  for (int x = 0; x < 16; ++x)
+#pragma unroll
+    for (int c = 0; c < TC; ++c) acc[x][c] = (wf32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nchunks = p.Cin / 16;
+  const int frow = lane & 15;
+  auto transform = [&](wf32x4 (&v)[16]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const wf32x4 a0 = v[0 * 4 + j], a1 = v[1 * 4 + j], a2 = v[2 * 4 + j], a3 = v[3 * 4 + j];
+      v[0 * 4 + j] = a0 - a2;
+      v[1 * 4 + j] = a1 + a2;
+      v[2 * 4 + j] = a2 - a1;
+      v[3 * 4 + j] = a1 - a3;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const wf32x4 b0 = v[i * 4 + 0], b1 = v[i * 4 + 1], b2 = v[i * 4 + 2], b3 = v[i * 4 + 3];
+      v[i * 4 + 0] = b0 - b2;
+      v[i * 4 + 1] = b1 + b2;
+      v[i * 4 + 2] = b2 - b1;
+      v[i * 4 + 3] = b1 - b3;
+    }
+  };
+  // 16 GEMM steps of one chunk, software-pipelined one step ahead: step x+1's
+  // B fragment is split (VALU) and its A fragments read (LDS) while step x's
+  // 6 TC MFMAs run; V[x+1]'s registers are refilled with patch element x+1
+  // of chunk `next` right after the split (prefetch without a second set)
+  auto gemm = [&](const char* ub, wf32x4 (&v)[16], int next, auto refill) {
+    if constexpr (X6_PIPE == 0 || (X6_PIPE == 2 && TC > 1)) {
+      // in-order steps: split, refill, fragment reads, MFMAs (the other
+      // wave of the SIMD covers the latencies)
+#pragma unroll
+      for (int x = 0; x < 16; ++x) {
+        X6A af[TC];
+        const X6B bf = x6_split(v[x]);
+        if constexpr (decltype(refill)::value) v[x] = load_one(next, x);
+        x6_read_a<TC>(af, ub, x, frow, q);
+        x6_step<TC>(acc[x], af, bf);
+      }
+    } else {
+      X6A af[2][TC];
+      X6B bf[2];
+      bf[0] = x6_split(v[0]);
+      if constexpr (decltype(refill)::value) v[0] = load_one(next, 0);
+      x6_read_a<TC>(af[0], ub, 0, frow, q);
+#pragma unroll
+      for (int x = 0; x < 16; ++x) {
+        if (x + 1 < 16) {
+          bf[(x + 1) & 1] = x6_split(v[x + 1]);
+          if constexpr (decltype(refill)::value) v[x + 1] = load_one(next, x + 1);
+          x6_read_a<TC>(af[(x + 1) & 1], ub, x + 1, frow, q);
+        }
+        x6_step<TC>(acc[x], af[x & 1], bf[x & 1]);
+        if (x + 1 < 16) {
+          // interleave: per MFMA one split VALU pair; the LDS reads early
+#pragma unroll
+          for (int i = 0; i < 3 * TC; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);          // MFMA
+            if (i < 2 * TC) __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);   // DS read
+            __builtin_amdgcn_sched_group_barrier(0x0002, X6_VALU_PER_MFMA(TC), 0);   // VALU
+          }
+          if constexpr (decltype(refill)::value)
+            __builtin_amdgcn_sched_group_barrier(0x0020, 1, 0);          // VMEM read
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  wf32x4 d[16];
+  issue_u(0, 0);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) d[e] = load_one(0, e);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int c = 0; c + 1 < nchunks; ++c) {
+    const int cur = c & 1;
+    issue_u(c + 1, cur ^ 1);
+    // keep the U DMA ahead of the patch loads in issue order (vmcnt below)
+    asm volatile("" ::: "memory");
+    transform(d);
+    gemm(lds + cur * U_BYTES, d, c + 1, std::true_type{});
+    // U of chunk c+1 landed; the 16 younger patch loads may stay in flight
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __syncthreads();
+  }
+  transform(d);
+  gemm(lds + ((nchunks - 1) & 1) * U_BYTES, d, -1, std::false_type{});
+  __syncthreads();                 // the epilogue's statistics reuse the U buffers
+  w_spatial_epilogue<TC, ST, WAVES>(p, lds, acc, tb, wave, tl, q, cb, lane, tvalid, f, ty, tx);
+}
+
+// ===========================================================================
+// Temporal F(4, 3) for the stride-1 3x1x1 convs (see conv_winot_f32_kernel):
+// a tile = 4 output frames of one pixel, 6 GEMM steps per 16-channel chunk,
+// optional BN + ReLU of the input on load. U per chunk: 6 x CT rows of 128 B.
+template <int TC, int WAVES, bool ST = false>
+__global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : 2) void conv_winot_x6_kernel(
+    const WinoParams p) {
+  constexpr int CT = 16 * TC, NT = 16 * WAVES;
+  constexpr int U_BYTES = 6 * CT * 128;
+  __shared__ __attribute__((aligned(16))) char lds[2 * U_BYTES];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wgid = w_xcd_remap();
+  const int cb = wgid % p.n_cblocks;
+  const int tb = wgid / p.n_cblocks;
+
+  const int tl = lane & 15, q = lane >> 4;
+  const int t = tb * NT + wave * 16 + tl;
+  int n = 0, tt = 0, hw = 0;
+  const bool tvalid = t < p.n_tiles;
+  if (tvalid) {
+    const int t1 = w_div(t, p.m_tw, p.s_tw);      // tiles_w = pixels per frame
+    hw = t - t1 * p.tiles_w;
+    n = w_div(t1, p.m_th, p.s_th);                // tiles_h = frame groups
+    tt = t1 - n * p.tiles_h;
+  }
+  const int T = p.H, HW = p.W;
+  const int fr0 = 4 * tt - 1;
+  int fmask = 0;
+#pragma unroll
+  for (int e = 0; e < 6; ++e) fmask |= (tvalid && fr0 + e >= 0 && fr0 + e < T) ? (1 << e) : 0;
+  const int pix0 = (n * T + fr0) * HW + hw;       // may be negative (padding)
+  const int frame_bytes = HW * p.Cin * 4;
+  const bool aff = p.in_ss != nullptr;            // uniform
+  const float* ssb = nullptr;
+  if (aff) ssb = p.in_ss + (size_t)(tvalid ? p.clip_seg[n] : 0) * 2 * p.Cin + 4 * q;
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, p.u_bytes, 0x00020000);
+
+  auto load_one = [&](int chunk, int e) -> wf32x4 {
+    const bool ok = ((fmask >> e) & 1) != 0;
+    const uint32_t off =
+        ok ? (uint32_t)(pix0 * p.Cin * 4 + chunk * 64 + q * 16 + e * frame_bytes) : WINO_INVALID;
+    return __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+  };
+  auto issue_u = [&](int chunk, int buf) {
+    const uint32_t base = ((uint32_t)chunk * (uint32_t)p.n_cblocks + (uint32_t)cb) * U_BYTES;
+    x6_issue_u<U_BYTES, WAVES>(ur, base, lds + buf * U_BYTES, wave, lane);
+  };
+
+  wf32x4 acc[6][TC];
+#pragma unroll
+  for (int x = 0; x < 6; ++x)
+#pragma unroll
+    for (int c = 0; c < TC; ++c) acc[x][c] = (wf32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto transform = [](wf32x4 (&v)[6]) {
+    const wf32x4 d0 = v[0], d1 = v[1], d2 = v[2], d3 = v[3], d4 = v[4], d5 = v[5];
+    const wf32x4 t0 = d4 - 4.f * d2, t1 = d3 - 4.f * d1;
+    const wf32x4 t2 = d4 - d2, t3 = 2.f * (d3 - d1);
+    v[0] = 4.f * d0 - 5.f * d2 + d4;
+    v[1] = t0 + t1;
+    v[2] = t0 - t1;
+    v[3] = t2 + t3;
+    v[4] = t2 - t3;
+    v[5] = 4.f * d1 - 5.f * d3 + d5;
+  };
+  const int frow = lane & 15;
+  auto gemm = [&](const char* ub, wf32x4 (&v)[6], int next, auto refill) {
+    X6A af[2][TC];
+    X6B bf[2];
+    bf[0] = x6_split(v[0]);
+    if constexpr (decltype(refill)::value) v[0] = load_one(next, 0);
+    x6_read_a<TC>(af[0], ub, 0, frow, q);
+#pragma unroll
+    for (int x = 0; x < 6; ++x) {
+      if (x + 1 < 6) {
+        bf[(x + 1) & 1] = x6_split(v[x + 1]);
+        if constexpr (decltype(refill)::value) v[x + 1] = load_one(next, x + 1);
+        x6_read_a<TC>(af[(x + 1) & 1], ub, x + 1, frow, q);
+      }
+      x6_step<TC>(acc[x], af[x & 1], bf[x & 1]);
+      if (x + 1 < 6) {
+#pragma unroll
+        for (int i = 0; i < 3 * TC; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);          // MFMA
+          if (i < 2 * TC) __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);   // DS read
+          __builtin_amdgcn_sched_group_barrier(0x0002, X6_VALU_PER_MFMA(TC), 0);   // VALU
+        }
+        if constexpr (decltype(refill)::value)
+          __builtin_amdgcn_sched_group_barrier(0x0020, 1, 0);          // VMEM read
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  const int nchunks = p.Cin / 16;
+  auto affine = [&](wf32x4 (&v)[6], const wf32x4& sc, const wf32x4& sh) {
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      const bool ok = ((fmask >> e) & 1) != 0;
+      wf32x4 t = v[e] * sc + sh;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t[k] = ok ? fmaxf(t[k], 0.f) : 0.f;
+      v[e] = t;
+    }
+  };
+  wf32x4 d[6];
+  wf32x4 sc = (wf32x4){1.f, 1.f, 1.f, 1.f}, sh = (wf32x4){0.f, 0.f, 0.f, 0.f};
+  issue_u(0, 0);
+#pragma unroll
+  for (int e = 0; e < 6; ++e) d[e] = load_one(0, e);
+  if (aff) {
+    sc = *(const wf32x4*)ssb;
+    sh = *(const wf32x4*)(ssb + p.Cin);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int c = 0; c + 1 < nchunks; ++c) {
+    const int cur = c & 1;
+    issue_u(c + 1, cur ^ 1);
+    asm volatile("" ::: "memory");
+    if (aff) affine(d, sc, sh);
+    transform(d);
+    gemm(lds + cur * U_BYTES, d, c + 1, std::true_type{});
+    if (aff) {                                            // next chunk's scale / shift
+      sc = *(const wf32x4*)(ssb + (c + 1) * 16);
+      sh = *(const wf32x4*)(ssb + p.Cin + (c + 1) * 16);
+    }
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");    // U landed (6 younger loads may fly)
+    __syncthreads();
+  }
+  if (aff) affine(d, sc, sh);
+  transform(d);
+  gemm(lds + ((nchunks - 1) & 1) * U_BYTES, d, -1, std::false_type{});
+  __syncthreads();
+  w_temporal_epilogue<TC, ST, WAVES>(p, lds, acc, tb, wave, tl, q, cb, lane, tvalid, n, tt, hw);
+}
+
+// ---------------------------------------------------------------------------
+static int x6_prepare(WinoParams& p, int tile_h, int tile_w_div, int CT, int NT, int xsteps) {
+  if (p.Cin % 16 != 0 || p.Cout % 4 != 0 || p.y_stride % 4 || (p.res && p.res_stride % 4))
+    return -2;
+  if (p.Cout > p.y_stride || (p.res && p.Cout > p.res_stride)) return -3;
+  const long long xb = (long long)p.F * p.H * p.W * p.Cin * 4;
+  if (xb > 0x7FFFFF00LL) return -5;
+  p.tiles_h = (p.H + tile_h - 1) / tile_h;
+  p.tiles_w = (p.W + tile_w_div - 1) / tile_w_div;
+  const long long nt = (long long)p.F * p.tiles_h * p.tiles_w;
+  if (nt > 0x7FFFFFFF) return -6;
+  p.n_tiles = (int)nt;
+  p.n_tblocks = (p.n_tiles + NT - 1) / NT;
+  p.n_cblocks = (p.Cout + CT - 1) / CT;
+  const long long ub = (long long)(p.Cin / 16) * p.n_cblocks * xsteps * CT * 128;
+  if (ub > 0x7FFFFF00LL) return -7;
+  p.x_bytes = (uint32_t)xb;
+  p.u_bytes = (uint32_t)ub;
+  w_magic((uint32_t)p.tiles_w, &p.m_tw, &p.s_tw);
+  w_magic((uint32_t)p.tiles_h, &p.m_th, &p.s_th);
+  const long long blocks = (long long)p.n_tblocks * p.n_cblocks;
+  if (blocks > 0x7FFFFFFF) return -8;
+  return 0;
+}
+
+template <typename K>
+static void x6_launch(K kernel, const WinoParams& p, int threads, hipStream_t stream) {
+  hipLaunchKernelGGL(kernel, dim3((unsigned)(p.n_tblocks * p.n_cblocks)), dim3(threads), 0, stream,
+                     p);
+}
+
+extern "C" {
+
+// Spatial F(2x2, 3x3) on bf16 MFMA (x6). variant 0 = TC 2 x 8 waves (128
+// tiles x 32 channels per block), 1 = TC 1 x 8 waves, 2 = TC 1 x 4 waves.
+// U layout [Cin/16][n_cblocks][16][16 TC][8 chunks of 8 bf16] (x6_chunk).
+// Returns 0, a negative contract code, or the hipError_t.
+int rnb_wino_x6_launch(const WinoParams* pp, int variant, hipStream_t stream) {
+  WinoParams p = *pp;
+  if (variant < 0 || variant > 2) return -1;
+  const int TC = variant == 0 ? 2 : 1, WAVES = variant == 2 ? 4 : 8;
+  if (p.F <= 0 || p.H <= 0 || p.W <= 0) return 0;
+  const int rc = x6_prepare(p, 2, 2, 16 * TC, 16 * WAVES, 16);
+  if (rc) return rc;
+  const bool st = p.out_stats != nullptr;
+  switch (variant) {
+    case 0:
+      if (st) x6_launch(conv_wino_x6_kernel<2, 8, true>, p, 512, stream);
+      else x6_launch(conv_wino_x6_kernel<2, 8>, p, 512, stream);
+      break;
+    case 1:
+      if (st) x6_launch(conv_wino_x6_kernel<1, 8, true>, p, 512, stream);
+      else x6_launch(conv_wino_x6_kernel<1, 8>, p, 512, stream);
+      break;
+    default:
+      if (st) x6_launch(conv_wino_x6_kernel<1, 4, true>, p, 256, stream);
+      else x6_launch(conv_wino_x6_kernel<1, 4>, p, 256, stream);
+      break;
+  }
+  return (int)hipGetLastError();
+}
+
+// Temporal F(4, 3) on bf16 MFMA (x6): p.F = clips, p.H = T, p.W = pixels per
+// frame. variant 0 = TC 4 x 8 waves (128 tiles x 64 channels per block, 96 KB
+// of LDS), 1 = TC 2 x 4 waves (64 x 32, 48 KB).
+// U layout [Cin/16][n_cblocks][6][16 TC][8 chunks of 8 bf16] (x6_chunk).
+int rnb_winot_x6_launch(const WinoParams* pp, int variant, hipStream_t stream) {
+  WinoParams p = *pp;
+  if (variant < 0 || variant > 1) return -1;
+  const int TC = variant == 0 ? 4 : 2, WAVES = variant == 0 ? 8 : 4;
+  if (p.F <= 0 || p.H <= 0 || p.W <= 0) return 0;
+  const int rc = x6_prepare(p, 4, 1, 16 * TC, 16 * WAVES, 6);
+  if (rc) return rc;
+  const bool st = p.out_stats != nullptr;
+  if (TC == 4) {
+    if (st) x6_launch(conv_winot_x6_kernel<4, 8, true>, p, 512, stream);
+    else x6_launch(conv_winot_x6_kernel<4, 8>, p, 512, stream);
+  } else {
+    if (st) x6_launch(conv_winot_x6_kernel<2, 4, true>, p, 256, stream);
+    else x6_launch(conv_winot_x6_kernel<2, 4>, p, 256, stream);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -25,7 +25,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 LIBRARIES = {
     "librnb_kernels.so": (["conv_igemm.hip", "conv_halo.hip", "conv_temporal.hip",
                            "video_ops.hip", "bn_ops.hip", "conv_halo_ws.hip", "conv21.hip",
-                           "conv_f32.hip", "conv_wino_f32.hip"], [], []),
+                           "conv_f32.hip", "conv_wino_f32.hip", "conv_wino_x6.hip"], [], []),
     "librnb_runtime.so": (["runtime.cpp"], [], []),
     "librnb_tracer.so": (["tracer.cpp"], [], ["-L%s/lib" % ROCM, "-lrocprofiler-sdk",
                                                "-Wl,-rpath,%s/lib" % ROCM]),
@@ -43,7 +43,8 @@ def _stale(target: str, sources) -> bool:
     if not os.path.exists(target):
         return True
     t = os.path.getmtime(target)
-    deps = list(sources) + [os.path.abspath(__file__)]
+    headers = [os.path.join(CSRC, h) for h in sorted(os.listdir(CSRC)) if h.endswith(".h")]
+    deps = list(sources) + headers + [os.path.abspath(__file__)]
     return any(os.path.getmtime(s) > t for s in deps)
 
 

@@ -70,19 +70,43 @@ WINO_DEFAULT = WINO_BASE + 8
 WINOT_BASE = 1030
 WINOT_TC = {WINOT_BASE + 0: 2, WINOT_BASE + 1: 4}
 WINOT_DEFAULT = WINOT_BASE + 1
-WINO_ALL = set(WINO_TC) | set(WINOT_TC)
+# the same two transforms with fp32 products on the bf16 matrix cores
+# (csrc/conv_wino_x6.hip: every fp32 operand split exactly into three bf16
+# parts, six bf16 products per fp32 product, fp32 accumulation; within fp32
+# rounding of the fp32-MFMA kernels). Spatial: 1050 = 32 channels x 128
+# tiles per block, 1051 / 1052 = 16 channels x 128 / 64 tiles; temporal:
+# 1060 = 64 channels x 128 tiles, 1061 = 32 x 64.
+WINOX_BASE = 1050
+WINOX_TC = {WINOX_BASE + 0: 2, WINOX_BASE + 1: 1, WINOX_BASE + 2: 1}
+WINOTX_BASE = 1060
+WINOTX_TC = {WINOTX_BASE + 0: 4, WINOTX_BASE + 1: 2}
+WINO_X6 = set(WINOX_TC) | set(WINOTX_TC)
+WINO_SPATIAL = set(WINO_TC) | set(WINOX_TC)
+WINO_TEMPORAL = set(WINOT_TC) | set(WINOTX_TC)
+WINO_ALL = WINO_SPATIAL | WINO_TEMPORAL
 # temporal F(4,3) pays off once most output frames see all 3 taps
 WINOT_MIN_T = 4
+
+
+def x6_enabled() -> bool:
+    """RNB_X6=0 keeps the Winograd convs on the fp32 MFMA kernels."""
+    return os.environ.get("RNB_X6", "1") != "0"
+
+
+def wino_default(temporal: bool) -> int:
+    if x6_enabled():
+        return WINOTX_BASE if temporal else WINOX_BASE
+    return WINOT_DEFAULT if temporal else WINO_DEFAULT
 
 # Winograd F(2x2, 3x3) transforms: U = G g G^T (host, fp64), V = B^T d B and
 # Y = A^T M A in the kernel
 _WINO_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
 
 
-def winograd_weights(w: torch.Tensor, cout: int, tc: int) -> torch.Tensor:
+def winograd_weights(w: torch.Tensor, cout: int, tc: int, x6: bool = False) -> torch.Tensor:
     """[Cout, Cin, 1, 3, 3] folded weights -> the kernel's U layout
     [Cin/16][n_cblocks][16 (x = 4i + j)][CT = 16 tc][16 channels], fp32,
-    output rows past Cout zero."""
+    output rows past Cout zero (``x6``: the split-bf16 layout, ``x6_pack``)."""
     co, ci = w.shape[:2]
     g = w.detach().double().reshape(co, ci, 3, 3)
     G = torch.tensor(_WINO_G, dtype=torch.float64)
@@ -91,9 +115,41 @@ def winograd_weights(w: torch.Tensor, cout: int, tc: int) -> torch.Tensor:
     nb = (cout + ct - 1) // ct
     full = torch.zeros(nb * ct, ci, 16, dtype=torch.float64)
     full[:co] = u.reshape(co, ci, 16)
+    if x6:
+        return x6_pack(full, tc)
     # [nb, ct, ci/16, 16ch, 16x] -> [ci/16, nb, 16x, ct, 16ch]
     t = full.reshape(nb, ct, ci // 16, 16, 16).permute(2, 0, 4, 1, 3)
     return t.contiguous().float()
+
+
+# x6 chunk permutation of a 128-B U row (csrc/conv_wino_x6.hip x6_chunk):
+# logical 16-B chunk c = 2 quad + half sits at c ^ _X6_S[(row % 16) >> 1]
+_X6_S = (0, 1, 0, 1, 6, 7, 6, 7)
+
+
+def x6_pack(u: torch.Tensor, tc: int) -> torch.Tensor:
+    """fp64 transformed weights [rows = nb * 16 tc, ci, X] -> the x6 kernels'
+    U layout [ci/16][nb][X][16 tc][8 chunks][8 bf16] as int16: per channel
+    quad two chunks (Ah | Am) and (Ah | Al) of the exact 3-way bf16 split of
+    the fp32-rounded weight (u = h + m + l), chunks permuted per row."""
+    rows, ci, X = u.shape
+    ct = 16 * tc
+    nb = rows // ct
+    u32 = u.float()
+    h = u32.bfloat16()
+    r = u32 - h.float()                       # exact
+    m = r.bfloat16()
+    lo = (r - m.float()).bfloat16()           # exact: r - m has <= 8 bits
+
+    def lay(t):                               # -> [ci/16, nb, X, ct, quad, 4]
+        return t.reshape(nb, ct, ci // 16, 4, 4, X).permute(2, 0, 5, 1, 3, 4)
+    hh, mm, ll = lay(h), lay(m), lay(lo)
+    chunks = torch.stack([torch.cat([hh, mm], -1), torch.cat([hh, ll], -1)], dim=-2)
+    logical = chunks.reshape(ci // 16, nb, X, ct, 8, 8)
+    s = torch.tensor([_X6_S[(rr % 16) >> 1] for rr in range(ct)], dtype=torch.int64)
+    idx = torch.arange(8, dtype=torch.int64)[None, :] ^ s[:, None]          # [ct, 8]
+    phys = logical.gather(4, idx[None, None, None, :, :, None].expand_as(logical))
+    return phys.contiguous().view(torch.int16)
 
 
 # F(4, 3) (temporal): U = G g, interpolation points 0, +-1, +-2, inf
@@ -101,9 +157,10 @@ _WINO_G43 = ((1 / 4, 0.0, 0.0), (-1 / 6, -1 / 6, -1 / 6), (-1 / 6, 1 / 6, -1 / 6
              (1 / 24, 1 / 12, 1 / 6), (1 / 24, -1 / 12, 1 / 6), (0.0, 0.0, 1.0))
 
 
-def winograd_t_weights(w: torch.Tensor, cout: int, tc: int) -> torch.Tensor:
+def winograd_t_weights(w: torch.Tensor, cout: int, tc: int, x6: bool = False) -> torch.Tensor:
     """[Cout, Cin, 3, 1, 1] folded weights -> the temporal F(4, 3) kernel's U
-    layout [Cin/16][n_cblocks][6][CT = 16 tc][16 channels], fp32."""
+    layout [Cin/16][n_cblocks][6][CT = 16 tc][16 channels], fp32 (``x6``: the
+    split-bf16 layout)."""
     co, ci = w.shape[:2]
     g = w.detach().double().reshape(co, ci, 3)
     G = torch.tensor(_WINO_G43, dtype=torch.float64)
@@ -112,6 +169,8 @@ def winograd_t_weights(w: torch.Tensor, cout: int, tc: int) -> torch.Tensor:
     nb = (cout + ct - 1) // ct
     full = torch.zeros(nb * ct, ci, 6, dtype=torch.float64)
     full[:co] = u
+    if x6:
+        return x6_pack(full, tc)
     t = full.reshape(nb, ct, ci // 16, 16, 6).permute(2, 0, 4, 1, 3)
     return t.contiguous().float()
 
@@ -152,16 +211,18 @@ class ConvLayerF32:
         # temporal F(4,3) for stride-1 3x1x1 convs with Cin_p % 16 == 0
         self.winot_ok = (geom.kernel == (3, 1, 1) and geom.stride == (1, 1, 1)
                          and geom.padding == (1, 0, 0) and geom.cin_p % 16 == 0)
-        self.wino_ids = (set(WINO_TC) if self.wino_ok else
-                         set(WINOT_TC) if self.winot_ok else set())
+        self.wino_ids = (WINO_SPATIAL if self.wino_ok else
+                         WINO_TEMPORAL if self.winot_ok else set())
         self._wino_u: Dict[Tuple[int, int], torch.Tensor] = {}
 
-    def wino_u(self, tc: int, m: int = 2, co0: int = 0, nco: Optional[int] = None) -> torch.Tensor:
+    def wino_u(self, tc: int, m: int = 2, co0: int = 0, nco: Optional[int] = None,
+               x6: bool = False) -> torch.Tensor:
         """Transformed weights of output channels [co0, co0 + nco) (default: all
         cout_p) with 16 tc channels per work unit: m = 2 spatial F(2x2, 3x3),
-        m = -4 temporal F(4, 3) (built once per (m, tc, co0, nco))."""
+        m = -4 temporal F(4, 3); ``x6`` = the split-bf16 layout (built once per
+        (m, tc, co0, nco, x6))."""
         nco = self.geom.cout_p - co0 if nco is None else nco
-        key = (m, tc, co0, nco)
+        key = (m, tc, co0, nco, x6)
         u = self._wino_u.get(key)
         if u is None:
             fn = {2: winograd_weights, -4: winograd_t_weights}[m]
@@ -169,7 +230,7 @@ class ConvLayerF32:
             if w.shape[1] < self.geom.cin_p:            # zero weights for pad channels
                 w = torch.cat([w, w.new_zeros((w.shape[0], self.geom.cin_p - w.shape[1])
                                               + tuple(w.shape[2:]))], dim=1)
-            u = self._wino_u[key] = fn(w, nco, tc).to(self.device)
+            u = self._wino_u[key] = fn(w, nco, tc, x6=x6).to(self.device)
         return u
 
     def wino_parts(self, cid: int):
@@ -179,6 +240,16 @@ class ConvLayerF32:
         (conv2's 144 = 128 + 16 instead of 160 channels of MFMA work)."""
         if cid in WINOT_TC:
             return [(0, self.geom.cout_p, WINOT_TC[cid], cid - WINOT_BASE)]
+        if cid in WINOTX_TC:
+            return [(0, self.geom.cout_p, WINOTX_TC[cid], cid - WINOTX_BASE)]
+        if cid in WINOX_TC:
+            tc, variant = WINOX_TC[cid], cid - WINOX_BASE
+            cp, ct = self.geom.cout_p, 16 * tc
+            main, rem = cp // ct * ct, cp % ct
+            if main > 0 and rem > 0 and rem % 16 == 0:
+                # tail of 16 channels: variant 1 (TC 1, 128 tiles per block)
+                return [(0, main, tc, variant), (main, rem, 1, 1)]
+            return [(0, cp, tc, variant)]
         tc, variant = WINO_TC[cid], cid - WINO_BASE
         cp, ct = self.geom.cout_p, 16 * tc
         main, rem = cp // ct * ct, cp % ct
@@ -190,11 +261,13 @@ class ConvLayerF32:
     def candidates(self):
         from .native import kernels
         c = list(range(len(kernels().f32_configs)))
-        return c + sorted(self.wino_ids)
+        ids = self.wino_ids if x6_enabled() else self.wino_ids - WINO_X6
+        return c + sorted(ids)
 
     def _launch_wino(self, x, y, residual, cid, stream, in_affine=None, out_stats=None):
         from .native import WinoParams, kernels
-        ft = cid in WINOT_TC
+        ft = cid in WINO_TEMPORAL
+        x6 = cid in WINO_X6
         m = -4 if ft else 2
         g = self.geom
         N, T, H, W, C = x.shape
@@ -243,9 +316,11 @@ class ConvLayerF32:
                                     tuple(y.shape)))
             p.clip_seg = clip_seg.data_ptr()
             p.clip_frames, p.stats_c = T, sums.shape[2]
-        launch = kernels().winot_f32 if ft else kernels().wino_f32
+        k = kernels()
+        launch = ((k.winot_x6 if ft else k.wino_x6) if x6 else
+                  (k.winot_f32 if ft else k.wino_f32))
         for co0, nco, tc, variant in self.wino_parts(cid):
-            u = self.wino_u(tc, m, co0, nco)
+            u = self.wino_u(tc, m, co0, nco, x6=x6)
             assert u.shape[0] * 16 == C and u.shape[1] * 16 * tc >= nco
             p.u = u.data_ptr()
             p.bias = self.bias.data_ptr() + 4 * co0
@@ -367,9 +442,9 @@ class ConvLayerF32:
                 cid = self.heuristic_config(N * To * Ho * Wo)
                 if os.environ.get("RNB_WINOGRAD", "1") != "0":
                     if self.wino_ok:
-                        cid = WINO_DEFAULT
+                        cid = wino_default(False)
                     elif self.winot_ok and T >= WINOT_MIN_T:
-                        cid = WINOT_DEFAULT
+                        cid = wino_default(True)
             self._config[key] = cid
         return cid
 
@@ -440,7 +515,7 @@ class ConvLayerF32:
     def accepts_input_affine(self, x_shape) -> bool:
         """True when this conv's kernel for ``x_shape`` can apply its input's
         BatchNorm + ReLU on load (``forward_hip(in_affine=...)``)."""
-        return self.config_for(x_shape) in WINOT_TC
+        return self.config_for(x_shape) in WINO_TEMPORAL
 
     def forward_hip(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                     out: Optional[torch.Tensor] = None, config: Optional[int] = None,

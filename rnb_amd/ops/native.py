@@ -143,7 +143,7 @@ class Conv21Params(ctypes.Structure):
 
 
 class WinoParams(ctypes.Structure):
-    """Mirror of ``struct WinoParams`` in csrc/conv_wino_f32.hip."""
+    """Mirror of ``struct WinoParams`` in csrc/wino_common.h."""
     _fields_ = [
         ("x", ctypes.c_void_p), ("u", ctypes.c_void_p), ("bias", ctypes.c_void_p),
         ("res", ctypes.c_void_p), ("y", ctypes.c_void_p),
@@ -300,6 +300,9 @@ class Kernels:
         lib.rnb_winot_f32_launch.argtypes = [ctypes.POINTER(WinoParams), ctypes.c_int,
                                              ctypes.c_void_p]
         lib.rnb_winot_f32_launch.restype = ctypes.c_int
+        for fn in (lib.rnb_wino_x6_launch, lib.rnb_winot_x6_launch):
+            fn.argtypes = [ctypes.POINTER(WinoParams), ctypes.c_int, ctypes.c_void_p]
+            fn.restype = ctypes.c_int
         if lib.rnb_wino_params_size() != ctypes.sizeof(WinoParams):
             raise NativeUnavailable("WinoParams layout mismatch: rebuild")
         if lib.rnb_conv_f32_params_size() != ctypes.sizeof(ConvParams):
@@ -333,6 +336,14 @@ class Kernels:
     def winot_f32(self, params: "WinoParams", variant: int, stream: int) -> None:
         _check(self.lib.rnb_winot_f32_launch(ctypes.byref(params), variant, stream),
                "conv_winot_f32 (variant %d)" % variant)
+
+    def wino_x6(self, params: "WinoParams", variant: int, stream: int) -> None:
+        _check(self.lib.rnb_wino_x6_launch(ctypes.byref(params), variant, stream),
+               "conv_wino_x6 (variant %d)" % variant)
+
+    def winot_x6(self, params: "WinoParams", variant: int, stream: int) -> None:
+        _check(self.lib.rnb_winot_x6_launch(ctypes.byref(params), variant, stream),
+               "conv_winot_x6 (variant %d)" % variant)
 
     def preprocess_f32(self, in_ptr, out_ptr, npix, mean, std, stream):
         m = (ctypes.c_float * 3)(*mean)

@@ -30,10 +30,11 @@ def main():
     dev = torch.device("cuda:0")
     stream = torch.cuda.current_stream().cuda_stream
     names = ["f32 16x16x4 (K=4)", "bf16 16x16x16 (K=16)", "bf16 16x16x32 (K=32)",
-             "bf16 32x32x8 (K=8)"]
-    flops = [16 * 16 * 4 * 2, 16 * 16 * 16 * 2, 16 * 16 * 32 * 2, 32 * 32 * 8 * 2]
+             "bf16 32x32x8 (K=8)", "bf16 16x16x16 2 chains", "bf16 16x16x16 1 chain"]
+    flops = [16 * 16 * 4 * 2, 16 * 16 * 16 * 2, 16 * 16 * 32 * 2, 32 * 32 * 8 * 2,
+             16 * 16 * 16 * 2, 16 * 16 * 16 * 2]
     iters = 2000
-    for kind in range(4):
+    for kind in range(6):
         for wps in (1, 2):
             blocks, threads = 256, 256 * wps
             out = torch.zeros(blocks * threads, device=dev)
@@ -59,7 +60,7 @@ def main():
             At = torch.from_numpy(A).to(dev)
             Bt = torch.from_numpy(B).to(dev)
             row = []
-            for mode in range(3):
+            for mode in range(4):
                 C = torch.zeros(16, 16, device=dev)
                 rc = lib.rnb_split_tile(ctypes.c_void_p(At.data_ptr()), ctypes.c_void_p(Bt.data_ptr()),
                                         ctypes.c_void_p(C.data_ptr()), K, mode, ctypes.c_void_p(stream))
@@ -67,8 +68,10 @@ def main():
                 torch.cuda.synchronize()
                 err = np.abs(C.cpu().numpy().astype(np.float64) - ref) / scale
                 row.append((err.max(), err.mean()))
-            print("K=%4d %-6s  max|err|/sum|ab|: fp32 %.2e  bf16x6 %.2e  bf16x3 %.2e   (mean %.1e %.1e %.1e)"
-                  % (K, dist, row[0][0], row[1][0], row[2][0], row[0][1], row[1][1], row[2][1]))
+            print("K=%4d %-6s  max|err|/sum|ab|: fp32 %.2e  bf16x6 %.2e  bf16x3 %.2e  "
+                  "bf16x6-rne %.2e  (mean %.1e %.1e %.1e %.1e)"
+                  % (K, dist, row[0][0], row[1][0], row[2][0], row[3][0], row[0][1], row[1][1],
+                     row[2][1], row[3][1]))
     return 0
 
 

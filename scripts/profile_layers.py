@@ -23,7 +23,11 @@ def tile_name(cid, f32=False):
     from rnb_amd.ops.native import kernels
     k = kernels()
     if f32:
-        from rnb_amd.ops.conv_f32 import WINO_SPLIT, WINO_TC, WINOT_TC
+        from rnb_amd.ops.conv_f32 import WINO_SPLIT, WINO_TC, WINOT_TC, WINOX_TC, WINOTX_TC
+        if cid in WINOTX_TC:
+            return "x6t_%d" % (16 * WINOTX_TC[cid])
+        if cid in WINOX_TC:
+            return "x6s_%d_%d" % (16 * WINOX_TC[cid], 64 if cid == 1052 else 128)
         if cid in WINOT_TC:
             return "wt4_%d" % (16 * WINOT_TC[cid])
         if cid in WINO_TC:

@@ -305,15 +305,16 @@ WINO_CASES = [  # (cin, cout, (T, H, W)): the stride-1 1x3x3 convs + odd frames
 
 
 def _wino_ids():
-    from rnb_amd.ops.conv_f32 import WINO_TC
-    return sorted(WINO_TC)
+    from rnb_amd.ops.conv_f32 import WINO_SPATIAL
+    return sorted(WINO_SPATIAL)
 
 
 @pytest.mark.parametrize("cid", _wino_ids())
 @pytest.mark.parametrize("case", WINO_CASES, ids=lambda c: "%dx%d_%s" % (c[0], c[1], c[2]))
 def test_winograd_f32_matches_fp64(case, cid):
-    """Fused Winograd F(2x2,3x3) (csrc/conv_wino_f32.hip) vs an fp64 conv:
-    within 1e-5 of the output scale, like the direct fp32 kernel."""
+    """Fused Winograd F(2x2,3x3) (csrc/conv_wino_f32.hip: fp32 MFMA;
+    csrc/conv_wino_x6.hip: fp32 products as six bf16 MFMA products) vs an
+    fp64 conv: within 1e-5 of the output scale, like the direct fp32 kernel."""
     cin, cout, thw = case
     layer = _layer(cin, cout, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=True)
     assert layer.wino_ok
@@ -348,15 +349,16 @@ WINOT_CASES = [  # (cin, cout, (T, H, W)): the stride-1 3x1x1 convs + odd frame 
 
 @pytest.mark.parametrize("case", WINOT_CASES, ids=lambda c: "%dx%d_%s" % (c[0], c[1], c[2]))
 def test_winograd_temporal_f32_matches_fp64(case):
-    """Temporal F(4, 3) (rnb_winot_f32_launch) vs an fp64 conv, every variant."""
-    from rnb_amd.ops.conv_f32 import WINOT_TC
+    """Temporal F(4, 3) (rnb_winot_f32_launch, rnb_winot_x6_launch) vs an
+    fp64 conv, every variant."""
+    from rnb_amd.ops.conv_f32 import WINO_TEMPORAL
     cin, cout, thw = case
     layer = _layer(cin, cout, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=True)
-    assert layer.winot_ok and layer.wino_ids == set(WINOT_TC)
+    assert layer.winot_ok and layer.wino_ids == WINO_TEMPORAL
     x = _input(2, thw, layer.geom.cin_p, cin)
     res = _input(2, thw, layer.geom.cout_p, cout, seed=5)
     ref = _ref64(layer, x, res)
-    for cid in sorted(WINOT_TC):
+    for cid in sorted(WINO_TEMPORAL):
         y = layer.forward_hip(x, res, config=cid)
         torch.cuda.synchronize()
         assert torch.all(y[..., cout:] == 0)
@@ -368,11 +370,11 @@ def test_winograd_temporal_f32_matches_fp64(case):
 def test_winograd_grid_sizes():
     """A one-block launch and a many-wave launch (more blocks than the chip
     holds at once) both equal the fp64 conv, spatial and temporal."""
-    from rnb_amd.ops.conv_f32 import WINO_TC, WINOT_TC
+    from rnb_amd.ops.conv_f32 import WINO_SPATIAL, WINO_TEMPORAL
     sp = _layer(32, 48, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False)
     tp = _layer(48, 32, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=False)
     for n, thw in ((1, (1, 6, 6)), (40, (4, 30, 30))):
-        for layer, ids in ((sp, WINO_TC), (tp, WINOT_TC)):
+        for layer, ids in ((sp, WINO_SPATIAL), (tp, WINO_TEMPORAL)):
             x = _input(n, thw, layer.geom.cin_p, layer.geom.cin)
             ref = _ref64(layer, x)
             for cid in sorted(ids):
@@ -425,13 +427,14 @@ def test_winograd_epilogue_stats_match_fp64_sums(kind):
     LDS reduction for blocks inside one video, per-wave atomics for blocks
     that straddle videos) equal fp64 sums of the conv output, for every
     statistics-capable variant, with zero-clip videos in the offsets."""
-    from rnb_amd.ops.conv_f32 import WINO_TC, WINOT_TC, WINO_BASE
+    from rnb_amd.ops.conv_f32 import WINO_TC, WINO_TEMPORAL, WINO_BASE, WINOX_TC
     if kind == "spatial":
         layer = _layer(64, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False)
-        shape, ids = (7, 4, 20, 28), [c for c in sorted(WINO_TC) if c - WINO_BASE >= 4]
+        shape = (7, 4, 20, 28)
+        ids = [c for c in sorted(WINO_TC) if c - WINO_BASE >= 4] + sorted(WINOX_TC)
     else:
         layer = _layer(64, 80, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=False)
-        shape, ids = (7, 8, 14, 14), sorted(WINOT_TC)
+        shape, ids = (7, 8, 14, 14), sorted(WINO_TEMPORAL)
     offs = [0, 2, 2, 3, 7]                    # video 1 has no clips
     clip_seg = torch.tensor([0, 0, 2, 3, 3, 3, 3], dtype=torch.int32, device=DEV)
     x = _input(shape[0], shape[1:], 64, 64)

@@ -262,3 +262,31 @@ def test_batch_bn_segments_follow_queued_items():
     assert torch.allclose(batcher_out, joint, atol=1e-5, rtol=1e-5)
     assert torch.allclose(gathered_batch, joint, atol=1e-5, rtol=1e-5)
     assert torch.allclose(gathered, per_video, atol=1e-5, rtol=1e-5)
+
+
+def test_x6_weight_pack_is_an_exact_split():
+    """csrc/conv_wino_x6.hip U layout (ops/conv_f32.x6_pack): for every row,
+    channel and transform position, h + m + l of the three bf16 parts equals
+    the fp32-rounded transformed weight exactly, and the 16-B chunks sit where
+    the kernel's x6_chunk reads them (logical chunk c of row r at c ^ s)."""
+    from rnb_amd.ops.conv_f32 import winograd_weights, winograd_t_weights, _X6_S
+    torch.manual_seed(0)
+    for fn, X, k in ((winograd_weights, 16, (1, 3, 3)), (winograd_t_weights, 6, (3, 1, 1))):
+        co, ci, tc = 40, 32, 2
+        w = torch.randn(co, ci, *k, dtype=torch.float64) * 0.05
+        ref = fn(w, co, tc).double()          # fp32 layout [ci/16, nb, X, ct, 16]
+        pk = fn(w, co, tc, x6=True)
+        ct = 16 * tc
+        nb = (co + ct - 1) // ct
+        assert pk.dtype == torch.int16 and tuple(pk.shape) == (ci // 16, nb, X, ct, 8, 8)
+        b = pk.view(torch.bfloat16).double()
+        for r in range(ct):
+            # mirror of x6_chunk: (0x76761010 >> 4 ((r >> 1) & 7)) & 7 on r % 16
+            s = (0x76761010 >> (4 * (((r % 16) >> 1) & 7))) & 7
+            assert s == _X6_S[(r % 16) >> 1]
+            for q in range(4):
+                hm = b[:, :, :, r, (2 * q) ^ s]          # (h | m) of quad q
+                hl = b[:, :, :, r, (2 * q + 1) ^ s]      # (h | l)
+                assert torch.equal(hm[..., :4], hl[..., :4])
+                got = hm[..., :4] + hm[..., 4:] + hl[..., 4:]
+                assert torch.equal(got, ref[:, :, :, r, 4 * q:4 * q + 4]), (fn.__name__, r, q)
