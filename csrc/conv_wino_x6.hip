@@ -37,12 +37,22 @@
 
 // 1: software-pipelined GEMM steps (split / fragment reads one step ahead,
 // interleaved with the MFMAs); 0: in-order steps; 2: pipelined where the
-// registers allow (TC 1: the TC 2 spatial kernel spills at 256 VGPRs)
+// registers allow (the TC 2 x 8-wave spatial kernel spills at 256 VGPRs;
+// with 4 waves a wave has 512)
 #ifndef X6_PIPE
 #define X6_PIPE 2
 #endif
-// the ~30 VALU ops of a step's split spread over its 3 TC MFMAs
-#define X6_VALU_PER_MFMA(TC) ((30 + 3 * (TC) - 1) / (3 * (TC)))
+// the ~24 VALU ops of a step (split + its share of the transform) spread
+// over its 3 TC MFMAs
+#define X6_VALU_PER_MFMA(TC) ((24 + 3 * (TC) - 1) / (3 * (TC)))
+// bottleneck experiments (scripts/x6_exp.py; results are garbage by design):
+// 1 no split VALU, 2 no MFMA, 3 no patch refill loads, 4 no U DMA after the
+// first chunk, 5 no input transform, 6 no epilogue
+#ifndef X6_EXP
+#define X6_EXP 0
+#endif
+// buffer offset past every tensor (x_bytes <= 0x7FFFFF00): padding loads
+#define X6_OOB 0x80000000u
 
 typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 wbf16x2 __attribute__((ext_vector_type(2)));
@@ -57,35 +67,54 @@ typedef unsigned int wu32x4 __attribute__((ext_vector_type(4)));
 //   (Ah | Am) x (Bh ; Bh) = Ah Bh + Am Bh
 //   (Ah | Al) x (Bm ; Bh) = Ah Bm + Al Bh
 //   (Ah | Am) x (Bl ; Bm) = Ah Bl + Am Bm
-struct X6B {                  // B fragments of one GEMM step
-  wu32x4 hh, mh, lm;
+typedef unsigned int wu32x8 __attribute__((ext_vector_type(8)));
+
+// B fragments of one GEMM step as one 8-register tuple
+//   R = (L01 L23 M01 M23 H01 H23 H01 H23)
+// so the three MFMA B operands are the overlapping quads R[0:4] = (Bl ; Bm),
+// R[2:6] = (Bm ; Bh) and R[4:8] = (Bh ; Bh): only H is stored twice.
+struct X6B {
+  wu32x8 r;
 };
 struct X6A {                  // A fragments of one GEMM step and channel group
   wu32x4 hm, hl;
 };
 
-static __device__ __forceinline__ uint32_t x6_pk(float a, float b) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((wf32x2){a, b}, wbf16x2));
+// upper halves of two fp32 bit patterns -> one bf16 pair (lo = a, hi = b)
+static __device__ __forceinline__ uint32_t x6_hi2(uint32_t a, uint32_t b) {
+  return __builtin_amdgcn_perm(b, a, 0x07060302u);
 }
 
-// exact 3-way split of 4 fp32 values (channels j = 0..3 of a B fragment)
+// exact 3-way split of 4 fp32 values (channels j = 0..3 of a B fragment) by
+// truncation: h = top 8 significant bits of x, m = top 8 of r = x - h (exact),
+// l = r - m (exact, <= 8 significant bits, so its truncation is exact too).
+// Per value pair: 4 v_and, 2 v_pk_add_f32, 3 v_perm (vs ~15 with RNE parts
+// rebuilt through shifts); the dropped products are still <= ~2^-22 |ab|
+// (profiles/r3_mfma_split.txt: as accurate as fp32 MFMA)
 static __device__ __forceinline__ X6B x6_split(const wf32x4& v) {
-  uint32_t h[2], m[2], l[2];
+  if constexpr (X6_EXP == 1) {
+    const uint32_t a = __float_as_uint(v[0]), b = __float_as_uint(v[1]);
+    const uint32_t c = __float_as_uint(v[2]), d = __float_as_uint(v[3]);
+    X6B f;
+    f.r = (wu32x8){a, b, c, d, a, b, c, d};
+    return f;
+  }
+  uint32_t H[2], M[2], L[2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    const float a = v[2 * k], b = v[2 * k + 1];
-    const uint32_t hh = x6_pk(a, b);
-    const float ra = a - __uint_as_float(hh << 16), rb = b - __uint_as_float(hh & 0xFFFF0000u);
-    const uint32_t mm = x6_pk(ra, rb);
-    const float la = ra - __uint_as_float(mm << 16), lb = rb - __uint_as_float(mm & 0xFFFF0000u);
-    h[k] = hh;
-    m[k] = mm;
-    l[k] = x6_pk(la, lb);
+    const wf32x2 x = (wf32x2){v[2 * k], v[2 * k + 1]};
+    const uint32_t xa = __float_as_uint(x[0]), xb = __float_as_uint(x[1]);
+    const wf32x2 h = (wf32x2){__uint_as_float(xa & 0xFFFF0000u), __uint_as_float(xb & 0xFFFF0000u)};
+    const wf32x2 r = x - h;
+    const uint32_t ra = __float_as_uint(r[0]), rb = __float_as_uint(r[1]);
+    const wf32x2 m = (wf32x2){__uint_as_float(ra & 0xFFFF0000u), __uint_as_float(rb & 0xFFFF0000u)};
+    const wf32x2 l = r - m;
+    H[k] = x6_hi2(xa, xb);
+    M[k] = x6_hi2(ra, rb);
+    L[k] = x6_hi2(__float_as_uint(l[0]), __float_as_uint(l[1]));
   }
   X6B f;
-  f.hh = (wu32x4){h[0], h[1], h[0], h[1]};
-  f.mh = (wu32x4){m[0], m[1], h[0], h[1]};
-  f.lm = (wu32x4){l[0], l[1], m[0], m[1]};
+  f.r = (wu32x8){L[0], L[1], M[0], M[1], H[0], H[1], H[0], H[1]};
   return f;
 }
 
@@ -99,12 +128,21 @@ static __device__ __forceinline__ wf32x4 x6_mma(const wu32x4& a, const wu32x4& b
 template <int TC>
 static __device__ __forceinline__ void x6_step(wf32x4 (&acc)[TC], const X6A (&a)[TC],
                                                const X6B& b) {
+  if constexpr (X6_EXP == 2) {
 #pragma unroll
-  for (int tc = 0; tc < TC; ++tc) acc[tc] = x6_mma(a[tc].hm, b.lm, acc[tc]);
+    for (int tc = 0; tc < TC; ++tc)
+      acc[tc][0] += __uint_as_float(a[tc].hm[0] ^ a[tc].hl[1] ^ b.r[0] ^ b.r[3] ^ b.r[5]);
+    return;
+  }
+  const wu32x4 lm = __builtin_shufflevector(b.r, b.r, 0, 1, 2, 3);
+  const wu32x4 mh = __builtin_shufflevector(b.r, b.r, 2, 3, 4, 5);
+  const wu32x4 hh = __builtin_shufflevector(b.r, b.r, 4, 5, 6, 7);
 #pragma unroll
-  for (int tc = 0; tc < TC; ++tc) acc[tc] = x6_mma(a[tc].hl, b.mh, acc[tc]);
+  for (int tc = 0; tc < TC; ++tc) acc[tc] = x6_mma(a[tc].hm, lm, acc[tc]);
 #pragma unroll
-  for (int tc = 0; tc < TC; ++tc) acc[tc] = x6_mma(a[tc].hm, b.hh, acc[tc]);
+  for (int tc = 0; tc < TC; ++tc) acc[tc] = x6_mma(a[tc].hl, mh, acc[tc]);
+#pragma unroll
+  for (int tc = 0; tc < TC; ++tc) acc[tc] = x6_mma(a[tc].hm, hh, acc[tc]);
 }
 
 // 16-B chunk permutation of a 128-B U row: logical chunk c = 2 q + half
@@ -185,13 +223,20 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
       __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ur =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, p.u_bytes, 0x00020000);
+  // per patch row: the lane's byte offset, or X6_OOB for a padding row (any
+  // small uniform delta added keeps it past the buffer: out-of-range buffer
+  // loads return 0); a padding column selects X6_OOB per load
+  uint32_t rowoff[4];
+#pragma unroll
+  for (int dy = 0; dy < 4; ++dy)
+    rowoff[dy] = ((rmask >> dy) & 1) ? (uint32_t)(pix0 * p.Cin * 4 + q * 16 + dy * row_bytes)
+                                     : X6_OOB;
+  const uint32_t cin4 = (uint32_t)p.Cin * 4;
 
   auto load_one = [&](int chunk, int e) -> wf32x4 {
     const int dy = e >> 2, dx = e & 3;
-    const bool ok = ((rmask >> dy) & (cmask >> dx) & 1) != 0;
-    const uint32_t off =
-        ok ? (uint32_t)(pix0 * p.Cin * 4 + chunk * 64 + q * 16 + dy * row_bytes + dx * p.Cin * 4)
-           : WINO_INVALID;
+    const uint32_t off = ((cmask >> dx) & 1) ? rowoff[dy] + (uint32_t)(dx * cin4 + chunk * 64)
+                                             : X6_OOB;
     return __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
   };
   auto issue_u = [&](int chunk, int buf) {
@@ -207,37 +252,70 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
 
   const int nchunks = p.Cin / 16;
   const int frow = lane & 15;
-  auto transform = [&](wf32x4 (&v)[16]) {
+  // Split input transform (as conv_wino_f32's PF 3 variants): the GEMM steps
+  // run in V-row order 0, 2, 1, 3 and the refill loads of the next chunk go
+  // out in that order, so a chunk starts on V row 0 (patch rows 0 and 2:
+  // loaded first) while patch rows 1 / 3 are still in flight.
+  // row_t: e_r = d_r B on patch row r (channel pairs, v_pk_add_f32)
+  auto row_t = [&](wf32x4 (&v)[16], int r) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const wf32x4 a0 = v[0 * 4 + j], a1 = v[1 * 4 + j], a2 = v[2 * 4 + j], a3 = v[3 * 4 + j];
-      v[0 * 4 + j] = a0 - a2;
-      v[1 * 4 + j] = a1 + a2;
-      v[2 * 4 + j] = a2 - a1;
-      v[3 * 4 + j] = a1 - a3;
-    }
+    for (int hf = 0; hf < 2; ++hf) {
+      const wf32x2 b0 = (wf32x2){v[r * 4 + 0][2 * hf], v[r * 4 + 0][2 * hf + 1]};
+      const wf32x2 b1 = (wf32x2){v[r * 4 + 1][2 * hf], v[r * 4 + 1][2 * hf + 1]};
+      const wf32x2 b2 = (wf32x2){v[r * 4 + 2][2 * hf], v[r * 4 + 2][2 * hf + 1]};
+      const wf32x2 b3 = (wf32x2){v[r * 4 + 3][2 * hf], v[r * 4 + 3][2 * hf + 1]};
+      const wf32x2 o[4] = {b0 - b2, b1 + b2, b2 - b1, b1 - b3};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const wf32x4 b0 = v[i * 4 + 0], b1 = v[i * 4 + 1], b2 = v[i * 4 + 2], b3 = v[i * 4 + 3];
-      v[i * 4 + 0] = b0 - b2;
-      v[i * 4 + 1] = b1 + b2;
-      v[i * 4 + 2] = b2 - b1;
-      v[i * 4 + 3] = b1 - b3;
+      for (int j = 0; j < 4; ++j) {
+        v[r * 4 + j][2 * hf] = o[j][0];
+        v[r * 4 + j][2 * hf + 1] = o[j][1];
+      }
     }
   };
-  // 16 GEMM steps of one chunk, software-pipelined one step ahead: step x+1's
-  // B fragment is split (VALU) and its A fragments read (LDS) while step x's
-  // 6 TC MFMAs run; V[x+1]'s registers are refilled with patch element x+1
-  // of chunk `next` right after the split (prefetch without a second set)
-  auto gemm = [&](const char* ub, wf32x4 (&v)[16], int next, auto refill) {
-    if constexpr (X6_PIPE == 0 || (X6_PIPE == 2 && TC > 1)) {
-      // in-order steps: split, refill, fragment reads, MFMAs (the other
-      // wave of the SIMD covers the latencies)
+  auto comb = [&](wf32x4& dst, const wf32x4& a, const wf32x4& b, bool add) {
 #pragma unroll
-      for (int x = 0; x < 16; ++x) {
+    for (int hf = 0; hf < 2; ++hf) {
+      const wf32x2 x = (wf32x2){a[2 * hf], a[2 * hf + 1]};
+      const wf32x2 y = (wf32x2){b[2 * hf], b[2 * hf + 1]};
+      const wf32x2 z = add ? x + y : x - y;
+      dst[2 * hf] = z[0];
+      dst[2 * hf + 1] = z[1];
+    }
+  };
+  auto transform_a = [&](wf32x4 (&v)[16]) {          // V row 0 (e2 kept in row 2)
+    if constexpr (X6_EXP == 5) return;
+    row_t(v, 0);
+    row_t(v, 2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) comb(v[j], v[j], v[8 + j], false);
+  };
+  auto transform_b = [&](wf32x4 (&v)[16]) {          // V rows 1-3, in place
+    if constexpr (X6_EXP == 5) return;
+    row_t(v, 1);
+    row_t(v, 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      comb(v[12 + j], v[4 + j], v[12 + j], false);   // V3 = e1 - e3
+      const wf32x4 e1 = v[4 + j];
+      comb(v[4 + j], e1, v[8 + j], true);            // V1 = e1 + e2
+      comb(v[8 + j], v[8 + j], e1, false);           // V2 = e2 - e1
+    }
+  };
+  constexpr int perm[16] = {0, 1, 2, 3, 8, 9, 10, 11, 4, 5, 6, 7, 12, 13, 14, 15};
+  // 16 GEMM steps of one chunk (after transform_a). In order: split, refill,
+  // fragment reads, MFMAs per step (the other wave of the SIMD covers the
+  // latencies). Pipelined: step k+1's B fragment is split (VALU) and its A
+  // fragments read (LDS) while step k's 3 TC MFMAs run. V[x]'s registers are
+  // refilled with patch element x of chunk `next` right after its split.
+  auto gemm = [&](const char* ub, wf32x4 (&v)[16], int next, auto refill) {
+    if constexpr (X6_PIPE == 0 || (X6_PIPE == 2 && TC > 1 && WAVES == 8)) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int x = perm[k];
+        if (k == 4) transform_b(v);
         X6A af[TC];
         const X6B bf = x6_split(v[x]);
-        if constexpr (decltype(refill)::value) v[x] = load_one(next, x);
+        if constexpr (decltype(refill)::value && X6_EXP != 3) v[x] = load_one(next, x);
         x6_read_a<TC>(af, ub, x, frow, q);
         x6_step<TC>(acc[x], af, bf);
       }
@@ -245,18 +323,21 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
       X6A af[2][TC];
       X6B bf[2];
       bf[0] = x6_split(v[0]);
-      if constexpr (decltype(refill)::value) v[0] = load_one(next, 0);
+      if constexpr (decltype(refill)::value && X6_EXP != 3) v[0] = load_one(next, 0);
       x6_read_a<TC>(af[0], ub, 0, frow, q);
 #pragma unroll
-      for (int x = 0; x < 16; ++x) {
-        if (x + 1 < 16) {
-          bf[(x + 1) & 1] = x6_split(v[x + 1]);
-          if constexpr (decltype(refill)::value) v[x + 1] = load_one(next, x + 1);
-          x6_read_a<TC>(af[(x + 1) & 1], ub, x + 1, frow, q);
+      for (int k = 0; k < 16; ++k) {
+        const int x = perm[k];
+        if (k + 1 < 16) {
+          const int xn = perm[k + 1];
+          if (k + 1 == 4) transform_b(v);
+          bf[(k + 1) & 1] = x6_split(v[xn]);
+          if constexpr (decltype(refill)::value && X6_EXP != 3) v[xn] = load_one(next, xn);
+          x6_read_a<TC>(af[(k + 1) & 1], ub, xn, frow, q);
         }
-        x6_step<TC>(acc[x], af[x & 1], bf[x & 1]);
-        if (x + 1 < 16) {
-          // interleave: per MFMA one split VALU pair; the LDS reads early
+        x6_step<TC>(acc[x], af[k & 1], bf[k & 1]);
+        if (k + 1 < 16) {
+          // interleave: per MFMA a share of the split VALU; the LDS reads early
 #pragma unroll
           for (int i = 0; i < 3 * TC; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);          // MFMA
@@ -279,18 +360,27 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
   __syncthreads();
   for (int c = 0; c + 1 < nchunks; ++c) {
     const int cur = c & 1;
-    issue_u(c + 1, cur ^ 1);
+    if (X6_EXP != 4) issue_u(c + 1, cur ^ 1);
     // keep the U DMA ahead of the patch loads in issue order (vmcnt below)
     asm volatile("" ::: "memory");
-    transform(d);
+    transform_a(d);
     gemm(lds + cur * U_BYTES, d, c + 1, std::true_type{});
     // U of chunk c+1 landed; the 16 younger patch loads may stay in flight
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     __syncthreads();
   }
-  transform(d);
+  transform_a(d);
   gemm(lds + ((nchunks - 1) & 1) * U_BYTES, d, -1, std::false_type{});
   __syncthreads();                 // the epilogue's statistics reuse the U buffers
+  if (X6_EXP == 6) {              // every accumulator stays live, no transform / stores
+    wf32x4 t = acc[0][0];
+#pragma unroll
+    for (int x = 0; x < 16; ++x)
+#pragma unroll
+      for (int c = 0; c < TC; ++c) t += acc[x][c];
+    if (t[0] + t[1] + t[2] + t[3] == 1.2345f && tvalid) p.y[0] = t[0];
+    return;
+  }
   w_spatial_epilogue<TC, ST, WAVES>(p, lds, acc, tb, wave, tl, q, cb, lane, tvalid, f, ty, tx);
 }
 
@@ -369,13 +459,13 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : 2) void conv_winot_x6_
     X6A af[2][TC];
     X6B bf[2];
     bf[0] = x6_split(v[0]);
-    if constexpr (decltype(refill)::value) v[0] = load_one(next, 0);
+    if constexpr (decltype(refill)::value && X6_EXP != 3) v[0] = load_one(next, 0);
     x6_read_a<TC>(af[0], ub, 0, frow, q);
 #pragma unroll
     for (int x = 0; x < 6; ++x) {
       if (x + 1 < 6) {
         bf[(x + 1) & 1] = x6_split(v[x + 1]);
-        if constexpr (decltype(refill)::value) v[x + 1] = load_one(next, x + 1);
+        if constexpr (decltype(refill)::value && X6_EXP != 3) v[x + 1] = load_one(next, x + 1);
         x6_read_a<TC>(af[(x + 1) & 1], ub, x + 1, frow, q);
       }
       x6_step<TC>(acc[x], af[x & 1], bf[x & 1]);
@@ -417,10 +507,10 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : 2) void conv_winot_x6_
   __syncthreads();
   for (int c = 0; c + 1 < nchunks; ++c) {
     const int cur = c & 1;
-    issue_u(c + 1, cur ^ 1);
+    if (X6_EXP != 4) issue_u(c + 1, cur ^ 1);
     asm volatile("" ::: "memory");
     if (aff) affine(d, sc, sh);
-    transform(d);
+    if (X6_EXP != 5) transform(d);
     gemm(lds + cur * U_BYTES, d, c + 1, std::true_type{});
     if (aff) {                                            // next chunk's scale / shift
       sc = *(const wf32x4*)(ssb + (c + 1) * 16);
@@ -430,7 +520,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : 2) void conv_winot_x6_
     __syncthreads();
   }
   if (aff) affine(d, sc, sh);
-  transform(d);
+  if (X6_EXP != 5) transform(d);
   gemm(lds + ((nchunks - 1) & 1) * U_BYTES, d, -1, std::false_type{});
   __syncthreads();
   w_temporal_epilogue<TC, ST, WAVES>(p, lds, acc, tb, wave, tl, q, cb, lane, tvalid, n, tt, hw);
@@ -470,13 +560,14 @@ static void x6_launch(K kernel, const WinoParams& p, int threads, hipStream_t st
 extern "C" {
 
 // Spatial F(2x2, 3x3) on bf16 MFMA (x6). variant 0 = TC 2 x 8 waves (128
-// tiles x 32 channels per block), 1 = TC 1 x 8 waves, 2 = TC 1 x 4 waves.
+// tiles x 32 channels per block), 1 = TC 1 x 8 waves, 2 = TC 1 x 4 waves,
+// 3 = TC 2 x 4 waves (one wave per SIMD, software-pipelined steps).
 // U layout [Cin/16][n_cblocks][16][16 TC][8 chunks of 8 bf16] (x6_chunk).
 // Returns 0, a negative contract code, or the hipError_t.
 int rnb_wino_x6_launch(const WinoParams* pp, int variant, hipStream_t stream) {
   WinoParams p = *pp;
-  if (variant < 0 || variant > 2) return -1;
-  const int TC = variant == 0 ? 2 : 1, WAVES = variant == 2 ? 4 : 8;
+  if (variant < 0 || variant > 3) return -1;
+  const int TC = (variant == 0 || variant == 3) ? 2 : 1, WAVES = variant >= 2 ? 4 : 8;
   if (p.F <= 0 || p.H <= 0 || p.W <= 0) return 0;
   const int rc = x6_prepare(p, 2, 2, 16 * TC, 16 * WAVES, 16);
   if (rc) return rc;
@@ -490,9 +581,13 @@ int rnb_wino_x6_launch(const WinoParams* pp, int variant, hipStream_t stream) {
       if (st) x6_launch(conv_wino_x6_kernel<1, 8, true>, p, 512, stream);
       else x6_launch(conv_wino_x6_kernel<1, 8>, p, 512, stream);
       break;
-    default:
+    case 2:
       if (st) x6_launch(conv_wino_x6_kernel<1, 4, true>, p, 256, stream);
       else x6_launch(conv_wino_x6_kernel<1, 4>, p, 256, stream);
+      break;
+    default:
+      if (st) x6_launch(conv_wino_x6_kernel<2, 4, true>, p, 256, stream);
+      else x6_launch(conv_wino_x6_kernel<2, 4>, p, 256, stream);
       break;
   }
   return (int)hipGetLastError();

@@ -319,6 +319,7 @@ def run(args) -> dict:
         print("[ERROR] job aborted: %s" % (dog.failed or "barrier timeout",), flush=True)
 
     summaries = TimeCardSummary()
+    ring_stats = {}
     n_final = sum(len(g.gpus) for g in spec.steps[-1].groups)
     got = 0
     deadline = time.time() + (60.0 if not broken else 5.0)
@@ -332,6 +333,19 @@ def run(args) -> dict:
         if msg[0] == "summary":
             summaries.merge_from(msg[4])
             got += 1
+        elif msg[0] == "ring_stats":
+            for k, v in msg[4].items():
+                ring_stats[k] = ring_stats.get(k, 0) + v
+    # ring counters are sent before fin_bar; pick up any still in the pipe
+    drain_until = time.time() + 0.3
+    while time.time() < drain_until:
+        try:
+            msg = result_queue.get(timeout=0.05)
+        except Exception:
+            continue
+        if msg[0] == "ring_stats":
+            for k, v in msg[4].items():
+                ring_stats[k] = ring_stats.get(k, 0) + v
     for _, p in procs:
         p.join(RESERVED_CHILD_EXIT_GRACE_S if not broken else 5.0)
         if p.exitcode is None:
@@ -343,7 +357,10 @@ def run(args) -> dict:
               "termination_flag": TerminationFlag.NAMES.get(flag.value, flag.value),
               "videos_target": args.videos, "videos_done": max(0, counter.value - warm),
               "warmup_videos": warm,
-              "mean_interval_ms": args.mean_interval_ms, "ok": False}
+              "mean_interval_ms": args.mean_interval_ms, "ok": False,
+              # HIP-IPC stream waits ROCm refused on already-completed events
+              # (parallel/transport.py host fallback), summed over runners
+              "stale_event_waits": int(ring_stats.get("stale_event_waits", 0))}
     if time_start is not None and time_end is not None:
         if warm and phase_start[0] > 0:
             time_start = phase_start[0]          # timed window starts after warm-up

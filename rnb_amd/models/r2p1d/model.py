@@ -53,6 +53,11 @@ from .sampler import R2P1DSampler
 
 DEFAULT_MAX_CLIPS = 15
 CLIP_SHAPE = (8, 112, 112)
+# output sampling for numerics checks of a served run (bench.py): the loader
+# tags every CHECK_EVERY-th video with its decode source, and a final-step
+# runner with RNB_CHECK_DIR set writes those videos' logits there
+CHECK_EVERY = int(os.environ.get("RNB_CHECK_EVERY", "61"))
+CHECK_MAX = int(os.environ.get("RNB_CHECK_MAX", "8"))
 DEFAULT_DTYPE = "fp32"       # the reference computes in fp32 (model.py:149,225)
 
 
@@ -177,6 +182,8 @@ class R2P1DRunner(RunnerModel):
             torch.cuda.current_stream(device).synchronize()
         self._gather_ptr = None
         self._gather_buf = None
+        self._check_dir = os.environ.get("RNB_CHECK_DIR") or None
+        self._checked = 0
 
     # consumer-side batching (runner.py): up to max_batch_videos queued
     # videos per call, their rows pulled into the graph's static input
@@ -229,10 +236,40 @@ class R2P1DRunner(RunnerModel):
             return None
         offs = [0]
         for r in rows:
-            offs.append(offs[-1] + int(r))
-        return offs if offs[-1] == n else None
+            if int(r) > 0:             # empty segments (0-row items) add no BN segment
+                offs.append(offs[-1] + int(r))
+        if offs[-1] != n or len(offs) < 3:
+            return None
+        return offs
+
+    def _keep_samples(self, y: torch.Tensor, time_card) -> None:
+        """RNB_CHECK_DIR: write the logits of tagged videos (loader
+        ``clip_src``) of this call, at most CHECK_MAX per runner, for an
+        offline recomputation (bench.py ``numerics``)."""
+        cards = time_card.time_cards if isinstance(time_card, TimeCardList) else [time_card]
+        rows = (list(time_card.item_rows) if isinstance(time_card, TimeCardList)
+                and getattr(time_card, "item_rows", None) else [y.shape[0]])
+        if len(rows) != len(cards):
+            return                     # Batcher items: several videos per segment
+        from ...numerics import write_sample
+        off = 0
+        for tc, n in zip(cards, rows):
+            src = tc.extra.get("clip_src")
+            if (src is not None and self._checked < CHECK_MAX and n == len(src[1]) and n
+                    and tc.sub_id is None):
+                self._checked += 1
+                write_sample(self._check_dir, tc.id, "runner", src[0], src[1],
+                             y[off:off + n].float().cpu().numpy(), self.bn_mode,
+                             str(self.dtype))
+            off += n
 
     def __call__(self, tensors, non_tensors, time_card):
+        out = self._call(tensors, non_tensors, time_card)
+        if self._check_dir and self.end_index == 5 and time_card is not None:
+            self._keep_samples(out[0][0], time_card)
+        return out
+
+    def _call(self, tensors, non_tensors, time_card):
         x = tensors[0]
         offs = (self._clip_offsets(time_card, x.shape[0]) if self.bn_mode == "batch"
                 else None)
@@ -287,23 +324,26 @@ class R2P1DLoader(RunnerModel):
         if device.type == "cuda":
             torch.cuda.current_stream(device).synchronize()
 
-    def load(self, path: str, out: Optional[torch.Tensor] = None):
+    def load(self, path: str, out: Optional[torch.Tensor] = None, time_card=None):
         vid, length = self.decoder.probe(path)
         starts = self.sampler.sample(length) or []
         if len(starts) > self.max_clips:
             starts = starts[:self.max_clips]
+        if time_card is not None and time_card.id % CHECK_EVERY == 0:
+            # what a numerics check needs to decode the same clips again
+            time_card.extra["clip_src"] = (int(vid), [int(s) for s in starts])
         return self.decoder.decode(vid, starts, out=None if out is None else
                                    out[:len(starts)])
 
     def __call__(self, tensors, non_tensors, time_card):
-        frames = self.load(non_tensors)
+        frames = self.load(non_tensors, time_card=time_card)
         time_card.num_clips = int(frames.shape[0])
         return (frames,), None, time_card
 
     def call_into(self, tensors, non_tensors, time_card, out):
         """Decode straight into the output slot ``out[0]`` (runner.py direct_out:
         no staging tensor, no slot copy)."""
-        frames = self.load(non_tensors, out=out[0])
+        frames = self.load(non_tensors, out=out[0], time_card=time_card)
         time_card.num_clips = int(frames.shape[0])
         return (frames,), None, time_card
 
@@ -386,6 +426,8 @@ class R2P1DAggregator(RunnerModel):
         super().__init__(device)
         self.aggregate = int(aggregate)
         self.results = {}
+        self._check_dir = os.environ.get("RNB_CHECK_DIR") or None
+        self._checked = 0
 
     def _sum(self, tensor) -> np.ndarray:
         return tensor.detach().float().cpu().numpy().sum(axis=0)
@@ -421,6 +463,12 @@ class R2P1DAggregator(RunnerModel):
                 self.results[tc.id] = (total, got)
                 continue
             del self.results[tc.id]
+            src = got[0].extra.get("clip_src")
+            if src is not None and self._check_dir and self._checked < CHECK_MAX:
+                from ...numerics import write_sample
+                self._checked += 1
+                write_sample(self._check_dir, tc.id, "aggregate", src[0], src[1], total,
+                             segments=self.aggregate)
             done_cards.append(TimeCard.merge(got))
             outs.append(int(total.argmax()))
         if not done_cards:

@@ -74,10 +74,11 @@ WINOT_DEFAULT = WINOT_BASE + 1
 # (csrc/conv_wino_x6.hip: every fp32 operand split exactly into three bf16
 # parts, six bf16 products per fp32 product, fp32 accumulation; within fp32
 # rounding of the fp32-MFMA kernels). Spatial: 1050 = 32 channels x 128
-# tiles per block, 1051 / 1052 = 16 channels x 128 / 64 tiles; temporal:
+# tiles per block, 1051 / 1052 = 16 channels x 128 / 64 tiles, 1053 = 32
+# channels x 64 tiles (one wave per SIMD, pipelined); temporal:
 # 1060 = 64 channels x 128 tiles, 1061 = 32 x 64.
 WINOX_BASE = 1050
-WINOX_TC = {WINOX_BASE + 0: 2, WINOX_BASE + 1: 1, WINOX_BASE + 2: 1}
+WINOX_TC = {WINOX_BASE + 0: 2, WINOX_BASE + 1: 1, WINOX_BASE + 2: 1, WINOX_BASE + 3: 2}
 WINOTX_BASE = 1060
 WINOTX_TC = {WINOTX_BASE + 0: 4, WINOTX_BASE + 1: 2}
 WINO_X6 = set(WINOX_TC) | set(WINOTX_TC)
@@ -94,9 +95,13 @@ def x6_enabled() -> bool:
 
 
 def wino_default(temporal: bool) -> int:
-    if x6_enabled():
-        return WINOTX_BASE if temporal else WINOX_BASE
-    return WINOT_DEFAULT if temporal else WINO_DEFAULT
+    """Untuned Winograd config: the x6 temporal kernel (0.83 vs 0.97 ms on
+    conv2's temporal conv at 128 clips) and the fp32-MFMA spatial kernel
+    (x6 wins only at conv4/5 sizes: profiles/r3_x6_v1_layers.txt); the
+    autotuner picks per layer and batch."""
+    if temporal:
+        return WINOTX_BASE if x6_enabled() else WINOT_DEFAULT
+    return WINO_DEFAULT
 
 # Winograd F(2x2, 3x3) transforms: U = G g G^T (host, fp64), V = B^T d B and
 # Y = A^T M A in the kernel

@@ -14,6 +14,13 @@ bridges that with a *claim handshake* (SURVEY.md §7.4 item 3):
    the slot's valid rows to the claimer (several claims per batched group),
    waits for completion with a timeout, then frees the slot.
 
+A consumer that gathers several items into one model call posts all their
+claims first and launches all their ``irecv``s as ONE ``batch_isend_irecv``
+group (``flush_recvs``, called by the runner once per call); on RCCL the
+receives are ordered on the consumer's stream (no host synchronisation),
+and the process group's timeout is the watchdog. The producer may decode
+straight into a send slot (``slot_views`` / ``commit``, runner direct_out).
+
 Per (src, dst) pair the claims are served in the order the consumer posted
 them, so sends and receives match. All participating runners form one
 ``torch.distributed`` world (backend ``nccl`` = RCCL on ROCm; ``gloo`` for the
@@ -26,6 +33,7 @@ from __future__ import annotations
 import os
 import queue
 import threading
+import time
 from typing import Optional
 
 import torch
@@ -51,8 +59,9 @@ def init_dist(info: Optional[DistInfo], device: torch.device) -> None:
     kwargs = {}
     if info.backend == "nccl":
         kwargs["device_id"] = device
+    # the group timeout is the watchdog of stream-ordered RCCL receives
     dist.init_process_group(info.backend, store=store, rank=info.rank,
-                            world_size=info.world_size, **kwargs)
+                            world_size=info.world_size, timeout=_timeout(), **kwargs)
     # one collective first: batched point-to-point groups may then involve
     # only the two peers of an edge (torch.distributed.batch_isend_irecv)
     dist.barrier()
@@ -82,6 +91,40 @@ MAX_CLAIMS_PER_BATCH = 16
 def _timeout():
     from datetime import timedelta
     return timedelta(seconds=float(os.environ.get(RCCL_TIMEOUT_ENV, "120")))
+
+
+# receives posted by RcclRing.read_into in this process, launched together by
+# flush_recvs (one batch_isend_irecv group per model call)
+_pending_recvs = []
+
+
+def flush_recvs() -> int:
+    """Launch every receive ``read_into`` posted since the last flush as one
+    group. RCCL: the current stream waits for them (ordered on the GPU, the
+    host does not block; a stuck sender trips the group timeout). gloo (CPU):
+    wait on the host, raising TimeoutError after RNB_RCCL_TIMEOUT_S. Returns
+    the number of receives."""
+    if not _pending_recvs:
+        return 0
+    import torch.distributed as dist
+    ops = list(_pending_recvs)
+    _pending_recvs.clear()
+    works = dist.batch_isend_irecv(ops)
+    if _state["backend"] == "nccl":
+        for w in works:
+            w.wait()
+        return len(ops)
+    t0 = time.time()
+    for w in works:
+        # gloo completes a receive inside wait(); the group timeout (set at
+        # init to RNB_RCCL_TIMEOUT_S) bounds it
+        if not w.wait(_timeout()):
+            raise TimeoutError("RCCL receive not served within %s s (%s)"
+                               % (_timeout().total_seconds(), RCCL_TIMEOUT_ENV))
+    if time.time() - t0 > _timeout().total_seconds():
+        raise TimeoutError("RCCL receives took %.0f s (> %s)" % (time.time() - t0,
+                                                                 RCCL_TIMEOUT_ENV))
+    return len(ops)
 
 
 class RcclRing(RingBase):
@@ -182,6 +225,31 @@ class RcclRing(RingBase):
         if self._error is not None:
             raise RuntimeError("RCCL sender of ring %s failed: %s" % (self.name, self._error))
 
+    @property
+    def gpu_ordered(self) -> bool:
+        """Slot data is ordered for the sender by a "written" event, so the
+        producer need not synchronise its stream per item."""
+        return self._written is not None
+
+    def slot_views(self, idx: int):
+        """The send slot's tensors (full capacity): a producer model writes its
+        output here directly (runner direct_out), then ``commit``s."""
+        return self._slots[idx]
+
+    def begin_write(self, idx: int, stream=None) -> None:
+        # a slot is free only after its send completed (sender thread)
+        self.raise_if_failed()
+
+    def commit(self, idx: int, rows, stream=None) -> int:
+        """Publish slot ``idx`` holding ``rows`` valid rows per tensor, its
+        data enqueued on ``stream``."""
+        self.raise_if_failed()
+        if self._written is not None:
+            # GPU-ordered: the sender's stream waits on this event
+            self._written[idx].record(stream or torch.cuda.current_stream(self.device))
+        self._set_valid(idx, rows)
+        return self._publish(idx)
+
     def write(self, idx, tensors):
         self.raise_if_failed()
         rows = []
@@ -193,11 +261,7 @@ class RcclRing(RingBase):
             if b:
                 dst[:b].copy_(src)
             rows.append(b)
-        if self._written is not None:
-            # GPU-ordered: the sender's stream waits on this event
-            self._written[idx].record(torch.cuda.current_stream(self.device))
-        self._set_valid(idx, rows)
-        return self._publish(idx)
+        return self.commit(idx, rows)
 
     def descriptor(self):
         return self.producer_rank
@@ -210,20 +274,32 @@ class RcclRing(RingBase):
             self._thread = None
 
     # ---- consumer ----
+    deferred_reads = True     # the runner calls flush_recvs() after its pulls
+
+    def consumer_attach(self, device, key=None):
+        super().consumer_attach(device, key)
+        if device.type == "cuda" and self.producer_gpu >= 0 and \
+                self.producer_gpu != device.index:
+            try:
+                from ..ops import native
+                ok = native.runtime().can_access_peer(device.index, self.producer_gpu)
+            except Exception as err:           # logged, not fatal
+                ok = "unknown (%s)" % err
+            print("[ring %s] rccl edge gpu %d -> gpu %d, peer access %s"
+                  % (self.name, self.producer_gpu, device.index, ok), flush=True)
+
     def read_into(self, idx, placeholders, descriptor=None):
+        """Claim slot ``idx`` and post its receives into ``placeholders``
+        (rows [0, b)); they are launched by ``flush_recvs`` together with the
+        other items of the call, so the views are valid only after it."""
         import torch.distributed as dist
         src = self.producer_rank if descriptor is None else descriptor
-        ops, out = [], []
+        out = []
         for ph, rows in zip(placeholders, self.valid_rows(idx)):
             if rows:
-                ops.append(dist.P2POp(dist.irecv, ph[:rows], src))
+                _pending_recvs.append(dist.P2POp(dist.irecv, ph[:rows], src))
             out.append(ph[:rows])
         self.claims.put((idx, my_rank()))
-        works = dist.batch_isend_irecv(ops) if ops else []
-        for w in works:
-            w.wait(_timeout())
-        if placeholders and placeholders[0].is_cuda:
-            torch.cuda.current_stream(placeholders[0].device).synchronize()
         return out
 
     def release(self, idx):

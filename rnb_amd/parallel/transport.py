@@ -427,6 +427,16 @@ class IpcRing(RingBase):
     def consumer_attach(self, device, key=None):
         """``key`` = (step, group, instance) of this consumer (see set_consumers)."""
         super().consumer_attach(device)
+        if device.type == "cuda" and self.producer_gpu >= 0 and \
+                self.producer_gpu != device.index:
+            # cross-GPU edge: the pull is a peer copy over xGMI
+            try:
+                from ..ops import native
+                ok = native.runtime().can_access_peer(device.index, self.producer_gpu)
+            except Exception as err:           # logged, not fatal
+                ok = "unknown (%s)" % err
+            print("[ring %s] ipc edge gpu %d -> gpu %d, peer access %s"
+                  % (self.name, self.producer_gpu, device.index, ok), flush=True)
         if not self.gpu_ordered or device.type != "cuda":
             return
         from ..ops import native

@@ -272,6 +272,8 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 ring.release(signal.tensor_idx)
                 time.sleep(0.3)
             out = ring.read_into(signal.tensor_idx, dst, signal.ring)
+            if getattr(ring, "deferred_reads", False):
+                deferred["rccl"] = True     # receives launched by flush_reads()
             if fault != "early_release":
                 ring.verify(signal.tensor_idx, signal.gen, "after pull")
             elif signal.gen is not None and ring.gen[signal.tensor_idx] != signal.gen:
@@ -280,6 +282,15 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                                     % (ring.name, signal.tensor_idx))
             ring.release(signal.tensor_idx)
             return out
+
+        deferred = {"rccl": False}
+
+        def flush_reads():
+            """RCCL input rings post receives per item; launch them as one group."""
+            if deferred["rccl"]:
+                from .parallel.rccl_channel import flush_recvs
+                deferred["rccl"] = False
+                flush_recvs()
 
         def rows_of(signal):
             return shared_input_rings[signal.group_idx][signal.instance_idx].rows_of(
@@ -379,6 +390,7 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                     cards.extend(cards_of(tc))
                     nts.append(nt)
                     item_rows.append(r)
+                flush_reads()
                 tensor_inputs = tuple(d[:rows] for d in dst)
                 time_card = TimeCardList(cards, item_rows)
                 gstats["calls"] += 1
@@ -387,6 +399,7 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 non_tensor_inputs = nts
             elif signal is not None:
                 tensor_inputs = pull(signal, placeholders)
+                flush_reads()
             else:
                 tensor_inputs = None
 
@@ -460,6 +473,10 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             print("[runner %d/%d/%d gpu %d] IPC stream waits refused by ROCm on completed "
                   "events: %d on input rings, %d on the output ring"
                   % (step_idx, group_idx, instance_idx, g_idx, stale, stale_out), flush=True)
+        if result_queue is not None:
+            # per-runner transport counters for the launcher's JSON
+            result_queue.put(("ring_stats", step_idx, group_idx, instance_idx,
+                              {"stale_event_waits": int(stale) + int(stale_out)}))
         # ---- shutdown
         if not is_final_step:
             try:

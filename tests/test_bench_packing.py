@@ -35,3 +35,35 @@ def test_first_fit_fills_batches():
     assert clips(bench.pack_step(vids, 128, 64, "first-fit")) == [128, 15]
     with pytest.raises(ValueError):
         bench.pack_step(vids, 128, 64, "bogus")
+
+
+def test_served_logits_sampling_and_module_recheck(tmp_path, monkeypatch):
+    """bench.py ``numerics``: the loader tags sampled videos with their decode
+    source, the final-step runner writes their logits (RNB_CHECK_DIR), and
+    check_numerics recomputes them with the fp32 nn.Module one video per
+    forward (CPU here: the torch plan of the runner vs the module)."""
+    import argparse
+    import torch
+    import bench
+    from rnb_amd.models.r2p1d.model import R2P1DLoader, R2P1DRunner
+    from rnb_amd.timecard import TimeCard, TimeCardList
+    monkeypatch.setenv("RNB_CHECK_DIR", str(tmp_path))
+    cpu = torch.device("cpu")
+    loader = R2P1DLoader(cpu, seed=3, dtype="fp32", warmup=0)
+    runner = R2P1DRunner(cpu, depth=10, bn_mode="batch", dtype="fp32", warmup=0,
+                         max_clips=16, use_graphs=False, autotune=False)
+    cards, frames = [], []
+    for vid in (0, 61, 5):                       # ids 0 and 61 are sampled
+        tc = TimeCard(vid)
+        (f,), _, tc = loader(None, "synthetic://%d?frames=280" % (100 + vid), tc)
+        tc.extra["rows"] = f.shape[0]
+        cards.append(tc)
+        frames.append(f)
+    x = torch.cat(frames)
+    batch = TimeCardList(cards, [f.shape[0] for f in frames])
+    runner((x,), None, batch)
+    files = sorted(tmp_path.glob("runner_*.npz"))
+    assert len(files) == 2
+    res = bench.check_numerics(argparse.Namespace(depth=10), str(tmp_path), device=cpu)
+    assert res["videos_checked"] == 2 and res["top1_agree"] == 1.0, res
+    assert res["max_rel_err"] < 1e-4, res

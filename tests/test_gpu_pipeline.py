@@ -4,7 +4,7 @@ import os
 
 import pytest
 
-from test_pipeline_e2e import IT, M, run_cfg
+from test_pipeline_e2e import IT, M, checked_run, run_cfg
 
 pytestmark = pytest.mark.gpu
 
@@ -16,8 +16,8 @@ def test_whole_pipeline_ipc_ring_gpu(tmp_path):
         {"model": M + "R2P1DLoader", "queue_groups": [{"gpus": [0], "out_queues": [0]}],
          "num_shared_tensors": 16},
         {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [0, 0], "in_queue": 0}]}]}
-    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "60", "-mi", "0", timeout=600)
-    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    proc, res, _ = checked_run(tmp_path, cfg, "-v", "60", "-mi", "0", timeout=600, depth=18,
+                               bn_mode="batch", device="cuda:0", tol=5e-4, min_videos=4)
     assert res["ok"] and res["videos_per_s"] > 5, res
 
 
@@ -31,9 +31,9 @@ def test_segment_pipeline_gpu_to_cpu_aggregator(tmp_path):
         {"model": M + "R2P1DAggregator", "queue_groups": [{"gpus": [-1], "in_queue": 0}],
          "aggregate": 3}]}
     # race checker on: every IPC slot pull is verified against its generation
-    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "30", "-mi", "0", timeout=600,
-                           env={"RNB_CHECK_RINGS": "1"})
-    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    proc, res, _ = checked_run(tmp_path, cfg, "-v", "30", "-mi", "0", timeout=600,
+                               env={"RNB_CHECK_RINGS": "1"}, depth=18, bn_mode="batch",
+                               device="cuda:0", tol=5e-4, min_videos=4)
     assert res["ok"]
 
 
@@ -46,8 +46,8 @@ def test_layer_split_ipc_gpu(tmp_path):
          "start_index": 1, "end_index": 3, "num_shared_tensors": 4},
         {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [0], "in_queue": 0}],
          "start_index": 4, "end_index": 5}]}
-    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "30", "-mi", "5", timeout=600)
-    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    proc, res, _ = checked_run(tmp_path, cfg, "-v", "30", "-mi", "5", timeout=600, depth=18,
+                               bn_mode="batch", device="cuda:0", tol=5e-4, min_videos=4)
     assert res["ok"] and res["latency"]["count"] > 0
 
 
@@ -59,10 +59,10 @@ def test_gather_pipeline_two_runners_race_checked(tmp_path):
         {"model": M + "R2P1DLoader", "queue_groups": [{"gpus": [0], "out_queues": [0]}]},
         {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [0, 0], "in_queue": 0}],
          "max_clips": 32, "max_batch_videos": 8, "bucket_step": 8}]}
-    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "96", "-mi", "0", "--warmup-videos", "16",
-                           "--latency-seconds", "1", timeout=600,
-                           env={"RNB_CHECK_RINGS": "1"})
-    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    proc, res, _ = checked_run(tmp_path, cfg, "-v", "96", "-mi", "0", "--warmup-videos", "16",
+                               "--latency-seconds", "1", timeout=600,
+                               env={"RNB_CHECK_RINGS": "1"}, depth=18, bn_mode="batch",
+                               device="cuda:0", tol=5e-4, min_videos=8)
     assert res["ok"] and res["latency"]["count"] == 96
     assert res["latency_phase"]["count"] > 0
 

@@ -290,3 +290,14 @@ def test_x6_weight_pack_is_an_exact_split():
                 assert torch.equal(hm[..., :4], hl[..., :4])
                 got = hm[..., :4] + hm[..., 4:] + hl[..., 4:]
                 assert torch.equal(got, ref[:, :, :, r, 4 * q:4 * q + 4]), (fn.__name__, r, q)
+
+
+def test_batch_bn_offsets_skip_empty_segments():
+    """Segment pipelines (reference config/r2p1d-segment.json) send 0-row
+    segments for 1-clip videos; a gathered call's BN offsets skip them, so a
+    bucket of b clips never needs more than b + 1 offsets."""
+    from rnb_amd.timecard import TimeCardList
+    cards = [TimeCard(i) for i in range(6)]
+    tl = TimeCardList(cards, [1, 0, 0, 5, 0, 2])
+    assert R2P1DRunner._clip_offsets(tl, 8) == [0, 1, 6, 8]
+    assert R2P1DRunner._clip_offsets(TimeCardList(cards[:3], [3, 0, 0]), 3) is None

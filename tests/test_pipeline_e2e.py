@@ -37,6 +37,25 @@ def run_cfg(tmp_path, cfg, *args, env=None, timeout=240):
     return proc, res, time.time() - t0
 
 
+def checked_run(tmp_path, cfg, *args, depth, bn_mode, device="cpu", tol=1e-4, env=None,
+                timeout=240, min_videos=1):
+    """run_cfg with output sampling on (rnb_amd/numerics.py): every 2nd video's
+    served logits are recomputed with the fp32 nn.Module (one forward per
+    video, per segment for segmented videos) and must agree."""
+    import torch
+    from rnb_amd.numerics import recheck
+    check = tmp_path / "check"
+    check.mkdir()
+    e = dict(env or {}, RNB_CHECK_DIR=str(check), RNB_CHECK_EVERY="2")
+    proc, res, dt = run_cfg(tmp_path, cfg, *args, env=e, timeout=timeout)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    num = recheck(str(check), depth, torch.device(device), bn_mode=bn_mode)
+    print("numerics:", num)
+    assert num["videos_checked"] >= min_videos, num
+    assert num["top1_agree"] >= 0.99 and num["max_rel_err"] <= tol, num
+    return proc, res, num
+
+
 def test_check_flag():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "benchmark.py"), "--check"],
                          capture_output=True, text=True, timeout=120,
@@ -84,8 +103,9 @@ def test_segment_parallel_with_aggregator(tmp_path):
          "num_shared_tensors": 4},
         {"model": M + "R2P1DAggregator", "queue_groups": [{"gpus": [-1], "in_queue": 0}],
          "aggregate": 2}]}
-    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "5", "-mi", "0")
-    assert proc.returncode == 0, proc.stdout + proc.stderr
+    # served outputs: every 2nd video re-joined by the aggregator is checked
+    # against the fp32 module run once per segment
+    proc, res, _ = checked_run(tmp_path, cfg, "-v", "5", "-mi", "0", depth=10, bn_mode="batch")
     assert res["ok"]
     log = tmp_path / "logs" / res["job_id"] / "g-1-group0-0.txt"
     header = log.read_text().splitlines()[0].split()
@@ -302,9 +322,22 @@ def test_segments_through_batching_runner_rejoined_by_aggregator(tmp_path):
          "queue_groups": [{"gpus": [-1, -1], "in_queue": 0, "out_queues": [0]}]},
         {"model": M + "R2P1DAggregator", "aggregate": 2,
          "queue_groups": [{"gpus": [-1], "in_queue": 0}]}]}
-    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "6", "-mi", "0")
-    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    proc, res, _ = checked_run(tmp_path, cfg, "-v", "6", "-mi", "0", depth=10, bn_mode="batch")
     assert res["ok"] and res["videos_done"] == 6
+
+
+def test_gathered_fp32_batch_bn_outputs_match_module(tmp_path):
+    """Consumer-side batching with the reference's BN numerics (fp32, per-video
+    batch statistics): several videos per model call, and every sampled
+    video's logits equal the fp32 module's one-video forward."""
+    cfg = {"video_path_iterator": IT, "defaults": dict(SMALL, dtype="fp32", bn_mode="batch"),
+           "pipeline": [
+               {"model": M + "R2P1DLoader", "queue_groups": [{"gpus": [-1], "out_queues": [0]}]},
+               {"model": M + "R2P1DRunner", "max_clips": 8, "max_batch_videos": 4,
+                "queue_groups": [{"gpus": [-1, -1], "in_queue": 0}]}]}
+    proc, res, num = checked_run(tmp_path, cfg, "-v", "8", "-mi", "0", depth=10,
+                                 bn_mode="batch", min_videos=2)
+    assert res["ok"]
 
 
 def test_bench_pipeline_configs_parse():

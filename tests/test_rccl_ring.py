@@ -63,7 +63,9 @@ def _rccl_timeout_rank(rank, store_path, ring, out_q):
             ring.producer_rank = 0
             ph = [torch.zeros((1, 2))]
             try:
+                from rnb_amd.parallel.rccl_channel import flush_recvs
                 ring.read_into(0, ph, 0)
+                flush_recvs()
                 out_q.put(("consumer", "returned"))
             except Exception as err:          # the timeout, not a hang
                 out_q.put(("consumer", type(err).__name__))
