@@ -86,6 +86,10 @@ def parse_args(argv=None):
                          "crosses xGMI; global shares one queue across all GPUs")
     ap.add_argument("--segments", type=int, default=None,
                     help="(segment) segments per video (default min(4, GPUs), >= 2)")
+    ap.add_argument("--aggregators", type=int, default=1,
+                    help="(segment) CPU aggregator replicas; > 1 routes runner outputs by "
+                         "request id (IdHashSelector) so a video's segments meet in one "
+                         "replica (1 = the reference's single aggregator)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--bn", default="batch", choices=["eval", "batch"],
                     help="batch (default): the reference's numerics -- it never calls "
@@ -202,12 +206,15 @@ def pipeline_config(args, n_gpus: int) -> dict:
         # is split into S segments that runners on any GPU take (peer copies
         # over xGMI), re-joined by the aggregator on the CPU
         seg = args.segments or max(2, min(4, n_gpus))
+        na = max(1, args.aggregators)
+        rgroup = {"gpus": runner_gpus, "in_queue": 0, "out_queues": list(range(na))}
+        if na > 1:
+            rgroup["queue_selector"] = "rnb_amd.selector.IdHashSelector"
         steps = [{"model": LOADER, "num_segments": seg,
                   "queue_groups": [{"gpus": loader_gpus, "out_queues": [0]}]},
-                 dict(runner, queue_groups=[{"gpus": runner_gpus, "in_queue": 0,
-                                             "out_queues": [0]}]),
+                 dict(runner, queue_groups=[rgroup]),
                  {"model": "rnb_amd.models.r2p1d.model.R2P1DAggregator", "aggregate": seg,
-                  "queue_groups": [{"gpus": [-1], "in_queue": 0}]}]
+                  "queue_groups": [{"gpus": [-1], "in_queue": a} for a in range(na)]}]
     else:
         raise ValueError(args.pipeline)
     if args.slots:
@@ -298,6 +305,7 @@ def main(argv=None) -> int:
                     "random-init weights",
             "p50_ms": round(lat.get("p50_ms", float("nan")), 3),
             "p99_ms": round(lat.get("p99_ms", float("nan")), 3),
+            "latency_tail_breakdown": lat.get("tail_breakdown"),
             "latency_offered_videos_per_s": round(lat.get("offered_videos_per_s", 0.0), 1),
             "latency_requests": lat.get("count", 0),
             "latency_mi10": None if mi_phase is None else {

@@ -383,11 +383,12 @@ def run(args) -> dict:
             base = PHASE_BASE + PHASE_FIELDS * i
             if phase_start[base] <= 0:
                 continue
-            ph = dict(summaries.latency_stats(min_id=int(phase_start[base + 2]),
-                                              max_id=int(phase_start[base + 3])),
+            lo, hi = int(phase_start[base + 2]), int(phase_start[base + 3])
+            ph = dict(summaries.latency_stats(min_id=lo, max_id=hi),
                       offered_videos_per_s=phase_start[base + 1], seconds=lat_s,
                       kind=kind, **({"mean_interval_ms": val} if kind == "mi" else
                                     {"load": val}))
+            ph["tail_breakdown"] = summaries.tail_breakdown(min_id=lo, max_id=hi)
             phases.append(ph)
             print("Latency phase (%s %g): %.1f videos/s offered (Poisson), p50 %.2f ms "
                   "p99 %.2f ms (%d requests)" % (kind, val, ph["offered_videos_per_s"],

@@ -10,7 +10,11 @@ a flat plan of fused ops:
   the epilogue: K25; downsamplebn: K26);
 * layer 5 ends in the fused pool + linear head (K28).
 
-Activations are NDHWC bf16 with channels padded to 8. Execution backends:
+Activations are NDHWC: fp32 with channels padded to 4 (the reference's
+precision, ``dtype=float32``) or bf16 padded to 8. With ``bn_mode='batch'``
+(the reference's training-mode BatchNorm) BN is not folded: each conv runs
+unfolded and a per-video-segment BN follows it (ops/bn.py). Execution
+backends:
 
 ``hip``    the CDNA4 kernels (default on GPU);
 ``torch``  the same folded plan through ``F.conv3d`` (CPU path, and the
@@ -22,8 +26,10 @@ Activations are NDHWC bf16 with channels padded to 8. Execution backends:
 ``GraphedEngine`` wraps a ``hip`` engine with one HIP graph per clip-count
 bucket (torch.cuda.CUDAGraph capture of the ctypes launches, shared memory
 pool), which removes the ~80 kernel launches per forward from the host path
-(SURVEY.md §7.1). Clip rows are independent in eval mode, so a batch is padded
-up to its bucket and the padded rows are discarded.
+(SURVEY.md §7.1). A batch is padded up to its bucket and the padded rows are
+discarded: in eval mode clip rows are independent; in batch mode the graph
+reads the videos' clip offsets from a static device tensor, so the padding
+rows sit outside every video's statistics.
 """
 from __future__ import annotations
 

@@ -3,9 +3,13 @@
 The reference never calls ``.eval()``, so every BatchNorm3d
 normalises with the statistics of the batch it is given and updates its
 running statistics as a side effect. ``BatchNormBatch`` reproduces that on
-the HIP backend (csrc/bn_ops.hip: two-pass per-channel mean/variance +
-fused normalise/affine/residual/ReLU); ``forward_torch`` is the fp32
-reference of the same op and the CPU path.
+the HIP backend per video segment (csrc/bn_ops.hip): fp64 per-video sums
+come from the producing Winograd conv's epilogue or from a one-pass
+shifted-sum statistics kernel, a finalize kernel turns them into scale/shift
+rows plus the running-statistics update, and the normalise/affine/residual/
+ReLU is either a fused apply pass or done on load by the next (temporal
+Winograd) conv. ``forward_torch`` is the fp32 reference of the same op and
+the CPU path.
 """
 from __future__ import annotations
 

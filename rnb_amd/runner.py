@@ -299,7 +299,8 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         def cards_of(tc):
             return list(tc.time_cards) if isinstance(tc, TimeCardList) else [tc]
 
-        pending = []                  # an item taken out of the queue but not run yet
+        pending = []                  # items taken out of the queue but not run yet
+        group_key = getattr(selector, "group_key", None)
         gstats = {"calls": 0, "items": 0, "rows": 0}
         # RNB_PROFILE_STAGES=1: where this runner's host time goes (seconds per
         # phase: queue wait, slot pulls, model call, output publish)
@@ -344,6 +345,22 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 items, rows = [tpl], rows_of(signal)
                 t0 = time.time()
                 deadline = t0 + max_wait_s
+                # a selector that routes by request (IdHashSelector) needs
+                # every card of a batch in one routing class: items of other
+                # classes wait in `pending` for a later call
+                key = group_key(time_card) if group_key is not None else None
+                while key is not None and len(items) < max_items and rows < max_rows:
+                    same = next((i for i, it in enumerate(pending)
+                                 if it is not None and it[0] is not None
+                                 and group_key(it[2]) == key
+                                 and rows + rows_of(it[0]) <= max_rows), None)
+                    if same is None:
+                        break
+                    nxt = pending.pop(same)
+                    nxt[2].add_gpu(g_idx)
+                    nxt[2].record("runner%d_start" % step_idx)
+                    items.append(nxt)
+                    rows += rows_of(nxt[0])
                 while len(items) < max_items and rows < max_rows:
                     # while this replica's previous batch is still running on
                     # the GPU, a launch now would only queue behind it: keep
@@ -363,6 +380,11 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                         break
                     if nxt is None:
                         continue            # end-of-stream wake-up marker
+                    if key is not None and nxt[0] is not None and group_key(nxt[2]) != key:
+                        pending.insert(0, nxt)      # other routing class: a later call
+                        if len(pending) > 4 * max_items:
+                            break
+                        continue
                     if nxt[0] is None or rows + rows_of(nxt[0]) > max_rows:
                         pending.append(nxt)
                         break

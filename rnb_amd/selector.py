@@ -44,3 +44,21 @@ class ShortestQueueSelector(QueueSelector):
         except (NotImplementedError, AttributeError):
             return self._rr.select(tensors, non_tensors, time_card)
         return min(range(len(sizes)), key=sizes.__getitem__)
+
+
+class IdHashSelector(QueueSelector):
+    """Routes by request id: ``time_card.id % num_queues`` (rnb_amd addition).
+
+    With one aggregator per out-queue, every segment of a video reaches the
+    same aggregator replica (reference model.py:238-285 re-joins segments by
+    id in a single aggregator process). A batched output is routed by its
+    first card; ``group_key`` lets a gathering runner build batches whose
+    cards all route to the same queue (runner.py gather)."""
+
+    def group_key(self, time_card):
+        cards = getattr(time_card, "time_cards", None)
+        tc = cards[0] if cards else time_card
+        return tc.id % self.num_queues
+
+    def select(self, tensors, non_tensors, time_card):
+        return self.group_key(time_card)

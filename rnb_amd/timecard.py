@@ -270,6 +270,35 @@ class TimeCardSummary:
                       max_id: Optional[int] = None) -> Dict[str, float]:
         return percentile_stats(self.end_to_end(num_skips, min_id, max_id))
 
+    def tail_breakdown(self, min_id: Optional[int] = None, max_id: Optional[int] = None,
+                       q: float = 0.99) -> Dict[str, object]:
+        """Where the slowest requests' time goes: mean per-stage time (ms
+        between consecutive keys) of the requests at or above the ``q``
+        latency quantile vs. those around the median (45-55 %), plus their
+        clip counts and how many of them share a model call's start time with
+        others (gathered). Keys are the TimeCard's own (enqueue_filename,
+        runner0_start, ...)."""
+        if not self.keys:
+            return {}
+        keep = self._select(min_id, max_id)
+        mat = np.asarray([self.summary[k] for k in self.keys], dtype=np.float64)[:, keep]
+        if mat.shape[1] < 10:
+            return {}
+        lat = mat.max(axis=0) - mat[0]
+        order = np.argsort(lat)
+        n = len(lat)
+        tail = order[n - max(1, int(round(n * (1.0 - q)))):]
+        mid = order[int(0.45 * n):max(int(0.55 * n), int(0.45 * n) + 1)]
+        out: Dict[str, object] = {"requests": int(n), "tail_requests": int(len(tail)),
+                                  "tail_latency_ms": float(lat[tail].mean() * 1e3),
+                                  "median_latency_ms": float(lat[mid].mean() * 1e3),
+                                  "stages": OrderedDict()}
+        for i, (prv, nxt) in enumerate(zip(self.keys[:-1], self.keys[1:])):
+            d = (mat[i + 1] - mat[i]) * 1e3
+            out["stages"]["%s -> %s" % (prv, nxt)] = {"tail_ms": round(float(d[tail].mean()), 3),
+                                                      "median_ms": round(float(d[mid].mean()), 3)}
+        return out
+
     def print_summary(self, num_skips: int) -> None:
         """Mean Δ between consecutive keys (reference format) + percentiles."""
         if self.keys and len(self.summary[self.keys[0]]) <= num_skips:

@@ -98,3 +98,25 @@ def test_tables_and_cli(tmp_path):
                          capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert png.stat().st_size > 1000
+
+
+def test_tail_breakdown_attributes_the_slow_stage():
+    """TimeCardSummary.tail_breakdown: the slowest 1 % of requests whose
+    extra time sits in one stage show it there, not in the others."""
+    from rnb_amd.timecard import TimeCard, TimeCardSummary
+    s = TimeCardSummary()
+    for i in range(200):
+        tc = TimeCard(i)
+        t = 100.0 + i
+        slow = 0.050 if i % 100 == 7 else 0.0          # 2 requests: +50 ms in the queue
+        for key, dt in (("enqueue_filename", 0.0), ("runner0_start", 0.001 + slow),
+                        ("inference0_start", 0.0001), ("inference0_finish", 0.002)):
+            t += dt
+            tc.timings[key] = t
+        s.register(tc)
+    tb = s.tail_breakdown()
+    st = tb["stages"]
+    assert tb["tail_requests"] == 2
+    assert abs(st["enqueue_filename -> runner0_start"]["tail_ms"] - 51.0) < 0.1
+    assert abs(st["enqueue_filename -> runner0_start"]["median_ms"] - 1.0) < 0.1
+    assert abs(st["inference0_start -> inference0_finish"]["tail_ms"] - 2.0) < 0.1

@@ -38,7 +38,7 @@ def run_cfg(tmp_path, cfg, *args, env=None, timeout=240):
 
 
 def checked_run(tmp_path, cfg, *args, depth, bn_mode, device="cpu", tol=1e-4, env=None,
-                timeout=240, min_videos=1):
+                timeout=240, min_videos=1, every=2):
     """run_cfg with output sampling on (rnb_amd/numerics.py): every 2nd video's
     served logits are recomputed with the fp32 nn.Module (one forward per
     video, per segment for segmented videos) and must agree."""
@@ -46,7 +46,7 @@ def checked_run(tmp_path, cfg, *args, depth, bn_mode, device="cpu", tol=1e-4, en
     from rnb_amd.numerics import recheck
     check = tmp_path / "check"
     check.mkdir()
-    e = dict(env or {}, RNB_CHECK_DIR=str(check), RNB_CHECK_EVERY="2")
+    e = dict(env or {}, RNB_CHECK_DIR=str(check), RNB_CHECK_EVERY=str(every))
     proc, res, dt = run_cfg(tmp_path, cfg, *args, env=e, timeout=timeout)
     assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
     num = recheck(str(check), depth, torch.device(device), bn_mode=bn_mode)
@@ -324,6 +324,32 @@ def test_segments_through_batching_runner_rejoined_by_aggregator(tmp_path):
          "queue_groups": [{"gpus": [-1], "in_queue": 0}]}]}
     proc, res, _ = checked_run(tmp_path, cfg, "-v", "6", "-mi", "0", depth=10, bn_mode="batch")
     assert res["ok"] and res["videos_done"] == 6
+
+
+def test_segment_aggregator_replicas_routed_by_id(tmp_path):
+    """Two aggregator replicas behind an IdHashSelector: batching runners keep
+    each call inside one routing class, so all segments of a video meet in
+    the same replica (each replica's log holds only its class of ids, every
+    video completes) and the re-joined outputs match the module."""
+    cfg = {"video_path_iterator": IT, "defaults": SMALL, "pipeline": [
+        {"model": M + "R2P1DLoader", "num_segments": 2,
+         "queue_groups": [{"gpus": [-1], "out_queues": [0]}]},
+        {"model": M + "R2P1DRunner", "max_clips": 8, "max_batch_videos": 4,
+         "queue_groups": [{"gpus": [-1, -1], "in_queue": 0, "out_queues": [0, 1],
+                           "queue_selector": "rnb_amd.selector.IdHashSelector"}]},
+        {"model": M + "R2P1DAggregator", "aggregate": 2,
+         "queue_groups": [{"gpus": [-1], "in_queue": 0}, {"gpus": [-1], "in_queue": 1}]}]}
+    proc, res, _ = checked_run(tmp_path, cfg, "-v", "10", "-mi", "0", depth=10,
+                               bn_mode="batch", min_videos=6, every=1)
+    assert res["ok"] and res["videos_done"] >= 10
+    # every re-joined video was dumped by the aggregator process that merged it
+    by_pid = {}
+    for f in (tmp_path / "check").glob("aggregate_v*_p*.npz"):
+        vid, pid = f.stem.split("_")[1:]
+        by_pid.setdefault(pid, []).append(int(vid[1:]))
+    assert len(by_pid) == 2, by_pid
+    for ids in by_pid.values():
+        assert len({i % 2 for i in ids}) == 1, by_pid
 
 
 def test_gathered_fp32_batch_bn_outputs_match_module(tmp_path):
