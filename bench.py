@@ -275,10 +275,7 @@ def main(argv=None) -> int:
         return 2
     if args.pipeline == "fused":
         return run_fused(args)
-    import torch.distributed as dist
-    if world > 1:
-        # coordination only (gloo, CPU): the GPUs belong to the launcher's processes
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    store = _rank_store(rank, world) if world > 1 else None
     rc, line = 0, None
     if rank == 0:
         res = run_pipeline(args, world)
@@ -342,15 +339,37 @@ def main(argv=None) -> int:
         if args.gpus == 1 and args.literal and args.pipeline == "aggressive":
             rec["literal"] = run_literal_extras(args)
         line = json.dumps(rec)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    if store is not None:
+        # every rank waits for rank 0's run (its launcher drives all GPUs)
+        store.add("bench_ranks_done", 1)
+        deadline = time.time() + args.barrier_timeout + 3600
+        while int(store.add("bench_ranks_done", 0)) < world:
+            if time.time() > deadline:
+                print("bench.py: ranks did not all finish", file=sys.stderr)
+                return 3
+            time.sleep(0.2)
     if rank == 0:
         print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     return rc
+
+
+def _rank_store(rank: int, world: int):
+    """Coordination of the torchrun ranks in pipeline mode through the
+    rendezvous TCP store only. A gloo process group would make every rank's
+    process open the GPU device (device enumeration at init), which would
+    count against the per-GPU process budget next to the launcher's
+    loader/runner processes; the GPUs belong to the launcher's processes."""
+    import torch.distributed as dist
+    from datetime import timedelta
+    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = int(os.environ.get("MASTER_PORT", "29500"))
+    agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
+    # under torchrun the agent already serves the store on MASTER_PORT
+    return dist.TCPStore(addr, port, world, is_master=(rank == 0 and not agent),
+                         timeout=timedelta(seconds=1800))
 
 
 def run_cross_gpu_extras(args) -> dict:

@@ -194,6 +194,7 @@ class TimeCardSummary:
         self.gpus_per_inference: List[List[tuple]] = []
         self.keys: List[str] = []
         self.ids: List[int] = []
+        self.clips: List[int] = []
 
     def register(self, time_card: TimeCard) -> None:
         """Stash one finished request; key order must match earlier ones."""
@@ -208,6 +209,7 @@ class TimeCardSummary:
             self.summary[key].append(ts)
         self.gpus_per_inference.append(time_card.gpus)
         self.ids.append(time_card.id)
+        self.clips.append(-1 if time_card.num_clips is None else int(time_card.num_clips))
 
     def __len__(self) -> int:
         return len(self.ids)
@@ -226,6 +228,7 @@ class TimeCardSummary:
             self.summary[key].extend(other.summary[key])
         self.gpus_per_inference.extend(other.gpus_per_inference)
         self.ids.extend(other.ids)
+        self.clips.extend(getattr(other, "clips", [-1] * len(other.ids)))
 
     def mean_deltas(self, num_skips: int) -> "OrderedDict[str, float]":
         out: "OrderedDict[str, float]" = OrderedDict()
@@ -293,6 +296,12 @@ class TimeCardSummary:
                                   "tail_latency_ms": float(lat[tail].mean() * 1e3),
                                   "median_latency_ms": float(lat[mid].mean() * 1e3),
                                   "stages": OrderedDict()}
+        clips = np.asarray(self.clips, dtype=np.int64)
+        if len(clips) == len(self.ids):
+            clips = clips[keep]
+            if (clips >= 0).all():
+                out["tail_mean_clips"] = round(float(clips[tail].mean()), 2)
+                out["median_mean_clips"] = round(float(clips[mid].mean()), 2)
         for i, (prv, nxt) in enumerate(zip(self.keys[:-1], self.keys[1:])):
             d = (mat[i + 1] - mat[i]) * 1e3
             out["stages"]["%s -> %s" % (prv, nxt)] = {"tail_ms": round(float(d[tail].mean()), 3),

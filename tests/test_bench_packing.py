@@ -67,3 +67,30 @@ def test_served_logits_sampling_and_module_recheck(tmp_path, monkeypatch):
     res = bench.check_numerics(argparse.Namespace(depth=10), str(tmp_path), device=cpu)
     assert res["videos_checked"] == 2 and res["top1_agree"] == 1.0, res
     assert res["max_rel_err"] < 1e-4, res
+
+
+def test_bench_ranks_coordinate_through_the_rendezvous_store(tmp_path):
+    """Pipeline mode: torchrun ranks meet through the rendezvous TCP store
+    (bench._rank_store), not a gloo group whose init would open the GPU in
+    every rank process."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "ranks.py"
+    script.write_text(
+        "import os, sys, time\n"
+        "sys.path.insert(0, %r)\n"
+        "import bench\n"
+        "r, w = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])\n"
+        "st = bench._rank_store(r, w)\n"
+        "st.add('n', 1)\n"
+        "while int(st.add('n', 0)) < w:\n"
+        "    time.sleep(0.05)\n"
+        "print('rank-ok', r, flush=True)\n" % root)
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "3", "--master-addr", "127.0.0.1",
+                          "--master-port", "29677", str(script)],
+                         capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert sorted(l for l in out.stdout.splitlines() if l.startswith("rank-ok")) == \
+        ["rank-ok 0", "rank-ok 1", "rank-ok 2"]
