@@ -332,12 +332,14 @@ def main(argv=None) -> int:
                        "bucket_step": args.bucket_step,
                        "job_wall_s": round(res.get("wall_s", 0.0), 1)},
         }
-        if res.get("check_dir"):
-            rec["numerics"] = check_numerics(args, res["check_dir"])
+        # extra runs first: the numerics check opens the GPU in this process,
+        # and the extras' launchers bring their own loader/runner processes
         if args.gpus > 1 and args.cross_gpu_extras and args.pipeline == "aggressive":
             rec["cross_gpu"] = run_cross_gpu_extras(args)
         if args.gpus == 1 and args.literal and args.pipeline == "aggressive":
             rec["literal"] = run_literal_extras(args)
+        if res.get("check_dir"):
+            rec["numerics"] = check_numerics(args, res["check_dir"])
         line = json.dumps(rec)
     if store is not None:
         # every rank waits for rank 0's run (its launcher drives all GPUs)
@@ -396,7 +398,8 @@ def run_cross_gpu_extras(args) -> dict:
                "--gpus", str(args.gpus), "--steps", str(args.cross_gpu_steps),
                "--warmup", "1", "--dtype", args.dtype, "--bn", args.bn,
                "--depth", str(args.depth), "--latency-seconds", "2",
-               "--no-cross-gpu-extras", "--json-out", path]
+               "--loaders", str(args.loaders), "--replicas", str(args.replicas),
+               "--no-check", "--no-cross-gpu-extras", "--json-out", path]
         env = {k: v for k, v in os.environ.items()
                if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
                             "MASTER_ADDR", "MASTER_PORT", "GROUP_RANK", "ROLE_RANK",

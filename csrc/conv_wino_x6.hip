@@ -196,42 +196,61 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wgid = w_xcd_remap();
-  const int cb = wgid % p.n_cblocks;
-  const int tb = wgid / p.n_cblocks;
-
   const int tl = lane & 15, q = lane >> 4;
-  const int t = tb * NT + wave * 16 + tl;
-  int f = 0, ty = 0, tx = 0;
-  const bool tvalid = t < p.n_tiles;
-  if (tvalid) {
-    const int t1 = w_div(t, p.m_tw, p.s_tw);
-    tx = t - t1 * p.tiles_w;
-    f = w_div(t1, p.m_th, p.s_th);
-    ty = t1 - f * p.tiles_h;
-  }
-  const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
-  int rmask = 0, cmask = 0;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    rmask |= (tvalid && y0 + d >= 0 && y0 + d < p.H) ? (1 << d) : 0;
-    cmask |= (x0 + d >= 0 && x0 + d < p.W) ? (1 << d) : 0;
-  }
-  const int pix0 = (f * p.H + y0) * p.W + x0;           // may be negative (padding)
   const int row_bytes = p.W * p.Cin * 4;
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ur =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, p.u_bytes, 0x00020000);
+  const uint32_t cin4 = (uint32_t)p.Cin * 4;
+
+  // Persistent blocks: a block walks work units (tile block tb, channel
+  // block cb) u = first, first + per_xcd_stride, ...; the units of one XCD
+  // form a contiguous range, so the blocks running there at once share
+  // their tile blocks' input patches in that XCD's L2. The next unit's first
+  // U chunk and input patch are loaded before this unit's epilogue, so the
+  // epilogue's stores and the next prologue's loads overlap (one block per
+  // CU: nothing else would hide them).
+  const int n_units = p.n_tblocks * p.n_cblocks;
+  const int nblk = gridDim.x, xcd = blockIdx.x & 7;
+  const int per_x = (nblk + 7 - xcd) >> 3;                     // blocks on this XCD
+  const int lo_u = (int)((long long)n_units * xcd / 8);
+  const int hi_u = (int)((long long)n_units * (xcd + 1) / 8);
+  int unit = lo_u + (blockIdx.x >> 3);
+  const int ustride = per_x;
+
+  int cb = 0, tb = 0, f = 0, ty = 0, tx = 0, cmask = 0;
+  bool tvalid = false;
   // per patch row: the lane's byte offset, or X6_OOB for a padding row (any
   // small uniform delta added keeps it past the buffer: out-of-range buffer
   // loads return 0); a padding column selects X6_OOB per load
   uint32_t rowoff[4];
+  auto set_unit = [&](int u) {
+    cb = u % p.n_cblocks;
+    tb = u / p.n_cblocks;
+    const int t = tb * NT + wave * 16 + tl;
+    f = ty = tx = 0;
+    tvalid = t < p.n_tiles;
+    if (tvalid) {
+      const int t1 = w_div(t, p.m_tw, p.s_tw);
+      tx = t - t1 * p.tiles_w;
+      f = w_div(t1, p.m_th, p.s_th);
+      ty = t1 - f * p.tiles_h;
+    }
+    const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
+    int rmask = 0;
+    cmask = 0;
 #pragma unroll
-  for (int dy = 0; dy < 4; ++dy)
-    rowoff[dy] = ((rmask >> dy) & 1) ? (uint32_t)(pix0 * p.Cin * 4 + q * 16 + dy * row_bytes)
-                                     : X6_OOB;
-  const uint32_t cin4 = (uint32_t)p.Cin * 4;
+    for (int d = 0; d < 4; ++d) {
+      rmask |= (tvalid && y0 + d >= 0 && y0 + d < p.H) ? (1 << d) : 0;
+      cmask |= (x0 + d >= 0 && x0 + d < p.W) ? (1 << d) : 0;
+    }
+    const int pix0 = (f * p.H + y0) * p.W + x0;         // may be negative (padding)
+#pragma unroll
+    for (int dy = 0; dy < 4; ++dy)
+      rowoff[dy] = ((rmask >> dy) & 1) ? (uint32_t)(pix0 * p.Cin * 4 + q * 16 + dy * row_bytes)
+                                       : X6_OOB;
+  };
 
   auto load_one = [&](int chunk, int e) -> wf32x4 {
     const int dy = e >> 2, dx = e & 3;
@@ -245,10 +264,6 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
   };
 
   wf32x4 acc[16][TC];
-#pragma unroll
-  for (int x = 0; x < 16; ++x)
-#pragma unroll
-    for (int c = 0; c < TC; ++c) acc[x][c] = (wf32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nchunks = p.Cin / 16;
   const int frow = lane & 15;
@@ -353,35 +368,65 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
   };
 
   wf32x4 d[16];
+  if (unit >= hi_u) return;                          // more blocks than units here
+  int g = 0;                                         // chunks run so far (U buffer g & 1)
+  set_unit(unit);
   issue_u(0, 0);
 #pragma unroll
   for (int e = 0; e < 16; ++e) d[e] = load_one(0, e);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int c = 0; c + 1 < nchunks; ++c) {
-    const int cur = c & 1;
-    if (X6_EXP != 4) issue_u(c + 1, cur ^ 1);
-    // keep the U DMA ahead of the patch loads in issue order (vmcnt below)
-    asm volatile("" ::: "memory");
-    transform_a(d);
-    gemm(lds + cur * U_BYTES, d, c + 1, std::true_type{});
-    // U of chunk c+1 landed; the 16 younger patch loads may stay in flight
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    __syncthreads();
-  }
-  transform_a(d);
-  gemm(lds + ((nchunks - 1) & 1) * U_BYTES, d, -1, std::false_type{});
-  __syncthreads();                 // the epilogue's statistics reuse the U buffers
-  if (X6_EXP == 6) {              // every accumulator stays live, no transform / stores
-    wf32x4 t = acc[0][0];
+  while (true) {
 #pragma unroll
     for (int x = 0; x < 16; ++x)
 #pragma unroll
-      for (int c = 0; c < TC; ++c) t += acc[x][c];
-    if (t[0] + t[1] + t[2] + t[3] == 1.2345f && tvalid) p.y[0] = t[0];
-    return;
+      for (int c = 0; c < TC; ++c) acc[x][c] = (wf32x4){0.f, 0.f, 0.f, 0.f};
+    // the unit's chunk 0 (U DMA + patch) was issued before the previous
+    // unit's epilogue (or just above)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int c = 0; c + 1 < nchunks; ++c) {
+      const int cur = g & 1;
+      if (X6_EXP != 4) issue_u(c + 1, cur ^ 1);
+      // keep the U DMA ahead of the patch loads in issue order (vmcnt below)
+      asm volatile("" ::: "memory");
+      transform_a(d);
+      gemm(lds + cur * U_BYTES, d, c + 1, std::true_type{});
+      ++g;
+      // U of chunk c+1 landed; the 16 younger patch loads may stay in flight
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      __syncthreads();
+    }
+    transform_a(d);
+    gemm(lds + (g & 1) * U_BYTES, d, -1, std::false_type{});
+    ++g;
+    // every wave is done with this unit's last U buffer: it holds the
+    // epilogue's statistics scratch; the next unit's chunk 0 goes to the other
+    __syncthreads();
+    const int nxt = unit + ustride;
+    // this unit's coordinates for its epilogue, before set_unit moves on
+    const int e_cb = cb, e_tb = tb, e_f = f, e_ty = ty, e_tx = tx;
+    const bool e_valid = tvalid;
+    if (nxt < hi_u) {
+      set_unit(nxt);
+      issue_u(0, g & 1);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int e = 0; e < 16; ++e) d[e] = load_one(0, e);
+    }
+    char* scratch = lds + ((g - 1) & 1) * U_BYTES;
+    if (X6_EXP == 6) {              // every accumulator stays live, no transform / stores
+      wf32x4 t = acc[0][0];
+#pragma unroll
+      for (int x = 0; x < 16; ++x)
+#pragma unroll
+        for (int c = 0; c < TC; ++c) t += acc[x][c];
+      if (t[0] + t[1] + t[2] + t[3] == 1.2345f && e_valid) p.y[0] = t[0];
+    } else {
+      w_spatial_epilogue<TC, ST, WAVES>(p, scratch, acc, e_tb, wave, tl, q, e_cb, lane, e_valid,
+                                        e_f, e_ty, e_tx);
+    }
+    if (nxt >= hi_u) break;
+    unit = nxt;
   }
-  w_spatial_epilogue<TC, ST, WAVES>(p, lds, acc, tb, wave, tl, q, cb, lane, tvalid, f, ty, tx);
 }
 
 // ===========================================================================
@@ -557,6 +602,32 @@ static void x6_launch(K kernel, const WinoParams& p, int threads, hipStream_t st
                      p);
 }
 
+// compute units of the current device (cached per device)
+static int x6_num_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// persistent launch: per_cu resident blocks per CU, a multiple of 8 blocks
+// (every XCD owns a unit range and needs at least one block)
+template <typename K>
+static void x6_launch_persistent(K kernel, const WinoParams& p, int threads, int per_cu,
+                                 hipStream_t stream) {
+  const long long units = (long long)p.n_tblocks * p.n_cblocks;
+  long long grid = (long long)x6_num_cus() * per_cu;
+  if (grid > units) grid = units;
+  grid = (grid + 7) / 8 * 8;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(threads), 0, stream, p);
+}
+
 extern "C" {
 
 // Spatial F(2x2, 3x3) on bf16 MFMA (x6). variant 0 = TC 2 x 8 waves (128
@@ -574,20 +645,20 @@ int rnb_wino_x6_launch(const WinoParams* pp, int variant, hipStream_t stream) {
   const bool st = p.out_stats != nullptr;
   switch (variant) {
     case 0:
-      if (st) x6_launch(conv_wino_x6_kernel<2, 8, true>, p, 512, stream);
-      else x6_launch(conv_wino_x6_kernel<2, 8>, p, 512, stream);
+      if (st) x6_launch_persistent(conv_wino_x6_kernel<2, 8, true>, p, 512, 1, stream);
+      else x6_launch_persistent(conv_wino_x6_kernel<2, 8>, p, 512, 1, stream);
       break;
     case 1:
-      if (st) x6_launch(conv_wino_x6_kernel<1, 8, true>, p, 512, stream);
-      else x6_launch(conv_wino_x6_kernel<1, 8>, p, 512, stream);
+      if (st) x6_launch_persistent(conv_wino_x6_kernel<1, 8, true>, p, 512, 1, stream);
+      else x6_launch_persistent(conv_wino_x6_kernel<1, 8>, p, 512, 1, stream);
       break;
     case 2:
-      if (st) x6_launch(conv_wino_x6_kernel<1, 4, true>, p, 256, stream);
-      else x6_launch(conv_wino_x6_kernel<1, 4>, p, 256, stream);
+      if (st) x6_launch_persistent(conv_wino_x6_kernel<1, 4, true>, p, 256, 2, stream);
+      else x6_launch_persistent(conv_wino_x6_kernel<1, 4>, p, 256, 2, stream);
       break;
     default:
-      if (st) x6_launch(conv_wino_x6_kernel<2, 4, true>, p, 256, stream);
-      else x6_launch(conv_wino_x6_kernel<2, 4>, p, 256, stream);
+      if (st) x6_launch_persistent(conv_wino_x6_kernel<2, 4, true>, p, 256, 1, stream);
+      else x6_launch_persistent(conv_wino_x6_kernel<2, 4>, p, 256, 1, stream);
       break;
   }
   return (int)hipGetLastError();

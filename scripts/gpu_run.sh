@@ -65,11 +65,19 @@ for step in "$@"; do
     pmc) layer=${arg%%:*}; cfgs=${arg#*:}
          LAYER=$layer CFGS="${cfgs//,/ }" run pmc 900 bash scripts/gpu_pmc_conv.sh ;;
     fold) n=${arg:-2}
+          # torchrun ranks coordinate through the store (no GPU open); the
+          # launcher on rank 0 runs n loaders + n runners folded onto GPU 0
           export RNB_FOLD_GPUS=1
           run fold$n 900 python -m torch.distributed.run --nnodes=1 \
             --nproc-per-node "$n" --master-addr 127.0.0.1 --master-port 29631 bench.py \
             --gpus "$n" --steps 4 --warmup 1 --replicas 1 --loaders 1 \
             --json-out gpurun_out/fold$n.json
+          unset RNB_FOLD_GPUS ;;
+    foldl) n=${arg:-8}
+          # the same topology from one bench process (no torchrun ranks)
+          export RNB_FOLD_GPUS=1
+          run foldl$n 900 python bench.py --gpus "$n" --steps 4 --warmup 1 --replicas 1 \
+            --loaders 1 --json-out gpurun_out/foldl$n.json
           unset RNB_FOLD_GPUS ;;
     repro) run repro 150 bash scripts/ipc_event_repro.sh "${arg:-2000}" ;;
     mfma) run mfma 120 python -u scripts/mfma_split.py ;;
