@@ -430,6 +430,295 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
 }
 
 // ===========================================================================
+// Spatial F(2x2, 3x3) with the 16 GEMM positions split over a wave pair
+// ("x6h"): wave (tg, xh) of a block of 8 computes V rows 2 xh, 2 xh + 1 (GEMM
+// steps x = 8 xh .. 8 xh + 7) for the 16 tiles of tile group tg. Each wave
+// then holds 8 x TC accumulator quads instead of 16 x TC (64 fewer VGPRs at
+// TC 2) and loads 3 of the 4 patch rows, which leaves the registers for
+// software-pipelined steps (the split and fragment reads of step k+1 under
+// step k's MFMAs) at two waves per SIMD -- the full-x kernel above runs its
+// steps in order, latency-bound. The output transform is finished per
+// output row after an LDS exchange of one row partial between the pair.
+//
+// Patch rows per wave, as slots S0 S1 S2 (V row a = e(S0) - e(S2), V row b =
+// s e(S1) + e(S2), e = d B per patch row):
+//   xh 0: S = (d0, d1, d2), s = +1: V0 = e0 - e2, V1 = e1 + e2
+//   xh 1: S = (d2, d3, d1), s = -1: V2 = e2 - e1, V3 = e1 - e3
+// The steps run V row a first; S0's next-chunk loads go out as row a's steps
+// consume it, S2's after row b is formed, S1's during row b's steps.
+template <int TC, bool ST = false>
+__global__ __launch_bounds__(512, 1) void conv_wino_x6h_kernel(const WinoParams p) {
+  constexpr int CT = 16 * TC, NT = 64, WAVES = 8;
+  constexpr int U_BYTES = 16 * CT * 128;
+  static_assert(8 * TC * 4 * 64 * 16 <= U_BYTES, "epilogue exchange fits one U buffer");
+  __shared__ __attribute__((aligned(16))) char lds[2 * U_BYTES];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tg = wave >> 1, xh = wave & 1;
+  const int tl = lane & 15, q = lane >> 4;
+  const int row_bytes = p.W * p.Cin * 4;
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ur =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.u, (short)0, p.u_bytes, 0x00020000);
+  const uint32_t cin4 = (uint32_t)p.Cin * 4;
+  const float sgn = xh ? -1.f : 1.f;
+
+  // persistent blocks, XCD-contiguous unit ranges (see conv_wino_x6_kernel)
+  const int n_units = p.n_tblocks * p.n_cblocks;
+  const int nblk = gridDim.x, xcd = blockIdx.x & 7;
+  const int per_x = (nblk + 7 - xcd) >> 3;
+  const int lo_u = (int)((long long)n_units * xcd / 8);
+  const int hi_u = (int)((long long)n_units * (xcd + 1) / 8);
+  int unit = lo_u + (blockIdx.x >> 3);
+
+  int cb = 0, tb = 0, f = 0, ty = 0, tx = 0, cmask = 0;
+  bool tvalid = false;
+  uint32_t rowoff[3];                                // slots S0 S1 S2
+  auto set_unit = [&](int u) {
+    cb = u % p.n_cblocks;
+    tb = u / p.n_cblocks;
+    const int t = tb * NT + tg * 16 + tl;
+    f = ty = tx = 0;
+    tvalid = t < p.n_tiles;
+    if (tvalid) {
+      const int t1 = w_div(t, p.m_tw, p.s_tw);
+      tx = t - t1 * p.tiles_w;
+      f = w_div(t1, p.m_th, p.s_th);
+      ty = t1 - f * p.tiles_h;
+    }
+    const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
+    cmask = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) cmask |= (x0 + d >= 0 && x0 + d < p.W) ? (1 << d) : 0;
+    const int pix0 = (f * p.H + y0) * p.W + x0;       // may be negative (padding)
+#pragma unroll
+    for (int sl = 0; sl < 3; ++sl) {
+      const int dy = xh ? (sl == 0 ? 2 : sl == 1 ? 3 : 1) : sl;
+      const bool ok = tvalid && y0 + dy >= 0 && y0 + dy < p.H;
+      rowoff[sl] = ok ? (uint32_t)(pix0 * p.Cin * 4 + q * 16 + dy * row_bytes) : X6_OOB;
+    }
+  };
+  // element e = 4 slot + dx of this lane's 3-row patch, chunk `chunk`
+  auto load_one = [&](int chunk, int e) -> wf32x4 {
+    const int sl = e >> 2, dx = e & 3;
+    const uint32_t off = ((cmask >> dx) & 1) ? rowoff[sl] + (uint32_t)(dx * cin4 + chunk * 64)
+                                             : X6_OOB;
+    return __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+  };
+  auto issue_u = [&](int chunk, int buf) {
+    const uint32_t base = ((uint32_t)chunk * (uint32_t)p.n_cblocks + (uint32_t)cb) * U_BYTES;
+    x6_issue_u<U_BYTES, WAVES>(ur, base, lds + buf * U_BYTES, wave, lane);
+  };
+
+  // e = d B on slot sl (channel pairs, v_pk_add_f32)
+  auto row_t = [&](wf32x4 (&v)[12], int sl) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const wf32x2 b0 = (wf32x2){v[sl * 4 + 0][2 * hf], v[sl * 4 + 0][2 * hf + 1]};
+      const wf32x2 b1 = (wf32x2){v[sl * 4 + 1][2 * hf], v[sl * 4 + 1][2 * hf + 1]};
+      const wf32x2 b2 = (wf32x2){v[sl * 4 + 2][2 * hf], v[sl * 4 + 2][2 * hf + 1]};
+      const wf32x2 b3 = (wf32x2){v[sl * 4 + 3][2 * hf], v[sl * 4 + 3][2 * hf + 1]};
+      const wf32x2 o[4] = {b0 - b2, b1 + b2, b2 - b1, b1 - b3};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[sl * 4 + j][2 * hf] = o[j][0];
+        v[sl * 4 + j][2 * hf + 1] = o[j][1];
+      }
+    }
+  };
+  auto transform_a = [&](wf32x4 (&v)[12]) {          // V row a = e(S0) - e(S2) -> v[0..3]
+    if constexpr (X6_EXP == 5) return;
+    row_t(v, 0);
+    row_t(v, 2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = v[j] - v[8 + j];
+  };
+  auto transform_b = [&](wf32x4 (&v)[12]) {          // V row b = s e(S1) + e(S2) -> v[4..7]
+    if constexpr (X6_EXP == 5) return;
+    row_t(v, 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[4 + j] = sgn * v[4 + j] + v[8 + j];
+  };
+
+  wf32x4 acc[8][TC];
+  const int frow = lane & 15;
+  // 8 GEMM steps of one chunk, pipelined one step ahead; step k uses V
+  // element v[k] and U rows x = 8 xh + k. refill: the next chunk's patch goes
+  // into the slots as they free up (S0 during row a, S2 after transform_b,
+  // S1 during row b)
+  auto gemm = [&](const char* ub, wf32x4 (&v)[12], int next, auto refill) {
+    constexpr bool RF = decltype(refill)::value && X6_EXP != 3;
+    X6A af[2][TC];
+    X6B bf[2];
+    bf[0] = x6_split(v[0]);
+    if constexpr (RF) v[0] = load_one(next, 0);
+    x6_read_a<TC>(af[0], ub, 8 * xh, frow, q);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k + 1 < 8) {
+        if (k + 1 == 4) {
+          transform_b(v);
+          if constexpr (RF) {
+#pragma unroll
+            for (int e = 8; e < 12; ++e) v[e] = load_one(next, e);
+          }
+        }
+        bf[(k + 1) & 1] = x6_split(v[k + 1]);
+        if constexpr (RF) v[k + 1] = load_one(next, k + 1);
+        x6_read_a<TC>(af[(k + 1) & 1], ub, 8 * xh + k + 1, frow, q);
+      }
+      x6_step<TC>(acc[k], af[k & 1], bf[k & 1]);
+      if (k + 1 < 8) {
+#pragma unroll
+        for (int i = 0; i < 3 * TC; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);          // MFMA
+          if (i < 2 * TC) __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);   // DS read
+          __builtin_amdgcn_sched_group_barrier(0x0002, X6_VALU_PER_MFMA(TC), 0);   // VALU
+        }
+        if constexpr (RF) __builtin_amdgcn_sched_group_barrier(0x0020, 1, 0);   // VMEM read
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  const int nchunks = p.Cin / 16;
+  wf32x4 d[12];
+  if (unit >= hi_u) return;
+  int g = 0;
+  set_unit(unit);
+  issue_u(0, 0);
+#pragma unroll
+  for (int e = 0; e < 12; ++e) d[e] = load_one(0, e);
+  while (true) {
+#pragma unroll
+    for (int x = 0; x < 8; ++x)
+#pragma unroll
+      for (int c = 0; c < TC; ++c) acc[x][c] = (wf32x4){0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int c = 0; c + 1 < nchunks; ++c) {
+      const int cur = g & 1;
+      if (X6_EXP != 4) issue_u(c + 1, cur ^ 1);
+      asm volatile("" ::: "memory");
+      transform_a(d);
+      gemm(lds + cur * U_BYTES, d, c + 1, std::true_type{});
+      ++g;
+      // U of chunk c+1 landed; the 12 younger patch loads may stay in flight
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      __syncthreads();
+    }
+    transform_a(d);
+    gemm(lds + (g & 1) * U_BYTES, d, -1, std::false_type{});
+    ++g;
+    __syncthreads();                 // every wave is done with the last U buffer
+    const int nxt = unit + per_x;
+    const int e_cb = cb, e_tb = tb, e_f = f, e_ty = ty, e_tx = tx;
+    const bool e_valid = tvalid;
+    if (nxt < hi_u) {                // next unit's chunk 0 flies during the epilogue
+      set_unit(nxt);
+      issue_u(0, g & 1);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int e = 0; e < 12; ++e) d[e] = load_one(0, e);
+    }
+    char* scratch = lds + ((g - 1) & 1) * U_BYTES;
+    if (X6_EXP == 6) {
+      wf32x4 t = acc[0][0];
+#pragma unroll
+      for (int x = 0; x < 8; ++x)
+#pragma unroll
+        for (int c = 0; c < TC; ++c) t += acc[x][c];
+      if (t[0] + t[1] + t[2] + t[3] == 1.2345f && e_valid) p.y[0] = t[0];
+    } else {
+      // ---- output transform, row-split over the pair ----
+      // M rows 2 xh + a (a = 0, 1): acc[4 a + j]. Row partials of A^T M:
+      //   xh 0: p0 = M0 + M1, p1 = M1        xh 1: q0 = M2, q1 = -M2 - M3
+      // output row 0 = p0 + q0 (finished by xh 0), row 1 = p1 + q1 (xh 1):
+      // each wave sends the partial of the partner's row (xh 0: p1, xh 1: q0)
+      wf32x4* xch = (wf32x4*)scratch;                 // [wave][tc][j][lane]
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          xch[((wave * TC + tc) * 4 + j) * 64 + lane] = xh ? acc[j][tc] : acc[4 + j][tc];
+      __syncthreads();
+      wf32x4 t[TC][4];
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const wf32x4 other = xch[(((wave ^ 1) * TC + tc) * 4 + j) * 64 + lane];
+          t[tc][j] = xh ? other - acc[j][tc] - acc[4 + j][tc]      // p1 + q1
+                        : acc[j][tc] + acc[4 + j][tc] + other;    // p0 + q0
+        }
+      constexpr bool stats = ST;
+      const int oy = 2 * e_ty + xh, ox = 2 * e_tx;
+      const bool has_res = p.res != nullptr;
+      const int seg = (stats && e_valid) ? p.clip_seg[e_f / p.clip_frames] : 0;
+      bool buni = false;
+      int bseg = 0;
+      if constexpr (stats) {
+        const int ta = e_tb * NT, tz = min(e_tb * NT + NT - 1, p.n_tiles - 1);
+        const int fa = w_div(w_div(ta, p.m_tw, p.s_tw), p.m_th, p.s_th);
+        const int fz = w_div(w_div(tz, p.m_tw, p.s_tw), p.m_th, p.s_th);
+        bseg = p.clip_seg[fa / p.clip_frames];
+        buni = bseg == p.clip_seg[fz / p.clip_frames];
+      }
+      double s1[TC][4], s2[TC][4];
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc) {
+        const int co = e_cb * CT + tc * 16 + 4 * q;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s1[tc][k] = s2[tc][k] = 0.0;
+        if (co >= p.Cout || !e_valid || oy >= p.H) {
+          if (stats && !buni) w_commit_stats(p, lane, false, seg, co, s1[tc], s2[tc]);
+          continue;
+        }
+        const float4 b4 = *(const float4*)(p.bias + co);
+        const wf32x4 bias = (wf32x4){b4.x, b4.y, b4.z, b4.w};
+        wf32x4 o[2];
+        o[0] = t[tc][0] + t[tc][1] + t[tc][2] + bias;
+        o[1] = t[tc][1] - t[tc][2] - t[tc][3] + bias;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          if (ox + b >= p.W) continue;
+          const long long pix = ((long long)e_f * p.H + oy) * p.W + ox + b;
+          wf32x4 val = o[b];
+          if (has_res) {
+            const float4 r4 = *(const float4*)(p.res + pix * p.res_stride + co);
+            val += (wf32x4){r4.x, r4.y, r4.z, r4.w};
+          }
+          if (p.relu) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) val[k] = fmaxf(val[k], 0.f);
+          }
+          *(float4*)(p.y + pix * p.y_stride + co) = make_float4(val[0], val[1], val[2], val[3]);
+          if (stats) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              s1[tc][k] += (double)val[k];
+              s2[tc][k] += (double)val[k] * (double)val[k];
+            }
+          }
+        }
+        if (stats && !buni) w_commit_stats(p, lane, true, seg, co, s1[tc], s2[tc]);
+      }
+      if constexpr (stats) {
+        // every wave's lanes hold partial sums of 16 tiles' half-tiles; the
+        // block reduction adds all 8 waves' rows (w_block_stats, 8 waves)
+        if (buni) w_block_stats<TC, 8>(p, scratch, wave, tl, q, e_cb, bseg, s1, s2);
+      }
+    }
+    if (nxt >= hi_u) break;
+    unit = nxt;
+    // the exchange / statistics scratch is the buffer chunk 1 will DMA into:
+    // the barrier at the top of the loop orders them
+  }
+}
+
+// ===========================================================================
 // Temporal F(4, 3) for the stride-1 3x1x1 convs (see conv_winot_f32_kernel):
 // a tile = 4 output frames of one pixel, 6 GEMM steps per 16-channel chunk,
 // optional BN + ReLU of the input on load. U per chunk: 6 x CT rows of 128 B.
@@ -632,17 +921,31 @@ extern "C" {
 
 // Spatial F(2x2, 3x3) on bf16 MFMA (x6). variant 0 = TC 2 x 8 waves (128
 // tiles x 32 channels per block), 1 = TC 1 x 8 waves, 2 = TC 1 x 4 waves,
-// 3 = TC 2 x 4 waves (one wave per SIMD, software-pipelined steps).
+// 3 = TC 2 x 4 waves (one wave per SIMD, software-pipelined steps),
+// 4 / 5 = wave-pair x-split kernel (conv_wino_x6h_kernel) at TC 2 / 1.
 // U layout [Cin/16][n_cblocks][16][16 TC][8 chunks of 8 bf16] (x6_chunk).
 // Returns 0, a negative contract code, or the hipError_t.
 int rnb_wino_x6_launch(const WinoParams* pp, int variant, hipStream_t stream) {
   WinoParams p = *pp;
-  if (variant < 0 || variant > 3) return -1;
-  const int TC = (variant == 0 || variant == 3) ? 2 : 1, WAVES = variant >= 2 ? 4 : 8;
+  if (variant < 0 || variant > 5) return -1;
   if (p.F <= 0 || p.H <= 0 || p.W <= 0) return 0;
+  const bool st = p.out_stats != nullptr;
+  if (variant >= 4) {              // wave-pair x-split kernel: 64 tiles x 16 TC channels
+    const int TC = variant == 4 ? 2 : 1;
+    const int rc = x6_prepare(p, 2, 2, 16 * TC, 64, 16);
+    if (rc) return rc;
+    if (TC == 2) {
+      if (st) x6_launch_persistent(conv_wino_x6h_kernel<2, true>, p, 512, 1, stream);
+      else x6_launch_persistent(conv_wino_x6h_kernel<2>, p, 512, 1, stream);
+    } else {
+      if (st) x6_launch_persistent(conv_wino_x6h_kernel<1, true>, p, 512, 1, stream);
+      else x6_launch_persistent(conv_wino_x6h_kernel<1>, p, 512, 1, stream);
+    }
+    return (int)hipGetLastError();
+  }
+  const int TC = (variant == 0 || variant == 3) ? 2 : 1, WAVES = variant >= 2 ? 4 : 8;
   const int rc = x6_prepare(p, 2, 2, 16 * TC, 16 * WAVES, 16);
   if (rc) return rc;
-  const bool st = p.out_stats != nullptr;
   switch (variant) {
     case 0:
       if (st) x6_launch_persistent(conv_wino_x6_kernel<2, 8, true>, p, 512, 1, stream);

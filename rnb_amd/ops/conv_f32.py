@@ -75,10 +75,12 @@ WINOT_DEFAULT = WINOT_BASE + 1
 # parts, six bf16 products per fp32 product, fp32 accumulation; within fp32
 # rounding of the fp32-MFMA kernels). Spatial: 1050 = 32 channels x 128
 # tiles per block, 1051 / 1052 = 16 channels x 128 / 64 tiles, 1053 = 32
-# channels x 64 tiles (one wave per SIMD, pipelined); temporal:
+# channels x 64 tiles (one wave per SIMD, pipelined), 1054 / 1055 = 32 / 16
+# channels x 64 tiles with the GEMM positions split over a wave pair; temporal:
 # 1060 = 64 channels x 128 tiles, 1061 = 32 x 64.
 WINOX_BASE = 1050
-WINOX_TC = {WINOX_BASE + 0: 2, WINOX_BASE + 1: 1, WINOX_BASE + 2: 1, WINOX_BASE + 3: 2}
+WINOX_TC = {WINOX_BASE + 0: 2, WINOX_BASE + 1: 1, WINOX_BASE + 2: 1, WINOX_BASE + 3: 2,
+            WINOX_BASE + 4: 2, WINOX_BASE + 5: 1}
 WINOTX_BASE = 1060
 WINOTX_TC = {WINOTX_BASE + 0: 4, WINOTX_BASE + 1: 2}
 WINO_X6 = set(WINOX_TC) | set(WINOTX_TC)
@@ -252,8 +254,8 @@ class ConvLayerF32:
             cp, ct = self.geom.cout_p, 16 * tc
             main, rem = cp // ct * ct, cp % ct
             if main > 0 and rem > 0 and rem % 16 == 0:
-                # tail of 16 channels: variant 1 (TC 1, 128 tiles per block)
-                return [(0, main, tc, variant), (main, rem, 1, 1)]
+                # tail of 16 channels: TC 1 of the same kernel family
+                return [(0, main, tc, variant), (main, rem, 1, 5 if variant >= 4 else 1)]
             return [(0, cp, tc, variant)]
         tc, variant = WINO_TC[cid], cid - WINO_BASE
         cp, ct = self.geom.cout_p, 16 * tc

@@ -27,6 +27,8 @@ def tile_name(cid, f32=False):
         if cid in WINOTX_TC:
             return "x6t_%d" % (16 * WINOTX_TC[cid])
         if cid in WINOX_TC:
+            if cid in (1054, 1055):
+                return "x6h_%d" % (16 * WINOX_TC[cid])
             return "x6s_%d_%d" % (16 * WINOX_TC[cid], 64 if cid in (1052, 1053) else 128)
         if cid in WINOT_TC:
             return "wt4_%d" % (16 * WINOT_TC[cid])
