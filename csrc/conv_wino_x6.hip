@@ -54,43 +54,11 @@
 // buffer offset past every tensor (x_bytes <= 0x7FFFFF00): padding loads
 #define X6_OOB 0x80000000u
 
-typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
+#include "x6_common.h"
+
 typedef __bf16 wbf16x2 __attribute__((ext_vector_type(2)));
-typedef float wf32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int wu32x4 __attribute__((ext_vector_type(4)));
 
-// v_mfma_f32_16x16x32_bf16 sums 32 products per output; lane (col n, quad
-// q) supplies k = 8q .. 8q+7 of B and lane (row m, q) the same k of A. Each
-// lane keeps 4 channels (4q .. 4q+3 of the 16-channel chunk), so its 8 k
-// slots carry two bf16 parts of those 4 channels, and the six products
-// pair up into three MFMAs:
-//   (Ah | Am) x (Bh ; Bh) = Ah Bh + Am Bh
-//   (Ah | Al) x (Bm ; Bh) = Ah Bm + Al Bh
-//   (Ah | Am) x (Bl ; Bm) = Ah Bl + Am Bm
-typedef unsigned int wu32x8 __attribute__((ext_vector_type(8)));
-
-// B fragments of one GEMM step as one 8-register tuple
-//   R = (L01 L23 M01 M23 H01 H23 H01 H23)
-// so the three MFMA B operands are the overlapping quads R[0:4] = (Bl ; Bm),
-// R[2:6] = (Bm ; Bh) and R[4:8] = (Bh ; Bh): only H is stored twice.
-struct X6B {
-  wu32x8 r;
-};
-struct X6A {                  // A fragments of one GEMM step and channel group
-  wu32x4 hm, hl;
-};
-
-// upper halves of two fp32 bit patterns -> one bf16 pair (lo = a, hi = b)
-static __device__ __forceinline__ uint32_t x6_hi2(uint32_t a, uint32_t b) {
-  return __builtin_amdgcn_perm(b, a, 0x07060302u);
-}
-
-// exact 3-way split of 4 fp32 values (channels j = 0..3 of a B fragment) by
-// truncation: h = top 8 significant bits of x, m = top 8 of r = x - h (exact),
-// l = r - m (exact, <= 8 significant bits, so its truncation is exact too).
-// Per value pair: 4 v_and, 2 v_pk_add_f32, 3 v_perm (vs ~15 with RNE parts
-// rebuilt through shifts); the dropped products are still <= ~2^-22 |ab|
-// (profiles/r3_mfma_split.txt: as accurate as fp32 MFMA)
+// x6_split_exact, or the bottleneck experiment without the split VALU
 static __device__ __forceinline__ X6B x6_split(const wf32x4& v) {
   if constexpr (X6_EXP == 1) {
     const uint32_t a = __float_as_uint(v[0]), b = __float_as_uint(v[1]);
@@ -99,28 +67,7 @@ static __device__ __forceinline__ X6B x6_split(const wf32x4& v) {
     f.r = (wu32x8){a, b, c, d, a, b, c, d};
     return f;
   }
-  uint32_t H[2], M[2], L[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const wf32x2 x = (wf32x2){v[2 * k], v[2 * k + 1]};
-    const uint32_t xa = __float_as_uint(x[0]), xb = __float_as_uint(x[1]);
-    const wf32x2 h = (wf32x2){__uint_as_float(xa & 0xFFFF0000u), __uint_as_float(xb & 0xFFFF0000u)};
-    const wf32x2 r = x - h;
-    const uint32_t ra = __float_as_uint(r[0]), rb = __float_as_uint(r[1]);
-    const wf32x2 m = (wf32x2){__uint_as_float(ra & 0xFFFF0000u), __uint_as_float(rb & 0xFFFF0000u)};
-    const wf32x2 l = r - m;
-    H[k] = x6_hi2(xa, xb);
-    M[k] = x6_hi2(ra, rb);
-    L[k] = x6_hi2(__float_as_uint(l[0]), __float_as_uint(l[1]));
-  }
-  X6B f;
-  f.r = (wu32x8){L[0], L[1], M[0], M[1], H[0], H[1], H[0], H[1]};
-  return f;
-}
-
-static __device__ __forceinline__ wf32x4 x6_mma(const wu32x4& a, const wu32x4& b, const wf32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(wbf16x8, a),
-                                                 __builtin_bit_cast(wbf16x8, b), c, 0, 0, 0);
+  return x6_split_exact(v);
 }
 
 // the six products of one GEMM step into acc[tc] (3 MFMAs per channel
@@ -143,15 +90,6 @@ static __device__ __forceinline__ void x6_step(wf32x4 (&acc)[TC], const X6A (&a)
   for (int tc = 0; tc < TC; ++tc) acc[tc] = x6_mma(a[tc].hl, mh, acc[tc]);
 #pragma unroll
   for (int tc = 0; tc < TC; ++tc) acc[tc] = x6_mma(a[tc].hm, hh, acc[tc]);
-}
-
-// 16-B chunk permutation of a 128-B U row: logical chunk c = 2 q + half
-// (q = channel quad, half 0 = (Ah | Am), 1 = (Ah | Al)) lives at physical
-// chunk c ^ s(row >> 1 & 7), s = [0, 1, 0, 1, 6, 7, 6, 7], which makes the
-// ds_read_b128 fragment reads of every 16-lane group conflict free
-// (rows alternate between the two 128-B halves of the 64 banks)
-static __device__ __forceinline__ int x6_chunk(int c, int row) {
-  return c ^ ((0x76761010 >> (4 * ((row >> 1) & 7))) & 7);
 }
 
 // A fragments (weights) of GEMM step x for the lane's row frow / quad q

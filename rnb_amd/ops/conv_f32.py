@@ -89,6 +89,43 @@ WINO_TEMPORAL = set(WINOT_TC) | set(WINOTX_TC)
 WINO_ALL = WINO_SPATIAL | WINO_TEMPORAL
 # temporal F(4,3) pays off once most output frames see all 3 taps
 WINOT_MIN_T = 4
+# fp32 direct implicit-GEMM convs on the bf16 matrix cores (csrc/conv_x6.hip,
+# products split exactly into bf16 parts as the x6 Winograd kernels): config
+# X6D_BASE + i of rnb_conv_x6_launch; weight rows are padded by X6_ROW_SLACK
+# (>= the widest channel tile, 288)
+X6D_BASE = 1100
+X6_ROW_SLACK = 288
+
+
+def is_x6d(cid: int) -> bool:
+    from .native import kernels
+    return X6D_BASE <= cid < X6D_BASE + len(kernels().x6_configs)
+
+
+def x6_direct_weights(wmat: torch.Tensor) -> torch.Tensor:
+    """fp32 weight matrix [rows, K] (K % 16 == 0, k = tap * Cin_p + c) -> the
+    x6 direct kernel's split layout [K / 16][rows][8 chunks][8 bf16] as
+    int16: per 16-channel step and row, per channel quad q the chunks
+    (Ah | Am) and (Ah | Al) of the exact 3-way bf16 split (a = h + m + l),
+    chunk c = 2 q + half stored at c ^ _X6_S[(row % 16) >> 1] (x6_chunk)."""
+    rows, K = wmat.shape
+    assert K % 16 == 0, K
+    u32 = wmat.float().cpu()
+    h = u32.bfloat16()
+    r = u32 - h.float()                       # exact
+    m = r.bfloat16()
+    lo = (r - m.float()).bfloat16()           # exact: r - m has <= 8 bits
+    steps = K // 16
+
+    def lay(t):                               # -> [rows, steps, quad, 4]
+        return t.reshape(rows, steps, 4, 4)
+    hh, mm, ll = lay(h), lay(m), lay(lo)
+    chunks = torch.stack([torch.cat([hh, mm], -1), torch.cat([hh, ll], -1)], dim=-2)
+    logical = chunks.reshape(rows, steps, 8, 8)
+    sw = torch.tensor([_X6_S[(rr % 16) >> 1] for rr in range(rows)], dtype=torch.int64)
+    idx = torch.arange(8, dtype=torch.int64)[None, :] ^ sw[:, None]            # [rows, 8]
+    phys = logical.gather(2, idx[:, None, :, None].expand_as(logical))
+    return phys.permute(1, 0, 2, 3).contiguous().view(torch.int16)
 
 
 def x6_enabled() -> bool:
@@ -221,6 +258,20 @@ class ConvLayerF32:
         self.wino_ids = (WINO_SPATIAL if self.wino_ok else
                          WINO_TEMPORAL if self.winot_ok else set())
         self._wino_u: Dict[Tuple[int, int], torch.Tensor] = {}
+        self.k16 = pad_to(self.k_total, 16)
+        self._x6d = None                     # (split weights, bias) for the x6 direct kernel
+
+    def x6d_buffers(self):
+        """(split weight matrix [K16/16][rows][64] int16, bias [rows] fp32),
+        rows = Cout_p + X6_ROW_SLACK, built once."""
+        if self._x6d is None:
+            rows = self.geom.cout_p + X6_ROW_SLACK
+            w = torch.zeros(rows, self.k16, dtype=torch.float32)
+            w[:self.geom.cout, :self.k_total] = self.wmat[:self.geom.cout, :self.k_total].cpu()
+            b = torch.zeros(rows, dtype=torch.float32)
+            b[:self.geom.cout] = self.bias[:self.geom.cout].cpu()
+            self._x6d = (x6_direct_weights(w).to(self.device), b.to(self.device))
+        return self._x6d
 
     def wino_u(self, tc: int, m: int = 2, co0: int = 0, nco: Optional[int] = None,
                x6: bool = False) -> torch.Tensor:
@@ -268,6 +319,8 @@ class ConvLayerF32:
     def candidates(self):
         from .native import kernels
         c = list(range(len(kernels().f32_configs)))
+        if x6_enabled():
+            c += [X6D_BASE + i for i in range(len(kernels().x6_configs))]
         ids = self.wino_ids if x6_enabled() else self.wino_ids - WINO_X6
         return c + sorted(ids)
 
@@ -368,8 +421,9 @@ class ConvLayerF32:
         return tab
 
     def params(self, x: torch.Tensor, y: torch.Tensor, residual: Optional[torch.Tensor],
-               n0: int = 0, n1: Optional[int] = None):
-        """Launch parameters for clips [n0, n1) of the batch."""
+               n0: int = 0, n1: Optional[int] = None, x6: bool = False):
+        """Launch parameters for clips [n0, n1) of the batch (``x6``: for the
+        x6 direct kernel: split weights, K rounded to 16)."""
         from .native import ConvParams
         g = self.geom
         N, T, H, W, C = x.shape
@@ -400,6 +454,10 @@ class ConvLayerF32:
         p.w_rows = self.wmat.shape[0]
         p.ktab = self.ktab(T, H, W, x.device).data_ptr()
         p.row_mode = 0
+        if x6:
+            wx, bx = self.x6d_buffers()
+            p.w, p.bias = wx.data_ptr(), bx.data_ptr()
+            p.K_pad, p.w_rows = self.k16, bx.shape[0]
         return p
 
     def chunk_clips(self, x_shape, y_shape, res_stride: int = 0) -> int:
@@ -441,7 +499,10 @@ class ConvLayerF32:
                 cid = tuning.nearest(tkey, N * T * H * W)
             if cid is not None and cid in WINO_ALL and cid not in self.wino_ids:
                 cid = None
-            if cid is not None and cid not in WINO_ALL and cid >= len(_configs()):
+            if cid is not None and is_x6d(cid) and not x6_enabled():
+                cid = None
+            if (cid is not None and cid not in WINO_ALL and not is_x6d(cid)
+                    and cid >= len(_configs())):
                 cid = None
             if cid is None:
                 N, T, H, W, _ = x_shape
@@ -474,9 +535,13 @@ class ConvLayerF32:
             raise ValueError("%s: fused input/output BN needs a Winograd config" % self.name)
         step = self.chunk_clips(x.shape, y.shape,
                                 residual.shape[-1] if residual is not None else 0)
+        x6 = is_x6d(cid)
         for n0 in range(0, N, step):
-            k.conv_f32(self.params(x, y, residual, n0, min(N, n0 + step)), cid,
-                       stream.cuda_stream)
+            p = self.params(x, y, residual, n0, min(N, n0 + step), x6=x6)
+            if x6:
+                k.conv_x6(p, cid - X6D_BASE, stream.cuda_stream)
+            else:
+                k.conv_f32(p, cid, stream.cuda_stream)
 
     def autotune(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                  reps: int = 3) -> int:
@@ -486,7 +551,8 @@ class ConvLayerF32:
         tkey = self._tune_key(x.shape, x.device)
         cached = tuning.get(tkey)
         if cached is not None and (cached < len(kernels().f32_configs) or
-                                   cached in self.wino_ids):
+                                   cached in self.wino_ids or
+                                   (is_x6d(cached) and x6_enabled())):
             self._config[tuple(x.shape[:4])] = cached
             return cached
         y = torch.empty(self.out_shape(x.shape), dtype=torch.float32, device=x.device)

@@ -287,6 +287,11 @@ class Kernels:
         lib.rnb_conv_f32_config_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                                  ctypes.POINTER(ctypes.c_int)]
         lib.rnb_conv_f32_max_bytes.restype = ctypes.c_longlong
+        lib.rnb_conv_x6_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
+                                           ctypes.c_void_p]
+        lib.rnb_conv_x6_launch.restype = ctypes.c_int
+        lib.rnb_conv_x6_config_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                                ctypes.POINTER(ctypes.c_int)]
         lib.rnb_preprocess_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
                                            ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
@@ -313,6 +318,11 @@ class Kernels:
             lib.rnb_conv_f32_config_info(i, ctypes.byref(p), ctypes.byref(c))
             self.f32_configs.append((p.value, c.value))
         self.f32_max_bytes = lib.rnb_conv_f32_max_bytes()
+        self.x6_configs = []       # (pixel tile, channel tile) per x6 direct config
+        for i in range(lib.rnb_conv_x6_num_configs()):
+            p, c = ctypes.c_int(), ctypes.c_int()
+            lib.rnb_conv_x6_config_info(i, ctypes.byref(p), ctypes.byref(c))
+            self.x6_configs.append((p.value, c.value))
         self.configs = []          # (pixel tile, channel tile) per config id
         self.stages = []           # LDS staging depth per config id
         for i in range(lib.rnb_conv_num_configs()):
@@ -328,6 +338,10 @@ class Kernels:
     def conv_f32(self, params: ConvParams, config_id: int, stream: int) -> None:
         _check(self.lib.rnb_conv_f32_launch(ctypes.byref(params), config_id, stream),
                "conv_f32 (config %d)" % config_id)
+
+    def conv_x6(self, params: ConvParams, config_id: int, stream: int) -> None:
+        _check(self.lib.rnb_conv_x6_launch(ctypes.byref(params), config_id, stream),
+               "conv_x6 (config %d)" % config_id)
 
     def wino_f32(self, params: "WinoParams", variant: int, stream: int) -> None:
         _check(self.lib.rnb_wino_f32_launch(ctypes.byref(params), variant, stream),

@@ -34,6 +34,9 @@ def tile_name(cid, f32=False):
             return "wt4_%d" % (16 * WINOT_TC[cid])
         if cid in WINO_TC:
             return "wino%d%s" % (16 * WINO_TC[cid], "s" if cid in WINO_SPLIT else "")
+        from rnb_amd.ops.conv_f32 import X6D_BASE, is_x6d
+        if is_x6d(cid):
+            return "x6d_%dx%d" % k.x6_configs[cid - X6D_BASE]
         return "%dx%d" % k.f32_configs[cid]
     if cid >= len(k.configs):
         from rnb_amd.ops.conv import SPECIAL_NAMES

@@ -126,6 +126,66 @@ def test_f32_temporal_tap_skip_and_stem_exact(k, s, p, thw):
         assert torch.equal(y[..., :72].cpu(), ref), cfg
 
 
+def _x6d_ids():
+    from rnb_amd.ops.conv_f32 import X6D_BASE
+    return [X6D_BASE + i for i in range(12)]
+
+
+@pytest.mark.parametrize("cid", _x6d_ids())
+def test_x6_direct_every_config_exact_integers(cid):
+    """x6 direct kernel (csrc/conv_x6.hip): small integers split exactly into
+    their high bf16 part, so every config must match the fp64 conv bit for bit
+    (odd M tail, padded Cout, residual + ReLU epilogue, 3x3 padding)."""
+    from rnb_amd.ops.conv_f32 import is_x6d
+    if not is_x6d(cid):
+        pytest.skip("config not built")
+    layer = _layer(64, 150, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=True, integer=True)
+    x = _input(1, (2, 15, 13), 64, 64, integer=True)
+    res = _input(1, (2, 15, 13), layer.geom.cout_p, 150, integer=True, seed=3)
+    y = layer.forward_hip(x, res, config=cid)
+    torch.cuda.synchronize()
+    ref = _ref64(layer, x, res).float()
+    assert torch.equal(y[..., :150].cpu(), ref)
+    assert torch.all(y[..., 150:] == 0)
+
+
+@pytest.mark.parametrize("case", F32_CASES, ids=lambda c: "%dx%d_k%s_s%s" % (
+    c[0], c[1], "".join(map(str, c[2])), "".join(map(str, c[3]))))
+def test_x6_direct_matches_fp64(case):
+    """Every R(2+1)D conv shape through the x6 direct kernel (its widest and
+    a 4-wave-pair config) within 1e-5 of the fp64 conv, like the fp32-MFMA
+    kernel: the split products are fp32-accurate."""
+    from rnb_amd.ops.conv_f32 import X6D_BASE
+    cin, cout, k, s, p, thw = case
+    layer = _layer(cin, cout, k, s, p)
+    x = _input(2, thw, layer.geom.cin_p, cin)
+    ref = _ref64(layer, x)
+    scale = ref.abs().max().item()
+    for cid in (X6D_BASE + 0, X6D_BASE + 9, X6D_BASE + 5):
+        y = layer.forward_hip(x, config=cid)
+        torch.cuda.synchronize()
+        assert torch.all(y[..., cout:] == 0), "padding channels must be zero"
+        err = (y[..., :cout].double().cpu() - ref).abs().max().item()
+        assert err <= 1e-5 * scale, (cid, err, scale)
+
+
+@pytest.mark.parametrize("k,s,p,thw", [((3, 1, 1), (1, 1, 1), (1, 0, 0), (8, 9, 7)),
+                                       ((3, 1, 1), (2, 1, 1), (1, 0, 0), (4, 5, 6)),
+                                       ((3, 1, 1), (1, 1, 1), (1, 0, 0), (1, 7, 7)),
+                                       ((1, 7, 7), (1, 2, 2), (0, 3, 3), (2, 19, 17))])
+def test_x6_direct_temporal_tap_skip_and_stem_exact(k, s, p, thw):
+    """Temporal taps that read only padding are skipped per tile (T = 1: only
+    the centre tap); the stem's 3-channel 7x7 gather; exact on integers."""
+    cin = 3 if k == (1, 7, 7) else 40
+    layer = _layer(cin, 72, k, s, p, relu=False, integer=True)
+    x = _input(3, thw, layer.geom.cin_p, cin, integer=True)
+    ref = _ref64(layer, x).float()
+    for cid in _x6d_ids():
+        y = layer.forward_hip(x, config=cid)
+        torch.cuda.synchronize()
+        assert torch.equal(y[..., :72].cpu(), ref), cid
+
+
 def test_f32_batch_split_over_2gib():
     """conv2's 144-channel fp32 intermediate exceeds 2 GiB at 150 clips: the
     layer splits the launch into clip chunks (32-bit buffer offsets)."""
