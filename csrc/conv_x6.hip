@@ -35,6 +35,12 @@
 #include "x6_common.h"
 
 #define X6D_INVALID 0xFFFFFFF0u
+// bottleneck experiments (scripts/x6d_exp.py; results are garbage by design):
+// 1 no split VALU, 2 no MFMA, 3 no activation DMA after the prologue, 4 no
+// weight DMA after the prologue, 6 no epilogue, 7 no per-step wait + barrier
+#ifndef X6D_EXP
+#define X6D_EXP 0
+#endif
 
 // physical 16-B chunk of logical chunk c in a 64-B activation row r: rows
 // r, r + 4, r + 8, r + 12 share a bank quarter, g = [0, 3, 2, 1] keeps the
@@ -67,9 +73,38 @@ static __device__ __forceinline__ void x6d_dma16(const x6d_u32x4& rsrc, uint32_t
                : "memory");
 }
 
-template <int TP, int TC, int WP, int WC, int NS>
-__global__ __launch_bounds__(64 * WP * WC, 1)
-void conv_x6_kernel(const ConvF32Params p) {
+// training-mode BN statistics of the output, accumulated in the epilogue
+// (as the Winograd kernels' WinoParams.out_stats): per video and channel the
+// fp64 sum and sum of squares of the stored values
+struct X6DStats {
+  double* sums;          // [nseg][2][stats_c], zeroed by the caller
+  const int* clip_seg;   // [N]: video (segment) of each clip of this launch
+  int stats_c;
+};
+
+// sum over the 16 lanes of a DPP row (every lane gets it): quad swaps, then
+// the half-row and row mirrors
+static __device__ __forceinline__ float x6d_dpp_add(float v, int ctrl_sel) {
+  int t;
+  const int iv = __float_as_int(v);
+  switch (ctrl_sel) {
+    case 0: t = __builtin_amdgcn_update_dpp(iv, iv, 0xB1, 0xF, 0xF, false); break;   // [1,0,3,2]
+    case 1: t = __builtin_amdgcn_update_dpp(iv, iv, 0x4E, 0xF, 0xF, false); break;   // [2,3,0,1]
+    case 2: t = __builtin_amdgcn_update_dpp(iv, iv, 0x141, 0xF, 0xF, false); break;  // half mirror
+    default: t = __builtin_amdgcn_update_dpp(iv, iv, 0x140, 0xF, 0xF, false); break; // mirror
+  }
+  return v + __int_as_float(t);
+}
+static __device__ __forceinline__ float x6d_row16_sum(float v) {
+  v = x6d_dpp_add(v, 0);
+  v = x6d_dpp_add(v, 1);
+  v = x6d_dpp_add(v, 2);
+  return x6d_dpp_add(v, 3);
+}
+
+template <int TP, int TC, int WP, int WC, int NS, bool PIPE, int MINB, bool ST>
+__global__ __launch_bounds__(64 * WP * WC, MINB)
+void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
   constexpr int NW = WP * WC;
   constexpr int P_TILE = WP * TP * 16, C_TILE = WC * TC * 16;
   constexpr int ACT_BYTES = P_TILE * 64;            // 16 fp32 channels per pixel row
@@ -80,7 +115,7 @@ void conv_x6_kernel(const ConvF32Params p) {
   constexpr int W_INSTR = (W_TOTAL + NW - 1) / NW;
   constexpr int VM_STAGE = A_INSTR + W_INSTR;       // DMAs per lane per step
   static_assert(P_TILE % (16 * NW) == 0, "activation DMA split");
-  static_assert(NS == 2 || NS == 3, "2 or 3 LDS stages");
+  static_assert(PIPE ? (NS == 3 || NS == 4) : (NS == 2 || NS == 3), "LDS stages");
   __shared__ __attribute__((aligned(16))) char lds[NS * BUF];
 
   const int lane = threadIdx.x & 63;
@@ -134,6 +169,7 @@ void conv_x6_kernel(const ConvF32Params p) {
     char* base = lds + slot * BUF;
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) {
+      if (X6D_EXP == 3 && s >= NS - 1) break;
       const bool ok = (rmask[i] & ey) == ey;
       const uint32_t off = ok ? (uint32_t)(rbase[i] + ex) : X6D_INVALID;
       x6d_dma16(xr, off, base + (wave * A_INSTR + i) * 1024);
@@ -141,6 +177,7 @@ void conv_x6_kernel(const ConvF32Params p) {
     const uint32_t wbase = ((uint32_t)s * (uint32_t)p.w_rows + (uint32_t)c0) * 128u;
 #pragma unroll
     for (int j = 0; j < W_INSTR; ++j) {
+      if (X6D_EXP == 4 && s >= NS - 1) break;
       // waves past the last instruction repeat it (same bytes to the same
       // place), so every wave issues VM_STAGE DMAs per step
       const int instr = (W_TOTAL % NW == 0) ? wave + NW * j : min(wave + NW * j, W_TOTAL - 1);
@@ -160,27 +197,36 @@ void conv_x6_kernel(const ConvF32Params p) {
 
   const int a_chunk = x6d_swz(fq, frow) << 4;
   const int w_hm = x6_chunk(2 * fq, frow) << 4, w_hl = x6_chunk(2 * fq + 1, frow) << 4;
-  auto compute = [&](int slot) {
-    const char* ab = lds + slot * BUF;
-    const char* wb = ab + ACT_BYTES;
-    X6B bf[TP];
+  // B fragment tp of the step in `slot`: 4 channels of one pixel, split
+  auto load_b = [&](int slot, int tp) -> X6B {
+    const int row = (wp * TP + tp) * 16 + frow;
+    const x6f32x4 v = *(const x6f32x4*)(lds + slot * BUF + row * 64 + a_chunk);
+    if constexpr (X6D_EXP == 1) {
+      const uint32_t a = __float_as_uint(v[0]), b = __float_as_uint(v[1]);
+      const uint32_t c = __float_as_uint(v[2]), d = __float_as_uint(v[3]);
+      X6B f;
+      f.r = (wu32x8){a, b, c, d, a, b, c, d};
+      return f;
+    }
+    return x6_split_exact(v);
+  };
+  // the 3 TP MFMAs of channel tile tc of the step in `slot`
+  auto mma_tc = [&](int slot, int tc, const X6B (&bf)[TP]) {
+    const char* wrow = lds + slot * BUF + ACT_BYTES + ((wc * TC + tc) * 16 + frow) * 128;
+    const wu32x4 hm = *(const wu32x4*)(wrow + w_hm);
+    const wu32x4 hl = *(const wu32x4*)(wrow + w_hl);
+    if constexpr (X6D_EXP == 2) {
 #pragma unroll
-    for (int tp = 0; tp < TP; ++tp) {
-      const int row = (wp * TP + tp) * 16 + frow;
-      bf[tp] = x6_split_exact(*(const x6f32x4*)(ab + row * 64 + a_chunk));
+      for (int tp = 0; tp < TP; ++tp)
+        acc[tp][tc][0] += __uint_as_float(hm[0] ^ hl[1] ^ bf[tp].r[0] ^ bf[tp].r[3] ^ bf[tp].r[5]);
+      return;
     }
 #pragma unroll
-    for (int tc = 0; tc < TC; ++tc) {
-      const char* wrow = wb + ((wc * TC + tc) * 16 + frow) * 128;
-      const wu32x4 hm = *(const wu32x4*)(wrow + w_hm);
-      const wu32x4 hl = *(const wu32x4*)(wrow + w_hl);
+    for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = x6_mma(hm, x6_b_lm(bf[tp]), acc[tp][tc]);
 #pragma unroll
-      for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = x6_mma(hm, x6_b_lm(bf[tp]), acc[tp][tc]);
+    for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = x6_mma(hl, x6_b_mh(bf[tp]), acc[tp][tc]);
 #pragma unroll
-      for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = x6_mma(hl, x6_b_mh(bf[tp]), acc[tp][tc]);
-#pragma unroll
-      for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = x6_mma(hm, x6_b_hh(bf[tp]), acc[tp][tc]);
-    }
+    for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = x6_mma(hm, x6_b_hh(bf[tp]), acc[tp][tc]);
   };
 
   // K-step range: for a (KT x 1 x 1) conv whose tile lies inside one clip, a
@@ -206,25 +252,75 @@ void conv_x6_kernel(const ConvF32Params p) {
     }
   }
 
-  // prologue: steps s_begin .. s_begin + NS - 2 in flight, the first landed
+  // prologue: steps s_begin .. s_begin + NS - 2 in flight
 #pragma unroll
   for (int i = 0; i + 1 < NS; ++i)
     if (s_begin + i < s_end) issue(s_begin + i, i);
-  if (NS == 3 && s_begin + 1 < s_end) x6d_wait_vm<VM_STAGE>();
-  else x6d_wait_vm<0>();
-  x6d_barrier();
-  for (int s = s_begin; s < s_end; ++s) {
-    const int it = s - s_begin;
-    // slot (it + NS - 1) % NS was read in step s - 1, which every wave
-    // finished before the last barrier
-    if (s + NS - 1 < s_end) issue(s + NS - 1, (it + NS - 1) % NS);
-    compute(it % NS);
-    // step s + 1 landed in this wave (NS 3: step s + 2 stays in flight) ...
-    if (NS == 3 && s + 2 < s_end) x6d_wait_vm<VM_STAGE>();
+  if constexpr (!PIPE) {
+    // step s's fragments are read and split at its start; the wait at the
+    // end of step s - 1 retires step s (NS 3: step s + 1 stays in flight)
+    if (NS == 3 && s_begin + 1 < s_end) x6d_wait_vm<VM_STAGE>();
     else x6d_wait_vm<0>();
-    x6d_barrier();                  // ... and in every wave
+    x6d_barrier();
+    for (int s = s_begin; s < s_end; ++s) {
+      const int it = s - s_begin;
+      // slot (it + NS - 1) % NS was read in step s - 1, which every wave
+      // finished before the last barrier
+      if (s + NS - 1 < s_end) issue(s + NS - 1, (it + NS - 1) % NS);
+      X6B bf[TP];
+#pragma unroll
+      for (int tp = 0; tp < TP; ++tp) bf[tp] = load_b(it % NS, tp);
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc) mma_tc(it % NS, tc, bf);
+      if (X6D_EXP == 7 && s + 1 < s_end) continue;
+      if (NS == 3 && s + 2 < s_end) x6d_wait_vm<VM_STAGE>();
+      else x6d_wait_vm<0>();
+      x6d_barrier();
+    }
+  } else {
+    // software-pipelined: step s + 1's B fragments are read and split between
+    // step s's channel tiles, so the MFMAs never wait on a split. The wait at
+    // the end of step s - 1 retires step s + 1 (NS 4: step s + 2 may fly).
+    if (NS == 4 && s_begin + 2 < s_end) x6d_wait_vm<VM_STAGE>();
+    else x6d_wait_vm<0>();
+    x6d_barrier();
+    X6B bf[TP];
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp) bf[tp] = load_b(0, tp);
+    for (int s = s_begin; s < s_end; ++s) {
+      const int it = s - s_begin;
+      // slot (it + NS - 1) % NS: step s - 1 (W) and its B fragments (read in
+      // step s - 2) are done in every wave (last barrier)
+      if (s + NS - 1 < s_end) issue(s + NS - 1, (it + NS - 1) % NS);
+      const int cs = it % NS, ns = (it + 1) % NS;
+      const bool more = s + 1 < s_end;
+      X6B bn[TP];
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc) {
+        mma_tc(cs, tc, bf);
+        if (tc < TP && more) bn[tc] = load_b(ns, tc);
+      }
+#pragma unroll
+      for (int tp = TC; tp < TP; ++tp)
+        if (more) bn[tp] = load_b(ns, tp);
+#pragma unroll
+      for (int tp = 0; tp < TP; ++tp) bf[tp] = bn[tp];
+      if (X6D_EXP == 7 && s + 1 < s_end) continue;
+      if (NS == 4 && s + 3 < s_end) x6d_wait_vm<VM_STAGE>();
+      else x6d_wait_vm<0>();
+      x6d_barrier();
+    }
   }
 
+  if (X6D_EXP == 6) {                // every accumulator stays live, no stores
+    x6f32x4 t = acc[0][0];
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp)
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc) t += acc[tp][tc];
+    if (t[0] + t[1] + t[2] + t[3] == 1.2345f) p.y[0] = t[0];
+    return;
+  }
   // ---- epilogue: (+ residual) (+ ReLU) -> fp32, one 16-B store per tile ----
   const uint32_t y_bytes = (uint32_t)p.M * (uint32_t)p.y_stride * 4u;
   const __amdgpu_buffer_rsrc_t yr =
@@ -233,29 +329,127 @@ void conv_x6_kernel(const ConvF32Params p) {
   const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(has_res ? p.res : p.y), (short)0,
       has_res ? (uint32_t)p.M * (uint32_t)p.res_stride * 4u : 0u, 0x00020000);
+  if constexpr (!ST) {
 #pragma unroll
-  for (int tp = 0; tp < TP; ++tp) {
-    const int m = p0 + (wp * TP + tp) * 16 + frow;
-    x6f32x4 r[TC];
+    for (int tp = 0; tp < TP; ++tp) {
+      const int m = p0 + (wp * TP + tp) * 16 + frow;
+      x6f32x4 r[TC];
 #pragma unroll
-    for (int tc = 0; tc < TC; ++tc) {
-      const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
-      const bool ok = has_res && m < p.M && c < p.Cout_p;
-      r[tc] = has_res ? __builtin_amdgcn_raw_buffer_load_b128(
-                            rr, ok ? (uint32_t)(m * p.res_stride + c) * 4u : X6D_INVALID, 0, 0)
-                      : (x6f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int tc = 0; tc < TC; ++tc) {
-      const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
-      const bool ok = m < p.M && c < p.Cout_p;
-      x6f32x4 v = acc[tp][tc] + r[tc];
-      if (p.relu) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+      for (int tc = 0; tc < TC; ++tc) {
+        const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
+        const bool ok = has_res && m < p.M && c < p.Cout_p;
+        r[tc] = has_res ? __builtin_amdgcn_raw_buffer_load_b128(
+                              rr, ok ? (uint32_t)(m * p.res_stride + c) * 4u : X6D_INVALID, 0, 0)
+                        : (x6f32x4){0.f, 0.f, 0.f, 0.f};
       }
-      __builtin_amdgcn_raw_buffer_store_b128(
-          v, yr, ok ? (uint32_t)(m * p.y_stride + c) * 4u : X6D_INVALID, 0, 0);
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc) {
+        const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
+        const bool ok = m < p.M && c < p.Cout_p;
+        x6f32x4 v = acc[tp][tc] + r[tc];
+        if (p.relu) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v, yr, ok ? (uint32_t)(m * p.y_stride + c) * 4u : X6D_INVALID, 0, 0);
+      }
+    }
+  } else {
+    // channel tiles outer (one tile's sums live at a time). Rows are
+    // clip-major, so a block's videos are the contiguous range seg_lo ..
+    // seg_hi. One video (the common case): each lane sums its TP rows, the 16
+    // lanes of a channel quad reduce by shuffles, one LDS add per channel and
+    // wave. Several videos: LDS adds per row into per-video slots. Then one
+    // fp64 atomic per video, channel and statistic per block.
+    constexpr int NT = 64 * NW;
+    int na, nz, t_, h_, w_;
+    f32_decode_row(p, p0, na, t_, h_, w_);
+    f32_decode_row(p, min(p0 + P_TILE, p.M) - 1, nz, t_, h_, w_);
+    const int seg_lo = __builtin_amdgcn_readfirstlane(st.clip_seg[__builtin_amdgcn_readfirstlane(na)]);
+    const int seg_hi = __builtin_amdgcn_readfirstlane(st.clip_seg[__builtin_amdgcn_readfirstlane(nz)]);
+    const int nseg = seg_hi - seg_lo + 1;
+    const bool uni = nseg == 1;
+    const bool in_lds = nseg * C_TILE * 16 <= NS * BUF;
+    double* red = (double*)lds;                       // [nseg][C_TILE][2]
+    if (in_lds)
+      for (int i = threadIdx.x; i < nseg * C_TILE * 2; i += NT) red[i] = 0.0;
+    __syncthreads();                                  // no DMA in flight here
+#pragma unroll
+    for (int tc = 0; tc < TC; ++tc) {
+      const int cl = (wc * TC + tc) * 16 + 4 * fq;
+      const int c = c0 + cl;
+      x6f32x4 r[TP];
+#pragma unroll
+      for (int tp = 0; tp < TP; ++tp) {
+        const int m = p0 + (wp * TP + tp) * 16 + frow;
+        const bool ok = has_res && m < p.M && c < p.Cout_p;
+        r[tp] = has_res ? __builtin_amdgcn_raw_buffer_load_b128(
+                              rr, ok ? (uint32_t)(m * p.res_stride + c) * 4u : X6D_INVALID, 0, 0)
+                        : (x6f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+      // lane partials over its TP rows in fp32 (<= 4 values), the 16-lane
+      // reduction in fp32 by DPP, everything after in fp64
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int tp = 0; tp < TP; ++tp) {
+        const int m = p0 + (wp * TP + tp) * 16 + frow;
+        const bool ok = m < p.M && c < p.Cout_p;
+        x6f32x4 v = acc[tp][tc] + r[tp];
+        if (p.relu) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v, yr, ok ? (uint32_t)(m * p.y_stride + c) * 4u : X6D_INVALID, 0, 0);
+        if (!ok) continue;
+        if (uni) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            s1[j] += v[j];
+            s2[j] = fmaf(v[j], v[j], s2[j]);
+          }
+        } else {
+          int n, tt, hh, ww;
+          f32_decode_row(p, m, n, tt, hh, ww);
+          const int sg = st.clip_seg[n];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const double a = (double)v[j], b = (double)v[j] * (double)v[j];
+            if (in_lds) {
+              atomicAdd(red + ((size_t)(sg - seg_lo) * C_TILE + cl + j) * 2, a);
+              atomicAdd(red + ((size_t)(sg - seg_lo) * C_TILE + cl + j) * 2 + 1, b);
+            } else {
+              atomicAdd(st.sums + ((size_t)sg * 2) * st.stats_c + c + j, a);
+              atomicAdd(st.sums + ((size_t)sg * 2 + 1) * st.stats_c + c + j, b);
+            }
+          }
+        }
+      }
+      if (uni) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s1[j] = x6d_row16_sum(s1[j]);
+          s2[j] = x6d_row16_sum(s2[j]);
+        }
+        if (frow == 0 && c < p.Cout_p) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            atomicAdd(red + (cl + j) * 2, (double)s1[j]);
+            atomicAdd(red + (cl + j) * 2 + 1, (double)s2[j]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (in_lds) {
+      for (int i = threadIdx.x; i < nseg * C_TILE; i += NT) {
+        const int sg = seg_lo + i / C_TILE, c = c0 + i % C_TILE;
+        if (c < p.Cout_p) {
+          atomicAdd(st.sums + ((size_t)sg * 2) * st.stats_c + c, red[i * 2]);
+          atomicAdd(st.sums + ((size_t)sg * 2 + 1) * st.stats_c + c, red[i * 2 + 1]);
+        }
+      }
     }
   }
 }
@@ -265,24 +459,35 @@ void conv_x6_kernel(const ConvF32Params p) {
 // ---------------------------------------------------------------------------
 struct ConvX6Config {
   int p_tile, c_tile, threads;
-  void (*kernel)(const ConvF32Params);
+  void (*kernel)(const ConvF32Params, const X6DStats);
+  void (*kernel_st)(const ConvF32Params, const X6DStats);    // + epilogue BN statistics
 };
 
-#define X6DCFG(TP, TC, WP, WC, NS) \
-  {WP * TP * 16, WC * TC * 16, 64 * WP * WC, conv_x6_kernel<TP, TC, WP, WC, NS>}
+#define X6DCFG(TP, TC, WP, WC, NS, PIPE, MINB)                                        \
+  {WP * TP * 16, WC * TC * 16, 64 * WP * WC,                                           \
+   conv_x6_kernel<TP, TC, WP, WC, NS, PIPE, MINB, false>,                              \
+   conv_x6_kernel<TP, TC, WP, WC, NS, PIPE, MINB, true>}
+// (profiles/r3_x6d_sweep_v1.txt: 2 LDS stages beat 3 on every shape, and the
+// pipelined variant wins only where the split is a large share)
 static const ConvX6Config kX6Configs[] = {
-    X6DCFG(4, 9, 8, 1, 3),   // 0: 512 px x 144 ch (conv2 spatial; 288/576/1152 = k x 144)
-    X6DCFG(2, 9, 8, 1, 3),   // 1: 256 px x 144 ch
-    X6DCFG(4, 8, 8, 1, 3),   // 2: 512 px x 128 ch
-    X6DCFG(4, 4, 8, 1, 3),   // 3: 512 px x  64 ch (conv2 temporal)
-    X6DCFG(2, 8, 8, 1, 3),   // 4: 256 px x 128 ch
-    X6DCFG(2, 4, 8, 1, 3),   // 5: 256 px x  64 ch
-    X6DCFG(4, 6, 8, 1, 3),   // 6: 512 px x  96 ch (stem: 83 channels)
-    X6DCFG(2, 6, 8, 1, 3),   // 7: 256 px x  96 ch
-    X6DCFG(1, 8, 8, 1, 3),   // 8: 128 px x 128 ch (few pixels)
-    X6DCFG(2, 9, 4, 2, 3),   // 9: 128 px x 288 ch
-    X6DCFG(4, 9, 8, 1, 2),   // 10: 512 px x 144 ch, 2 stages
-    X6DCFG(2, 8, 4, 2, 3),   // 11: 128 px x 256 ch
+    X6DCFG(4, 9, 8, 1, 2, false, 1),   // 0: 512 px x 144 ch (conv2/3/4/5 spatial: k x 144)
+    X6DCFG(3, 9, 8, 1, 2, false, 1),   // 1: 384 px x 144 ch
+    X6DCFG(2, 9, 8, 1, 2, false, 1),   // 2: 256 px x 144 ch
+    X6DCFG(2, 9, 8, 1, 2, false, 2),   // 3: 256 px x 144 ch, 2 blocks per CU
+    X6DCFG(4, 8, 8, 1, 2, false, 1),   // 4: 512 px x 128 ch
+    X6DCFG(2, 8, 8, 1, 2, false, 2),   // 5: 256 px x 128 ch, 2 blocks per CU
+    X6DCFG(1, 8, 8, 1, 2, false, 2),   // 6: 128 px x 128 ch, 2 blocks per CU (few pixels)
+    X6DCFG(4, 4, 8, 1, 2, false, 1),   // 7: 512 px x  64 ch (conv2 temporal)
+    X6DCFG(2, 4, 8, 1, 2, false, 2),   // 8: 256 px x  64 ch, 2 blocks per CU
+    X6DCFG(4, 6, 8, 1, 2, false, 1),   // 9: 512 px x  96 ch (stem: 83 channels)
+    X6DCFG(2, 6, 8, 1, 2, false, 2),   // 10: 256 px x  96 ch, 2 blocks per CU
+    X6DCFG(4, 9, 8, 1, 3, false, 1),   // 11: 512 px x 144 ch, 3 stages
+    X6DCFG(1, 8, 8, 1, 3, false, 1),   // 12: 128 px x 128 ch, 3 stages
+    X6DCFG(2, 4, 8, 1, 3, false, 1),   // 13: 256 px x  64 ch, 3 stages
+    X6DCFG(4, 8, 8, 1, 3, true, 1),    // 14: 512 px x 128 ch, pipelined
+    X6DCFG(4, 6, 8, 1, 3, true, 1),    // 15: 512 px x  96 ch, pipelined
+    X6DCFG(4, 9, 8, 1, 3, true, 1),    // 16: 512 px x 144 ch, pipelined
+    X6DCFG(2, 4, 4, 2, 2, false, 3),   // 17: 128 px x 128 ch, 4 waves, 3 blocks per CU
 };
 static const int kNumX6Configs = sizeof(kX6Configs) / sizeof(kX6Configs[0]);
 
@@ -299,8 +504,11 @@ int rnb_conv_x6_config_info(int id, int* p_tile, int* c_tile) {
 
 // p.w = split weights [K_pad / 16][w_rows][8 chunks x 8 bf16] (x6_chunk
 // order per row), p.K_pad = K rounded up to 16, p.ktab >= K_pad / 4 entries.
+// sums (nullable): add each video's per-channel sum and sum of squares of
+// the output to sums[clip_seg[clip]][2][stats_c] (fp64, channels < Cout_p).
 // Returns 0, a negative contract code, or the hipError_t of the launch.
-int rnb_conv_x6_launch(const ConvF32Params* pp, int config_id, hipStream_t stream) {
+int rnb_conv_x6_launch_stats(const ConvF32Params* pp, int config_id, hipStream_t stream,
+                             double* sums, const int* clip_seg, int stats_c) {
   if (config_id < 0 || config_id >= kNumX6Configs) return -1;
   ConvF32Params p = *pp;
   const ConvX6Config& cfg = kX6Configs[config_id];
@@ -326,8 +534,18 @@ int rnb_conv_x6_launch(const ConvF32Params* pp, int config_id, hipStream_t strea
   if (blocks > 0x7FFFFFFF) return -7;
   if (p.n_ctiles * cfg.c_tile > p.w_rows) return -8;
   if (!p.ktab) return -9;
-  hipLaunchKernelGGL(cfg.kernel, dim3((unsigned)blocks), dim3(cfg.threads), 0, stream, p);
+  if (sums && (!clip_seg || stats_c < p.Cout_p)) return -12;
+  X6DStats st;
+  st.sums = sums;
+  st.clip_seg = clip_seg;
+  st.stats_c = stats_c;
+  hipLaunchKernelGGL(sums ? cfg.kernel_st : cfg.kernel, dim3((unsigned)blocks), dim3(cfg.threads),
+                     0, stream, p, st);
   return (int)hipGetLastError();
+}
+
+int rnb_conv_x6_launch(const ConvF32Params* pp, int config_id, hipStream_t stream) {
+  return rnb_conv_x6_launch_stats(pp, config_id, stream, nullptr, nullptr, 0);
 }
 
 }  // extern "C"

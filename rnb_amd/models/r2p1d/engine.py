@@ -182,6 +182,9 @@ class R2P1DEngine:
             # reference numerics: conv (unfolded) -> BN with batch statistics
             # -> (+ residual) -> ReLU
             layer = self._conv(conv, None, False, name, src, dst, cin_pad, cout_pad)
+            if self.f32 and os.environ.get("RNB_BN_EPILOGUE_STATS", "1") == "1":
+                # this conv's epilogue accumulates the BN statistics: tune it so
+                layer.tune_with_stats = True
             bnop = BatchNormBatch(bn, layer.geom.cout_p, self.device)
             self.ops.append(PlanOp("conv", layer, src, dst, res, bn=bnop, bn_relu=relu))
         else:

@@ -259,6 +259,9 @@ class ConvLayerF32:
                          WINO_TEMPORAL if self.winot_ok else set())
         self._wino_u: Dict[Tuple[int, int], torch.Tensor] = {}
         self.k16 = pad_to(self.k_total, 16)
+        # the conv runs with out_stats (training-mode BN after it): autotune
+        # only the configs that accumulate them, timed with the statistics on
+        self.tune_with_stats = False
         self._x6d = None                     # (split weights, bias) for the x6 direct kernel
 
     def x6d_buffers(self):
@@ -483,7 +486,8 @@ class ConvLayerF32:
         return best
 
     def _tune_key(self, x_shape, device) -> str:
-        return tuning.make_key("f32", self.geom, tuple(x_shape[:4]), _device_name(device))
+        return tuning.make_key("f32st" if self.tune_with_stats else "f32", self.geom,
+                               tuple(x_shape[:4]), _device_name(device))
 
     def config_for(self, x_shape) -> int:
         """Tile config for this input shape: tuned (this layer, or any layer of
@@ -531,14 +535,27 @@ class ConvLayerF32:
                                   residual[n0:n1] if residual is not None else None, cid,
                                   stream, aff, ost)
             return
-        if in_affine is not None or out_stats is not None:
-            raise ValueError("%s: fused input/output BN needs a Winograd config" % self.name)
+        x6 = is_x6d(cid)
+        if in_affine is not None or (out_stats is not None and not x6):
+            raise ValueError("%s: fused input BN needs a temporal Winograd config, output BN "
+                             "statistics a Winograd or x6 direct config" % self.name)
+        if out_stats is not None:
+            sums, clip_seg = out_stats
+            if (sums.dim() != 3 or sums.shape[1] != 2 or sums.shape[2] < self.geom.cout_p
+                    or sums.dtype != torch.float64 or not sums.is_contiguous()
+                    or clip_seg.dtype != torch.int32 or clip_seg.numel() != N
+                    or not clip_seg.is_contiguous()):
+                raise ValueError("%s: output BN sums %s / clip_seg %s do not match y %s"
+                                 % (self.name, tuple(sums.shape), tuple(clip_seg.shape),
+                                    tuple(y.shape)))
         step = self.chunk_clips(x.shape, y.shape,
                                 residual.shape[-1] if residual is not None else 0)
-        x6 = is_x6d(cid)
         for n0 in range(0, N, step):
             p = self.params(x, y, residual, n0, min(N, n0 + step), x6=x6)
-            if x6:
+            if x6 and out_stats is not None:
+                k.conv_x6(p, cid - X6D_BASE, stream.cuda_stream, out_stats[0].data_ptr(),
+                          out_stats[1].data_ptr() + 4 * n0, out_stats[0].shape[2])
+            elif x6:
                 k.conv_x6(p, cid - X6D_BASE, stream.cuda_stream)
             else:
                 k.conv_f32(p, cid, stream.cuda_stream)
@@ -559,17 +576,23 @@ class ConvLayerF32:
         stream = torch.cuda.current_stream(x.device)
         best, best_t = None, None
         verbose = os.environ.get("RNB_TUNE_VERBOSE") == "1"
-        for cid in self.candidates():
+        cands, ost = self.candidates(), None
+        if self.tune_with_stats:
+            cands = [c for c in cands if c in WINO_ALL or is_x6d(c)] or cands
+            ost = (torch.zeros((1, 2, self.geom.cout_p), dtype=torch.float64, device=x.device),
+                   torch.zeros(x.shape[0], dtype=torch.int32, device=x.device))
+        for cid in cands:
             if verbose:
                 print("[tune] %s x=%s res=%s cid=%d" % (
                     self.name, tuple(x.shape), None if residual is None else
                     tuple(residual.shape), cid), flush=True)
-            self._launch_all(x, y, residual, cid, stream)       # warm
+            o = ost if ost is not None and (cid in WINO_ALL or is_x6d(cid)) else None
+            self._launch_all(x, y, residual, cid, stream, out_stats=o)       # warm
             start = torch.cuda.Event(enable_timing=True)
             end = torch.cuda.Event(enable_timing=True)
             start.record(stream)
             for _ in range(reps):
-                self._launch_all(x, y, residual, cid, stream)
+                self._launch_all(x, y, residual, cid, stream, out_stats=o)
             end.record(stream)
             end.synchronize()
             t = start.elapsed_time(end) / reps
@@ -583,7 +606,8 @@ class ConvLayerF32:
     def emits_output_stats(self, x_shape) -> bool:
         """True when this conv's kernel for ``x_shape`` accumulates its output's
         per-video BN sums in the epilogue (``forward_hip(out_stats=...)``)."""
-        return self.config_for(x_shape) in WINO_ALL
+        cid = self.config_for(x_shape)
+        return cid in WINO_ALL or is_x6d(cid)
 
     def accepts_input_affine(self, x_shape) -> bool:
         """True when this conv's kernel for ``x_shape`` can apply its input's
@@ -598,7 +622,7 @@ class ConvLayerF32:
         here on load (temporal Winograd configs only). ``out_stats`` = (sums
         fp64 [nseg, 2, >=Cout_p] zeroed, clip_seg): the epilogue adds each
         video's per-channel sum and sum of squares of the output (Winograd
-        configs only)."""
+        and x6 direct configs)."""
         if x.dtype != torch.float32 or not x.is_contiguous():
             raise ValueError("%s: expected contiguous fp32 NDHWC input" % self.name)
         y = out if out is not None else torch.empty(self.out_shape(x.shape),

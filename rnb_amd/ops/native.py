@@ -290,6 +290,10 @@ class Kernels:
         lib.rnb_conv_x6_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
                                            ctypes.c_void_p]
         lib.rnb_conv_x6_launch.restype = ctypes.c_int
+        lib.rnb_conv_x6_launch_stats.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
+                                                 ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_int]
+        lib.rnb_conv_x6_launch_stats.restype = ctypes.c_int
         lib.rnb_conv_x6_config_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                                 ctypes.POINTER(ctypes.c_int)]
         lib.rnb_preprocess_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
@@ -339,8 +343,12 @@ class Kernels:
         _check(self.lib.rnb_conv_f32_launch(ctypes.byref(params), config_id, stream),
                "conv_f32 (config %d)" % config_id)
 
-    def conv_x6(self, params: ConvParams, config_id: int, stream: int) -> None:
-        _check(self.lib.rnb_conv_x6_launch(ctypes.byref(params), config_id, stream),
+    def conv_x6(self, params: ConvParams, config_id: int, stream: int, sums: int = 0,
+                clip_seg: int = 0, stats_c: int = 0) -> None:
+        """x6 direct conv; ``sums`` (fp64 [nseg][2][stats_c] device pointer, with
+        ``clip_seg`` int32 [N]): add the output's per-video BN sums."""
+        _check(self.lib.rnb_conv_x6_launch_stats(ctypes.byref(params), config_id, stream,
+                                                 sums or None, clip_seg or None, stats_c),
                "conv_x6 (config %d)" % config_id)
 
     def wino_f32(self, params: "WinoParams", variant: int, stream: int) -> None:

@@ -23,5 +23,5 @@ for cfg in $CFGS; do
     echo "cfg $cfg pass $i rc=$rc $(grep -h 'config' $d.log | tail -1)"
     if [ $rc -ne 0 ]; then tail -3 $d.log; fi
   done
-  echo "== cfg $cfg"; KNAME=conv_wino python scripts/pmc_summary.py $OUT/c${cfg}
+  echo "== cfg $cfg"; KNAME=${KNAME:-conv_} python scripts/pmc_summary.py $OUT/c${cfg}
 done

@@ -14,6 +14,7 @@
 #   layers[:CLIPS]        per-conv table of the fp32 R(2+1)D-34 forward (autotuned)
 #   wino[:CLIPS]          every Winograd variant per layer shape (fp32)
 #   x6exp                 x6 Winograd bottleneck experiments (scripts/x6_exp.py)
+#   x6dexp                x6 direct-conv bottleneck experiments (scripts/x6d_exp.py)
 #   bnbreak[:CLIPS]       kernel breakdown of one graphed batch-BN forward (rocprofv3)
 #   pmc:LAYER:CFGS        per-dispatch PMC passes of one conv (scripts/gpu_pmc_conv.sh)
 #   fold:N                bench.py --gpus N through torchrun, all ranks folded onto GPU 0
@@ -54,6 +55,8 @@ for step in "$@"; do
     wino) run wino 400 python scripts/profile_layers.py --depth 34 --clips "${arg:-128}" \
             --dtype fp32 --list-wino --reps 5 ;;
     x6exp) run x6exp 300 python -u scripts/x6_exp.py run ;;
+    x6dexp) run x6dexp 300 python -u scripts/x6d_exp.py run ;;
+    x6dsweep) run x6dsweep 300 python -u scripts/x6d_exp.py sweep ;;
     bnbreak)
       rm -rf gpurun_out/bnbreak
       run bnbreak 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/bnbreak -o run \

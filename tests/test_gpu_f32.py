@@ -128,7 +128,7 @@ def test_f32_temporal_tap_skip_and_stem_exact(k, s, p, thw):
 
 def _x6d_ids():
     from rnb_amd.ops.conv_f32 import X6D_BASE
-    return [X6D_BASE + i for i in range(12)]
+    return [X6D_BASE + i for i in range(24)]
 
 
 @pytest.mark.parametrize("cid", _x6d_ids())
@@ -161,7 +161,7 @@ def test_x6_direct_matches_fp64(case):
     x = _input(2, thw, layer.geom.cin_p, cin)
     ref = _ref64(layer, x)
     scale = ref.abs().max().item()
-    for cid in (X6D_BASE + 0, X6D_BASE + 9, X6D_BASE + 5):
+    for cid in (X6D_BASE + 0, X6D_BASE + 9, X6D_BASE + 5, X6D_BASE + 12, X6D_BASE + 14):
         y = layer.forward_hip(x, config=cid)
         torch.cuda.synchronize()
         assert torch.all(y[..., cout:] == 0), "padding channels must be zero"
@@ -180,7 +180,8 @@ def test_x6_direct_temporal_tap_skip_and_stem_exact(k, s, p, thw):
     layer = _layer(cin, 72, k, s, p, relu=False, integer=True)
     x = _input(3, thw, layer.geom.cin_p, cin, integer=True)
     ref = _ref64(layer, x).float()
-    for cid in _x6d_ids():
+    from rnb_amd.ops.conv_f32 import is_x6d
+    for cid in [c for c in _x6d_ids() if is_x6d(c)]:
         y = layer.forward_hip(x, config=cid)
         torch.cuda.synchronize()
         assert torch.equal(y[..., :72].cpu(), ref), cid
@@ -508,6 +509,34 @@ def test_winograd_epilogue_stats_match_fp64_sums(kind):
             got = sums[v, :, :layer.geom.cout].cpu()
             assert torch.allclose(got[0], seg.sum(0), rtol=1e-9, atol=1e-6), (cid, v)
             assert torch.allclose(got[1], (seg * seg).sum(0), rtol=1e-9, atol=1e-6), (cid, v)
+
+
+@pytest.mark.parametrize("shape,kern", [((7, 4, 20, 28), (1, 3, 3)), ((9, 2, 7, 7), (3, 1, 1)),
+                                         ((5, 1, 7, 7), (1, 3, 3))])
+def test_x6_direct_epilogue_stats_match_fp64_sums(shape, kern):
+    """Per-video BN sums from the x6 direct epilogue (one-video blocks: lane
+    sums + shuffles + one atomic per channel per block; blocks over several
+    videos: per-row LDS adds into per-video slots) equal fp64 sums of the
+    output for every config, with a zero-clip video and clips of 49 rows
+    (several videos per 16-row tile)."""
+    from rnb_amd.ops.conv_f32 import is_x6d
+    pad = (0, 1, 1) if kern == (1, 3, 3) else (1, 0, 0)
+    layer = _layer(64, 144, kern, (1, 1, 1), pad, relu=False)
+    n = shape[0]
+    seg = sorted([0, 0, 2] + [3] * (n - 3))
+    offs = [0] + [sum(1 for v in seg if v <= k) for k in range(4)]
+    clip_seg = torch.tensor(seg, dtype=torch.int32, device=DEV)
+    x = _input(n, shape[1:], 64, 64)
+    for cid in [c for c in _x6d_ids() if is_x6d(c)]:
+        sums = torch.zeros((4, 2, layer.geom.cout_p), dtype=torch.float64, device=DEV)
+        y = layer.forward_hip(x, config=cid, out_stats=(sums, clip_seg))
+        torch.cuda.synchronize()
+        yd = y[..., :layer.geom.cout].double().cpu()
+        for v in range(4):
+            part = yd[offs[v]:offs[v + 1]].reshape(-1, layer.geom.cout)
+            got = sums[v, :, :layer.geom.cout].cpu()
+            assert torch.allclose(got[0], part.sum(0), rtol=1e-9, atol=1e-6), (cid, v)
+            assert torch.allclose(got[1], (part * part).sum(0), rtol=1e-9, atol=1e-6), (cid, v)
 
 
 def test_deferred_batch_bn_into_temporal_winograd_matches_separate_apply(monkeypatch):
