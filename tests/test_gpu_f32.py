@@ -535,8 +535,11 @@ def test_x6_direct_epilogue_stats_match_fp64_sums(shape, kern):
         for v in range(4):
             part = yd[offs[v]:offs[v + 1]].reshape(-1, layer.geom.cout)
             got = sums[v, :, :layer.geom.cout].cpu()
-            assert torch.allclose(got[0], part.sum(0), rtol=1e-9, atol=1e-6), (cid, v)
-            assert torch.allclose(got[1], (part * part).sum(0), rtol=1e-9, atol=1e-6), (cid, v)
+            # lane partials (<= 4 rows) and the 16-lane reduction are fp32:
+            # bounded by a few fp32 ulps of the sum of magnitudes
+            tol1 = 1e-6 * part.abs().sum(0) + 1e-9
+            assert ((got[0] - part.sum(0)).abs() <= tol1).all(), (cid, v)
+            assert torch.allclose(got[1], (part * part).sum(0), rtol=1e-6, atol=1e-9), (cid, v)
 
 
 def test_deferred_batch_bn_into_temporal_winograd_matches_separate_apply(monkeypatch):
