@@ -109,10 +109,13 @@ def parse_args(argv=None):
                          "replicas: 386/483/572/463/511 videos/s, "
                          "profiles/r2_whole_replicas_sweep.txt)")
     ap.add_argument("--loaders", type=int, default=2, help="loader processes per GPU")
-    ap.add_argument("--video-batch", type=int, default=64,
+    ap.add_argument("--video-batch", type=int, default=128,
                     help="max videos per model invocation (consumer-side batching)")
-    ap.add_argument("--clips-per-batch", type=int, default=128,
-                    help="clip capacity of one model invocation (largest graph bucket)")
+    ap.add_argument("--clips-per-batch", type=int, default=256,
+                    help="clip capacity of one model invocation (largest graph bucket): "
+                         "256 clips / 128 videos beat 128 / 64 by 4.8%% in interleaved "
+                         "runs (1090 vs 1040 videos/s, profiles/r3_bench_batch_sweep.txt; "
+                         "a 256-clip R(2+1)D-34 runner holds ~19 GB)")
     ap.add_argument("--bucket-step", type=int, default=4,
                     help="HIP-graph clip buckets every this many clips")
     ap.add_argument("--batch-wait-ms", type=float, default=0.0,
