@@ -102,6 +102,157 @@ static __device__ __forceinline__ float x6d_row16_sum(float v) {
   return x6d_dpp_add(v, 3);
 }
 
+// Epilogue of the x6 direct kernels: (+ residual) (+ ReLU) -> fp32 stores,
+// one 16-B store per tile, and (ST) the per-video BN sums. Rows m < m_end of
+// [p0, p_hi) are valid; `lds` (lds_bytes) is free scratch (no DMA in flight).
+template <int TP, int TC, int NW, int CT_ALL, bool ST>
+static __device__ __forceinline__ void x6d_epilogue(const ConvF32Params& p, const X6DStats& st,
+                                                    x6f32x4 (&acc)[TP][TC], int p0, int m_end,
+                                                    int p_hi, int c0, int wp, int wc, int lane,
+                                                    char* lds, int lds_bytes) {
+  const int frow = lane & 15, fq = lane >> 4;
+  if (X6D_EXP == 6) {                // every accumulator stays live, no stores
+    x6f32x4 t = acc[0][0];
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp)
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc) t += acc[tp][tc];
+    if (t[0] + t[1] + t[2] + t[3] == 1.2345f) p.y[0] = t[0];
+    return;
+  }
+  // ---- epilogue: (+ residual) (+ ReLU) -> fp32, one 16-B store per tile ----
+  const uint32_t y_bytes = (uint32_t)p.M * (uint32_t)p.y_stride * 4u;
+  const __amdgpu_buffer_rsrc_t yr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.y, (short)0, y_bytes, 0x00020000);
+  const bool has_res = p.res != nullptr;
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(has_res ? p.res : p.y), (short)0,
+      has_res ? (uint32_t)p.M * (uint32_t)p.res_stride * 4u : 0u, 0x00020000);
+  if constexpr (!ST) {
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp) {
+      const int m = p0 + (wp * TP + tp) * 16 + frow;
+      x6f32x4 r[TC];
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc) {
+        const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
+        const bool ok = has_res && m < m_end && c < p.Cout_p;
+        r[tc] = has_res ? __builtin_amdgcn_raw_buffer_load_b128(
+                              rr, ok ? (uint32_t)(m * p.res_stride + c) * 4u : X6D_INVALID, 0, 0)
+                        : (x6f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc) {
+        const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
+        const bool ok = m < m_end && c < p.Cout_p;
+        x6f32x4 v = acc[tp][tc] + r[tc];
+        if (p.relu) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v, yr, ok ? (uint32_t)(m * p.y_stride + c) * 4u : X6D_INVALID, 0, 0);
+      }
+    }
+  } else {
+    // channel tiles outer (one tile's sums live at a time). Rows are
+    // clip-major, so a block's videos are the contiguous range seg_lo ..
+    // seg_hi. One video (the common case): each lane sums its TP rows, the 16
+    // lanes of a channel quad reduce by shuffles, one LDS add per channel and
+    // wave. Several videos: LDS adds per row into per-video slots. Then one
+    // fp64 atomic per video, channel and statistic per block.
+    constexpr int NT = 64 * NW;
+    int na, nz, t_, h_, w_;
+    f32_decode_row(p, p0, na, t_, h_, w_);
+    f32_decode_row(p, min(p_hi, m_end) - 1, nz, t_, h_, w_);
+    const int seg_lo = __builtin_amdgcn_readfirstlane(st.clip_seg[__builtin_amdgcn_readfirstlane(na)]);
+    const int seg_hi = __builtin_amdgcn_readfirstlane(st.clip_seg[__builtin_amdgcn_readfirstlane(nz)]);
+    const int nseg = seg_hi - seg_lo + 1;
+    const bool uni = nseg == 1;
+    const bool in_lds = nseg * CT_ALL * 16 <= lds_bytes;
+    double* red = (double*)lds;                       // [nseg][CT_ALL][2]
+    if (in_lds)
+      for (int i = threadIdx.x; i < nseg * CT_ALL * 2; i += NT) red[i] = 0.0;
+    __syncthreads();                                  // no DMA in flight here
+#pragma unroll
+    for (int tc = 0; tc < TC; ++tc) {
+      const int cl = (wc * TC + tc) * 16 + 4 * fq;
+      const int c = c0 + cl;
+      x6f32x4 r[TP];
+#pragma unroll
+      for (int tp = 0; tp < TP; ++tp) {
+        const int m = p0 + (wp * TP + tp) * 16 + frow;
+        const bool ok = has_res && m < m_end && c < p.Cout_p;
+        r[tp] = has_res ? __builtin_amdgcn_raw_buffer_load_b128(
+                              rr, ok ? (uint32_t)(m * p.res_stride + c) * 4u : X6D_INVALID, 0, 0)
+                        : (x6f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+      // lane partials over its TP rows in fp32 (<= 4 values), the 16-lane
+      // reduction in fp32 by DPP, everything after in fp64
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int tp = 0; tp < TP; ++tp) {
+        const int m = p0 + (wp * TP + tp) * 16 + frow;
+        const bool ok = m < m_end && c < p.Cout_p;
+        x6f32x4 v = acc[tp][tc] + r[tp];
+        if (p.relu) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v, yr, ok ? (uint32_t)(m * p.y_stride + c) * 4u : X6D_INVALID, 0, 0);
+        if (!ok) continue;
+        if (uni) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            s1[j] += v[j];
+            s2[j] = fmaf(v[j], v[j], s2[j]);
+          }
+        } else {
+          int n, tt, hh, ww;
+          f32_decode_row(p, m, n, tt, hh, ww);
+          const int sg = st.clip_seg[n];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const double a = (double)v[j], b = (double)v[j] * (double)v[j];
+            if (in_lds) {
+              atomicAdd(red + ((size_t)(sg - seg_lo) * CT_ALL + cl + j) * 2, a);
+              atomicAdd(red + ((size_t)(sg - seg_lo) * CT_ALL + cl + j) * 2 + 1, b);
+            } else {
+              atomicAdd(st.sums + ((size_t)sg * 2) * st.stats_c + c + j, a);
+              atomicAdd(st.sums + ((size_t)sg * 2 + 1) * st.stats_c + c + j, b);
+            }
+          }
+        }
+      }
+      if (uni) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s1[j] = x6d_row16_sum(s1[j]);
+          s2[j] = x6d_row16_sum(s2[j]);
+        }
+        if (frow == 0 && c < p.Cout_p) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            atomicAdd(red + (cl + j) * 2, (double)s1[j]);
+            atomicAdd(red + (cl + j) * 2 + 1, (double)s2[j]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (in_lds) {
+      for (int i = threadIdx.x; i < nseg * CT_ALL; i += NT) {
+        const int sg = seg_lo + i / CT_ALL, c = c0 + i % CT_ALL;
+        if (c < p.Cout_p) {
+          atomicAdd(st.sums + ((size_t)sg * 2) * st.stats_c + c, red[i * 2]);
+          atomicAdd(st.sums + ((size_t)sg * 2 + 1) * st.stats_c + c, red[i * 2 + 1]);
+        }
+      }
+    }
+  }
+}
+
 template <int TP, int TC, int WP, int WC, int NS, bool PIPE, int MINB, bool ST>
 __global__ __launch_bounds__(64 * WP * WC, MINB)
 void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
@@ -312,146 +463,175 @@ void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
     }
   }
 
-  if (X6D_EXP == 6) {                // every accumulator stays live, no stores
-    x6f32x4 t = acc[0][0];
+  x6d_epilogue<TP, TC, NW, C_TILE, ST>(p, st, acc, p0, p.M, p0 + P_TILE, c0, wp, wc, lane, lds,
+                               NS * BUF);
+}
+
+// ===========================================================================
+// Row-band halo kernel for the stride-1 1x3x3 convs (pad 1): a block owns R
+// full output rows of one frame (P = NW * TP * 16 >= R * W pixels, the rows
+// contiguous in NDHWC) x TC * 16 output channels. Per 16-channel input chunk
+// the (R + 2) x (W + 2) input patch is loaded ONCE, split into its bf16 parts
+// in registers and stored to LDS as ready-made MFMA B operands (R = L M H H
+// per channel quad, 128 B per pixel); the 9 taps are then 9 GEMM steps that
+// read shifted patch pixels -- no split VALU in the MFMA loop and 1/9 of the
+// gathered activation traffic of conv_x6_kernel. Only the weights stream per
+// step (LDS-DMA, double-buffered, counted vmcnt + raw barrier).
+// Patch pixel q's 16-B slots are XOR-permuted by g(q) = [5,6,4,1,0,7,3,0][q & 7]
+// (searched: conflict-free ds_read_b128 for any 16 consecutive pixels).
+static __device__ __forceinline__ int x6r_swz(int slot, int q) {
+  return slot ^ ((0x03701465 >> (4 * (q & 7))) & 7);
+}
+
+template <int NW, int TP, int TC, int HALO_PX, int G, bool ST>
+__global__ __launch_bounds__(64 * NW, 1)
+void conv_x6r_kernel(const ConvF32Params p, const X6DStats st) {
+  constexpr int P_TILE = NW * TP * 16, C_TILE = TC * 16;
+  constexpr int HALO_BYTES = HALO_PX * 128;
+  constexpr int W_BYTES = C_TILE * 128;
+  constexpr int W_TOTAL = C_TILE / 8;
+  constexpr int W_INSTR = (W_TOTAL + NW - 1) / NW;
+  constexpr int NT = 64 * NW;
+  constexpr int ITEMS = (HALO_PX * 4 + NT - 1) / NT;     // patch quads per lane
+  __shared__ __attribute__((aligned(16))) char lds[HALO_BYTES + 2 * G * W_BYTES];
+  char* const wbuf = lds + HALO_BYTES;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int frow = lane & 15, fq = lane >> 4;
+  const int W = p.W, H = p.H, W2 = p.W + 2;
+  const int R = p.ST;                        // rows per band (host: stride field reused)
+  const int bands = (H + R - 1) / R;
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int ctile = wgid % p.n_ctiles;
+  const int band = wgid / p.n_ctiles;
+  const int f = band / bands, r0 = (band - f * bands) * R;
+  const int c0 = ctile * C_TILE;
+  const int p0 = (f * H + r0) * W;                       // first output row (NDHWC)
+  const int m_end = p0 + min(R, H - r0) * W;             // valid rows of this band
+  const int nck = p.Cin_p / 16;
+
+  const x6d_u32x4 wr = x6d_rsrc(p.w, (uint32_t)(p.K_pad / 16) * (uint32_t)p.w_rows * 128u);
+  auto issue_w = [&](int s, int buf) {
+    const uint32_t wbase = ((uint32_t)s * (uint32_t)p.w_rows + (uint32_t)c0) * 128u;
 #pragma unroll
-    for (int tp = 0; tp < TP; ++tp)
+    for (int j = 0; j < W_INSTR; ++j) {
+      const int instr = (W_TOTAL % NW == 0) ? wave + NW * j : min(wave + NW * j, W_TOTAL - 1);
+      x6d_dma16(wr, wbase + (uint32_t)(instr * 1024 + lane * 16),
+                wbuf + buf * W_BYTES + instr * 1024);
+    }
+  };
+
+  // patch staging: item i = 4 q + quad of the (R + 2) x (W + 2) patch
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+  const int npx = (R + 2) * W2;
+  uint32_t src[ITEMS];
+  int dst[ITEMS];
 #pragma unroll
-      for (int tc = 0; tc < TC; ++tc) t += acc[tp][tc];
-    if (t[0] + t[1] + t[2] + t[3] == 1.2345f) p.y[0] = t[0];
-    return;
+  for (int i = 0; i < ITEMS; ++i) {
+    const int it = threadIdx.x + i * NT;
+    const int q = it >> 2, qd = it & 3;
+    const int hy = q / W2, hx = q - hy * W2;
+    const int y = r0 - 1 + hy, x = hx - 1;
+    const bool ok = it < 4 * npx && y >= 0 && y < H && x >= 0 && x < W;
+    src[i] = ok ? (uint32_t)((((f * H + y) * W + x) * p.Cin_p + qd * 4) * 4) : X6D_INVALID;
+    dst[i] = it < 4 * npx ? q * 128 : -1;
+    // slots 2 qd (R[0:4]) and 2 qd + 1 (R[4:8]) of patch pixel q
   }
-  // ---- epilogue: (+ residual) (+ ReLU) -> fp32, one 16-B store per tile ----
-  const uint32_t y_bytes = (uint32_t)p.M * (uint32_t)p.y_stride * 4u;
-  const __amdgpu_buffer_rsrc_t yr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.y, (short)0, y_bytes, 0x00020000);
-  const bool has_res = p.res != nullptr;
-  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(has_res ? p.res : p.y), (short)0,
-      has_res ? (uint32_t)p.M * (uint32_t)p.res_stride * 4u : 0u, 0x00020000);
-  if constexpr (!ST) {
+  auto stage = [&](int chunk) {
+    x6f32x4 v[ITEMS];
 #pragma unroll
-    for (int tp = 0; tp < TP; ++tp) {
-      const int m = p0 + (wp * TP + tp) * 16 + frow;
-      x6f32x4 r[TC];
+    for (int i = 0; i < ITEMS; ++i)
+      v[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          xr, src[i] == X6D_INVALID ? X6D_INVALID : src[i] + (uint32_t)(chunk * 64), 0, 0);
 #pragma unroll
-      for (int tc = 0; tc < TC; ++tc) {
-        const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
-        const bool ok = has_res && m < p.M && c < p.Cout_p;
-        r[tc] = has_res ? __builtin_amdgcn_raw_buffer_load_b128(
-                              rr, ok ? (uint32_t)(m * p.res_stride + c) * 4u : X6D_INVALID, 0, 0)
-                        : (x6f32x4){0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int tc = 0; tc < TC; ++tc) {
-        const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
-        const bool ok = m < p.M && c < p.Cout_p;
-        x6f32x4 v = acc[tp][tc] + r[tc];
-        if (p.relu) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(
-            v, yr, ok ? (uint32_t)(m * p.y_stride + c) * 4u : X6D_INVALID, 0, 0);
-      }
+    for (int i = 0; i < ITEMS; ++i) {
+      if (dst[i] < 0) continue;
+      const int it = threadIdx.x + i * NT;
+      const int q = it >> 2, qd = it & 3;
+      const X6B b = x6_split_exact(v[i]);
+      char* base = lds + dst[i];
+      *(wu32x4*)(base + (x6r_swz(2 * qd, q) << 4)) = __builtin_shufflevector(b.r, b.r, 0, 1, 2, 3);
+      *(wu32x4*)(base + (x6r_swz(2 * qd + 1, q) << 4)) =
+          __builtin_shufflevector(b.r, b.r, 4, 5, 6, 7);
     }
-  } else {
-    // channel tiles outer (one tile's sums live at a time). Rows are
-    // clip-major, so a block's videos are the contiguous range seg_lo ..
-    // seg_hi. One video (the common case): each lane sums its TP rows, the 16
-    // lanes of a channel quad reduce by shuffles, one LDS add per channel and
-    // wave. Several videos: LDS adds per row into per-video slots. Then one
-    // fp64 atomic per video, channel and statistic per block.
-    constexpr int NT = 64 * NW;
-    int na, nz, t_, h_, w_;
-    f32_decode_row(p, p0, na, t_, h_, w_);
-    f32_decode_row(p, min(p0 + P_TILE, p.M) - 1, nz, t_, h_, w_);
-    const int seg_lo = __builtin_amdgcn_readfirstlane(st.clip_seg[__builtin_amdgcn_readfirstlane(na)]);
-    const int seg_hi = __builtin_amdgcn_readfirstlane(st.clip_seg[__builtin_amdgcn_readfirstlane(nz)]);
-    const int nseg = seg_hi - seg_lo + 1;
-    const bool uni = nseg == 1;
-    const bool in_lds = nseg * C_TILE * 16 <= NS * BUF;
-    double* red = (double*)lds;                       // [nseg][C_TILE][2]
-    if (in_lds)
-      for (int i = threadIdx.x; i < nseg * C_TILE * 2; i += NT) red[i] = 0.0;
-    __syncthreads();                                  // no DMA in flight here
+  };
+
+  // this lane's output pixel of tile tp -> patch pixel at tap (0, 0)
+  int pq[TP];
 #pragma unroll
-    for (int tc = 0; tc < TC; ++tc) {
-      const int cl = (wc * TC + tc) * 16 + 4 * fq;
-      const int c = c0 + cl;
-      x6f32x4 r[TP];
+  for (int tp = 0; tp < TP; ++tp) {
+    const int pp = (wave * TP + tp) * 16 + frow;
+    const int py = pp / W;
+    // pixels past the band (P > R W) read pixel 0 and are never stored
+    pq[tp] = pp < R * W ? py * W2 + (pp - py * W) : 0;
+  }
+
+  x6f32x4 acc[TP][TC];
 #pragma unroll
-      for (int tp = 0; tp < TP; ++tp) {
-        const int m = p0 + (wp * TP + tp) * 16 + frow;
-        const bool ok = has_res && m < p.M && c < p.Cout_p;
-        r[tp] = has_res ? __builtin_amdgcn_raw_buffer_load_b128(
-                              rr, ok ? (uint32_t)(m * p.res_stride + c) * 4u : X6D_INVALID, 0, 0)
-                        : (x6f32x4){0.f, 0.f, 0.f, 0.f};
-      }
-      // lane partials over its TP rows in fp32 (<= 4 values), the 16-lane
-      // reduction in fp32 by DPP, everything after in fp64
-      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int b = 0; b < TC; ++b) {
+    const int c = c0 + b * 16 + 4 * fq;
+    const float4 b4 = *(const float4*)(p.bias + c);
 #pragma unroll
-      for (int tp = 0; tp < TP; ++tp) {
-        const int m = p0 + (wp * TP + tp) * 16 + frow;
-        const bool ok = m < p.M && c < p.Cout_p;
-        x6f32x4 v = acc[tp][tc] + r[tp];
-        if (p.relu) {
+    for (int a = 0; a < TP; ++a) acc[a][b] = (x6f32x4){b4.x, b4.y, b4.z, b4.w};
+  }
+  const int w_hm = x6_chunk(2 * fq, frow) << 4, w_hl = x6_chunk(2 * fq + 1, frow) << 4;
+
+  // steps in (chunk, tap) order, weight step index s = tap * nck + chunk, in
+  // sync groups of G taps of one chunk (taps 0..G-1, G..2G-1, ..): one wait +
+  // barrier per group; the next group's weights (G slots of the other half
+  // of the weight buffer) are DMA'd at the group's start
+  constexpr int NG = (9 + G - 1) / G;                    // groups per chunk
+  auto issue_group = [&](int c, int g, int half) {
+    for (int j = 0; j < G && g * G + j < 9; ++j) issue_w((g * G + j) * nck + c, half * G + j);
+  };
+  issue_group(0, 0, 0);
+  int half = 0;
+  for (int c = 0; c < nck; ++c) {
+    stage(c);                       // waits for its own loads (and the older W DMAs)
+    x6d_wait_vm<0>();
+    x6d_barrier();
+#pragma unroll 1
+    for (int g = 0; g < NG; ++g) {
+      if (g + 1 < NG) issue_group(c, g + 1, half ^ 1);
+      else if (c + 1 < nck) issue_group(c + 1, 0, half ^ 1);
+      for (int j = 0; j < G && g * G + j < 9; ++j) {
+        const int t = g * G + j;
+        const int toff = (t / 3) * W2 + (t % 3);
+        X6B bf[TP];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+        for (int tp = 0; tp < TP; ++tp) {
+          const int q = pq[tp] + toff;
+          const char* base = lds + q * 128;
+          const wu32x4 lo = *(const wu32x4*)(base + (x6r_swz(2 * fq, q) << 4));
+          const wu32x4 hi = *(const wu32x4*)(base + (x6r_swz(2 * fq + 1, q) << 4));
+          bf[tp].r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
         }
-        __builtin_amdgcn_raw_buffer_store_b128(
-            v, yr, ok ? (uint32_t)(m * p.y_stride + c) * 4u : X6D_INVALID, 0, 0);
-        if (!ok) continue;
-        if (uni) {
+        const char* wb = wbuf + (half * G + j) * W_BYTES;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            s1[j] += v[j];
-            s2[j] = fmaf(v[j], v[j], s2[j]);
-          }
-        } else {
-          int n, tt, hh, ww;
-          f32_decode_row(p, m, n, tt, hh, ww);
-          const int sg = st.clip_seg[n];
+        for (int tc = 0; tc < TC; ++tc) {
+          const char* wrow = wb + (tc * 16 + frow) * 128;
+          const wu32x4 hm = *(const wu32x4*)(wrow + w_hm);
+          const wu32x4 hl = *(const wu32x4*)(wrow + w_hl);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const double a = (double)v[j], b = (double)v[j] * (double)v[j];
-            if (in_lds) {
-              atomicAdd(red + ((size_t)(sg - seg_lo) * C_TILE + cl + j) * 2, a);
-              atomicAdd(red + ((size_t)(sg - seg_lo) * C_TILE + cl + j) * 2 + 1, b);
-            } else {
-              atomicAdd(st.sums + ((size_t)sg * 2) * st.stats_c + c + j, a);
-              atomicAdd(st.sums + ((size_t)sg * 2 + 1) * st.stats_c + c + j, b);
-            }
-          }
+          for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = x6_mma(hm, x6_b_lm(bf[tp]), acc[tp][tc]);
+#pragma unroll
+          for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = x6_mma(hl, x6_b_mh(bf[tp]), acc[tp][tc]);
+#pragma unroll
+          for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = x6_mma(hm, x6_b_hh(bf[tp]), acc[tp][tc]);
         }
       }
-      if (uni) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          s1[j] = x6d_row16_sum(s1[j]);
-          s2[j] = x6d_row16_sum(s2[j]);
-        }
-        if (frow == 0 && c < p.Cout_p) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            atomicAdd(red + (cl + j) * 2, (double)s1[j]);
-            atomicAdd(red + (cl + j) * 2 + 1, (double)s2[j]);
-          }
-        }
-      }
-    }
-    __syncthreads();
-    if (in_lds) {
-      for (int i = threadIdx.x; i < nseg * C_TILE; i += NT) {
-        const int sg = seg_lo + i / C_TILE, c = c0 + i % C_TILE;
-        if (c < p.Cout_p) {
-          atomicAdd(st.sums + ((size_t)sg * 2) * st.stats_c + c, red[i * 2]);
-          atomicAdd(st.sums + ((size_t)sg * 2 + 1) * st.stats_c + c, red[i * 2 + 1]);
-        }
-      }
+      x6d_wait_vm<0>();             // the next group's weights landed (this wave) ...
+      x6d_barrier();                // ... in every wave; this group's LDS reads are done
+      half ^= 1;
     }
   }
+  x6d_epilogue<TP, TC, NW, C_TILE, ST>(p, st, acc, p0, m_end, p0 + P_TILE, c0, wave, 0, lane,
+                                       lds, HALO_BYTES + 2 * G * W_BYTES);
 }
 
 // ---------------------------------------------------------------------------
@@ -488,6 +668,10 @@ static const ConvX6Config kX6Configs[] = {
     X6DCFG(4, 6, 8, 1, 3, true, 1),    // 15: 512 px x  96 ch, pipelined
     X6DCFG(4, 9, 8, 1, 3, true, 1),    // 16: 512 px x 144 ch, pipelined
     X6DCFG(2, 4, 4, 2, 2, false, 3),   // 17: 128 px x 128 ch, 4 waves, 3 blocks per CU
+    X6DCFG(2, 9, 16, 1, 2, false, 1),  // 18: 512 px x 144 ch, 16 waves (4 per SIMD)
+    X6DCFG(2, 8, 16, 1, 2, false, 1),  // 19: 512 px x 128 ch, 16 waves
+    X6DCFG(2, 4, 16, 1, 2, false, 1),  // 20: 512 px x  64 ch, 16 waves
+    X6DCFG(1, 8, 16, 1, 2, false, 1),  // 21: 256 px x 128 ch, 16 waves
 };
 static const int kNumX6Configs = sizeof(kX6Configs) / sizeof(kX6Configs[0]);
 
@@ -546,6 +730,65 @@ int rnb_conv_x6_launch_stats(const ConvF32Params* pp, int config_id, hipStream_t
 
 int rnb_conv_x6_launch(const ConvF32Params* pp, int config_id, hipStream_t stream) {
   return rnb_conv_x6_launch_stats(pp, config_id, stream, nullptr, nullptr, 0);
+}
+
+// Row-band halo kernel (conv_x6r_kernel): 1x3x3 stride 1 pad 1 only.
+// variant: 0 = 7 waves x 4 tiles (448 px), 1 = 14 waves x 2 tiles (448 px),
+// 2 = 7 waves x 3 tiles (336 px), 3 / 4 = 0 / 1 with 2 taps per barrier,
+// 5 = 2 with 2 taps per barrier; 144 channels per block. A band is
+// floor(P / W) rows (the rest of the block's pixels idle).
+struct ConvX6RConfig {
+  int nw, tp, halo_px;
+  void (*kernel)(const ConvF32Params, const X6DStats);
+  void (*kernel_st)(const ConvF32Params, const X6DStats);
+};
+#define X6RCFG(NW, TP, HALO, G)                                                   \
+  {NW, TP, HALO, conv_x6r_kernel<NW, TP, 9, HALO, G, false>,                       \
+   conv_x6r_kernel<NW, TP, 9, HALO, G, true>}
+static const ConvX6RConfig kX6RConfigs[] = {
+    X6RCFG(7, 4, 600, 1), X6RCFG(14, 2, 600, 1), X6RCFG(7, 3, 480, 1),
+    X6RCFG(7, 4, 600, 2), X6RCFG(14, 2, 600, 2), X6RCFG(7, 3, 480, 2),
+};
+
+int rnb_conv_x6r_num_variants() { return (int)(sizeof(kX6RConfigs) / sizeof(kX6RConfigs[0])); }
+
+int rnb_conv_x6r_launch(const ConvF32Params* pp, int variant, hipStream_t stream, double* sums,
+                        const int* clip_seg, int stats_c) {
+  if (variant < 0 || variant >= rnb_conv_x6r_num_variants()) return -1;
+  ConvF32Params p = *pp;
+  const ConvX6RConfig& cfg = kX6RConfigs[variant];
+  if (p.KT != 1 || p.KH != 3 || p.KW != 3 || p.PH != 1 || p.PW != 1 || p.PT != 0) return -2;
+  if (p.SH != 1 || p.SW != 1 || p.ST != 1 || p.Cin_p % 16 != 0 || p.Cout_p % 4 != 0) return -2;
+  if (p.K_pad < 9 * p.Cin_p || p.K_pad % 16 != 0) return -3;
+  if (p.M <= 0) return 0;
+  if (p.y_stride < p.Cout_p || p.y_stride % 4 != 0 || (p.res && (p.res_stride < p.Cout_p ||
+                                                               p.res_stride % 4 != 0)))
+    return -4;
+  const long long xb = (long long)p.N * p.T * p.H * p.W * p.Cin_p * 4;
+  if (xb > 0x7FFFFF00LL || (long long)p.M * p.y_stride * 4 > 0x7FFFFF00LL) return -5;
+  if (p.res && (long long)p.M * p.res_stride * 4 > 0x7FFFFF00LL) return -6;
+  const int ptile = cfg.nw * cfg.tp * 16;
+  const int R = ptile / p.W;
+  if (R < 1 || (R + 2) * (p.W + 2) > cfg.halo_px) return -13;
+  if ((long long)(p.K_pad / 16) * p.w_rows * 128 > 0x7FFFFF00LL) return -11;
+  p.x_bytes = (uint32_t)xb;
+  f32_magic_div((uint32_t)p.Wo, &p.mWo, &p.sWo);
+  f32_magic_div((uint32_t)p.Ho, &p.mHo, &p.sHo);
+  f32_magic_div((uint32_t)p.To, &p.mTo, &p.sTo);
+  p.ST = R;                                    // rows per band (read by the kernel)
+  const int bands = (p.H + R - 1) / R;
+  p.n_ctiles = (p.Cout_p + 143) / 144;
+  if (p.n_ctiles * 144 > p.w_rows) return -8;
+  const long long blocks = (long long)p.N * p.T * bands * p.n_ctiles;
+  if (blocks > 0x7FFFFFFF) return -7;
+  if (sums && (!clip_seg || stats_c < p.Cout_p)) return -12;
+  X6DStats st;
+  st.sums = sums;
+  st.clip_seg = clip_seg;
+  st.stats_c = stats_c;
+  hipLaunchKernelGGL(sums ? cfg.kernel_st : cfg.kernel, dim3((unsigned)blocks),
+                     dim3(64 * cfg.nw), 0, stream, p, st);
+  return (int)hipGetLastError();
 }
 
 }  // extern "C"

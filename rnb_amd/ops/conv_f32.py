@@ -98,8 +98,19 @@ X6_ROW_SLACK = 288
 
 
 def is_x6d(cid: int) -> bool:
+    """x6 direct config (csrc/conv_x6.hip conv_x6_kernel or, from X6R_BASE,
+    the row-band halo kernel conv_x6r_kernel)."""
     from .native import kernels
-    return X6D_BASE <= cid < X6D_BASE + len(kernels().x6_configs)
+    return (X6D_BASE <= cid < X6D_BASE + len(kernels().x6_configs)) or is_x6r(cid)
+
+
+# row-band halo variants of the x6 direct conv (1x3x3 stride 1 pad 1 only)
+X6R_BASE = 1150
+
+
+def is_x6r(cid: int) -> bool:
+    from .native import kernels
+    return X6R_BASE <= cid < X6R_BASE + kernels().x6r_variants
 
 
 def x6_direct_weights(wmat: torch.Tensor) -> torch.Tensor:
@@ -324,6 +335,8 @@ class ConvLayerF32:
         c = list(range(len(kernels().f32_configs)))
         if x6_enabled():
             c += [X6D_BASE + i for i in range(len(kernels().x6_configs))]
+            if self.wino_ok:
+                c += [X6R_BASE + i for i in range(kernels().x6r_variants)]
         ids = self.wino_ids if x6_enabled() else self.wino_ids - WINO_X6
         return c + sorted(ids)
 
@@ -552,7 +565,16 @@ class ConvLayerF32:
                                 residual.shape[-1] if residual is not None else 0)
         for n0 in range(0, N, step):
             p = self.params(x, y, residual, n0, min(N, n0 + step), x6=x6)
-            if x6 and out_stats is not None:
+            if is_x6r(cid):
+                if not self.wino_ok:
+                    raise ValueError("%s: the row-band x6 kernel takes 1x3x3 stride-1 convs"
+                                     % self.name)
+                if out_stats is not None:
+                    k.conv_x6r(p, cid - X6R_BASE, stream.cuda_stream, out_stats[0].data_ptr(),
+                               out_stats[1].data_ptr() + 4 * n0, out_stats[0].shape[2])
+                else:
+                    k.conv_x6r(p, cid - X6R_BASE, stream.cuda_stream)
+            elif x6 and out_stats is not None:
                 k.conv_x6(p, cid - X6D_BASE, stream.cuda_stream, out_stats[0].data_ptr(),
                           out_stats[1].data_ptr() + 4 * n0, out_stats[0].shape[2])
             elif x6:

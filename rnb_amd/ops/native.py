@@ -294,6 +294,10 @@ class Kernels:
                                                  ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.c_void_p, ctypes.c_int]
         lib.rnb_conv_x6_launch_stats.restype = ctypes.c_int
+        lib.rnb_conv_x6r_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_int]
+        lib.rnb_conv_x6r_launch.restype = ctypes.c_int
         lib.rnb_conv_x6_config_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                                 ctypes.POINTER(ctypes.c_int)]
         lib.rnb_preprocess_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
@@ -322,6 +326,7 @@ class Kernels:
             lib.rnb_conv_f32_config_info(i, ctypes.byref(p), ctypes.byref(c))
             self.f32_configs.append((p.value, c.value))
         self.f32_max_bytes = lib.rnb_conv_f32_max_bytes()
+        self.x6r_variants = lib.rnb_conv_x6r_num_variants()
         self.x6_configs = []       # (pixel tile, channel tile) per x6 direct config
         for i in range(lib.rnb_conv_x6_num_configs()):
             p, c = ctypes.c_int(), ctypes.c_int()
@@ -350,6 +355,13 @@ class Kernels:
         _check(self.lib.rnb_conv_x6_launch_stats(ctypes.byref(params), config_id, stream,
                                                  sums or None, clip_seg or None, stats_c),
                "conv_x6 (config %d)" % config_id)
+
+    def conv_x6r(self, params: ConvParams, variant: int, stream: int, sums: int = 0,
+                 clip_seg: int = 0, stats_c: int = 0) -> None:
+        """x6 row-band halo conv (1x3x3 stride 1 pad 1), optional BN sums."""
+        _check(self.lib.rnb_conv_x6r_launch(ctypes.byref(params), variant, stream,
+                                            sums or None, clip_seg or None, stats_c),
+               "conv_x6r (variant %d)" % variant)
 
     def wino_f32(self, params: "WinoParams", variant: int, stream: int) -> None:
         _check(self.lib.rnb_wino_f32_launch(ctypes.byref(params), variant, stream),

@@ -93,8 +93,12 @@ def sweep(clips=128, reps=5):
         ost = (torch.zeros((1, 2, g.cout_p), dtype=torch.float64, device=dev),
                torch.zeros(clips, dtype=torch.int32, device=dev))
         row = []
-        for i, (pt, ct) in enumerate(kernels().x6_configs):
-            cid = X6D_BASE + i
+        from rnb_amd.ops.conv_f32 import X6R_BASE
+        ids = [(X6D_BASE + i, "%d:%dx%d" % (i, pt, ct))
+               for i, (pt, ct) in enumerate(kernels().x6_configs)]
+        if layer.wino_ok:
+            ids += [(X6R_BASE + v, "r%d" % v) for v in range(kernels().x6r_variants)]
+        for cid, label in ids:
             layer.forward_hip(x, out=y, config=cid, out_stats=ost)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
@@ -103,7 +107,7 @@ def sweep(clips=128, reps=5):
             e.record()
             e.synchronize()
             ms = s.elapsed_time(e) / reps
-            row.append("%d:%dx%d %.3f" % (i, pt, ct, ms))
+            row.append("%s %.3f" % (label, ms))
         best = min(row, key=lambda r: float(r.split()[-1]))
         print("%-16s %d clips: best %s (%.0f TF) | %s" % (
             name, clips, best, fl / float(best.split()[-1]) / 1e9, ", ".join(row)), flush=True)

@@ -161,7 +161,11 @@ def test_x6_direct_matches_fp64(case):
     x = _input(2, thw, layer.geom.cin_p, cin)
     ref = _ref64(layer, x)
     scale = ref.abs().max().item()
-    for cid in (X6D_BASE + 0, X6D_BASE + 9, X6D_BASE + 5, X6D_BASE + 12, X6D_BASE + 14):
+    from rnb_amd.ops.conv_f32 import X6R_BASE
+    ids = [X6D_BASE + 0, X6D_BASE + 9, X6D_BASE + 5, X6D_BASE + 12, X6D_BASE + 14]
+    if layer.wino_ok:
+        ids += [X6R_BASE + 0, X6R_BASE + 1]
+    for cid in ids:
         y = layer.forward_hip(x, config=cid)
         torch.cuda.synchronize()
         assert torch.all(y[..., cout:] == 0), "padding channels must be zero"
@@ -509,6 +513,40 @@ def test_winograd_epilogue_stats_match_fp64_sums(kind):
             got = sums[v, :, :layer.geom.cout].cpu()
             assert torch.allclose(got[0], seg.sum(0), rtol=1e-9, atol=1e-6), (cid, v)
             assert torch.allclose(got[1], (seg * seg).sum(0), rtol=1e-9, atol=1e-6), (cid, v)
+
+
+@pytest.mark.parametrize("thw", [(2, 15, 13), (3, 56, 56), (2, 28, 28), (1, 7, 7)])
+def test_x6_rowband_exact_integers_and_stats(thw):
+    """Row-band halo x6 kernel (conv_x6r_kernel): bit-exact on small integers
+    (bands of whole rows, partial last band, 3x3 padding at frame edges,
+    residual + ReLU epilogue), every variant; epilogue BN sums vs fp64."""
+    from rnb_amd.ops.conv_f32 import X6R_BASE, is_x6r
+    layer = _layer(64, 150, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=True, integer=True)
+    x = _input(2, thw, 64, 64, integer=True)
+    res = _input(2, thw, layer.geom.cout_p, 150, integer=True, seed=3)
+    ref = _ref64(layer, x, res).float()
+    nvar = 0
+    for cid in range(X6R_BASE, X6R_BASE + 8):
+        if not is_x6r(cid):
+            continue
+        nvar += 1
+        y = layer.forward_hip(x, res, config=cid)
+        torch.cuda.synchronize()
+        assert torch.equal(y[..., :150].cpu(), ref), cid
+    assert nvar > 0
+    lay2 = _layer(64, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False)
+    xf = _input(3, thw, 64, 64)
+    seg = torch.tensor([0, 2, 2], dtype=torch.int32, device=DEV)
+    for cid in range(X6R_BASE, X6R_BASE + nvar):
+        sums = torch.zeros((3, 2, lay2.geom.cout_p), dtype=torch.float64, device=DEV)
+        y = lay2.forward_hip(xf, config=cid, out_stats=(sums, seg))
+        torch.cuda.synchronize()
+        yd = y[..., :144].double().cpu()
+        for v, (a, b) in enumerate([(0, 1), (1, 1), (1, 3)]):
+            part = yd[a:b].reshape(-1, 144)
+            got = sums[v, :, :144].cpu()
+            assert ((got[0] - part.sum(0)).abs() <= 1e-6 * part.abs().sum(0) + 1e-9).all()
+            assert torch.allclose(got[1], (part * part).sum(0), rtol=1e-6, atol=1e-9)
 
 
 @pytest.mark.parametrize("shape,kern", [((7, 4, 20, 28), (1, 3, 3)), ((9, 2, 7, 7), (3, 1, 1)),
