@@ -80,6 +80,11 @@ struct X6DStats {
   double* sums;          // [nseg][2][stats_c], zeroed by the caller
   const int* clip_seg;   // [N]: video (segment) of each clip of this launch
   int stats_c;
+  // split-K (conv_x6_kernel only): ksplit > 1 = the block's share of the K
+  // steps is written raw (no bias / epilogue) to ws[split][M][Cout_p] and
+  // x6d_splitk_reduce_kernel finishes the conv
+  int ksplit;
+  float* ws;
 };
 
 // sum over the 16 lanes of a DPP row (every lane gets it): quad swaps, then
@@ -277,7 +282,9 @@ void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
   // of one XCD take consecutive tile ids
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int wgid0 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int ksplit = st.ksplit > 1 ? st.ksplit : 1;
+  const int kidx = wgid0 % ksplit, wgid = wgid0 / ksplit;
   const int ctile = wgid % p.n_ctiles;
   const int ptile = wgid / p.n_ctiles;
   const int p0 = ptile * P_TILE;
@@ -341,7 +348,8 @@ void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
 #pragma unroll
   for (int b = 0; b < TC; ++b) {
     const int c = c0 + (wc * TC + b) * 16 + 4 * fq;
-    const float4 b4 = *(const float4*)(p.bias + c);   // w_rows >= n_ctiles * C_TILE
+    float4 b4 = *(const float4*)(p.bias + c);         // w_rows >= n_ctiles * C_TILE
+    if (ksplit > 1) b4 = make_float4(0.f, 0.f, 0.f, 0.f);   // the reduce adds it
 #pragma unroll
     for (int a = 0; a < TP; ++a) acc[a][b] = (x6f32x4){b4.x, b4.y, b4.z, b4.w};
   }
@@ -403,6 +411,13 @@ void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
     }
   }
 
+  if (ksplit > 1) {                 // this split's share of the steps
+    const int len = s_end - s_begin;
+    const int a = s_begin + (int)((long long)len * kidx / ksplit);
+    const int b = s_begin + (int)((long long)len * (kidx + 1) / ksplit);
+    s_begin = a;
+    s_end = b;
+  }
   // prologue: steps s_begin .. s_begin + NS - 2 in flight
 #pragma unroll
   for (int i = 0; i + 1 < NS; ++i)
@@ -463,8 +478,105 @@ void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
     }
   }
 
+  if (ksplit > 1) {                 // raw partial sums -> ws[kidx][m][c]
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp) {
+      const int m = p0 + (wp * TP + tp) * 16 + frow;
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc) {
+        const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
+        if (m < p.M && c < p.Cout_p)
+          *(x6f32x4*)(st.ws + ((size_t)kidx * p.M + m) * p.Cout_p + c) = acc[tp][tc];
+      }
+    }
+    return;
+  }
   x6d_epilogue<TP, TC, NW, C_TILE, ST>(p, st, acc, p0, p.M, p0 + P_TILE, c0, wp, wc, lane, lds,
                                NS * BUF);
+}
+
+// Split-K finish: y = sum of the ksplit (<= 16) partials + bias (+ residual)
+// (ReLU), plus the per-video BN sums. Block = 64 channel quads x 8 row
+// threads of RPT rows each (64 x 16 B coalesced per row). A block inside one
+// video reduces its threads' sums through LDS (one fp64 atomic per channel
+// and statistic per block); otherwise each thread commits per video change.
+__global__ __launch_bounds__(512) void x6d_splitk_reduce_kernel(const ConvF32Params p,
+                                                                const X6DStats st, int rpt,
+                                                                int rows_per_clip) {
+  __shared__ double red[8][64][8];
+  const int tx = threadIdx.x, ty = threadIdx.y;
+  const int cq = blockIdx.x * 64 + tx;
+  const int c = 4 * cq;
+  const bool cok = c < p.Cout_p;
+  const int rb = blockIdx.y * 8 * rpt;                     // the block's rows
+  const int rb1 = min(p.M, rb + 8 * rpt);
+  const int r0 = min(rb1, rb + ty * rpt), r1 = min(rb1, r0 + rpt);
+  const bool stats = st.sums != nullptr;
+  const bool uni = stats && st.clip_seg[rb / rows_per_clip] == st.clip_seg[(rb1 - 1) / rows_per_clip];
+  const float4 b4 = cok ? *(const float4*)(p.bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  int cur = -1;
+  auto flush = [&]() {
+    if (cur < 0) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      atomicAdd(st.sums + ((size_t)cur * 2) * st.stats_c + c + j, s1[j]);
+      atomicAdd(st.sums + ((size_t)cur * 2 + 1) * st.stats_c + c + j, s2[j]);
+      s1[j] = s2[j] = 0.0;
+    }
+  };
+  for (int m = r0; cok && m < r1; ++m) {
+    // all partials of the row in flight at once (ksplit <= 16)
+    x6f32x4 part[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      part[k] = k < st.ksplit ? *(const x6f32x4*)(st.ws + ((size_t)k * p.M + m) * p.Cout_p + c)
+                              : (x6f32x4){0.f, 0.f, 0.f, 0.f};
+    x6f32x4 v = (x6f32x4){b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += part[k];
+    if (p.res) v += *(const x6f32x4*)(p.res + (size_t)m * p.res_stride + c);
+    if (p.relu) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+    }
+    *(x6f32x4*)(p.y + (size_t)m * p.y_stride + c) = v;
+    if (stats) {
+      if (!uni) {
+        const int sg = st.clip_seg[m / rows_per_clip];
+        if (sg != cur) {
+          flush();
+          cur = sg;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s1[j] += (double)v[j];
+        s2[j] += (double)v[j] * (double)v[j];
+      }
+    }
+  }
+  if (!stats) return;
+  if (!uni) {
+    if (cok) flush();
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    red[ty][tx][j] = s1[j];
+    red[ty][tx][4 + j] = s2[j];
+  }
+  __syncthreads();
+  if (ty == 0 && cok) {
+    const int sg = st.clip_seg[rb / rows_per_clip];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      double t = 0.0;
+#pragma unroll
+      for (int y = 0; y < 8; ++y) t += red[y][tx][j];
+      atomicAdd(st.sums + ((size_t)sg * 2 + (j >> 2)) * st.stats_c + c + (j & 3), t);
+    }
+  }
 }
 
 // ===========================================================================
@@ -691,8 +803,9 @@ int rnb_conv_x6_config_info(int id, int* p_tile, int* c_tile) {
 // sums (nullable): add each video's per-channel sum and sum of squares of
 // the output to sums[clip_seg[clip]][2][stats_c] (fp64, channels < Cout_p).
 // Returns 0, a negative contract code, or the hipError_t of the launch.
-int rnb_conv_x6_launch_stats(const ConvF32Params* pp, int config_id, hipStream_t stream,
-                             double* sums, const int* clip_seg, int stats_c) {
+int rnb_conv_x6_launch_splitk(const ConvF32Params* pp, int config_id, hipStream_t stream,
+                              double* sums, const int* clip_seg, int stats_c, int ksplit,
+                              float* ws) {
   if (config_id < 0 || config_id >= kNumX6Configs) return -1;
   ConvF32Params p = *pp;
   const ConvX6Config& cfg = kX6Configs[config_id];
@@ -723,13 +836,36 @@ int rnb_conv_x6_launch_stats(const ConvF32Params* pp, int config_id, hipStream_t
   st.sums = sums;
   st.clip_seg = clip_seg;
   st.stats_c = stats_c;
+  st.ksplit = 1;
+  st.ws = nullptr;
+  if (ksplit > 1) {
+    // split-K: raw partials per split, then the reduce kernel (bias,
+    // residual, ReLU, statistics); ws holds ksplit x M x Cout_p floats
+    if (!ws || ksplit > 16) return -14;
+    st.ksplit = ksplit;
+    st.ws = ws;
+    hipLaunchKernelGGL(cfg.kernel, dim3((unsigned)(blocks * ksplit)), dim3(cfg.threads), 0, stream,
+                       p, st);
+    const int rpt = 4;                     // rows per thread: many threads, short chains
+    const int rows_per_clip = p.To * p.Ho * p.Wo;
+    hipLaunchKernelGGL(x6d_splitk_reduce_kernel,
+                       dim3((unsigned)((p.Cout_p / 4 + 63) / 64),
+                            (unsigned)((p.M + 8 * rpt - 1) / (8 * rpt))),
+                       dim3(64, 8), 0, stream, p, st, rpt, rows_per_clip);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(sums ? cfg.kernel_st : cfg.kernel, dim3((unsigned)blocks), dim3(cfg.threads),
                      0, stream, p, st);
   return (int)hipGetLastError();
 }
 
+int rnb_conv_x6_launch_stats(const ConvF32Params* pp, int config_id, hipStream_t stream,
+                             double* sums, const int* clip_seg, int stats_c) {
+  return rnb_conv_x6_launch_splitk(pp, config_id, stream, sums, clip_seg, stats_c, 1, nullptr);
+}
+
 int rnb_conv_x6_launch(const ConvF32Params* pp, int config_id, hipStream_t stream) {
-  return rnb_conv_x6_launch_stats(pp, config_id, stream, nullptr, nullptr, 0);
+  return rnb_conv_x6_launch_splitk(pp, config_id, stream, nullptr, nullptr, 0, 1, nullptr);
 }
 
 // Row-band halo kernel (conv_x6r_kernel): 1x3x3 stride 1 pad 1 only.
@@ -786,6 +922,8 @@ int rnb_conv_x6r_launch(const ConvF32Params* pp, int variant, hipStream_t stream
   st.sums = sums;
   st.clip_seg = clip_seg;
   st.stats_c = stats_c;
+  st.ksplit = 1;
+  st.ws = nullptr;
   hipLaunchKernelGGL(sums ? cfg.kernel_st : cfg.kernel, dim3((unsigned)blocks),
                      dim3(64 * cfg.nw), 0, stream, p, st);
   return (int)hipGetLastError();

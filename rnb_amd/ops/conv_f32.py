@@ -101,7 +101,8 @@ def is_x6d(cid: int) -> bool:
     """x6 direct config (csrc/conv_x6.hip conv_x6_kernel or, from X6R_BASE,
     the row-band halo kernel conv_x6r_kernel)."""
     from .native import kernels
-    return (X6D_BASE <= cid < X6D_BASE + len(kernels().x6_configs)) or is_x6r(cid)
+    return ((X6D_BASE <= cid < X6D_BASE + len(kernels().x6_configs)) or is_x6r(cid)
+            or is_x6k(cid))
 
 
 # row-band halo variants of the x6 direct conv (1x3x3 stride 1 pad 1 only)
@@ -111,6 +112,20 @@ X6R_BASE = 1150
 def is_x6r(cid: int) -> bool:
     from .native import kernels
     return X6R_BASE <= cid < X6R_BASE + kernels().x6r_variants
+
+
+# split-K variants of small-tile x6 direct configs for layers with few tiles
+# (conv4/conv5 at small clip counts: 1-8 blocks of 72-288 K steps otherwise):
+# X6K_BASE + j runs x6 config X6K_CONFIGS[j] with K split over ksplit blocks
+# per tile (ksplit_for), partials in a per-layer workspace, then a reduce
+# kernel (bias, residual, ReLU, BN sums)
+X6K_BASE = 1200
+X6K_CONFIGS = (2, 5, 6, 8, 17)
+X6K_TARGET_BLOCKS = 512
+
+
+def is_x6k(cid: int) -> bool:
+    return X6K_BASE <= cid < X6K_BASE + len(X6K_CONFIGS)
 
 
 def x6_direct_weights(wmat: torch.Tensor) -> torch.Tensor:
@@ -274,6 +289,24 @@ class ConvLayerF32:
         # only the configs that accumulate them, timed with the statistics on
         self.tune_with_stats = False
         self._x6d = None                     # (split weights, bias) for the x6 direct kernel
+        self._x6k_ws: Dict[int, torch.Tensor] = {}
+
+    def ksplit_for(self, cid: int, x_shape) -> int:
+        """Blocks per tile of split-K config ``cid`` for this input: enough to
+        put ~X6K_TARGET_BLOCKS blocks in flight, at least 8 K steps each."""
+        from .native import kernels
+        pt, ct = kernels().x6_configs[X6K_CONFIGS[cid - X6K_BASE]]
+        N, T, H, W, _ = x_shape
+        To, Ho, Wo = self.geom.out_thw(T, H, W)
+        blocks = math.ceil(N * To * Ho * Wo / pt) * math.ceil(self.geom.cout_p / ct)
+        return int(max(1, min(16, X6K_TARGET_BLOCKS // max(blocks, 1), self.k16 // 16 // 8)))
+
+    def x6k_workspace(self, numel: int) -> torch.Tensor:
+        """fp32 split-K partials, one persistent buffer per size (graph-safe)."""
+        ws = self._x6k_ws.get(numel)
+        if ws is None:
+            ws = self._x6k_ws[numel] = torch.empty(numel, dtype=torch.float32, device=self.device)
+        return ws
 
     def x6d_buffers(self):
         """(split weight matrix [K16/16][rows][64] int16, bias [rows] fp32),
@@ -330,13 +363,16 @@ class ConvLayerF32:
             return [(0, main, tc, variant), (main, rem, rem // 16, 6 + rem // 16)]
         return [(0, cp, tc, variant)]
 
-    def candidates(self):
+    def candidates(self, x_shape=None):
         from .native import kernels
         c = list(range(len(kernels().f32_configs)))
         if x6_enabled():
             c += [X6D_BASE + i for i in range(len(kernels().x6_configs))]
             if self.wino_ok:
                 c += [X6R_BASE + i for i in range(kernels().x6r_variants)]
+            if x_shape is not None:
+                c += [X6K_BASE + j for j in range(len(X6K_CONFIGS))
+                      if self.ksplit_for(X6K_BASE + j, x_shape) > 1]
         ids = self.wino_ids if x6_enabled() else self.wino_ids - WINO_X6
         return c + sorted(ids)
 
@@ -574,6 +610,16 @@ class ConvLayerF32:
                                out_stats[1].data_ptr() + 4 * n0, out_stats[0].shape[2])
                 else:
                     k.conv_x6r(p, cid - X6R_BASE, stream.cuda_stream)
+            elif is_x6k(cid):
+                ks = self.ksplit_for(cid, x[n0:min(N, n0 + step)].shape)
+                ws = self.x6k_workspace(ks * p.M * self.geom.cout_p) if ks > 1 else None
+                if out_stats is not None:
+                    k.conv_x6(p, X6K_CONFIGS[cid - X6K_BASE], stream.cuda_stream,
+                              out_stats[0].data_ptr(), out_stats[1].data_ptr() + 4 * n0,
+                              out_stats[0].shape[2], ks, ws.data_ptr() if ws is not None else 0)
+                else:
+                    k.conv_x6(p, X6K_CONFIGS[cid - X6K_BASE], stream.cuda_stream, 0, 0, 0, ks,
+                              ws.data_ptr() if ws is not None else 0)
             elif x6 and out_stats is not None:
                 k.conv_x6(p, cid - X6D_BASE, stream.cuda_stream, out_stats[0].data_ptr(),
                           out_stats[1].data_ptr() + 4 * n0, out_stats[0].shape[2])
@@ -598,7 +644,7 @@ class ConvLayerF32:
         stream = torch.cuda.current_stream(x.device)
         best, best_t = None, None
         verbose = os.environ.get("RNB_TUNE_VERBOSE") == "1"
-        cands, ost = self.candidates(), None
+        cands, ost = self.candidates(x.shape), None
         if self.tune_with_stats:
             cands = [c for c in cands if c in WINO_ALL or is_x6d(c)] or cands
             ost = (torch.zeros((1, 2, self.geom.cout_p), dtype=torch.float64, device=x.device),

@@ -294,6 +294,11 @@ class Kernels:
                                                  ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.c_void_p, ctypes.c_int]
         lib.rnb_conv_x6_launch_stats.restype = ctypes.c_int
+        lib.rnb_conv_x6_launch_splitk.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
+                                                  ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_void_p]
+        lib.rnb_conv_x6_launch_splitk.restype = ctypes.c_int
         lib.rnb_conv_x6r_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
                                             ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_int]
@@ -349,12 +354,15 @@ class Kernels:
                "conv_f32 (config %d)" % config_id)
 
     def conv_x6(self, params: ConvParams, config_id: int, stream: int, sums: int = 0,
-                clip_seg: int = 0, stats_c: int = 0) -> None:
+                clip_seg: int = 0, stats_c: int = 0, ksplit: int = 1, ws: int = 0) -> None:
         """x6 direct conv; ``sums`` (fp64 [nseg][2][stats_c] device pointer, with
-        ``clip_seg`` int32 [N]): add the output's per-video BN sums."""
-        _check(self.lib.rnb_conv_x6_launch_stats(ctypes.byref(params), config_id, stream,
-                                                 sums or None, clip_seg or None, stats_c),
-               "conv_x6 (config %d)" % config_id)
+        ``clip_seg`` int32 [N]): add the output's per-video BN sums. ``ksplit`` >
+        1: split-K over that many blocks per tile with ``ws`` (fp32, ksplit x M x
+        Cout_p) for the partials, finished by a reduce kernel."""
+        _check(self.lib.rnb_conv_x6_launch_splitk(ctypes.byref(params), config_id, stream,
+                                                  sums or None, clip_seg or None, stats_c,
+                                                  ksplit, ws or None),
+               "conv_x6 (config %d, ksplit %d)" % (config_id, ksplit))
 
     def conv_x6r(self, params: ConvParams, variant: int, stream: int, sums: int = 0,
                  clip_seg: int = 0, stats_c: int = 0) -> None:

@@ -57,6 +57,7 @@ for step in "$@"; do
     x6exp) run x6exp 300 python -u scripts/x6_exp.py run ;;
     x6dexp) run x6dexp 300 python -u scripts/x6d_exp.py run ;;
     x6dsweep) run x6dsweep 300 python -u scripts/x6d_exp.py sweep ;;
+    x6dsmall) run x6dsmall 300 python -u scripts/x6d_exp.py small ;;
     bnbreak)
       rm -rf gpurun_out/bnbreak
       run bnbreak 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/bnbreak -o run \

@@ -34,9 +34,12 @@ def tile_name(cid, f32=False):
             return "wt4_%d" % (16 * WINOT_TC[cid])
         if cid in WINO_TC:
             return "wino%d%s" % (16 * WINO_TC[cid], "s" if cid in WINO_SPLIT else "")
-        from rnb_amd.ops.conv_f32 import X6D_BASE, X6R_BASE, is_x6d, is_x6r
+        from rnb_amd.ops.conv_f32 import (X6D_BASE, X6R_BASE, X6K_BASE, X6K_CONFIGS, is_x6d,
+                                          is_x6r, is_x6k)
         if is_x6r(cid):
             return "x6r_%d" % (cid - X6R_BASE)
+        if is_x6k(cid):
+            return "x6k_%dx%d" % k.x6_configs[X6K_CONFIGS[cid - X6K_BASE]]
         if is_x6d(cid):
             return "x6d_%dx%d" % k.x6_configs[cid - X6D_BASE]
         return "%dx%d" % k.f32_configs[cid]

@@ -118,5 +118,45 @@ if __name__ == "__main__":
         build()
     elif sys.argv[1:] == ["sweep"]:
         sweep()
-    else:
+    elif sys.argv[1:] != ["small"]:
         run()
+
+
+def small(clips=4, reps=20):
+    """Every candidate config of the conv4/conv5 shapes at a small clip count
+    (one-video calls), ms, with the BN statistics on where a config takes them."""
+    import torch
+    from rnb_amd.ops.conv_f32 import ConvLayerF32, f32_geom, WINO_ALL, is_x6d
+    dev = torch.device("cuda:0")
+    shapes = [("conv4 spatial", 256, 576, (1, 3, 3), (1, 1, 1), (0, 1, 1), (2, 14, 14)),
+              ("conv4 temporal", 576, 256, (3, 1, 1), (1, 1, 1), (1, 0, 0), (2, 14, 14)),
+              ("conv5 spatial", 512, 1152, (1, 3, 3), (1, 1, 1), (0, 1, 1), (1, 7, 7)),
+              ("conv5 temporal", 1152, 512, (1, 1, 1), (1, 1, 1), (0, 0, 0), (1, 7, 7))]
+    for name, cin, cout, kern, stride, pad, (T, H, W) in shapes:
+        g = f32_geom(cin, cout, kern, stride, pad)
+        layer = ConvLayerF32(torch.randn(cout, cin, *kern) * 0.05, torch.zeros(cout), g, False,
+                             dev, name)
+        x = torch.randn(clips, T, H, W, g.cin_p, device=dev)
+        y = torch.empty(layer.out_shape(x.shape), device=dev)
+        ost = (torch.zeros((1, 2, g.cout_p), dtype=torch.float64, device=dev),
+               torch.zeros(clips, dtype=torch.int32, device=dev))
+        row = []
+        for cid, stats in [(c, st) for c in layer.candidates(x.shape) for st in (True, False)]:
+            if stats and not (cid in WINO_ALL or is_x6d(cid)):
+                continue
+            o = ost if stats else None
+            layer.forward_hip(x, out=y, config=cid, out_stats=o)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                layer.forward_hip(x, out=y, config=cid, out_stats=o)
+            e.record()
+            e.synchronize()
+            row.append((s.elapsed_time(e) / reps, cid, "s" if stats else ""))
+        row.sort()
+        print("%-15s %d clips: %s" % (name, clips, ", ".join("%d%s %.4f" % (c, f, t)
+                                                            for t, c, f in row[:16])), flush=True)
+
+
+if __name__ == "__main__" and sys.argv[1:] == ["small"]:
+    small()

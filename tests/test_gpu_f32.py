@@ -515,6 +515,41 @@ def test_winograd_epilogue_stats_match_fp64_sums(kind):
             assert torch.allclose(got[1], (seg * seg).sum(0), rtol=1e-9, atol=1e-6), (cid, v)
 
 
+@pytest.mark.parametrize("k,s,p,thw,cin", [((1, 3, 3), (1, 1, 1), (0, 1, 1), (1, 7, 7), 64),
+                                           ((3, 1, 1), (1, 1, 1), (1, 0, 0), (2, 7, 7), 256),
+                                           ((1, 3, 3), (1, 2, 2), (0, 1, 1), (2, 14, 14), 64)])
+def test_x6_splitk_exact_integers_and_stats(k, s, p, thw, cin):
+    """Split-K x6 configs (small-M layers: partials per split + reduce kernel
+    with bias / residual / ReLU / per-video BN sums): bit-exact on small
+    integers, sums vs fp64, for every split config with ksplit > 1."""
+    from rnb_amd.ops.conv_f32 import X6K_BASE, X6K_CONFIGS
+    layer = _layer(cin, 150, k, s, p, relu=True, integer=True)
+    x = _input(3, thw, cin, cin, integer=True)
+    oshape = layer.out_shape(x.shape)
+    res = _input(3, oshape[1:4], layer.geom.cout_p, 150, integer=True, seed=3)
+    ref = _ref64(layer, x, res).float()
+    ids = [c for c in range(X6K_BASE, X6K_BASE + len(X6K_CONFIGS))
+           if layer.ksplit_for(c, x.shape) > 1]
+    assert ids, "no split-K config splits this shape"
+    for cid in ids:
+        y = layer.forward_hip(x, res, config=cid)
+        torch.cuda.synchronize()
+        assert torch.equal(y[..., :150].cpu(), ref), (cid, layer.ksplit_for(cid, x.shape))
+    lay2 = _layer(cin, 144, k, s, p, relu=False)
+    xf = _input(3, thw, cin, cin)
+    seg = torch.tensor([0, 2, 2], dtype=torch.int32, device=DEV)
+    for cid in ids:
+        sums = torch.zeros((3, 2, lay2.geom.cout_p), dtype=torch.float64, device=DEV)
+        y = lay2.forward_hip(xf, config=cid, out_stats=(sums, seg))
+        torch.cuda.synchronize()
+        yd = y[..., :144].double().cpu()
+        for v, (a, b) in enumerate([(0, 1), (1, 1), (1, 3)]):
+            part = yd[a:b].reshape(-1, 144)
+            got = sums[v, :, :144].cpu()
+            assert torch.allclose(got[0], part.sum(0), rtol=1e-9, atol=1e-6), (cid, v)
+            assert torch.allclose(got[1], (part * part).sum(0), rtol=1e-9, atol=1e-6), (cid, v)
+
+
 @pytest.mark.parametrize("thw", [(2, 15, 13), (3, 56, 56), (2, 28, 28), (1, 7, 7)])
 def test_x6_rowband_exact_integers_and_stats(thw):
     """Row-band halo x6 kernel (conv_x6r_kernel): bit-exact on small integers
