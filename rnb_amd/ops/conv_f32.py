@@ -370,7 +370,7 @@ class ConvLayerF32:
             c += [X6D_BASE + i for i in range(len(kernels().x6_configs))]
             if self.wino_ok:
                 c += [X6R_BASE + i for i in range(kernels().x6r_variants)]
-            if x_shape is not None:
+            if x_shape is not None and os.environ.get("RNB_X6K", "1") != "0":
                 c += [X6K_BASE + j for j in range(len(X6K_CONFIGS))
                       if self.ksplit_for(X6K_BASE + j, x_shape) > 1]
         ids = self.wino_ids if x6_enabled() else self.wino_ids - WINO_X6

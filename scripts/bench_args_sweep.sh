@@ -15,8 +15,13 @@ for args in "${SW[@]}"; do
   # the bench prints little while it tunes: a heartbeat keeps the call alive
   ( while sleep 60; do echo "  ... $(date +%T) $(wc -l < $log 2>/dev/null) lines"; done ) &
   hb=$!
-  timeout -k 10 600 python bench.py --steps "${STEPS:-20}" --warmup 2 --no-literal --no-check \
-    $args > $log 2>&1
+  # an entry may start with ENV=VALUE words (exported for that run only)
+  envs=(); rest=()
+  for w in $args; do
+    if [[ ${#rest[@]} -eq 0 && $w == *=* && $w != --* ]]; then envs+=("$w"); else rest+=("$w"); fi
+  done
+  env "${envs[@]}" timeout -k 10 600 python bench.py --steps "${STEPS:-20}" --warmup 2 \
+    --no-literal --no-check "${rest[@]}" > $log 2>&1
   rc=$?
   kill $hb 2>/dev/null
   grep -h '"metric"' $log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['p50_ms'], d['p99_ms'], d['config']['job_wall_s'])"
