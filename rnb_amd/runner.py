@@ -28,7 +28,8 @@ from queue import Empty, Full
 NUM_EXIT_MARKERS = 10
 NUM_SUMMARY_SKIPS = 10
 QUEUE_POLL_S = 0.1
-# with RNB_ADAPTIVE_GATHER=1, consumer-side batching keeps gathering at most this
+# adaptive gather (default; RNB_ADAPTIVE_GATHER=0 disables): consumer-side
+# batching keeps gathering at most this
 # long while the replica's previous batch still runs on the GPU
 INFLIGHT_GATHER_S = 0.05
 
@@ -136,8 +137,10 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         # buffer their rows are pulled into (RunnerModel.gather_limits)
         gather = getattr(model, "gather_limits", None)
         gather = gather() if callable(gather) else None
-        # measured neutral on throughput at 1 GPU (profiles/NOTES.md): opt-in
-        adaptive_gather = os.environ.get("RNB_ADAPTIVE_GATHER", "0") == "1"
+        # on by default since round 3: +3.7 % videos/s in interleaved A/B runs of
+        # the headline with the x6 kernels (profiles/r3_adaptive_gather_ab.txt;
+        # round 2 measured it neutral); RNB_ADAPTIVE_GATHER=0 turns it off
+        adaptive_gather = os.environ.get("RNB_ADAPTIVE_GATHER", "1") == "1"
         inflight = None             # completion event of this replica's last batch
         # producer writes straight into its output slot (no staging copy)
         direct_out = (shared_output_ring is not None and num_segments == 1
