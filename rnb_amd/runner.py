@@ -31,7 +31,7 @@ QUEUE_POLL_S = 0.1
 # adaptive gather (default; RNB_ADAPTIVE_GATHER=0 disables): consumer-side
 # batching keeps gathering at most this
 # long while the replica's previous batch still runs on the GPU
-INFLIGHT_GATHER_S = 0.05
+INFLIGHT_GATHER_S = float(os.environ.get("RNB_INFLIGHT_GATHER_MS", "50")) / 1000.0
 
 
 def _set_flag(flag, value, only_if_unset=True):
