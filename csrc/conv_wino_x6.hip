@@ -47,7 +47,8 @@
 #define X6_VALU_PER_MFMA(TC) ((24 + 3 * (TC) - 1) / (3 * (TC)))
 // bottleneck experiments (scripts/x6_exp.py; results are garbage by design):
 // 1 no split VALU, 2 no MFMA, 3 no patch refill loads, 4 no U DMA after the
-// first chunk, 5 no input transform, 6 no epilogue
+// first chunk, 5 no input transform, 6 no epilogue; 7 (exact) equal wave
+// priorities
 #ifndef X6_EXP
 #define X6_EXP 0
 #endif
@@ -134,6 +135,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // static priority for the second half of the waves (conv_x6.hip); X6_EXP 7 = off
+  if (X6_EXP != 7 && wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
   const int tl = lane & 15, q = lane >> 4;
   const int row_bytes = p.W * p.Cin * 4;
   const __amdgpu_buffer_rsrc_t xr =
@@ -393,6 +396,8 @@ __global__ __launch_bounds__(512, 1) void conv_wino_x6h_kernel(const WinoParams 
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // static priority for the second half of the waves (conv_x6.hip); X6_EXP 7 = off
+  if (X6_EXP != 7 && wave >= 8 / 2) __builtin_amdgcn_s_setprio(1);
   const int tg = wave >> 1, xh = wave & 1;
   const int tl = lane & 15, q = lane >> 4;
   const int row_bytes = p.W * p.Cin * 4;
@@ -669,6 +674,8 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : 2) void conv_winot_x6_
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // static priority for the second half of the waves (conv_x6.hip); X6_EXP 7 = off
+  if (X6_EXP != 7 && wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
   const int wgid = w_xcd_remap();
   const int cb = wgid % p.n_cblocks;
   const int tb = wgid / p.n_cblocks;

@@ -37,7 +37,8 @@
 #define X6D_INVALID 0xFFFFFFF0u
 // bottleneck experiments (scripts/x6d_exp.py; results are garbage by design):
 // 1 no split VALU, 2 no MFMA, 3 no activation DMA after the prologue, 4 no
-// weight DMA after the prologue, 6 no epilogue, 7 no per-step wait + barrier
+// weight DMA after the prologue, 6 no epilogue, 7 no per-step wait + barrier;
+// 8 (exact) equal wave priorities (no s_setprio 1 for the second half)
 #ifndef X6D_EXP
 #define X6D_EXP 0
 #endif
@@ -422,6 +423,10 @@ void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
 #pragma unroll
   for (int i = 0; i + 1 < NS; ++i)
     if (s_begin + i < s_end) issue(s_begin + i, i);
+  // static priority for the second half of the waves (the arbitration
+  // losers, MI355X_MICROARCH.md item 4): 1-2 % in interleaved A/B runs
+  // (profiles/r3_x6_exp_interleaved.txt); X6D_EXP 8 keeps equal priorities
+  if (X6D_EXP != 8 && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   if constexpr (!PIPE) {
     // step s's fragments are read and split at its start; the wait at the
     // end of step s - 1 retires step s (NS 3: step s + 1 stays in flight)
@@ -701,6 +706,7 @@ void conv_x6r_kernel(const ConvF32Params p, const X6DStats st) {
   auto issue_group = [&](int c, int g, int half) {
     for (int j = 0; j < G && g * G + j < 9; ++j) issue_w((g * G + j) * nck + c, half * G + j);
   };
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);     // as conv_x6_kernel
   issue_group(0, 0, 0);
   int half = 0;
   for (int c = 0; c < nck; ++c) {
