@@ -441,6 +441,132 @@ __global__ __launch_bounds__(1024) void bn_seg_finalize_running_f32_kernel(BnSeg
   }
 }
 
+// Walk finalize + apply in ONE dispatch (producer epilogue sums, <= 16
+// videos): a one-video call's BNs were two ~5 us dispatches each, the walk
+// above and the apply below. Block 0 walks every segment in order for the
+// mean / var / ss outputs and the running update (8 segments' sums in
+// flight); blocks 1.. own rpb rows each and, per segment their rows touch,
+// turn the segment's fp64 sums into scale / shift in LDS (the walk's
+// formulas, so the output is bit-identical) and apply it. The sums are
+// re-armed by the LAST block to take a ticket: every block has consumed the
+// sums it read (the values went into registers / LDS before the barrier)
+// when it takes its ticket, so no fence is needed -- only the last block
+// writes, nothing reads after it, and the next producer runs after the
+// kernel boundary.
+#define BN_WA_MAX_C 512
+__global__ __launch_bounds__(256) void bn_seg_walk_apply_f32_kernel(
+    BnSegParams p, double* sums, int sums_c, int* ticket, float* z, const float* res,
+    int relu, long long M, int z_stride, int res_stride, int rpb) {
+  __shared__ float lsc[BN_WA_MAX_C], lsh[BN_WA_MAX_C];
+  __shared__ int last;
+  const int C = p.C, CQ = C / 4, tid = threadIdx.x;
+  if (blockIdx.x == 0) {
+    for (int c = tid; c < C; c += 256) {
+      const bool upd = p.running_mean != nullptr && c < p.channels;
+      float rm = upd ? p.running_mean[c] : 0.f, rv = upd ? p.running_var[c] : 0.f;
+      const float g = p.gamma[c], b = p.beta[c];
+      for (int s0 = 0; s0 < p.nseg; s0 += 8) {     // 8 segments' sums in flight
+        double a1[8], a2[8];
+        int rows[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int sc = s0 + u < p.nseg ? s0 + u : p.nseg - 1;
+          rows[u] = (p.coffs[sc + 1] - p.coffs[sc]) * p.rpc;
+          a1[u] = sums[(size_t)sc * 2 * sums_c + c];
+          a2[u] = sums[(size_t)sc * 2 * sums_c + sums_c + c];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int s = s0 + u;
+          if (s >= p.nseg) break;
+          float mu = 0.f, va = 0.f;
+          if (rows[u] > 0) {
+            const double m = a1[u] / (double)rows[u];
+            mu = (float)m;
+            va = (float)fmax(a2[u] / (double)rows[u] - m * m, 0.0);
+          }
+          p.mean[(size_t)s * C + c] = mu;
+          p.var[(size_t)s * C + c] = va;
+          const float sc = g * rsqrtf(va + p.eps);
+          p.ss[(size_t)s * 2 * C + c] = sc;
+          p.ss[(size_t)s * 2 * C + C + c] = b - mu * sc;
+          if (upd && rows[u] >= 2) {
+            rm = (1.f - p.momentum) * rm + p.momentum * mu;
+            rv = (1.f - p.momentum) * rv +
+                 p.momentum * va * ((float)rows[u] / (float)(rows[u] - 1));
+          }
+        }
+      }
+      if (upd) {
+        p.running_mean[c] = rm;
+        p.running_var[c] = rv;
+      }
+    }
+  } else {
+    const long long lo_row = (long long)p.coffs[0] * p.rpc;
+    const long long hi_row = (long long)p.coffs[p.nseg] * p.rpc;
+    const long long b0 = (long long)(blockIdx.x - 1) * rpb;
+    const long long r0 = max(b0, lo_row), r1 = min(min(b0 + rpb, M), hi_row);
+    const int QL = CQ < 256 ? CQ : 256, RL = 256 / QL;   // channel-quad / row lanes
+    const int ql = tid % QL, rl = tid / QL;
+    if (r0 < r1) {
+      int lo = 0, hi = p.nseg - 1;                 // last s with start(s) <= r0
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((long long)p.coffs[mid] * p.rpc <= r0) lo = mid; else hi = mid - 1;
+      }
+      for (int s = lo;; ++s) {
+        const long long s0 = (long long)p.coffs[s] * p.rpc, s1 = (long long)p.coffs[s + 1] * p.rpc;
+        __syncthreads();                           // the previous segment's apply is done
+        for (int c = tid; c < C; c += 256) {
+          const int rows = (int)(s1 - s0);
+          const double a1 = sums[(size_t)s * 2 * sums_c + c];
+          const double a2 = sums[(size_t)s * 2 * sums_c + sums_c + c];
+          float mu = 0.f, va = 0.f;
+          if (rows > 0) {
+            const double m = a1 / (double)rows;
+            mu = (float)m;
+            va = (float)fmax(a2 / (double)rows - m * m, 0.0);
+          }
+          const float sc = p.gamma[c] * rsqrtf(va + p.eps);
+          lsc[c] = sc;
+          lsh[c] = p.beta[c] - mu * sc;
+        }
+        __syncthreads();
+        const long long a = max(r0, s0), b = min(r1, s1);
+        if (rl < RL) {
+          for (int q = ql; q < CQ; q += QL) {
+            const int c = q * 4;
+            const float4 sc = *(const float4*)&lsc[c], sh = *(const float4*)&lsh[c];
+            for (long long r = a + rl; r < b; r += RL) {
+              const float4 v = *(const float4*)(p.y + (size_t)r * p.stride + c);
+              float o[4] = {fmaf(v.x, sc.x, sh.x), fmaf(v.y, sc.y, sh.y), fmaf(v.z, sc.z, sh.z),
+                            fmaf(v.w, sc.w, sh.w)};
+              if (res) {
+                const float4 rv = *(const float4*)(res + (size_t)r * res_stride + c);
+                o[0] += rv.x; o[1] += rv.y; o[2] += rv.z; o[3] += rv.w;
+              }
+              if (relu) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) o[k] = fmaxf(o[k], 0.f);
+              }
+              *(float4*)(z + (size_t)r * z_stride + c) = make_float4(o[0], o[1], o[2], o[3]);
+            }
+          }
+        }
+        if (s1 >= r1) break;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (last) {
+    for (int i = tid; i < p.nseg * 2 * C; i += 256) sums[(size_t)(i / C) * sums_c + i % C] = 0.0;
+    if (tid == 0) atomicExch(ticket, 0);
+  }
+}
+
 // r = (1-m)^K r + acc over the K segments with >= 2 rows; re-arms acc
 __global__ __launch_bounds__(256) void bn_seg_running_f32_kernel(BnSegParams p) {
   const int c = blockIdx.x * 256 + threadIdx.x;
@@ -592,6 +718,34 @@ int rnb_bn_seg_stats_from_sums_f32(double* sums, int sums_c, const int* coffs, i
   if (running_mean != nullptr)
     hipLaunchKernelGGL(bn_seg_running_f32_kernel, dim3((channels + 255) / 256), dim3(256), 0,
                        stream, p);
+  return (int)hipGetLastError();
+}
+
+// rnb_bn_seg_stats_from_sums_f32 + rnb_bn_seg_apply_f32 in one dispatch
+// (bn_seg_walk_apply_f32_kernel) for nseg <= 16; ticket: device int, zero
+// before the first launch (the kernel leaves it zero). -5: not eligible.
+int rnb_bn_seg_walk_apply_f32(double* sums, int sums_c, int* ticket, const int* coffs, int nseg,
+                              int rpc, int C, const float* gamma, const float* beta, float eps,
+                              float momentum, int channels, float* running_mean,
+                              float* running_var, float* mean, float* var, float* ss,
+                              const float* y, float* z, const float* res, int relu, long long M,
+                              int y_stride, int z_stride, int res_stride, hipStream_t stream) {
+  if (M <= 0 || C <= 0 || nseg <= 0) return 0;
+  if (nseg > BN_WALK_MAX_SEG || C > BN_WA_MAX_C) return -5;
+  if (C % 4 || y_stride % 4 || z_stride % 4 || (res && res_stride % 4) || rpc <= 0 ||
+      sums_c < C || channels > C)
+    return -2;
+  if (M > 0x7FFFFFFFLL) return -3;
+  BnSegParams p = {};
+  p.y = y; p.coffs = coffs; p.nseg = nseg; p.rpc = rpc; p.C = C; p.stride = y_stride; p.bps = 1;
+  p.gamma = gamma; p.beta = beta; p.eps = eps; p.momentum = momentum;
+  p.channels = channels; p.running_mean = running_mean; p.running_var = running_var;
+  p.mean = mean; p.var = var; p.ss = ss;
+  // ~4096 float4 per apply block: 256 rows at 64 channels, 32 at 512
+  const int rpb = 16384 / C > 8 ? 16384 / C : 8;
+  const unsigned blocks = 1 + (unsigned)((M + rpb - 1) / rpb);
+  hipLaunchKernelGGL(bn_seg_walk_apply_f32_kernel, dim3(blocks), dim3(256), 0, stream, p, sums,
+                     sums_c, ticket, z, res, relu, M, z_stride, res_stride, rpb);
   return (int)hipGetLastError();
 }
 

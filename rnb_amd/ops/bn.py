@@ -14,9 +14,13 @@ the CPU path.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
+
+
+WALK_APPLY_MAX_SEG = 16     # csrc/bn_ops.hip BN_WALK_MAX_SEG
 
 
 class BatchNormBatch:
@@ -99,6 +103,9 @@ class BatchNormBatch:
         if segments is None:
             segments, rpc = self._whole(M, y.device), 1
         nseg = segments.numel() - 1
+        if (sums is not None and nseg <= WALK_APPLY_MAX_SEG and C <= 512
+                and os.environ.get("RNB_BN_WALK_APPLY", "0") == "1"):
+            return self._walk_apply_f32(y, residual, relu, z, segments, sums, rpc)
         # statistics, scale / shift and the running update (three small
         # kernels, or the producer epilogue's sums), then the apply
         ss = self.scale_shift_f32(y, segments, sums, rpc)
@@ -108,6 +115,39 @@ class BatchNormBatch:
                            segments.data_ptr(), nseg, rpc, ss.data_ptr(), 1 if relu else 0,
                            M, C, Cs, z.shape[-1],
                            residual.shape[-1] if residual is not None else 0, stream)
+        return z
+
+    def _walk_apply_f32(self, y, residual, relu, z, segments, sums, rpc):
+        """Statistics from the producer's epilogue sums, running update and the
+        apply in one dispatch (csrc/bn_ops.hip bn_seg_walk_apply_f32_kernel,
+        <= 16 videos): bit-identical to the walk + apply pair. Opt-in
+        (RNB_BN_WALK_APPLY=1): 40 fewer dispatches per one-video forward but
+        3-4 % slower inside the graphs (profiles/r3_bn_walk_apply_ab.txt)."""
+        from .native import kernels
+        N, T, H, W, Cs = y.shape
+        M, C = N * T * H * W, self.channels_p
+        nseg = segments.numel() - 1
+        if (sums.dtype != torch.float64 or not sums.is_contiguous() or sums.dim() != 3
+                or sums.shape[0] < nseg or sums.shape[1] != 2 or sums.shape[2] < C):
+            raise ValueError("epilogue sums %s do not match %d segments x %d channels"
+                             % (tuple(sums.shape), nseg, C))
+        ticket = getattr(self, "_ticket", None)
+        if ticket is None or ticket.device != y.device:
+            ticket = self._ticket = torch.zeros(1, dtype=torch.int32, device=y.device)
+        mean = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
+        var = torch.empty((nseg, C), dtype=torch.float32, device=y.device)
+        ss = torch.empty((nseg, 2, C), dtype=torch.float32, device=y.device)
+        run = self.update_running
+        stream = torch.cuda.current_stream(y.device).cuda_stream
+        kernels().bn_seg_walk_apply_f32(
+            sums.data_ptr(), sums.shape[2], ticket.data_ptr(), segments.data_ptr(), nseg, rpc, C,
+            self.gamma.data_ptr(), self.beta.data_ptr(), self.eps, self.momentum, self.channels,
+            self.running_mean.data_ptr() if run else None,
+            self.running_var.data_ptr() if run else None,
+            mean.data_ptr(), var.data_ptr(), ss.data_ptr(), y.data_ptr(), z.data_ptr(),
+            residual.data_ptr() if residual is not None else None, 1 if relu else 0, M, Cs,
+            z.shape[-1], residual.shape[-1] if residual is not None else 0, stream)
+        self.mean, self.var = mean[-1], var[-1]
         return z
 
     def _whole(self, M: int, device) -> torch.Tensor:

@@ -254,6 +254,13 @@ class Kernels:
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
             ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_int,
             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        lib.rnb_bn_seg_walk_apply_f32.argtypes = [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+            ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+            ctypes.c_float, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_int, ctypes.c_longlong, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+            ctypes.c_void_p]
         lib.rnb_video_reduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_void_p]
@@ -467,6 +474,15 @@ class Kernels:
         _check(self.lib.rnb_bn_seg_apply_f32(y_ptr, z_ptr, res_ptr, coffs_ptr, nseg, rpc,
                                              ss_ptr, relu, M, C, y_stride, z_stride, res_stride,
                                              stream), "bn_seg_apply_f32")
+
+    def bn_seg_walk_apply_f32(self, sums_ptr, sums_c, ticket_ptr, coffs_ptr, nseg, rpc, C,
+                              gamma_ptr, beta_ptr, eps, momentum, channels, rmean_ptr, rvar_ptr,
+                              mean_ptr, var_ptr, ss_ptr, y_ptr, z_ptr, res_ptr, relu, M,
+                              y_stride, z_stride, res_stride, stream):
+        _check(self.lib.rnb_bn_seg_walk_apply_f32(
+            sums_ptr, sums_c, ticket_ptr, coffs_ptr, nseg, rpc, C, gamma_ptr, beta_ptr, eps,
+            momentum, channels, rmean_ptr, rvar_ptr, mean_ptr, var_ptr, ss_ptr, y_ptr, z_ptr,
+            res_ptr, relu, M, y_stride, z_stride, res_stride, stream), "bn_seg_walk_apply_f32")
 
     def clipgen_u8(self, out_ptr, vids_ptr, starts_ptr, nclips, F, H, W, stream):
         _check(self.lib.rnb_clipgen_u8(out_ptr, vids_ptr, starts_ptr, nclips, F, H, W,

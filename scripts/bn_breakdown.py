@@ -22,10 +22,12 @@ FAMILIES = (
     ("wino spatial", r"conv_wino_f32_kernel"),
     ("wino temporal", r"conv_winot_f32_kernel"),
     ("conv direct", r"conv_f32_kernel"),
+    ("bn walk+apply", r"bn_seg_walk_apply"),
     ("bn sums", r"bn_seg_sums"),
     ("bn finalize", r"bn_seg_finalize"),
     ("bn running", r"bn_seg_running"),
     ("bn apply", r"bn_seg_apply"),
+    ("split-K reduce", r"x6d_splitk_reduce"),
     ("torch elementwise", r"at::native|elementwise|reduce_kernel"),
     ("copies", r"copyBuffer|fillBuffer"),
 )

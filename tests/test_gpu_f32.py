@@ -712,3 +712,81 @@ def test_bn_fused_finalize_running_matches_split_kernels_and_torch(source, nseg)
             rv = (1 - bn.momentum) * rv + bn.momentum * part.var(0, unbiased=True)
     assert torch.allclose(outs[0][3].double(), rm, atol=1e-5)
     assert torch.allclose(outs[0][4].double(), rv, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("nseg,res,relu", [(1, False, True), (5, True, True), (16, True, False)])
+def test_bn_walk_apply_one_dispatch_matches_walk_plus_apply(nseg, res, relu):
+    """The one-dispatch finalize + apply from epilogue sums (<= 16 videos)
+    against the walk + apply pair: bit-identical output, statistics, scale /
+    shift and running statistics; clip offsets (rpc > 1) with empty and
+    one-clip videos, graph-bucket padding rows left untouched, in place
+    (z is y, as the engine calls it), sums re-armed and the ticket left at
+    zero (second call)."""
+    import os
+    from rnb_amd.ops.bn import BatchNormBatch
+    C, rpc = 88, 37
+    bn = torch.nn.BatchNorm3d(C)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-1, 1)
+        bn.running_var.uniform_(0.5, 2)
+    g = torch.Generator().manual_seed(11 + nseg)
+    clips = [int(r) for r in torch.randint(0, 4, (nseg,), generator=g)]
+    if nseg > 3:
+        clips[1], clips[2] = 0, 1
+    offs = [0]
+    for c in clips:
+        offs.append(offs[-1] + c)
+    n_clips = offs[-1] + 2                              # two padding clips
+    M = n_clips * rpc
+    seg = torch.tensor(offs, dtype=torch.int32, device=DEV)
+    y0 = (torch.randn((n_clips, 1, 1, rpc, C), generator=g) * 2 + 0.5).to(DEV)
+    r = torch.randn((n_clips, 1, 1, rpc, C), generator=g).to(DEV) if res else None
+    yd = y0.reshape(M, C).double()
+
+    def fresh_sums():
+        s = torch.zeros((max(nseg, 4), 2, C), dtype=torch.float64, device=DEV)
+        for i in range(nseg):
+            a, b = offs[i] * rpc, offs[i + 1] * rpc
+            s[i, 0] = yd[a:b].sum(0)
+            s[i, 1] = (yd[a:b] * yd[a:b]).sum(0)
+        return s[:nseg]
+
+    outs = []
+    for mode in ("1", "0"):
+        os.environ["RNB_BN_WALK_APPLY"] = mode
+        try:
+            op = BatchNormBatch(bn, C, DEV)
+            for _ in range(2):
+                y = y0.clone()
+                sums = fresh_sums()
+                z = op.forward_hip(y, r, relu, out=y, segments=seg, sums=sums, rpc=rpc)
+                torch.cuda.synchronize()
+                assert z.data_ptr() == y.data_ptr()
+                assert float(sums.abs().sum()) == 0.0, "epilogue sums must be re-armed"
+                if mode == "1":
+                    assert int(op._ticket.item()) == 0
+        finally:
+            os.environ.pop("RNB_BN_WALK_APPLY", None)
+        outs.append([t.cpu() for t in (z, op.mean, op.var, op.running_mean, op.running_var)])
+    # the output is bit-identical; the statistics and the running update to
+    # an ulp (the two kernels may contract the EMA's multiply-adds differently)
+    assert torch.equal(outs[0][0], outs[1][0])
+    for i, (a, b) in enumerate(zip(outs[0][1:], outs[1][1:])):
+        assert torch.allclose(a, b, rtol=1e-6, atol=1e-7), (i, (a - b).abs().max().item())
+    zc = outs[0][0].reshape(M, C)
+    assert torch.equal(zc[offs[-1] * rpc:], y0.reshape(M, C)[offs[-1] * rpc:].cpu())
+    # the apply itself against fp64
+    yc = yd.cpu()
+    for i in range(nseg):
+        a, b = offs[i] * rpc, offs[i + 1] * rpc
+        if b == a:
+            continue
+        mu, va = yc[a:b].mean(0), yc[a:b].var(0, unbiased=False)
+        ref = (yc[a:b] - mu) / torch.sqrt(va + bn.eps) * bn.weight.double() + bn.bias.double()
+        if res:
+            ref = ref + r.reshape(M, C)[a:b].double().cpu()
+        if relu:
+            ref = ref.clamp(min=0)
+        assert (zc[a:b].double() - ref).abs().max().item() < 1e-4
