@@ -651,20 +651,25 @@ class ConvLayerF32:
         # candidates are timed in rounds of alternating order, best round each:
         # timed once in a fixed order, whatever runs late wins by 5-15 % as
         # the clocks settle (profiles/r3_x6_exp_interleaved.txt)
-        def time_one(cid):
+        def time_one(cid, n):
             o = ost if ost is not None and (cid in WINO_ALL or is_x6d(cid)) else None
             self._launch_all(x, y, residual, cid, stream, out_stats=o)       # warm
             start = torch.cuda.Event(enable_timing=True)
             end = torch.cuda.Event(enable_timing=True)
             start.record(stream)
-            for _ in range(reps):
+            for _ in range(n):
                 self._launch_all(x, y, residual, cid, stream, out_stats=o)
             end.record(stream)
             end.synchronize()
-            return start.elapsed_time(end) / reps
+            return start.elapsed_time(end) / n
 
         times = {}
-        time_one(cands[0])                                   # settle the clocks
+        t0 = time_one(cands[0], reps)                        # settle the clocks
+        # small buckets: enough repetitions that a timing spans >= RNB_TUNE_MIN_MS
+        # (3 launches of a 20 us kernel time mostly launch gaps and noise)
+        min_ms = float(os.environ.get("RNB_TUNE_MIN_MS", "0.5"))
+        if min_ms > 0 and t0 > 0:
+            reps = max(reps, min(64, int(math.ceil(min_ms / t0))))
         rounds = max(1, int(os.environ.get("RNB_TUNE_ROUNDS", "2")))
         for rnd in range(rounds):
             for cid in (cands if rnd % 2 == 0 else cands[::-1]):
@@ -672,7 +677,7 @@ class ConvLayerF32:
                     print("[tune] %s x=%s res=%s cid=%d" % (
                         self.name, tuple(x.shape), None if residual is None else
                         tuple(residual.shape), cid), flush=True)
-                t = time_one(cid)
+                t = time_one(cid, reps)
                 times[cid] = min(times.get(cid, t), t)
         best = min(cands, key=lambda c: times[c])
         self._config[tuple(x.shape[:4])] = best
