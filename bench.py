@@ -86,6 +86,11 @@ def parse_args(argv=None):
                          "crosses xGMI; global shares one queue across all GPUs")
     ap.add_argument("--segments", type=int, default=None,
                     help="(segment) segments per video (default min(4, GPUs), >= 2)")
+    ap.add_argument("--segment-layout", default="spread", choices=["spread", "literal"],
+                    help="(segment) spread: loaders and runners on every GPU; literal: the "
+                         "reference's r2p1d-segment.json wiring -- loaders on GPU 0 only, "
+                         "runners on GPUs 1..N-1 pulling the segments over xGMI, CPU "
+                         "aggregator (needs --gpus >= 2)")
     ap.add_argument("--aggregators", type=int, default=1,
                     help="(segment) CPU aggregator replicas; > 1 routes runner outputs by "
                          "request id (IdHashSelector) so a video's segments meet in one "
@@ -143,11 +148,12 @@ def parse_args(argv=None):
     ap.add_argument("--packing", choices=["first-fit", "arrival"], default="first-fit")
     ap.add_argument("--fused-replicas", type=int, default=3)
     ap.add_argument("--no-cross-gpu-extras", dest="cross_gpu_extras", action="store_false",
-                    help="at --gpus > 1, skip the short global (xGMI IPC) and two-stage "
-                         "(RCCL) runs reported under cross_gpu")
+                    help="at --gpus > 1, skip the short global (xGMI IPC), literal segment "
+                         "(loader GPU 0 -> runner GPUs over xGMI) and two-stage (RCCL) runs "
+                         "reported under cross_gpu")
     ap.add_argument("--cross-gpu-steps", type=int, default=4)
-    ap.add_argument("--cross-gpu-timeout", type=float, default=240.0,
-                    help="total seconds for the cross-GPU extras (both topologies); the "
+    ap.add_argument("--cross-gpu-timeout", type=float, default=330.0,
+                    help="total seconds for the cross-GPU extras (all topologies); the "
                          "headline line is printed after them, so keep this bounded")
     ap.add_argument("--trace", type=str, default=None,
                     help="(fused) write a per-kernel time table of the timed steps")
@@ -210,6 +216,13 @@ def pipeline_config(args, n_gpus: int) -> dict:
         # over xGMI), re-joined by the aggregator on the CPU
         seg = args.segments or max(2, min(4, n_gpus))
         na = max(1, args.aggregators)
+        if args.segment_layout == "literal":
+            # reference config/r2p1d-segment.json: loader on GPU 0, runners on
+            # GPUs 1-7, aggregator on the CPU
+            if n_gpus < 2:
+                raise SystemExit("--segment-layout literal needs --gpus >= 2")
+            loader_gpus = [0] * args.loaders
+            runner_gpus = [g for g in gpus[1:] for _ in range(args.replicas)]
         rgroup = {"gpus": runner_gpus, "in_queue": 0, "out_queues": list(range(na))}
         if na > 1:
             rgroup["queue_selector"] = "rnb_amd.selector.IdHashSelector"
@@ -316,6 +329,10 @@ def main(argv=None) -> int:
                 "mean_ms": round(mi_phase.get("mean_ms", float("nan")), 3),
                 "requests": mi_phase.get("count", 0)},
             "stale_event_waits": res.get("stale_event_waits"),
+            # consumer-side gathering per phase: items / rows per model call and
+            # why each gather ended (runner.py GATHER_ENDS)
+            "gather": res.get("gather"),
+            "ipc_edges": res.get("ipc_edges"),
             "bulk_p50_ms": round(res.get("latency", {}).get("p50_ms", float("nan")), 3),
             "bulk_p99_ms": round(res.get("latency", {}).get("p99_ms", float("nan")), 3),
             "barrier_videos_per_s": round(res.get("videos_per_s", 0.0), 2),
@@ -343,6 +360,12 @@ def main(argv=None) -> int:
             rec["literal"] = run_literal_extras(args)
         if res.get("check_dir"):
             rec["numerics"] = check_numerics(args, res["check_dir"])
+            seg = ((rec.get("literal") or {}).get("config4_segment") or {}).get("numerics")
+            strata = rec["numerics"].get("strata")
+            if strata is not None and seg and "aggregate" in (seg.get("strata") or {}):
+                # literal config #4's re-joined segment videos (its own run)
+                strata["segment_rejoined"] = dict(seg["strata"]["aggregate"],
+                                                  run="literal config4_segment")
         line = json.dumps(rec)
     if store is not None:
         # every rank waits for rank 0's run (its launcher drives all GPUs)
@@ -387,7 +410,10 @@ def run_cross_gpu_extras(args) -> dict:
     import subprocess
     root = os.path.dirname(os.path.abspath(__file__))
     out = {}
-    topologies = ["global"] + (["two-stage"] if args.gpus % 2 == 0 else [])
+    # global: one shared queue over all GPUs; segment-literal: BASELINE config
+    # #4 as the reference wires it (loader GPU 0 -> runners on GPUs 1..N-1 ->
+    # CPU aggregator); two-stage: RCCL pairs (BASELINE config #3)
+    topologies = ["global", "segment-literal"] + (["two-stage"] if args.gpus % 2 == 0 else [])
     deadline = time.time() + args.cross_gpu_timeout
     for topo in topologies:
         budget = deadline - time.time()
@@ -397,7 +423,10 @@ def run_cross_gpu_extras(args) -> dict:
         path = os.path.join(root, "logs", "bench", "cross-%s-%dgpu.json" % (topo, args.gpus))
         if os.path.exists(path):
             os.remove(path)                     # never report a previous run's record
-        cmd = [sys.executable, os.path.join(root, "bench.py"), "--pipeline", topo,
+        pipe = ["--pipeline", topo]
+        if topo == "segment-literal":
+            pipe = ["--pipeline", "segment", "--segment-layout", "literal", "--segments", "3"]
+        cmd = [sys.executable, os.path.join(root, "bench.py")] + pipe + [
                "--gpus", str(args.gpus), "--steps", str(args.cross_gpu_steps),
                "--warmup", "1", "--dtype", args.dtype, "--bn", args.bn,
                "--depth", str(args.depth), "--latency-seconds", "2",
@@ -444,7 +473,8 @@ def check_numerics(args, check_dir: str, device=None) -> dict:
     mode, the reference's numerics), from the same decoded clips."""
     try:
         from rnb_amd.numerics import recheck
-        return recheck(check_dir, args.depth, device)
+        # aggregator samples carry no BN mode: the runners served args.bn
+        return recheck(check_dir, args.depth, device, bn_mode=getattr(args, "bn", None))
     except Exception as e:           # reported, never fatal for the headline
         return {"error": "%s: %s" % (type(e).__name__, str(e)[:200])}
 
@@ -487,7 +517,8 @@ def run_literal_extras(args) -> dict:
     runs = [("config2_whole", ["--pipeline", "whole", "--replicas", "1", "--loaders", "1",
                                "--steps", "2", "--warmup", "1", "--videos-per-step", "128",
                                "--latency-mi", "90", "--latency-load", "0",
-                               "--latency-seconds", "4"]),
+                               "--latency-seconds", "4", "--no-check"]),
+            # its numerics (re-joined segment videos) join the headline's strata
             ("config4_segment", ["--pipeline", "segment", "--segments", "3",
                                  "--steps", "2", "--warmup", "1", "--videos-per-step", "128",
                                  "--latency-seconds", "0"])]
@@ -501,7 +532,7 @@ def run_literal_extras(args) -> dict:
         t0 = time.time()
         path = os.path.join(root, "logs", "bench", "literal-%s.json" % key)
         argv = ["--gpus", "1", "--dtype", args.dtype, "--bn", args.bn, "--depth",
-                str(args.depth), "--no-check", "--no-literal"] + extra
+                str(args.depth), "--no-literal"] + extra
         try:
             sub = _run_sub_bench(argv, path, budget)
             mi = sub.get("latency_mi10") or {}
@@ -513,6 +544,8 @@ def run_literal_extras(args) -> dict:
             if mi:
                 out[key]["poisson"] = {k: mi.get(k) for k in ("mean_interval_ms", "p50_ms",
                                                                "p99_ms", "mean_ms", "requests")}
+            if sub.get("numerics") is not None:
+                out[key]["numerics"] = sub["numerics"]
         except Exception as e:       # reported, never fatal for the headline
             out[key] = {"error": "%s: %s" % (type(e).__name__, str(e)[:300]),
                         "wall_s": round(time.time() - t0, 1)}

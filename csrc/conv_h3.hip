@@ -1,0 +1,480 @@
+// fp32 direct implicit-GEMM 3-D convolution with the fp32 products on the
+// fp16 matrix cores ("h3"). Same GEMM view, gather table, activation staging
+// and epilogue as the x6 direct kernel (conv_x6.hip), but each fp32 operand
+// is split into TWO fp16 parts instead of three bf16 parts:
+//
+//   a s = ah + al + e,  ah = fp16(a s), al = fp16(a s - ah)   (both RNE)
+//
+// a s - ah is exact in fp32 and has <= 12 significant bits, so |e| <= one
+// fp32 ulp of a s (fp16 keeps 11). The weights are split the same way on the
+// host (after a per-layer power-of-two scale that puts their largest value
+// near 2^14), the activations in registers after scaling by in_scale = 2^6,
+// which keeps al a normal fp16 for |a| >= 2^-9 (smaller values keep an
+// absolute error below 2^-31) and inputs below 2^10 clear of the fp16 range.
+// The fp32 product is then
+//
+//   ah bh + al bh + ah bl   (+ al bl <= 2^-22 |ab|, dropped: NPROD 3)
+//
+// each product of two fp16 values exact in the fp32 accumulator, scaled by a
+// power of two that the epilogue removes exactly. The error per product
+// (<= ~2^-21 |ab| worst case, dropped term plus the two representation
+// errors) is the order of x6's dropped terms and of the rounding of fp32
+// accumulation over K >= 64 products; NPROD 4 keeps al bl as well (products
+// of the 22-bit representations exact).
+//
+// MFMA pairing: a K step is 32 channels (two 16-channel sub-steps s0, s1).
+// Lane (row/col, quad q) of v_mfma_f32_16x16x32_f16 supplies k = 8q .. 8q+7;
+// its first four k are channels 4q .. 4q+3 of s0, the last four the same
+// channels of s1. With A = (Ah0 | Ah1) and (Al0 | Al1) (one 16-B chunk each,
+// host layout) and B = (H0 ; H1), (L0 ; L1) (the lane's split activations):
+//
+//   (Al0|Al1) x (H0;H1) + (Ah0|Ah1) x (L0;L1) + (Ah0|Ah1) x (H0;H1)
+//
+// = 3 MFMAs per 32 channels, against 6 for x6 (3 per 16 channels): half the
+// matrix-core time, and 5 VALU per value pair for the split (v_pk_mul, one
+// v_cvt_pk_f16_f32 each way, two v_fma_mix_f32 for the exact residuals)
+// instead of 9.
+//
+// Staging (as conv_x6_kernel): the two sub-steps' gathered activations are
+// LDS-DMA'd into two 64-B-row planes with the x6 direct swizzle, the split
+// weights (128-B rows, x6_chunk order) linearly; 2 LDS stages, counted
+// vmcnt + raw barrier, gather-table entries through scalar loads.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "x6d_common.h"
+
+typedef _Float16 h3f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h3f16x2 __attribute__((ext_vector_type(2)));
+
+static __device__ __forceinline__ x6f32x4 h3_mma(const wu32x4& a, const wu32x4& b,
+                                                 const x6f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h3f16x8, a),
+                                                __builtin_bit_cast(h3f16x8, b), c, 0, 0, 0);
+}
+
+// a - h exactly, h the low (HI = 0) or high half of a packed fp16 pair (one
+// v_fma_mix_f32: the fp16 operand is widened exactly, a single rounding of
+// an exactly representable difference)
+template <int HI>
+static __device__ __forceinline__ float h3_residual(uint32_t hpk, float a) {
+  float r;
+  if constexpr (HI)
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hpk), "v"(a));
+  else
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[0,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hpk), "v"(a));
+  return r;
+}
+
+// split 4 fp32 values (already scaled) into packed fp16 hi (h[0..1]) and lo (l[0..1])
+static __device__ __forceinline__ void h3_split4(const x6f32x4& v, uint32_t* h, uint32_t* l) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const wf32x2 a = (wf32x2){v[2 * k], v[2 * k + 1]};
+    const uint32_t hu = __builtin_bit_cast(uint32_t, __builtin_convertvector(a, h3f16x2));
+    const wf32x2 r = (wf32x2){h3_residual<0>(hu, a[0]), h3_residual<1>(hu, a[1])};
+    h[k] = hu;
+    l[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, h3f16x2));
+  }
+}
+
+struct H3B {
+  wu32x4 h, l;               // (H0 ; H1), (L0 ; L1)
+};
+
+// input BatchNorm on load (AFF): per stage, the scale / shift of the step's
+// 32 channels for each clip the tile touches, [clip][sub][scale, shift][16]
+// (256 B per clip), DMA'd with the step's activations
+#define H3_AFF_CLIPS 8
+
+template <int TP, int TC, int WP, int WC, int MINB, bool ST, int NPROD, bool AFF>
+__global__ __launch_bounds__(64 * WP * WC, MINB)
+void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
+  constexpr int NS = 2;
+  constexpr int NW = WP * WC;
+  constexpr int P_TILE = WP * TP * 16, C_TILE = WC * TC * 16;
+  constexpr int PLANE = P_TILE * 64;               // one 16-channel sub-step, 64-B rows
+  constexpr int ACT_BYTES = 2 * PLANE;
+  constexpr int W_BYTES = C_TILE * 128;            // 32 split channels per weight row
+  constexpr int SS_BYTES = AFF ? H3_AFF_CLIPS * 256 : 0;
+  constexpr int BUF = ACT_BYTES + W_BYTES + SS_BYTES;
+  static_assert(!AFF || NW >= 2, "the scale/shift DMA takes two waves");
+  constexpr int A_INSTR = P_TILE / (16 * NW);      // per plane: 1 KB = 16 rows per DMA
+  constexpr int W_TOTAL = C_TILE / 8;              // 1 KB = 8 weight rows
+  constexpr int W_INSTR = (W_TOTAL + NW - 1) / NW;
+  constexpr int VM_STAGE = 2 * A_INSTR + W_INSTR;
+  static_assert(P_TILE % (16 * NW) == 0, "activation DMA split");
+  static_assert(NPROD == 3 || NPROD == 4, "products per fp32 product");
+  __shared__ __attribute__((aligned(16))) char lds[NS * BUF];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wp = wave / WC, wc = wave % WC;
+
+  // XCD-aware bijective block remap, split-K index (conv_x6_kernel)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wgid0 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int ksplit = st.ksplit > 1 ? st.ksplit : 1;
+  const int kidx = wgid0 % ksplit, wgid = wgid0 / ksplit;
+  const int ctile = wgid % p.n_ctiles;
+  const int ptile = wgid / p.n_ctiles;
+  const int p0 = ptile * P_TILE;
+  const int c0 = ctile * C_TILE;
+
+  // activation DMA (per plane, as conv_x6_kernel): lane -> row lane >> 2 of
+  // the instruction's 16, physical chunk lane & 3 holding logical chunk kc
+  const int lrow = lane >> 2;
+  const int kc = x6d_swz(lane & 3, lrow);
+  int rbase[A_INSTR], rmask[A_INSTR];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) {
+    const int m = p0 + (wave * A_INSTR + i) * 16 + lrow;
+    int mask = 0, base = 0;
+    int n, to, ho, wo;
+    if (f32_decode_row(p, m, n, to, ho, wo)) {
+      const int t0 = to * p.ST - p.PT, h0 = ho * p.SH - p.PH, w0 = wo * p.SW - p.PW;
+      mask = f32_range_mask(t0, p.KT, p.T) | (f32_range_mask(h0, p.KH, p.H) << 8) |
+             (f32_range_mask(w0, p.KW, p.W) << 16);
+      base = ((((n * p.T + t0) * p.H + h0) * p.W + w0) * p.Cin_p) * 4;
+    }
+    rbase[i] = base;
+    rmask[i] = mask;
+  }
+  const x6d_u32x4 xr = x6d_rsrc(p.x, p.x_bytes);
+  // split weights [K_pad / 32][w_rows][128 B]
+  const x6d_u32x4 wr = x6d_rsrc(p.w, (uint32_t)(p.K_pad / 32) * (uint32_t)p.w_rows * 128u);
+
+  // AFF: clips of the tile (clip_lo .. clip_lo + 7), the scale/shift DMA
+  // lane's clip / sub-step / row (scale or shift) / quad, and its video
+  const int rows_per_clip = p.To * p.Ho * p.Wo;
+  const int clip_lo = __builtin_amdgcn_readfirstlane(p0 / rows_per_clip);
+  const x6d_u32x4 sr = x6d_rsrc(st.in_ss, 0x7FFFFF00u);
+  uint32_t ss_off = X6D_INVALID;          // + channel base * 4 per step
+  int ss_sub = 0;
+  if constexpr (AFF) {
+    const int li = (wave & 1) * 64 + lane;            // waves 0 / 1 issue the two DMAs
+    const int ci = li >> 4, sub = (li >> 3) & 1, which = (li >> 2) & 1, q = li & 3;
+    const int clip = clip_lo + ci;
+    ss_sub = sub;
+    if (clip < p.N && clip * rows_per_clip < p0 + P_TILE) {
+      const int seg = st.in_seg[clip];
+      ss_off = (uint32_t)(((seg * 2 + which) * p.Cin_p + 4 * q) * 4);
+    }
+  }
+
+  auto issue = [&](int t, int slot) {
+    // the 8 gather-table entries of sub-steps 2t, 2t + 1 (scalar loads)
+    const __attribute__((address_space(4))) int* tab =
+        (const __attribute__((address_space(4))) int*)(p.ktab + t * 8);
+    int e[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) e[i] = tab[i];
+    const bool k1 = (kc & 1) != 0, k2 = (kc & 2) != 0;
+    char* base = lds + slot * BUF;
+    // the lane's entry by selects on scalar values (an indexed pick would
+    // become a scratch load, and its wait would drain the DMAs in flight)
+    const int ex0 = k2 ? (k1 ? e[6] : e[4]) : (k1 ? e[2] : e[0]);
+    const int ey0 = k2 ? (k1 ? e[7] : e[5]) : (k1 ? e[3] : e[1]);
+    const int ex1 = k2 ? (k1 ? e[14] : e[12]) : (k1 ? e[10] : e[8]);
+    const int ey1 = k2 ? (k1 ? e[15] : e[13]) : (k1 ? e[11] : e[9]);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int ex = sub ? ex1 : ex0;
+      const int ey = sub ? ey1 : ey0;
+#pragma unroll
+      for (int i = 0; i < A_INSTR; ++i) {
+        const bool ok = (rmask[i] & ey) == ey;
+        const uint32_t off = ok ? (uint32_t)(rbase[i] + ex) : X6D_INVALID;
+        x6d_dma16(xr, off, base + sub * PLANE + (wave * A_INSTR + i) * 1024);
+      }
+    }
+    const uint32_t wbase = ((uint32_t)t * (uint32_t)p.w_rows + (uint32_t)c0) * 128u;
+#pragma unroll
+    for (int j = 0; j < W_INSTR; ++j) {
+      const int instr = (W_TOTAL % NW == 0) ? wave + NW * j : min(wave + NW * j, W_TOTAL - 1);
+      x6d_dma16(wr, wbase + (uint32_t)(instr * 1024 + lane * 16), base + ACT_BYTES + instr * 1024);
+    }
+    if constexpr (AFF) {
+      // the input channels of sub-step 2t + ss_sub (Cin_p % 16 == 0: one tap)
+      if (wave < 2) {
+        const int cb = ((2 * t + ss_sub) * 16) % p.Cin_p;
+        x6d_dma16(sr, ss_off == X6D_INVALID ? X6D_INVALID : ss_off + (uint32_t)(cb * 4),
+                  base + ACT_BYTES + W_BYTES + wave * 1024);
+      }
+    }
+  };
+
+  const int frow = lane & 15, fq = lane >> 4;
+  x6f32x4 acc[TP][TC];                // bias / out_scale (split-K: 0, the reduce adds it)
+#pragma unroll
+  for (int b = 0; b < TC; ++b) {
+    const int c = c0 + (wc * TC + b) * 16 + 4 * fq;
+    float4 b4 = *(const float4*)(p.bias + c);
+    if (ksplit > 1) b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const x6f32x4 bv = (x6f32x4){b4.x, b4.y, b4.z, b4.w} * st.acc_scale;
+#pragma unroll
+    for (int a = 0; a < TP; ++a) acc[a][b] = bv;
+  }
+
+  const int a_chunk = x6d_swz(fq, frow) << 4;
+  const int w_hh = x6_chunk(2 * fq, frow) << 4, w_ll = x6_chunk(2 * fq + 1, frow) << 4;
+  const float in_scale = st.in_scale;
+  // AFF: the B rows' tap-validity masks and clip slots (padding taps must
+  // stay zero after the affine + ReLU)
+  int bmask[TP], bclip[TP];
+#pragma unroll
+  for (int tp = 0; tp < TP; ++tp) {
+    bmask[tp] = 0;
+    bclip[tp] = 0;
+    if constexpr (AFF) {
+      const int m = p0 + (wp * TP + tp) * 16 + frow;
+      int n, to, ho, wo;
+      if (f32_decode_row(p, m, n, to, ho, wo)) {
+        const int t0 = to * p.ST - p.PT, h0 = ho * p.SH - p.PH, w0 = wo * p.SW - p.PW;
+        bmask[tp] = f32_range_mask(t0, p.KT, p.T) | (f32_range_mask(h0, p.KH, p.H) << 8) |
+                    (f32_range_mask(w0, p.KW, p.W) << 16);
+        bclip[tp] = min(n - clip_lo, H3_AFF_CLIPS - 1) * 256;
+      }
+    }
+  }
+  int ey_cur[2] = {0, 0};                 // AFF: required tap bits of the current sub-steps
+  auto load_b = [&](int slot, int tp) -> H3B {
+    const int row = (wp * TP + tp) * 16 + frow;
+    const char* b0 = lds + slot * BUF + row * 64 + a_chunk;
+    x6f32x4 v0 = *(const x6f32x4*)b0;
+    x6f32x4 v1 = *(const x6f32x4*)(b0 + PLANE);
+    if constexpr (AFF) {
+      const char* ss = lds + slot * BUF + ACT_BYTES + W_BYTES + bclip[tp] + fq * 16;
+      const x6f32x4 sc0 = *(const x6f32x4*)ss, sh0 = *(const x6f32x4*)(ss + 64);
+      const x6f32x4 sc1 = *(const x6f32x4*)(ss + 128), sh1 = *(const x6f32x4*)(ss + 192);
+      const float m0 = (bmask[tp] & ey_cur[0]) == ey_cur[0] ? in_scale : 0.f;
+      const float m1 = (bmask[tp] & ey_cur[1]) == ey_cur[1] ? in_scale : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v0[j] = fmaxf(fmaf(v0[j], sc0[j], sh0[j]), 0.f) * m0;
+        v1[j] = fmaxf(fmaf(v1[j], sc1[j], sh1[j]), 0.f) * m1;
+      }
+    } else {
+      v0 *= in_scale;
+      v1 *= in_scale;
+    }
+    uint32_t h[4], l[4];
+    h3_split4(v0, h, l);
+    h3_split4(v1, h + 2, l + 2);
+    H3B f;
+    f.h = (wu32x4){h[0], h[1], h[2], h[3]};
+    f.l = (wu32x4){l[0], l[1], l[2], l[3]};
+    return f;
+  };
+  auto mma_tc = [&](int slot, int tc, const H3B (&bf)[TP]) {
+    const char* wrow = lds + slot * BUF + ACT_BYTES + ((wc * TC + tc) * 16 + frow) * 128;
+    const wu32x4 ah = *(const wu32x4*)(wrow + w_hh);
+    const wu32x4 al = *(const wu32x4*)(wrow + w_ll);
+    if constexpr (NPROD == 4) {
+#pragma unroll
+      for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(al, bf[tp].l, acc[tp][tc]);
+    }
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(al, bf[tp].h, acc[tp][tc]);
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(ah, bf[tp].l, acc[tp][tc]);
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(ah, bf[tp].h, acc[tp][tc]);
+  };
+
+  // K-step range in 16-channel steps (temporal tap skip as conv_x6_kernel),
+  // then in 32-channel steps
+  const int nsteps16 = p.K_pad / 16;
+  int s_begin = 0, s_end = nsteps16;
+  if (p.KH == 1 && p.KW == 1 && p.KT > 1) {
+    int n0, t0, n1, t1, hh, ww;
+    f32_decode_row(p, p0, n0, t0, hh, ww);
+    f32_decode_row(p, min(p0 + P_TILE, p.M) - 1, n1, t1, hh, ww);
+    n0 = __builtin_amdgcn_readfirstlane(n0);
+    n1 = __builtin_amdgcn_readfirstlane(n1);
+    t0 = __builtin_amdgcn_readfirstlane(t0);
+    t1 = __builtin_amdgcn_readfirstlane(t1);
+    if (n0 == n1) {
+      const int dt_lo = max(0, p.PT - t1 * p.ST);
+      const int dt_hi = min(p.KT - 1, p.T - 1 + p.PT - t0 * p.ST);
+      if (dt_hi >= dt_lo) {
+        s_begin = (dt_lo * p.Cin_p) / 16;
+        s_end = min(nsteps16, ((dt_hi + 1) * p.Cin_p + 15) / 16);
+      }
+    }
+  }
+  int t_begin = s_begin / 2, t_end = (s_end + 1) / 2;
+  if (ksplit > 1) {
+    const int len = t_end - t_begin;
+    const int a = t_begin + (int)((long long)len * kidx / ksplit);
+    const int b = t_begin + (int)((long long)len * (kidx + 1) / ksplit);
+    t_begin = a;
+    t_end = b;
+  }
+  if (t_begin < t_end) issue(t_begin, 0);
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);    // as conv_x6_kernel
+  x6d_wait_vm<0>();
+  x6d_barrier();
+  for (int t = t_begin; t < t_end; ++t) {
+    const int it = t - t_begin;
+    // slot (it + 1) & 1 was read in step t - 1, finished by every wave
+    if (t + 1 < t_end) issue(t + 1, (it + 1) & 1);
+    if constexpr (AFF) {
+      // the tap of sub-steps 2t, 2t + 1: quad 0's gather-table requirement
+      const __attribute__((address_space(4))) int* tab =
+          (const __attribute__((address_space(4))) int*)(p.ktab + t * 8);
+      ey_cur[0] = tab[1];
+      ey_cur[1] = tab[9];
+    }
+    H3B bf[TP];
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp) bf[tp] = load_b(it & 1, tp);
+#pragma unroll
+    for (int tc = 0; tc < TC; ++tc) mma_tc(it & 1, tc, bf);
+    x6d_wait_vm<0>();
+    x6d_barrier();
+  }
+
+  const float out_scale = st.out_scale;
+#pragma unroll
+  for (int tp = 0; tp < TP; ++tp)
+#pragma unroll
+    for (int tc = 0; tc < TC; ++tc) acc[tp][tc] *= out_scale;     // exact: a power of two
+  if (ksplit > 1) {                 // raw partial sums -> ws[kidx][m][c]
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp) {
+      const int m = p0 + (wp * TP + tp) * 16 + frow;
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc) {
+        const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
+        if (m < p.M && c < p.Cout_p)
+          *(x6f32x4*)(st.ws + ((size_t)kidx * p.M + m) * p.Cout_p + c) = acc[tp][tc];
+      }
+    }
+    return;
+  }
+  x6d_epilogue<TP, TC, NW, C_TILE, ST>(p, st, acc, p0, p.M, p0 + P_TILE, c0, wp, wc, lane, lds,
+                                       NS * BUF);
+}
+
+// ---------------------------------------------------------------------------
+// host side: config table + launcher (C ABI, ctypes)
+// ---------------------------------------------------------------------------
+struct ConvH3Config {
+  int p_tile, c_tile, threads;
+  void (*kernel)(const ConvF32Params, const X6DStats);
+  void (*kernel_st)(const ConvF32Params, const X6DStats);
+  void (*kernel_aff)(const ConvF32Params, const X6DStats);       // + input BN on load
+  void (*kernel_aff_st)(const ConvF32Params, const X6DStats);
+};
+
+#define H3CFG(TP, TC, WP, WC, MINB, NPROD)                                     \
+  {WP * TP * 16, WC * TC * 16, 64 * WP * WC,                                    \
+   conv_h3_kernel<TP, TC, WP, WC, MINB, false, NPROD, false>,                   \
+   conv_h3_kernel<TP, TC, WP, WC, MINB, true, NPROD, false>,                    \
+   conv_h3_kernel<TP, TC, WP, WC, MINB, false, NPROD, true>,                    \
+   conv_h3_kernel<TP, TC, WP, WC, MINB, true, NPROD, true>}
+// LDS per block = 2 stages x (P_TILE x 128 + C_TILE x 128) bytes
+static const ConvH3Config kH3Configs[] = {
+    H3CFG(2, 9, 8, 1, 1, 3),   //  0: 256 px x 144 ch (100 KB)
+    H3CFG(3, 9, 8, 1, 1, 3),   //  1: 384 px x 144 ch (132 KB)
+    H3CFG(1, 9, 8, 1, 2, 3),   //  2: 128 px x 144 ch, 2 blocks per CU (68 KB)
+    H3CFG(2, 8, 8, 1, 1, 3),   //  3: 256 px x 128 ch
+    H3CFG(1, 8, 8, 1, 2, 3),   //  4: 128 px x 128 ch, 2 blocks per CU
+    H3CFG(2, 4, 8, 1, 2, 3),   //  5: 256 px x  64 ch, 2 blocks per CU (80 KB)
+    H3CFG(3, 4, 8, 1, 1, 3),   //  6: 384 px x  64 ch
+    H3CFG(2, 6, 8, 1, 1, 3),   //  7: 256 px x  96 ch (stem)
+    H3CFG(1, 6, 8, 1, 2, 3),   //  8: 128 px x  96 ch, 2 blocks per CU
+    H3CFG(2, 4, 4, 2, 2, 3),   //  9: 128 px x 128 ch, 4 waves x 2, 2 blocks per CU
+    H3CFG(1, 8, 4, 1, 3, 3),   // 10:  64 px x 128 ch, 4 waves, 3 blocks per CU (48 KB)
+    H3CFG(2, 9, 8, 1, 1, 4),   // 11: config 0 with the fourth product
+    H3CFG(1, 9, 8, 1, 2, 4),   // 12: config 2 with the fourth product
+};
+static const int kNumH3Configs = sizeof(kH3Configs) / sizeof(kH3Configs[0]);
+
+extern "C" {
+
+int rnb_conv_h3_num_configs() { return kNumH3Configs; }
+
+int rnb_conv_h3_config_info(int id, int* p_tile, int* c_tile) {
+  if (id < 0 || id >= kNumH3Configs) return -1;
+  *p_tile = kH3Configs[id].p_tile;
+  *c_tile = kH3Configs[id].c_tile;
+  return 0;
+}
+
+// p.w = split weights [K_pad / 32][w_rows][8 chunks x 8 fp16] (x6_chunk order
+// per row: chunk 2 q = (Ah0 | Ah1), 2 q + 1 = (Al0 | Al1) of channel quad q
+// of the two 16-channel sub-steps), scaled by 2^sw; p.K_pad = K rounded up
+// to 32, p.ktab >= K_pad / 4 entries. in_scale = 2^sa (activations),
+// out_scale = 2^-(sa + sw). sums / ksplit / ws as rnb_conv_x6_launch_splitk.
+// Whether config ``config_id`` can apply the input BatchNorm on load for
+// this geometry: 16-channel sub-steps inside one tap, and a pixel tile that
+// touches at most H3_AFF_CLIPS clips.
+int rnb_conv_h3_affine_ok(int config_id, int cin_p, int rows_per_clip) {
+  if (config_id < 0 || config_id >= kNumH3Configs || cin_p % 16 != 0 || rows_per_clip <= 0)
+    return 0;
+  const int pt = kH3Configs[config_id].p_tile;
+  return (pt - 1) / rows_per_clip + 2 <= H3_AFF_CLIPS ? 1 : 0;
+}
+
+int rnb_conv_h3_launch(const ConvF32Params* pp, int config_id, hipStream_t stream, double* sums,
+                       const int* clip_seg, int stats_c, int ksplit, float* ws, float in_scale,
+                       float out_scale, const float* in_ss, const int* in_seg) {
+  if (config_id < 0 || config_id >= kNumH3Configs) return -1;
+  ConvF32Params p = *pp;
+  const ConvH3Config& cfg = kH3Configs[config_id];
+  if (p.Cin_p % 4 != 0 || p.Cout_p % 4 != 0 || p.K_pad % 32 != 0) return -2;
+  if (p.K_total > p.K_pad) return -3;
+  if (p.M <= 0) return 0;
+  if (p.y_stride < p.Cout_p || (p.res && p.res_stride < p.Cout_p)) return -4;
+  if (p.y_stride % 4 != 0 || (p.res && p.res_stride % 4 != 0)) return -4;
+  const long long xb = (long long)p.N * p.T * p.H * p.W * p.Cin_p * 4;
+  if (xb > 0x7FFFFF00LL) return -5;
+  if ((long long)p.M * p.y_stride * 4 > 0x7FFFFF00LL) return -6;
+  if (p.res && (long long)p.M * p.res_stride * 4 > 0x7FFFFF00LL) return -6;
+  if (p.KT > 8 || p.KH > 8 || p.KW > 8) return -10;
+  if ((long long)(p.K_pad / 32) * p.w_rows * 128 > 0x7FFFFF00LL) return -11;
+  if (!(in_scale > 0.f) || !(out_scale > 0.f)) return -15;
+  p.x_bytes = (uint32_t)xb;
+  f32_magic_div((uint32_t)p.Wo, &p.mWo, &p.sWo);
+  f32_magic_div((uint32_t)p.Ho, &p.mHo, &p.sHo);
+  f32_magic_div((uint32_t)p.To, &p.mTo, &p.sTo);
+  p.row_mode = 0;
+  p.n_ptiles = (p.M + cfg.p_tile - 1) / cfg.p_tile;
+  p.n_ctiles = (p.Cout_p + cfg.c_tile - 1) / cfg.c_tile;
+  const long long blocks = (long long)p.n_ptiles * p.n_ctiles;
+  if (blocks > 0x7FFFFFFF) return -7;
+  if (p.n_ctiles * cfg.c_tile > p.w_rows) return -8;
+  if (!p.ktab) return -9;
+  if (sums && (!clip_seg || stats_c < p.Cout_p)) return -12;
+  X6DStats st;
+  st.sums = sums;
+  st.clip_seg = clip_seg;
+  st.stats_c = stats_c;
+  st.ksplit = 1;
+  st.ws = nullptr;
+  st.in_scale = in_scale;
+  st.out_scale = out_scale;
+  st.acc_scale = 1.f / out_scale;            // exact: powers of two
+  st.in_ss = in_ss;
+  st.in_seg = in_seg;
+  const bool aff = in_ss != nullptr;
+  if (aff && (!in_seg || !rnb_conv_h3_affine_ok(config_id, p.Cin_p, p.To * p.Ho * p.Wo)))
+    return -16;
+  if (ksplit > 1) {
+    if (!ws || ksplit > 16) return -14;
+    st.ksplit = ksplit;
+    st.ws = ws;
+    hipLaunchKernelGGL(aff ? cfg.kernel_aff : cfg.kernel, dim3((unsigned)(blocks * ksplit)),
+                       dim3(cfg.threads), 0, stream, p, st);
+    return rnb_x6d_splitk_reduce(&p, &st, stream);
+  }
+  hipLaunchKernelGGL(aff ? (sums ? cfg.kernel_aff_st : cfg.kernel_aff)
+                         : (sums ? cfg.kernel_st : cfg.kernel),
+                     dim3((unsigned)blocks), dim3(cfg.threads), 0, stream, p, st);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -45,13 +45,6 @@
 // the ~24 VALU ops of a step (split + its share of the transform) spread
 // over its 3 TC MFMAs
 #define X6_VALU_PER_MFMA(TC) ((24 + 3 * (TC) - 1) / (3 * (TC)))
-// bottleneck experiments (scripts/x6_exp.py; results are garbage by design):
-// 1 no split VALU, 2 no MFMA, 3 no patch refill loads, 4 no U DMA after the
-// first chunk, 5 no input transform, 6 no epilogue; 7 (exact) equal wave
-// priorities
-#ifndef X6_EXP
-#define X6_EXP 0
-#endif
 // buffer offset past every tensor (x_bytes <= 0x7FFFFF00): padding loads
 #define X6_OOB 0x80000000u
 
@@ -59,15 +52,8 @@
 
 typedef __bf16 wbf16x2 __attribute__((ext_vector_type(2)));
 
-// x6_split_exact, or the bottleneck experiment without the split VALU
+// the exact 3-way split (x6_common.h)
 static __device__ __forceinline__ X6B x6_split(const wf32x4& v) {
-  if constexpr (X6_EXP == 1) {
-    const uint32_t a = __float_as_uint(v[0]), b = __float_as_uint(v[1]);
-    const uint32_t c = __float_as_uint(v[2]), d = __float_as_uint(v[3]);
-    X6B f;
-    f.r = (wu32x8){a, b, c, d, a, b, c, d};
-    return f;
-  }
   return x6_split_exact(v);
 }
 
@@ -76,12 +62,6 @@ static __device__ __forceinline__ X6B x6_split(const wf32x4& v) {
 template <int TC>
 static __device__ __forceinline__ void x6_step(wf32x4 (&acc)[TC], const X6A (&a)[TC],
                                                const X6B& b) {
-  if constexpr (X6_EXP == 2) {
-#pragma unroll
-    for (int tc = 0; tc < TC; ++tc)
-      acc[tc][0] += __uint_as_float(a[tc].hm[0] ^ a[tc].hl[1] ^ b.r[0] ^ b.r[3] ^ b.r[5]);
-    return;
-  }
   const wu32x4 lm = __builtin_shufflevector(b.r, b.r, 0, 1, 2, 3);
   const wu32x4 mh = __builtin_shufflevector(b.r, b.r, 2, 3, 4, 5);
   const wu32x4 hh = __builtin_shufflevector(b.r, b.r, 4, 5, 6, 7);
@@ -135,8 +115,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // static priority for the second half of the waves (conv_x6.hip); X6_EXP 7 = off
-  if (X6_EXP != 7 && wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
+  // static priority for the second half of the waves (conv_x6.hip)
+  if (wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
   const int tl = lane & 15, q = lane >> 4;
   const int row_bytes = p.W * p.Cin * 4;
   const __amdgpu_buffer_rsrc_t xr =
@@ -239,14 +219,12 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
     }
   };
   auto transform_a = [&](wf32x4 (&v)[16]) {          // V row 0 (e2 kept in row 2)
-    if constexpr (X6_EXP == 5) return;
     row_t(v, 0);
     row_t(v, 2);
 #pragma unroll
     for (int j = 0; j < 4; ++j) comb(v[j], v[j], v[8 + j], false);
   };
   auto transform_b = [&](wf32x4 (&v)[16]) {          // V rows 1-3, in place
-    if constexpr (X6_EXP == 5) return;
     row_t(v, 1);
     row_t(v, 3);
 #pragma unroll
@@ -271,7 +249,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
         if (k == 4) transform_b(v);
         X6A af[TC];
         const X6B bf = x6_split(v[x]);
-        if constexpr (decltype(refill)::value && X6_EXP != 3) v[x] = load_one(next, x);
+        if constexpr (decltype(refill)::value) v[x] = load_one(next, x);
         x6_read_a<TC>(af, ub, x, frow, q);
         x6_step<TC>(acc[x], af, bf);
       }
@@ -279,7 +257,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
       X6A af[2][TC];
       X6B bf[2];
       bf[0] = x6_split(v[0]);
-      if constexpr (decltype(refill)::value && X6_EXP != 3) v[0] = load_one(next, 0);
+      if constexpr (decltype(refill)::value) v[0] = load_one(next, 0);
       x6_read_a<TC>(af[0], ub, 0, frow, q);
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
@@ -288,7 +266,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
           const int xn = perm[k + 1];
           if (k + 1 == 4) transform_b(v);
           bf[(k + 1) & 1] = x6_split(v[xn]);
-          if constexpr (decltype(refill)::value && X6_EXP != 3) v[xn] = load_one(next, xn);
+          if constexpr (decltype(refill)::value) v[xn] = load_one(next, xn);
           x6_read_a<TC>(af[(k + 1) & 1], ub, xn, frow, q);
         }
         x6_step<TC>(acc[x], af[k & 1], bf[k & 1]);
@@ -326,7 +304,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
     __syncthreads();
     for (int c = 0; c + 1 < nchunks; ++c) {
       const int cur = g & 1;
-      if (X6_EXP != 4) issue_u(c + 1, cur ^ 1);
+      issue_u(c + 1, cur ^ 1);
       // keep the U DMA ahead of the patch loads in issue order (vmcnt below)
       asm volatile("" ::: "memory");
       transform_a(d);
@@ -354,17 +332,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_wino_x6_kernel(const WinoP
       for (int e = 0; e < 16; ++e) d[e] = load_one(0, e);
     }
     char* scratch = lds + ((g - 1) & 1) * U_BYTES;
-    if (X6_EXP == 6) {              // every accumulator stays live, no transform / stores
-      wf32x4 t = acc[0][0];
-#pragma unroll
-      for (int x = 0; x < 16; ++x)
-#pragma unroll
-        for (int c = 0; c < TC; ++c) t += acc[x][c];
-      if (t[0] + t[1] + t[2] + t[3] == 1.2345f && e_valid) p.y[0] = t[0];
-    } else {
-      w_spatial_epilogue<TC, ST, WAVES>(p, scratch, acc, e_tb, wave, tl, q, e_cb, lane, e_valid,
-                                        e_f, e_ty, e_tx);
-    }
+    w_spatial_epilogue<TC, ST, WAVES>(p, scratch, acc, e_tb, wave, tl, q, e_cb, lane, e_valid,
+                                      e_f, e_ty, e_tx);
     if (nxt >= hi_u) break;
     unit = nxt;
   }
@@ -396,8 +365,8 @@ __global__ __launch_bounds__(512, 1) void conv_wino_x6h_kernel(const WinoParams 
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // static priority for the second half of the waves (conv_x6.hip); X6_EXP 7 = off
-  if (X6_EXP != 7 && wave >= 8 / 2) __builtin_amdgcn_s_setprio(1);
+  // static priority for the second half of the waves (conv_x6.hip)
+  if (wave >= 8 / 2) __builtin_amdgcn_s_setprio(1);
   const int tg = wave >> 1, xh = wave & 1;
   const int tl = lane & 15, q = lane >> 4;
   const int row_bytes = p.W * p.Cin * 4;
@@ -472,14 +441,12 @@ __global__ __launch_bounds__(512, 1) void conv_wino_x6h_kernel(const WinoParams 
     }
   };
   auto transform_a = [&](wf32x4 (&v)[12]) {          // V row a = e(S0) - e(S2) -> v[0..3]
-    if constexpr (X6_EXP == 5) return;
     row_t(v, 0);
     row_t(v, 2);
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = v[j] - v[8 + j];
   };
   auto transform_b = [&](wf32x4 (&v)[12]) {          // V row b = s e(S1) + e(S2) -> v[4..7]
-    if constexpr (X6_EXP == 5) return;
     row_t(v, 1);
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[4 + j] = sgn * v[4 + j] + v[8 + j];
@@ -492,7 +459,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino_x6h_kernel(const WinoParams 
   // into the slots as they free up (S0 during row a, S2 after transform_b,
   // S1 during row b)
   auto gemm = [&](const char* ub, wf32x4 (&v)[12], int next, auto refill) {
-    constexpr bool RF = decltype(refill)::value && X6_EXP != 3;
+    constexpr bool RF = decltype(refill)::value;
     X6A af[2][TC];
     X6B bf[2];
     bf[0] = x6_split(v[0]);
@@ -543,7 +510,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino_x6h_kernel(const WinoParams 
     __syncthreads();
     for (int c = 0; c + 1 < nchunks; ++c) {
       const int cur = g & 1;
-      if (X6_EXP != 4) issue_u(c + 1, cur ^ 1);
+      issue_u(c + 1, cur ^ 1);
       asm volatile("" ::: "memory");
       transform_a(d);
       gemm(lds + cur * U_BYTES, d, c + 1, std::true_type{});
@@ -567,93 +534,85 @@ __global__ __launch_bounds__(512, 1) void conv_wino_x6h_kernel(const WinoParams 
       for (int e = 0; e < 12; ++e) d[e] = load_one(0, e);
     }
     char* scratch = lds + ((g - 1) & 1) * U_BYTES;
-    if (X6_EXP == 6) {
-      wf32x4 t = acc[0][0];
+    // ---- output transform, row-split over the pair ----
+    // M rows 2 xh + a (a = 0, 1): acc[4 a + j]. Row partials of A^T M:
+    //   xh 0: p0 = M0 + M1, p1 = M1        xh 1: q0 = M2, q1 = -M2 - M3
+    // output row 0 = p0 + q0 (finished by xh 0), row 1 = p1 + q1 (xh 1):
+    // each wave sends the partial of the partner's row (xh 0: p1, xh 1: q0)
+    wf32x4* xch = (wf32x4*)scratch;                 // [wave][tc][j][lane]
 #pragma unroll
-      for (int x = 0; x < 8; ++x)
+    for (int tc = 0; tc < TC; ++tc)
 #pragma unroll
-        for (int c = 0; c < TC; ++c) t += acc[x][c];
-      if (t[0] + t[1] + t[2] + t[3] == 1.2345f && e_valid) p.y[0] = t[0];
-    } else {
-      // ---- output transform, row-split over the pair ----
-      // M rows 2 xh + a (a = 0, 1): acc[4 a + j]. Row partials of A^T M:
-      //   xh 0: p0 = M0 + M1, p1 = M1        xh 1: q0 = M2, q1 = -M2 - M3
-      // output row 0 = p0 + q0 (finished by xh 0), row 1 = p1 + q1 (xh 1):
-      // each wave sends the partial of the partner's row (xh 0: p1, xh 1: q0)
-      wf32x4* xch = (wf32x4*)scratch;                 // [wave][tc][j][lane]
+      for (int j = 0; j < 4; ++j)
+        xch[((wave * TC + tc) * 4 + j) * 64 + lane] = xh ? acc[j][tc] : acc[4 + j][tc];
+    __syncthreads();
+    wf32x4 t[TC][4];
 #pragma unroll
-      for (int tc = 0; tc < TC; ++tc)
+    for (int tc = 0; tc < TC; ++tc)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          xch[((wave * TC + tc) * 4 + j) * 64 + lane] = xh ? acc[j][tc] : acc[4 + j][tc];
-      __syncthreads();
-      wf32x4 t[TC][4];
-#pragma unroll
-      for (int tc = 0; tc < TC; ++tc)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const wf32x4 other = xch[(((wave ^ 1) * TC + tc) * 4 + j) * 64 + lane];
-          t[tc][j] = xh ? other - acc[j][tc] - acc[4 + j][tc]      // p1 + q1
-                        : acc[j][tc] + acc[4 + j][tc] + other;    // p0 + q0
-        }
-      constexpr bool stats = ST;
-      const int oy = 2 * e_ty + xh, ox = 2 * e_tx;
-      const bool has_res = p.res != nullptr;
-      const int seg = (stats && e_valid) ? p.clip_seg[e_f / p.clip_frames] : 0;
-      bool buni = false;
-      int bseg = 0;
-      if constexpr (stats) {
-        const int ta = e_tb * NT, tz = min(e_tb * NT + NT - 1, p.n_tiles - 1);
-        const int fa = w_div(w_div(ta, p.m_tw, p.s_tw), p.m_th, p.s_th);
-        const int fz = w_div(w_div(tz, p.m_tw, p.s_tw), p.m_th, p.s_th);
-        bseg = p.clip_seg[fa / p.clip_frames];
-        buni = bseg == p.clip_seg[fz / p.clip_frames];
+      for (int j = 0; j < 4; ++j) {
+        const wf32x4 other = xch[(((wave ^ 1) * TC + tc) * 4 + j) * 64 + lane];
+        t[tc][j] = xh ? other - acc[j][tc] - acc[4 + j][tc]      // p1 + q1
+                      : acc[j][tc] + acc[4 + j][tc] + other;    // p0 + q0
       }
-      double s1[TC][4], s2[TC][4];
-#pragma unroll
-      for (int tc = 0; tc < TC; ++tc) {
-        const int co = e_cb * CT + tc * 16 + 4 * q;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s1[tc][k] = s2[tc][k] = 0.0;
-        if (co >= p.Cout || !e_valid || oy >= p.H) {
-          if (stats && !buni) w_commit_stats(p, lane, false, seg, co, s1[tc], s2[tc]);
-          continue;
-        }
-        const float4 b4 = *(const float4*)(p.bias + co);
-        const wf32x4 bias = (wf32x4){b4.x, b4.y, b4.z, b4.w};
-        wf32x4 o[2];
-        o[0] = t[tc][0] + t[tc][1] + t[tc][2] + bias;
-        o[1] = t[tc][1] - t[tc][2] - t[tc][3] + bias;
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          if (ox + b >= p.W) continue;
-          const long long pix = ((long long)e_f * p.H + oy) * p.W + ox + b;
-          wf32x4 val = o[b];
-          if (has_res) {
-            const float4 r4 = *(const float4*)(p.res + pix * p.res_stride + co);
-            val += (wf32x4){r4.x, r4.y, r4.z, r4.w};
-          }
-          if (p.relu) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) val[k] = fmaxf(val[k], 0.f);
-          }
-          *(float4*)(p.y + pix * p.y_stride + co) = make_float4(val[0], val[1], val[2], val[3]);
-          if (stats) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              s1[tc][k] += (double)val[k];
-              s2[tc][k] += (double)val[k] * (double)val[k];
-            }
-          }
-        }
-        if (stats && !buni) w_commit_stats(p, lane, true, seg, co, s1[tc], s2[tc]);
-      }
-      if constexpr (stats) {
-        // every wave's lanes hold partial sums of 16 tiles' half-tiles; the
-        // block reduction adds all 8 waves' rows (w_block_stats, 8 waves)
-        if (buni) w_block_stats<TC, 8>(p, scratch, wave, tl, q, e_cb, bseg, s1, s2);
-      }
+    constexpr bool stats = ST;
+    const int oy = 2 * e_ty + xh, ox = 2 * e_tx;
+    const bool has_res = p.res != nullptr;
+    const int seg = (stats && e_valid) ? p.clip_seg[e_f / p.clip_frames] : 0;
+    bool buni = false;
+    int bseg = 0;
+    if constexpr (stats) {
+      const int ta = e_tb * NT, tz = min(e_tb * NT + NT - 1, p.n_tiles - 1);
+      const int fa = w_div(w_div(ta, p.m_tw, p.s_tw), p.m_th, p.s_th);
+      const int fz = w_div(w_div(tz, p.m_tw, p.s_tw), p.m_th, p.s_th);
+      bseg = p.clip_seg[fa / p.clip_frames];
+      buni = bseg == p.clip_seg[fz / p.clip_frames];
     }
+    double s1[TC][4], s2[TC][4];
+#pragma unroll
+    for (int tc = 0; tc < TC; ++tc) {
+      const int co = e_cb * CT + tc * 16 + 4 * q;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s1[tc][k] = s2[tc][k] = 0.0;
+      if (co >= p.Cout || !e_valid || oy >= p.H) {
+        if (stats && !buni) w_commit_stats(p, lane, false, seg, co, s1[tc], s2[tc]);
+        continue;
+      }
+      const float4 b4 = *(const float4*)(p.bias + co);
+      const wf32x4 bias = (wf32x4){b4.x, b4.y, b4.z, b4.w};
+      wf32x4 o[2];
+      o[0] = t[tc][0] + t[tc][1] + t[tc][2] + bias;
+      o[1] = t[tc][1] - t[tc][2] - t[tc][3] + bias;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        if (ox + b >= p.W) continue;
+        const long long pix = ((long long)e_f * p.H + oy) * p.W + ox + b;
+        wf32x4 val = o[b];
+        if (has_res) {
+          const float4 r4 = *(const float4*)(p.res + pix * p.res_stride + co);
+          val += (wf32x4){r4.x, r4.y, r4.z, r4.w};
+        }
+        if (p.relu) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) val[k] = fmaxf(val[k], 0.f);
+        }
+        *(float4*)(p.y + pix * p.y_stride + co) = make_float4(val[0], val[1], val[2], val[3]);
+        if (stats) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            s1[tc][k] += (double)val[k];
+            s2[tc][k] += (double)val[k] * (double)val[k];
+          }
+        }
+      }
+      if (stats && !buni) w_commit_stats(p, lane, true, seg, co, s1[tc], s2[tc]);
+    }
+    if constexpr (stats) {
+      // every wave's lanes hold partial sums of 16 tiles' half-tiles; the
+      // block reduction adds all 8 waves' rows (w_block_stats, 8 waves)
+      if (buni) w_block_stats<TC, 8>(p, scratch, wave, tl, q, e_cb, bseg, s1, s2);
+    }
+  
     if (nxt >= hi_u) break;
     unit = nxt;
     // the exchange / statistics scratch is the buffer chunk 1 will DMA into:
@@ -674,8 +633,8 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : 2) void conv_winot_x6_
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // static priority for the second half of the waves (conv_x6.hip); X6_EXP 7 = off
-  if (X6_EXP != 7 && wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
+  // static priority for the second half of the waves (conv_x6.hip)
+  if (wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
   const int wgid = w_xcd_remap();
   const int cb = wgid % p.n_cblocks;
   const int tb = wgid / p.n_cblocks;
@@ -738,13 +697,13 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : 2) void conv_winot_x6_
     X6A af[2][TC];
     X6B bf[2];
     bf[0] = x6_split(v[0]);
-    if constexpr (decltype(refill)::value && X6_EXP != 3) v[0] = load_one(next, 0);
+    if constexpr (decltype(refill)::value) v[0] = load_one(next, 0);
     x6_read_a<TC>(af[0], ub, 0, frow, q);
 #pragma unroll
     for (int x = 0; x < 6; ++x) {
       if (x + 1 < 6) {
         bf[(x + 1) & 1] = x6_split(v[x + 1]);
-        if constexpr (decltype(refill)::value && X6_EXP != 3) v[x + 1] = load_one(next, x + 1);
+        if constexpr (decltype(refill)::value) v[x + 1] = load_one(next, x + 1);
         x6_read_a<TC>(af[(x + 1) & 1], ub, x + 1, frow, q);
       }
       x6_step<TC>(acc[x], af[x & 1], bf[x & 1]);
@@ -786,10 +745,10 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : 2) void conv_winot_x6_
   __syncthreads();
   for (int c = 0; c + 1 < nchunks; ++c) {
     const int cur = c & 1;
-    if (X6_EXP != 4) issue_u(c + 1, cur ^ 1);
+    issue_u(c + 1, cur ^ 1);
     asm volatile("" ::: "memory");
     if (aff) affine(d, sc, sh);
-    if (X6_EXP != 5) transform(d);
+    transform(d);
     gemm(lds + cur * U_BYTES, d, c + 1, std::true_type{});
     if (aff) {                                            // next chunk's scale / shift
       sc = *(const wf32x4*)(ssb + (c + 1) * 16);
@@ -799,7 +758,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : 2) void conv_winot_x6_
     __syncthreads();
   }
   if (aff) affine(d, sc, sh);
-  if (X6_EXP != 5) transform(d);
+  transform(d);
   gemm(lds + ((nchunks - 1) & 1) * U_BYTES, d, -1, std::false_type{});
   __syncthreads();
   w_temporal_epilogue<TC, ST, WAVES>(p, lds, acc, tb, wave, tl, q, cb, lane, tvalid, n, tt, hw);

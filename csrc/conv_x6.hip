@@ -34,230 +34,7 @@
 #include "conv_f32_common.h"
 #include "x6_common.h"
 
-#define X6D_INVALID 0xFFFFFFF0u
-// bottleneck experiments (scripts/x6d_exp.py; results are garbage by design):
-// 1 no split VALU, 2 no MFMA, 3 no activation DMA after the prologue, 4 no
-// weight DMA after the prologue, 6 no epilogue, 7 no per-step wait + barrier;
-// 8 (exact) equal wave priorities (no s_setprio 1 for the second half)
-#ifndef X6D_EXP
-#define X6D_EXP 0
-#endif
-
-// physical 16-B chunk of logical chunk c in a 64-B activation row r: rows
-// r, r + 4, r + 8, r + 12 share a bank quarter, g = [0, 3, 2, 1] keeps the
-// 16 lanes of every ds_read_b128 group on distinct banks
-static __device__ __forceinline__ int x6d_swz(int c, int r) {
-  return c ^ ((0x6C >> (2 * ((r >> 2) & 3))) & 3);     // g = [0, 3, 2, 1][(r >> 2) & 3]
-}
-
-template <int N>
-static __device__ __forceinline__ void x6d_wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-static __device__ __forceinline__ void x6d_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-// LDS-DMA of 16 B per lane to lds_dst + 16 lane. Issued from inline asm: the
-// compiler's wait insertion would otherwise drain every in-flight DMA
-// (vmcnt(0)) before the first ds_read after it, whatever LDS it reads; the
-// kernel orders the DMAs itself (counted vmcnt + barrier).
-typedef unsigned int x6d_u32x4 __attribute__((ext_vector_type(4)));
-static __device__ __forceinline__ x6d_u32x4 x6d_rsrc(const void* base, uint32_t bytes) {
-  const uint64_t a = (uint64_t)base;     // raw buffer: stride 0, out-of-range reads give 0
-  return (x6d_u32x4){(uint32_t)a, (uint32_t)(a >> 32) & 0xFFFFu, bytes, 0x00020000u};
-}
-static __device__ __forceinline__ void x6d_dma16(const x6d_u32x4& rsrc, uint32_t voff,
-                                                 const char* lds_dst) {
-  asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc),
-               "{m0}"((uint32_t)(uintptr_t)lds_dst)
-               : "memory");
-}
-
-// training-mode BN statistics of the output, accumulated in the epilogue
-// (as the Winograd kernels' WinoParams.out_stats): per video and channel the
-// fp64 sum and sum of squares of the stored values
-struct X6DStats {
-  double* sums;          // [nseg][2][stats_c], zeroed by the caller
-  const int* clip_seg;   // [N]: video (segment) of each clip of this launch
-  int stats_c;
-  // split-K (conv_x6_kernel only): ksplit > 1 = the block's share of the K
-  // steps is written raw (no bias / epilogue) to ws[split][M][Cout_p] and
-  // x6d_splitk_reduce_kernel finishes the conv
-  int ksplit;
-  float* ws;
-};
-
-// sum over the 16 lanes of a DPP row (every lane gets it): quad swaps, then
-// the half-row and row mirrors
-static __device__ __forceinline__ float x6d_dpp_add(float v, int ctrl_sel) {
-  int t;
-  const int iv = __float_as_int(v);
-  switch (ctrl_sel) {
-    case 0: t = __builtin_amdgcn_update_dpp(iv, iv, 0xB1, 0xF, 0xF, false); break;   // [1,0,3,2]
-    case 1: t = __builtin_amdgcn_update_dpp(iv, iv, 0x4E, 0xF, 0xF, false); break;   // [2,3,0,1]
-    case 2: t = __builtin_amdgcn_update_dpp(iv, iv, 0x141, 0xF, 0xF, false); break;  // half mirror
-    default: t = __builtin_amdgcn_update_dpp(iv, iv, 0x140, 0xF, 0xF, false); break; // mirror
-  }
-  return v + __int_as_float(t);
-}
-static __device__ __forceinline__ float x6d_row16_sum(float v) {
-  v = x6d_dpp_add(v, 0);
-  v = x6d_dpp_add(v, 1);
-  v = x6d_dpp_add(v, 2);
-  return x6d_dpp_add(v, 3);
-}
-
-// Epilogue of the x6 direct kernels: (+ residual) (+ ReLU) -> fp32 stores,
-// one 16-B store per tile, and (ST) the per-video BN sums. Rows m < m_end of
-// [p0, p_hi) are valid; `lds` (lds_bytes) is free scratch (no DMA in flight).
-template <int TP, int TC, int NW, int CT_ALL, bool ST>
-static __device__ __forceinline__ void x6d_epilogue(const ConvF32Params& p, const X6DStats& st,
-                                                    x6f32x4 (&acc)[TP][TC], int p0, int m_end,
-                                                    int p_hi, int c0, int wp, int wc, int lane,
-                                                    char* lds, int lds_bytes) {
-  const int frow = lane & 15, fq = lane >> 4;
-  if (X6D_EXP == 6) {                // every accumulator stays live, no stores
-    x6f32x4 t = acc[0][0];
-#pragma unroll
-    for (int tp = 0; tp < TP; ++tp)
-#pragma unroll
-      for (int tc = 0; tc < TC; ++tc) t += acc[tp][tc];
-    if (t[0] + t[1] + t[2] + t[3] == 1.2345f) p.y[0] = t[0];
-    return;
-  }
-  // ---- epilogue: (+ residual) (+ ReLU) -> fp32, one 16-B store per tile ----
-  const uint32_t y_bytes = (uint32_t)p.M * (uint32_t)p.y_stride * 4u;
-  const __amdgpu_buffer_rsrc_t yr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.y, (short)0, y_bytes, 0x00020000);
-  const bool has_res = p.res != nullptr;
-  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(has_res ? p.res : p.y), (short)0,
-      has_res ? (uint32_t)p.M * (uint32_t)p.res_stride * 4u : 0u, 0x00020000);
-  if constexpr (!ST) {
-#pragma unroll
-    for (int tp = 0; tp < TP; ++tp) {
-      const int m = p0 + (wp * TP + tp) * 16 + frow;
-      x6f32x4 r[TC];
-#pragma unroll
-      for (int tc = 0; tc < TC; ++tc) {
-        const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
-        const bool ok = has_res && m < m_end && c < p.Cout_p;
-        r[tc] = has_res ? __builtin_amdgcn_raw_buffer_load_b128(
-                              rr, ok ? (uint32_t)(m * p.res_stride + c) * 4u : X6D_INVALID, 0, 0)
-                        : (x6f32x4){0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int tc = 0; tc < TC; ++tc) {
-        const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
-        const bool ok = m < m_end && c < p.Cout_p;
-        x6f32x4 v = acc[tp][tc] + r[tc];
-        if (p.relu) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(
-            v, yr, ok ? (uint32_t)(m * p.y_stride + c) * 4u : X6D_INVALID, 0, 0);
-      }
-    }
-  } else {
-    // channel tiles outer (one tile's sums live at a time). Rows are
-    // clip-major, so a block's videos are the contiguous range seg_lo ..
-    // seg_hi. One video (the common case): each lane sums its TP rows, the 16
-    // lanes of a channel quad reduce by shuffles, one LDS add per channel and
-    // wave. Several videos: LDS adds per row into per-video slots. Then one
-    // fp64 atomic per video, channel and statistic per block.
-    constexpr int NT = 64 * NW;
-    int na, nz, t_, h_, w_;
-    f32_decode_row(p, p0, na, t_, h_, w_);
-    f32_decode_row(p, min(p_hi, m_end) - 1, nz, t_, h_, w_);
-    const int seg_lo = __builtin_amdgcn_readfirstlane(st.clip_seg[__builtin_amdgcn_readfirstlane(na)]);
-    const int seg_hi = __builtin_amdgcn_readfirstlane(st.clip_seg[__builtin_amdgcn_readfirstlane(nz)]);
-    const int nseg = seg_hi - seg_lo + 1;
-    const bool uni = nseg == 1;
-    const bool in_lds = nseg * CT_ALL * 16 <= lds_bytes;
-    double* red = (double*)lds;                       // [nseg][CT_ALL][2]
-    if (in_lds)
-      for (int i = threadIdx.x; i < nseg * CT_ALL * 2; i += NT) red[i] = 0.0;
-    __syncthreads();                                  // no DMA in flight here
-#pragma unroll
-    for (int tc = 0; tc < TC; ++tc) {
-      const int cl = (wc * TC + tc) * 16 + 4 * fq;
-      const int c = c0 + cl;
-      x6f32x4 r[TP];
-#pragma unroll
-      for (int tp = 0; tp < TP; ++tp) {
-        const int m = p0 + (wp * TP + tp) * 16 + frow;
-        const bool ok = has_res && m < m_end && c < p.Cout_p;
-        r[tp] = has_res ? __builtin_amdgcn_raw_buffer_load_b128(
-                              rr, ok ? (uint32_t)(m * p.res_stride + c) * 4u : X6D_INVALID, 0, 0)
-                        : (x6f32x4){0.f, 0.f, 0.f, 0.f};
-      }
-      // lane partials over its TP rows in fp32 (<= 4 values), the 16-lane
-      // reduction in fp32 by DPP, everything after in fp64
-      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int tp = 0; tp < TP; ++tp) {
-        const int m = p0 + (wp * TP + tp) * 16 + frow;
-        const bool ok = m < m_end && c < p.Cout_p;
-        x6f32x4 v = acc[tp][tc] + r[tp];
-        if (p.relu) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(
-            v, yr, ok ? (uint32_t)(m * p.y_stride + c) * 4u : X6D_INVALID, 0, 0);
-        if (!ok) continue;
-        if (uni) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            s1[j] += v[j];
-            s2[j] = fmaf(v[j], v[j], s2[j]);
-          }
-        } else {
-          int n, tt, hh, ww;
-          f32_decode_row(p, m, n, tt, hh, ww);
-          const int sg = st.clip_seg[n];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const double a = (double)v[j], b = (double)v[j] * (double)v[j];
-            if (in_lds) {
-              atomicAdd(red + ((size_t)(sg - seg_lo) * CT_ALL + cl + j) * 2, a);
-              atomicAdd(red + ((size_t)(sg - seg_lo) * CT_ALL + cl + j) * 2 + 1, b);
-            } else {
-              atomicAdd(st.sums + ((size_t)sg * 2) * st.stats_c + c + j, a);
-              atomicAdd(st.sums + ((size_t)sg * 2 + 1) * st.stats_c + c + j, b);
-            }
-          }
-        }
-      }
-      if (uni) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          s1[j] = x6d_row16_sum(s1[j]);
-          s2[j] = x6d_row16_sum(s2[j]);
-        }
-        if (frow == 0 && c < p.Cout_p) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            atomicAdd(red + (cl + j) * 2, (double)s1[j]);
-            atomicAdd(red + (cl + j) * 2 + 1, (double)s2[j]);
-          }
-        }
-      }
-    }
-    __syncthreads();
-    if (in_lds) {
-      for (int i = threadIdx.x; i < nseg * CT_ALL; i += NT) {
-        const int sg = seg_lo + i / CT_ALL, c = c0 + i % CT_ALL;
-        if (c < p.Cout_p) {
-          atomicAdd(st.sums + ((size_t)sg * 2) * st.stats_c + c, red[i * 2]);
-          atomicAdd(st.sums + ((size_t)sg * 2 + 1) * st.stats_c + c, red[i * 2 + 1]);
-        }
-      }
-    }
-  }
-}
+#include "x6d_common.h"
 
 template <int TP, int TC, int WP, int WC, int NS, bool PIPE, int MINB, bool ST>
 __global__ __launch_bounds__(64 * WP * WC, MINB)
@@ -328,7 +105,6 @@ void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
     char* base = lds + slot * BUF;
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) {
-      if (X6D_EXP == 3 && s >= NS - 1) break;
       const bool ok = (rmask[i] & ey) == ey;
       const uint32_t off = ok ? (uint32_t)(rbase[i] + ex) : X6D_INVALID;
       x6d_dma16(xr, off, base + (wave * A_INSTR + i) * 1024);
@@ -336,7 +112,6 @@ void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
     const uint32_t wbase = ((uint32_t)s * (uint32_t)p.w_rows + (uint32_t)c0) * 128u;
 #pragma unroll
     for (int j = 0; j < W_INSTR; ++j) {
-      if (X6D_EXP == 4 && s >= NS - 1) break;
       // waves past the last instruction repeat it (same bytes to the same
       // place), so every wave issues VM_STAGE DMAs per step
       const int instr = (W_TOTAL % NW == 0) ? wave + NW * j : min(wave + NW * j, W_TOTAL - 1);
@@ -361,13 +136,6 @@ void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
   auto load_b = [&](int slot, int tp) -> X6B {
     const int row = (wp * TP + tp) * 16 + frow;
     const x6f32x4 v = *(const x6f32x4*)(lds + slot * BUF + row * 64 + a_chunk);
-    if constexpr (X6D_EXP == 1) {
-      const uint32_t a = __float_as_uint(v[0]), b = __float_as_uint(v[1]);
-      const uint32_t c = __float_as_uint(v[2]), d = __float_as_uint(v[3]);
-      X6B f;
-      f.r = (wu32x8){a, b, c, d, a, b, c, d};
-      return f;
-    }
     return x6_split_exact(v);
   };
   // the 3 TP MFMAs of channel tile tc of the step in `slot`
@@ -375,12 +143,6 @@ void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
     const char* wrow = lds + slot * BUF + ACT_BYTES + ((wc * TC + tc) * 16 + frow) * 128;
     const wu32x4 hm = *(const wu32x4*)(wrow + w_hm);
     const wu32x4 hl = *(const wu32x4*)(wrow + w_hl);
-    if constexpr (X6D_EXP == 2) {
-#pragma unroll
-      for (int tp = 0; tp < TP; ++tp)
-        acc[tp][tc][0] += __uint_as_float(hm[0] ^ hl[1] ^ bf[tp].r[0] ^ bf[tp].r[3] ^ bf[tp].r[5]);
-      return;
-    }
 #pragma unroll
     for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = x6_mma(hm, x6_b_lm(bf[tp]), acc[tp][tc]);
 #pragma unroll
@@ -425,8 +187,8 @@ void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
     if (s_begin + i < s_end) issue(s_begin + i, i);
   // static priority for the second half of the waves (the arbitration
   // losers, MI355X_MICROARCH.md item 4): 1-2 % in interleaved A/B runs
-  // (profiles/r3_x6_exp_interleaved.txt); X6D_EXP 8 keeps equal priorities
-  if (X6D_EXP != 8 && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  // (profiles/r3_x6_exp_interleaved.txt)
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   if constexpr (!PIPE) {
     // step s's fragments are read and split at its start; the wait at the
     // end of step s - 1 retires step s (NS 3: step s + 1 stays in flight)
@@ -443,7 +205,6 @@ void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
       for (int tp = 0; tp < TP; ++tp) bf[tp] = load_b(it % NS, tp);
 #pragma unroll
       for (int tc = 0; tc < TC; ++tc) mma_tc(it % NS, tc, bf);
-      if (X6D_EXP == 7 && s + 1 < s_end) continue;
       if (NS == 3 && s + 2 < s_end) x6d_wait_vm<VM_STAGE>();
       else x6d_wait_vm<0>();
       x6d_barrier();
@@ -476,7 +237,6 @@ void conv_x6_kernel(const ConvF32Params p, const X6DStats st) {
         if (more) bn[tp] = load_b(ns, tp);
 #pragma unroll
       for (int tp = 0; tp < TP; ++tp) bf[tp] = bn[tp];
-      if (X6D_EXP == 7 && s + 1 < s_end) continue;
       if (NS == 4 && s + 3 < s_end) x6d_wait_vm<VM_STAGE>();
       else x6d_wait_vm<0>();
       x6d_barrier();
@@ -795,6 +555,16 @@ static const int kNumX6Configs = sizeof(kX6Configs) / sizeof(kX6Configs[0]);
 
 extern "C" {
 
+int rnb_x6d_splitk_reduce(const ConvF32Params* p, const X6DStats* st, hipStream_t stream) {
+  const int rpt = 4;                     // rows per thread: many threads, short chains
+  const int rows_per_clip = p->To * p->Ho * p->Wo;
+  hipLaunchKernelGGL(x6d_splitk_reduce_kernel,
+                     dim3((unsigned)((p->Cout_p / 4 + 63) / 64),
+                          (unsigned)((p->M + 8 * rpt - 1) / (8 * rpt))),
+                     dim3(64, 8), 0, stream, *p, *st, rpt, rows_per_clip);
+  return (int)hipGetLastError();
+}
+
 int rnb_conv_x6_num_configs() { return kNumX6Configs; }
 
 int rnb_conv_x6_config_info(int id, int* p_tile, int* c_tile) {
@@ -844,6 +614,9 @@ int rnb_conv_x6_launch_splitk(const ConvF32Params* pp, int config_id, hipStream_
   st.stats_c = stats_c;
   st.ksplit = 1;
   st.ws = nullptr;
+  st.in_scale = st.out_scale = st.acc_scale = 1.f;
+  st.in_ss = nullptr;
+  st.in_seg = nullptr;
   if (ksplit > 1) {
     // split-K: raw partials per split, then the reduce kernel (bias,
     // residual, ReLU, statistics); ws holds ksplit x M x Cout_p floats
@@ -852,13 +625,7 @@ int rnb_conv_x6_launch_splitk(const ConvF32Params* pp, int config_id, hipStream_
     st.ws = ws;
     hipLaunchKernelGGL(cfg.kernel, dim3((unsigned)(blocks * ksplit)), dim3(cfg.threads), 0, stream,
                        p, st);
-    const int rpt = 4;                     // rows per thread: many threads, short chains
-    const int rows_per_clip = p.To * p.Ho * p.Wo;
-    hipLaunchKernelGGL(x6d_splitk_reduce_kernel,
-                       dim3((unsigned)((p.Cout_p / 4 + 63) / 64),
-                            (unsigned)((p.M + 8 * rpt - 1) / (8 * rpt))),
-                       dim3(64, 8), 0, stream, p, st, rpt, rows_per_clip);
-    return (int)hipGetLastError();
+    return rnb_x6d_splitk_reduce(&p, &st, stream);
   }
   hipLaunchKernelGGL(sums ? cfg.kernel_st : cfg.kernel, dim3((unsigned)blocks), dim3(cfg.threads),
                      0, stream, p, st);
@@ -930,6 +697,9 @@ int rnb_conv_x6r_launch(const ConvF32Params* pp, int variant, hipStream_t stream
   st.stats_c = stats_c;
   st.ksplit = 1;
   st.ws = nullptr;
+  st.in_scale = st.out_scale = st.acc_scale = 1.f;
+  st.in_ss = nullptr;
+  st.in_seg = nullptr;
   hipLaunchKernelGGL(sums ? cfg.kernel_st : cfg.kernel, dim3((unsigned)blocks),
                      dim3(64 * cfg.nw), 0, stream, p, st);
   return (int)hipGetLastError();

@@ -105,6 +105,29 @@ int rnb_memcpy_peer_async(void* dst, int dst_dev, const void* src, int src_dev, 
 
 int rnb_stream_synchronize(void* stream) { return (int)hipStreamSynchronize((hipStream_t)stream); }
 
+// raw HIP streams (scripts/ipc_event_matrix.py compares them with torch's)
+int rnb_stream_create(int nonblocking, int priority, void** stream) {
+  hipStream_t s;
+  const hipError_t e = hipStreamCreateWithPriority(&s, nonblocking ? hipStreamNonBlocking : 0,
+                                                   priority);
+  *stream = (void*)s;
+  return (int)e;
+}
+
+int rnb_stream_destroy(void* stream) { return (int)hipStreamDestroy((hipStream_t)stream); }
+
+// ~cycles of busy wait on the stream (a pending record for the IPC-event tests)
+__global__ void rnb_spin_kernel(long long cycles) {
+  const long long t0 = clock64();
+  while (clock64() - t0 < cycles) {
+  }
+}
+
+int rnb_spin(void* stream, long long cycles) {
+  hipLaunchKernelGGL(rnb_spin_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, cycles);
+  return (int)hipGetLastError();
+}
+
 int rnb_can_access_peer(int dev, int peer, int* out) {
   return (int)hipDeviceCanAccessPeer(out, dev, peer);
 }

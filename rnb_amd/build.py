@@ -3,8 +3,10 @@
 ``python -m rnb_amd.build [--force] [-j N]`` compiles every library below with
 ``hipcc --offload-arch=gfx950`` into ``rnb_amd/_native/``. The libraries are
 plain C-ABI shared objects loaded with ctypes (``rnb_amd/ops/native.py``), so
-they do not depend on the PyTorch C++ ABI and build in seconds. A library is
-rebuilt only when one of its sources (or this file) is newer than the .so.
+they do not depend on the PyTorch C++ ABI. Every source compiles to its own
+object under ``build/obj/`` in parallel (``-j``) and the objects link into the
+.so; an object is rebuilt only when its source, a ``csrc`` header or this file
+is newer than it, and a library only when one of its objects is.
 """
 from __future__ import annotations
 
@@ -26,7 +28,7 @@ LIBRARIES = {
     "librnb_kernels.so": (["conv_igemm.hip", "conv_halo.hip", "conv_temporal.hip",
                            "video_ops.hip", "bn_ops.hip", "conv_halo_ws.hip", "conv21.hip",
                            "conv_f32.hip", "conv_wino_f32.hip", "conv_wino_x6.hip",
-                           "conv_x6.hip"], [], []),
+                           "conv_x6.hip", "conv_h3.hip"], [], []),
     "librnb_runtime.so": (["runtime.cpp"], [], []),
     "librnb_tracer.so": (["tracer.cpp"], [], ["-L%s/lib" % ROCM, "-lrocprofiler-sdk",
                                                "-Wl,-rpath,%s/lib" % ROCM]),
@@ -49,39 +51,61 @@ def _stale(target: str, sources) -> bool:
     return any(os.path.getmtime(s) > t for s in deps)
 
 
-def build_one(name: str, force: bool = False, verbose: bool = False) -> str:
+def _compile(src: str, obj: str, flags, verbose: bool) -> str:
+    os.makedirs(os.path.dirname(obj), exist_ok=True)
+    tmp = obj + ".tmp.%d" % os.getpid()
+    cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-c",
+           "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+           "-Wno-unused-result"] + list(flags) + [src, "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("compiling %s failed:\n%s\n%s" % (src, res.stdout, res.stderr))
+    os.replace(tmp, obj)
+    return obj
+
+
+def build_one(name: str, force: bool = False, verbose: bool = False, pool=None) -> str:
     srcs, flags, libs = LIBRARIES[name]
     srcs = [os.path.join(CSRC, s) for s in srcs]
     missing = [s for s in srcs if not os.path.exists(s)]
     if missing:
         raise FileNotFoundError("missing sources for %s: %s" % (name, missing))
     target = os.path.join(OUT, name)
-    if not force and not _stale(target, srcs):
+    objdir = os.path.join(ROOT, "build", "obj", ARCH)
+    objs = [os.path.join(objdir, os.path.basename(s) + ".o") for s in srcs]
+    todo = [(s, o) for s, o in zip(srcs, objs) if force or _stale(o, [s])]
+    if todo:
+        if pool is None:
+            for s, o in todo:
+                _compile(s, o, flags, verbose)
+        else:
+            for f in [pool.submit(_compile, s, o, flags, verbose) for s, o in todo]:
+                f.result()
+    if not force and not todo and os.path.exists(target) and \
+            all(os.path.getmtime(o) <= os.path.getmtime(target) for o in objs):
         return target
     os.makedirs(OUT, exist_ok=True)
     tmp = target + ".tmp.%d" % os.getpid()
-    cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC",
-           "-shared", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
-           "-Wno-unused-result"] + flags + srcs + ["-o", tmp] + libs
-    if verbose:
-        print(" ".join(cmd), flush=True)
+    cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-fPIC", "-shared"] + objs + ["-o", tmp] + libs
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
-        raise RuntimeError("building %s failed:\n%s\n%s" % (name, res.stdout, res.stderr))
+        raise RuntimeError("linking %s failed:\n%s\n%s" % (name, res.stdout, res.stderr))
     os.replace(tmp, target)
     return target
 
 
-def build_all(force: bool = False, jobs: int = 4, verbose: bool = False):
+def build_all(force: bool = False, jobs: int = 8, verbose: bool = False):
+    # one pool compiles the objects of every library; the libraries link in turn
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        futs = {n: ex.submit(build_one, n, force, verbose) for n in LIBRARIES}
-        return {n: f.result() for n, f in futs.items()}
+        return {n: build_one(n, force, verbose, ex) for n in LIBRARIES}
 
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("-j", "--jobs", type=int, default=4)
+    ap.add_argument("-j", "--jobs", type=int, default=8)
     ap.add_argument("-v", "--verbose", action="store_true")
     args = ap.parse_args(argv)
     for name, path in build_all(args.force, args.jobs, args.verbose).items():

@@ -296,6 +296,8 @@ def run(args) -> dict:
                                                           instance_idx)),
                                 stream_state=qt.get_stream_state(step_idx, group_idx)))
                 procs.append((p.name, p))
+    # request-id ranges of the phases, for the runners' per-phase gather stats
+    os.environ["RNB_PHASE_IDS"] = "%d,%d" % (warm, args.videos)
     for _, p in procs:
         p.start()
     dog = Watchdog(procs, flag, [sta_bar, fin_bar])
@@ -322,6 +324,15 @@ def run(args) -> dict:
     ring_stats = {}
     n_final = sum(len(g.gpus) for g in spec.steps[-1].groups)
     got = 0
+
+    def handle(msg):
+        nonlocal got
+        if msg[0] == "summary":
+            summaries.merge_from(msg[4])
+            got += 1
+        elif msg[0] == "ring_stats":
+            for k, v in msg[4].items():
+                ring_stats[k] = ring_stats.get(k, 0) + v
     deadline = time.time() + (60.0 if not broken else 5.0)
     while got < n_final and time.time() < deadline:
         try:
@@ -330,22 +341,16 @@ def run(args) -> dict:
             if all(p.exitcode is not None for _, p in procs):
                 break
             continue
-        if msg[0] == "summary":
-            summaries.merge_from(msg[4])
-            got += 1
-        elif msg[0] == "ring_stats":
-            for k, v in msg[4].items():
-                ring_stats[k] = ring_stats.get(k, 0) + v
-    # ring counters are sent before fin_bar; pick up any still in the pipe
+        handle(msg)
+    # runner counters are sent before fin_bar and a slow final runner's
+    # summary may come late: pick up whatever is still in the pipe
     drain_until = time.time() + 0.3
     while time.time() < drain_until:
         try:
             msg = result_queue.get(timeout=0.05)
         except Exception:
             continue
-        if msg[0] == "ring_stats":
-            for k, v in msg[4].items():
-                ring_stats[k] = ring_stats.get(k, 0) + v
+        handle(msg)
     for _, p in procs:
         p.join(RESERVED_CHILD_EXIT_GRACE_S if not broken else 5.0)
         if p.exitcode is None:
@@ -360,7 +365,11 @@ def run(args) -> dict:
               "mean_interval_ms": args.mean_interval_ms, "ok": False,
               # HIP-IPC stream waits ROCm refused on already-completed events
               # (parallel/transport.py host fallback), summed over runners
-              "stale_event_waits": int(ring_stats.get("stale_event_waits", 0))}
+              "stale_event_waits": int(ring_stats.get("stale_event_waits", 0)),
+              "gather": gather_summary(ring_stats),
+              # IPC slot-ring event waits per edge kind (same / cross GPU):
+              # GPU-ordered vs host fallback, plus handles held by consumers
+              "ipc_edges": ipc_summary(ring_stats)}
     if time_start is not None and time_end is not None:
         if warm and phase_start[0] > 0:
             time_start = phase_start[0]          # timed window starts after warm-up
@@ -420,6 +429,35 @@ def run(args) -> dict:
         with open(args.json_out, "w") as f:
             json.dump(result, f, indent=2)
     return result
+
+
+def gather_summary(stats: dict) -> dict:
+    """Per-phase consumer-side gather counters summed over runners
+    ("gather.<phase>.<key>" from runner.py): calls, items and rows per call
+    and why the gathers ended."""
+    out = {}
+    for k, v in stats.items():
+        if not k.startswith("gather."):
+            continue
+        _, ph, key = k.split(".", 2)
+        out.setdefault(ph, {})[key] = v
+    for ph, st in out.items():
+        calls = st.get("calls", 0)
+        if calls:
+            st["items_per_call"] = round(st.get("items", 0) / calls, 2)
+            st["rows_per_call"] = round(st.get("rows", 0) / calls, 2)
+        ends = {k[4:]: st.pop(k) for k in [k for k in st if k.startswith("end_")]}
+        st["ended_by"] = {k: v for k, v in sorted(ends.items()) if v}
+    return out
+
+
+def ipc_summary(stats: dict) -> dict:
+    out = {}
+    for k, v in stats.items():
+        if k.startswith("ipc."):
+            _, edge, key = k.split(".", 2)
+            out.setdefault(edge, {})[key] = v
+    return out
 
 
 def main(argv=None) -> int:

@@ -43,7 +43,7 @@ import torch
 from ...ops.bn import BatchNormBatch
 from ...ops.conv import ConvGeom, ConvLayer, StemConv, fold_bn, pad_to, CH_ALIGN
 from ...ops.conv21 import FusedSTConv
-from ...ops.conv_f32 import F32_ALIGN, WINOT_MIN_T, ConvLayerF32
+from ...ops.conv_f32 import F32_ALIGN, WINOT_MIN_T, ConvLayerF32, h3_enabled
 from ...ops.video import (Head, IN_CHANNELS_P, ndhwc_to_ncdhw, ncdhw_to_ndhwc,
                           packed_input_shape)
 from .network import (LAYER_CHANNELS, LAYER_INPUT_CTHW, LAYER_OUTPUT_CTHW,
@@ -233,11 +233,21 @@ class R2P1DEngine:
             uses[op.src] = uses.get(op.src, 0) + 1
             if op.res is not None:
                 uses[op.res] = uses.get(op.res, 0) + 1
+        # (temporal Winograd kernel) or by an h3 direct conv (csrc/conv_h3.hip,
+        # input channels in 16-channel steps: bn1 -> the block's second
+        # spatial conv, spatial BNs -> temporal convs on short clips)
+        h3_defer = os.environ.get("RNB_H3_DEFER", "1") != "0"
         self._defer_ok = [
             i + 1 < len(self.ops) and op.bn is not None and op.bn_relu and op.res is None
             and self.f32 and uses.get(op.dst, 0) == 1 and self.ops[i + 1].src == op.dst
-            and getattr(self.ops[i + 1].layer, "winot_ok", False)
+            and (getattr(self.ops[i + 1].layer, "winot_ok", False)
+                 or (h3_defer and h3_enabled() and self.ops[i + 1].layer.geom.cin_p % 16 == 0))
             for i, op in enumerate(self.ops)]
+        if self.bn_mode == "batch" and self.f32:
+            for i, ok in enumerate(self._defer_ok):
+                if ok and not getattr(self.ops[i + 1].layer, "winot_ok", False):
+                    # the consumer conv tunes among configs that apply the BN on load
+                    self.ops[i + 1].layer.tune_with_affine = True
 
     # ------------------------------------------------------------- metadata
     @property

@@ -56,8 +56,10 @@ CLIP_SHAPE = (8, 112, 112)
 # output sampling for numerics checks of a served run (bench.py): the loader
 # tags every CHECK_EVERY-th video with its decode source, and a final-step
 # runner with RNB_CHECK_DIR set writes those videos' logits there
-CHECK_EVERY = int(os.environ.get("RNB_CHECK_EVERY", "61"))
-CHECK_MAX = int(os.environ.get("RNB_CHECK_MAX", "8"))
+CHECK_EVERY = int(os.environ.get("RNB_CHECK_EVERY", "13"))
+# 15-clip videos are 1 in 11: tag more of them so every check covers them
+CHECK_EVERY_LARGE = int(os.environ.get("RNB_CHECK_EVERY_LARGE", "3"))
+CHECK_MAX = int(os.environ.get("RNB_CHECK_MAX", "6"))         # per stratum and process
 DEFAULT_DTYPE = "fp32"       # the reference computes in fp32 (model.py:149,225)
 
 
@@ -183,7 +185,7 @@ class R2P1DRunner(RunnerModel):
         self._gather_ptr = None
         self._gather_buf = None
         self._check_dir = os.environ.get("RNB_CHECK_DIR") or None
-        self._checked = 0
+        self._checked = {}               # samples written per stratum
 
     # consumer-side batching (runner.py): up to max_batch_videos queued
     # videos per call, their rows pulled into the graph's static input
@@ -251,16 +253,17 @@ class R2P1DRunner(RunnerModel):
                 and getattr(time_card, "item_rows", None) else [y.shape[0]])
         if len(rows) != len(cards):
             return                     # Batcher items: several videos per segment
-        from ...numerics import write_sample
-        off = 0
+        from ...numerics import stratum_of, write_sample
+        off, call_rows = 0, int(y.shape[0])
         for tc, n in zip(cards, rows):
             src = tc.extra.get("clip_src")
-            if (src is not None and self._checked < CHECK_MAX and n == len(src[1]) and n
-                    and tc.sub_id is None):
-                self._checked += 1
-                write_sample(self._check_dir, tc.id, "runner", src[0], src[1],
-                             y[off:off + n].float().cpu().numpy(), self.bn_mode,
-                             str(self.dtype))
+            if src is not None and n == len(src[1]) and n and tc.sub_id is None:
+                stratum = stratum_of("runner", n, call_rows)
+                if self._checked.get(stratum, 0) < CHECK_MAX:
+                    self._checked[stratum] = self._checked.get(stratum, 0) + 1
+                    write_sample(self._check_dir, tc.id, "runner", src[0], src[1],
+                                 y[off:off + n].float().cpu().numpy(), self.bn_mode,
+                                 str(self.dtype), call_rows=call_rows)
             off += n
 
     def __call__(self, tensors, non_tensors, time_card):
@@ -329,7 +332,8 @@ class R2P1DLoader(RunnerModel):
         starts = self.sampler.sample(length) or []
         if len(starts) > self.max_clips:
             starts = starts[:self.max_clips]
-        if time_card is not None and time_card.id % CHECK_EVERY == 0:
+        if time_card is not None and (time_card.id % CHECK_EVERY == 0 or (
+                len(starts) >= 15 and time_card.id % CHECK_EVERY_LARGE == 0)):
             # what a numerics check needs to decode the same clips again
             time_card.extra["clip_src"] = (int(vid), [int(s) for s in starts])
         return self.decoder.decode(vid, starts, out=None if out is None else

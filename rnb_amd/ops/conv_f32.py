@@ -98,11 +98,13 @@ X6_ROW_SLACK = 288
 
 
 def is_x6d(cid: int) -> bool:
-    """x6 direct config (csrc/conv_x6.hip conv_x6_kernel or, from X6R_BASE,
-    the row-band halo kernel conv_x6r_kernel)."""
+    """Direct config on the 16-bit matrix cores with epilogue BN statistics:
+    x6 (csrc/conv_x6.hip conv_x6_kernel, from X6R_BASE the row-band halo
+    kernel conv_x6r_kernel, from X6K_BASE split-K) or h3 (csrc/conv_h3.hip,
+    from H3D_BASE; split-K from H3K_BASE)."""
     from .native import kernels
     return ((X6D_BASE <= cid < X6D_BASE + len(kernels().x6_configs)) or is_x6r(cid)
-            or is_x6k(cid))
+            or is_x6k(cid) or is_h3(cid))
 
 
 # row-band halo variants of the x6 direct conv (1x3x3 stride 1 pad 1 only)
@@ -126,6 +128,69 @@ X6K_TARGET_BLOCKS = 512
 
 def is_x6k(cid: int) -> bool:
     return X6K_BASE <= cid < X6K_BASE + len(X6K_CONFIGS)
+
+
+# fp32 direct convs with the products on the fp16 matrix cores (csrc/conv_h3.hip:
+# every fp32 operand split into fp16 hi + lo, three products): config
+# H3D_BASE + i of rnb_conv_h3_launch, and split-K variants H3K_BASE + j of
+# the small-tile configs H3K_CONFIGS[j] (as X6K_*)
+H3D_BASE = 1300
+H3K_BASE = 1350
+H3K_CONFIGS = (2, 4, 5, 9, 10)
+# activations are split after scaling by 2^H3_IN_LOG2: fp16 lo parts stay
+# normal for |a| >= 2^-9 and inputs up to 2^10 stay in the fp16 range
+H3_IN_LOG2 = 6
+# weights are scaled so that their largest magnitude lies in [2^13, 2^14)
+H3_W_TOP_LOG2 = 13
+
+
+def is_h3(cid: int) -> bool:
+    from .native import kernels
+    return ((H3D_BASE <= cid < H3D_BASE + len(kernels().h3_configs))
+            or H3K_BASE <= cid < H3K_BASE + len(H3K_CONFIGS))
+
+
+def is_h3k(cid: int) -> bool:
+    return H3K_BASE <= cid < H3K_BASE + len(H3K_CONFIGS)
+
+
+def h3_enabled() -> bool:
+    """RNB_H3=0 keeps the direct convs on the x6 / fp32-MFMA kernels."""
+    return os.environ.get("RNB_H3", "1") != "0"
+
+
+def h3_weight_scale_log2(wmat: torch.Tensor) -> int:
+    """Power-of-two exponent sw that puts max |w| * 2^sw in [2^13, 2^14)."""
+    m = float(wmat.abs().max()) if wmat.numel() else 0.0
+    if m == 0.0:
+        return 0
+    return H3_W_TOP_LOG2 - int(math.floor(math.log2(m)))
+
+
+def h3_direct_weights(wmat: torch.Tensor, sw: int) -> torch.Tensor:
+    """fp32 weight matrix [rows, K] (K % 32 == 0, k = tap * Cin_p + c) ->
+    the h3 kernel's layout [K / 32][rows][8 chunks][8 fp16] as int16: per
+    32-channel step (sub-steps s0 = channels 0..15, s1 = 16..31), row and
+    channel quad q the chunks (Ah0 | Ah1) (logical 2 q) and (Al0 | Al1)
+    (2 q + 1) of the RNE fp16 split of w * 2^sw (a = h + l, h = fp16(a),
+    l = fp16(a - h)), chunk c stored at c ^ _X6_S[(row % 16) >> 1]."""
+    rows, K = wmat.shape
+    assert K % 32 == 0, K
+    a = wmat.float().cpu() * (2.0 ** sw)          # exact (power of two)
+    if a.abs().max() >= 32768:
+        raise ValueError("h3 weight scale 2^%d overflows fp16" % sw)
+    h = a.half()
+    lo = (a - h.float()).half()                   # a - h exact in fp32
+    steps = K // 32
+
+    def lay(t):                                   # -> [rows, steps, quad, sub, 4]
+        return t.reshape(rows, steps, 2, 4, 4).permute(0, 1, 3, 2, 4).reshape(rows, steps, 4, 8)
+    chunks = torch.stack([lay(h), lay(lo)], dim=-2)               # [rows, steps, 4, 2, 8]
+    logical = chunks.reshape(rows, steps, 8, 8)
+    sw_ = torch.tensor([_X6_S[(rr % 16) >> 1] for rr in range(rows)], dtype=torch.int64)
+    idx = torch.arange(8, dtype=torch.int64)[None, :] ^ sw_[:, None]           # [rows, 8]
+    phys = logical.gather(2, idx[:, None, :, None].expand_as(logical))
+    return phys.permute(1, 0, 2, 3).contiguous().view(torch.int16)
 
 
 def x6_direct_weights(wmat: torch.Tensor) -> torch.Tensor:
@@ -288,18 +353,29 @@ class ConvLayerF32:
         # the conv runs with out_stats (training-mode BN after it): autotune
         # only the configs that accumulate them, timed with the statistics on
         self.tune_with_stats = False
+        # a batch-BN producer before this conv defers its BatchNorm + ReLU into
+        # this conv's input loads: autotune only configs that can (temporal
+        # Winograd, h3 direct), timed with the affine on
+        self.tune_with_affine = False
         self._x6d = None                     # (split weights, bias) for the x6 direct kernel
+        self._h3d = None                     # (weights, bias, in_scale, out_scale) for h3
         self._x6k_ws: Dict[int, torch.Tensor] = {}
 
     def ksplit_for(self, cid: int, x_shape) -> int:
-        """Blocks per tile of split-K config ``cid`` for this input: enough to
-        put ~X6K_TARGET_BLOCKS blocks in flight, at least 8 K steps each."""
+        """Blocks per tile of split-K config ``cid`` (x6 or h3) for this input:
+        enough to put ~X6K_TARGET_BLOCKS blocks in flight, at least 8 K steps
+        each (16-channel steps for x6, 32-channel steps for h3)."""
         from .native import kernels
-        pt, ct = kernels().x6_configs[X6K_CONFIGS[cid - X6K_BASE]]
+        if is_h3k(cid):
+            pt, ct = kernels().h3_configs[H3K_CONFIGS[cid - H3K_BASE]]
+            nsteps = self.k_pad // 32
+        else:
+            pt, ct = kernels().x6_configs[X6K_CONFIGS[cid - X6K_BASE]]
+            nsteps = self.k16 // 16
         N, T, H, W, _ = x_shape
         To, Ho, Wo = self.geom.out_thw(T, H, W)
         blocks = math.ceil(N * To * Ho * Wo / pt) * math.ceil(self.geom.cout_p / ct)
-        return int(max(1, min(16, X6K_TARGET_BLOCKS // max(blocks, 1), self.k16 // 16 // 8)))
+        return int(max(1, min(16, X6K_TARGET_BLOCKS // max(blocks, 1), nsteps // 8)))
 
     def x6k_workspace(self, numel: int) -> torch.Tensor:
         """fp32 split-K partials, one persistent buffer per size (graph-safe)."""
@@ -319,6 +395,20 @@ class ConvLayerF32:
             b[:self.geom.cout] = self.bias[:self.geom.cout].cpu()
             self._x6d = (x6_direct_weights(w).to(self.device), b.to(self.device))
         return self._x6d
+
+    def h3d_buffers(self):
+        """(h3 split weights [K_pad/32][rows][64] int16, bias [rows] fp32,
+        in_scale, out_scale), rows = Cout_p + X6_ROW_SLACK, built once."""
+        if self._h3d is None:
+            rows = self.geom.cout_p + X6_ROW_SLACK
+            w = torch.zeros(rows, self.k_pad, dtype=torch.float32)
+            w[:self.geom.cout, :self.k_total] = self.wmat[:self.geom.cout, :self.k_total].cpu()
+            b = torch.zeros(rows, dtype=torch.float32)
+            b[:self.geom.cout] = self.bias[:self.geom.cout].cpu()
+            sw = h3_weight_scale_log2(w)
+            self._h3d = (h3_direct_weights(w, sw).to(self.device), b.to(self.device),
+                         float(2.0 ** H3_IN_LOG2), float(2.0 ** -(H3_IN_LOG2 + sw)))
+        return self._h3d
 
     def wino_u(self, tc: int, m: int = 2, co0: int = 0, nco: Optional[int] = None,
                x6: bool = False) -> torch.Tensor:
@@ -373,6 +463,11 @@ class ConvLayerF32:
             if x_shape is not None and os.environ.get("RNB_X6K", "1") != "0":
                 c += [X6K_BASE + j for j in range(len(X6K_CONFIGS))
                       if self.ksplit_for(X6K_BASE + j, x_shape) > 1]
+        if h3_enabled():
+            c += [H3D_BASE + i for i in range(len(kernels().h3_configs))]
+            if x_shape is not None and os.environ.get("RNB_X6K", "1") != "0":
+                c += [H3K_BASE + j for j in range(len(H3K_CONFIGS))
+                      if self.ksplit_for(H3K_BASE + j, x_shape) > 1]
         ids = self.wino_ids if x6_enabled() else self.wino_ids - WINO_X6
         return c + sorted(ids)
 
@@ -473,9 +568,10 @@ class ConvLayerF32:
         return tab
 
     def params(self, x: torch.Tensor, y: torch.Tensor, residual: Optional[torch.Tensor],
-               n0: int = 0, n1: Optional[int] = None, x6: bool = False):
+               n0: int = 0, n1: Optional[int] = None, x6: bool = False, h3: bool = False):
         """Launch parameters for clips [n0, n1) of the batch (``x6``: for the
-        x6 direct kernel: split weights, K rounded to 16)."""
+        x6 direct kernel: split weights, K rounded to 16; ``h3``: for the h3
+        kernel: split fp16 weights, K rounded to 32)."""
         from .native import ConvParams
         g = self.geom
         N, T, H, W, C = x.shape
@@ -506,7 +602,11 @@ class ConvLayerF32:
         p.w_rows = self.wmat.shape[0]
         p.ktab = self.ktab(T, H, W, x.device).data_ptr()
         p.row_mode = 0
-        if x6:
+        if h3:
+            wx, bx, _, _ = self.h3d_buffers()
+            p.w, p.bias = wx.data_ptr(), bx.data_ptr()
+            p.K_pad, p.w_rows = self.k_pad, bx.shape[0]
+        elif x6:
             wx, bx = self.x6d_buffers()
             p.w, p.bias = wx.data_ptr(), bx.data_ptr()
             p.K_pad, p.w_rows = self.k16, bx.shape[0]
@@ -535,8 +635,9 @@ class ConvLayerF32:
         return best
 
     def _tune_key(self, x_shape, device) -> str:
-        return tuning.make_key("f32st" if self.tune_with_stats else "f32", self.geom,
-                               tuple(x_shape[:4]), _device_name(device))
+        kind = ("f32st" if self.tune_with_stats else "f32") + \
+            ("aff" if self.tune_with_affine else "")
+        return tuning.make_key(kind, self.geom, tuple(x_shape[:4]), _device_name(device))
 
     def config_for(self, x_shape) -> int:
         """Tile config for this input shape: tuned (this layer, or any layer of
@@ -552,7 +653,9 @@ class ConvLayerF32:
                 cid = tuning.nearest(tkey, N * T * H * W)
             if cid is not None and cid in WINO_ALL and cid not in self.wino_ids:
                 cid = None
-            if cid is not None and is_x6d(cid) and not x6_enabled():
+            if cid is not None and is_x6d(cid) and not is_h3(cid) and not x6_enabled():
+                cid = None
+            if cid is not None and is_h3(cid) and not h3_enabled():
                 cid = None
             if (cid is not None and cid not in WINO_ALL and not is_x6d(cid)
                     and cid >= len(_configs())):
@@ -568,6 +671,18 @@ class ConvLayerF32:
                         cid = wino_default(True)
             self._config[key] = cid
         return cid
+
+    def affine_ok(self, cid: int, x_shape) -> bool:
+        """Whether config ``cid`` can apply the input's BN + ReLU on load."""
+        if cid in WINO_TEMPORAL:
+            return True
+        if not is_h3(cid):
+            return False
+        from .native import kernels
+        conf = H3K_CONFIGS[cid - H3K_BASE] if is_h3k(cid) else cid - H3D_BASE
+        _, T, H, W, _ = x_shape
+        To, Ho, Wo = self.geom.out_thw(T, H, W)
+        return kernels().conv_h3_affine_ok(conf, self.geom.cin_p, To * Ho * Wo)
 
     def _launch_all(self, x, y, residual, cid, stream, in_affine=None, out_stats=None):
         from .native import kernels
@@ -585,9 +700,19 @@ class ConvLayerF32:
                                   stream, aff, ost)
             return
         x6 = is_x6d(cid)
-        if in_affine is not None or (out_stats is not None and not x6):
-            raise ValueError("%s: fused input BN needs a temporal Winograd config, output BN "
-                             "statistics a Winograd or x6 direct config" % self.name)
+        if (in_affine is not None and not is_h3(cid)) or (out_stats is not None and not x6):
+            raise ValueError("%s: fused input BN needs a temporal Winograd or h3 config, "
+                             "output BN statistics a Winograd, x6 or h3 direct config"
+                             % self.name)
+        if in_affine is not None:
+            ss, aseg = in_affine
+            C = x.shape[-1]
+            if (ss.dim() != 3 or ss.shape[1:] != (2, C) or ss.dtype != torch.float32
+                    or not ss.is_contiguous() or aseg.dtype != torch.int32
+                    or aseg.numel() != N or not aseg.is_contiguous()):
+                raise ValueError("%s: input BN scale/shift %s / clip_seg %s do not match x %s"
+                                 % (self.name, tuple(ss.shape), tuple(aseg.shape),
+                                    tuple(x.shape)))
         if out_stats is not None:
             sums, clip_seg = out_stats
             if (sums.dim() != 3 or sums.shape[1] != 2 or sums.shape[2] < self.geom.cout_p
@@ -599,9 +724,27 @@ class ConvLayerF32:
                                     tuple(y.shape)))
         step = self.chunk_clips(x.shape, y.shape,
                                 residual.shape[-1] if residual is not None else 0)
+        h3 = is_h3(cid)
         for n0 in range(0, N, step):
-            p = self.params(x, y, residual, n0, min(N, n0 + step), x6=x6)
-            if is_x6r(cid):
+            p = self.params(x, y, residual, n0, min(N, n0 + step), x6=x6 and not h3, h3=h3)
+            if h3:
+                _, _, s_in, s_out = self.h3d_buffers()
+                ks, ws = 1, None
+                conf = cid - H3D_BASE
+                if is_h3k(cid):
+                    conf = H3K_CONFIGS[cid - H3K_BASE]
+                    ks = self.ksplit_for(cid, x[n0:min(N, n0 + step)].shape)
+                    ws = self.x6k_workspace(ks * p.M * self.geom.cout_p) if ks > 1 else None
+                aff = ((in_affine[0].data_ptr(), in_affine[1].data_ptr() + 4 * n0)
+                       if in_affine is not None else (0, 0))
+                if out_stats is not None:
+                    k.conv_h3(p, conf, stream.cuda_stream, s_in, s_out, out_stats[0].data_ptr(),
+                              out_stats[1].data_ptr() + 4 * n0, out_stats[0].shape[2], ks,
+                              ws.data_ptr() if ws is not None else 0, *aff)
+                else:
+                    k.conv_h3(p, conf, stream.cuda_stream, s_in, s_out, 0, 0, 0, ks,
+                              ws.data_ptr() if ws is not None else 0, *aff)
+            elif is_x6r(cid):
                 if not self.wino_ok:
                     raise ValueError("%s: the row-band x6 kernel takes 1x3x3 stride-1 convs"
                                      % self.name)
@@ -637,28 +780,37 @@ class ConvLayerF32:
         cached = tuning.get(tkey)
         if cached is not None and (cached < len(kernels().f32_configs) or
                                    cached in self.wino_ids or
-                                   (is_x6d(cached) and x6_enabled())):
+                                   (is_h3(cached) and h3_enabled()) or
+                                   (is_x6d(cached) and not is_h3(cached) and x6_enabled())):
             self._config[tuple(x.shape[:4])] = cached
             return cached
         y = torch.empty(self.out_shape(x.shape), dtype=torch.float32, device=x.device)
         stream = torch.cuda.current_stream(x.device)
         verbose = os.environ.get("RNB_TUNE_VERBOSE") == "1"
-        cands, ost = self.candidates(x.shape), None
+        cands, ost, aff = self.candidates(x.shape), None, None
         if self.tune_with_stats:
             cands = [c for c in cands if c in WINO_ALL or is_x6d(c)] or cands
             ost = (torch.zeros((1, 2, self.geom.cout_p), dtype=torch.float64, device=x.device),
                    torch.zeros(x.shape[0], dtype=torch.int32, device=x.device))
+        if self.tune_with_affine:
+            ok = [c for c in cands if self.affine_ok(c, x.shape)]
+            if ok:
+                cands = ok
+                ss = torch.ones((1, 2, x.shape[-1]), dtype=torch.float32, device=x.device)
+                ss[:, 1] = 0.0
+                aff = (ss, torch.zeros(x.shape[0], dtype=torch.int32, device=x.device))
         # candidates are timed in rounds of alternating order, best round each:
         # timed once in a fixed order, whatever runs late wins by 5-15 % as
         # the clocks settle (profiles/r3_x6_exp_interleaved.txt)
         def time_one(cid, n):
             o = ost if ost is not None and (cid in WINO_ALL or is_x6d(cid)) else None
-            self._launch_all(x, y, residual, cid, stream, out_stats=o)       # warm
+            a = aff if aff is not None and self.affine_ok(cid, x.shape) else None
+            self._launch_all(x, y, residual, cid, stream, in_affine=a, out_stats=o)   # warm
             start = torch.cuda.Event(enable_timing=True)
             end = torch.cuda.Event(enable_timing=True)
             start.record(stream)
             for _ in range(n):
-                self._launch_all(x, y, residual, cid, stream, out_stats=o)
+                self._launch_all(x, y, residual, cid, stream, in_affine=a, out_stats=o)
             end.record(stream)
             end.synchronize()
             return start.elapsed_time(end) / n
@@ -693,8 +845,9 @@ class ConvLayerF32:
 
     def accepts_input_affine(self, x_shape) -> bool:
         """True when this conv's kernel for ``x_shape`` can apply its input's
-        BatchNorm + ReLU on load (``forward_hip(in_affine=...)``)."""
-        return self.config_for(x_shape) in WINO_TEMPORAL
+        BatchNorm + ReLU on load (``forward_hip(in_affine=...)``): temporal
+        Winograd, or h3 direct when its tile fits (``affine_ok``)."""
+        return self.affine_ok(self.config_for(x_shape), x_shape)
 
     def forward_hip(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                     out: Optional[torch.Tensor] = None, config: Optional[int] = None,

@@ -312,6 +312,16 @@ class Kernels:
         lib.rnb_conv_x6r_launch.restype = ctypes.c_int
         lib.rnb_conv_x6_config_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                                 ctypes.POINTER(ctypes.c_int)]
+        lib.rnb_conv_h3_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_float, ctypes.c_float, ctypes.c_void_p,
+                                           ctypes.c_void_p]
+        lib.rnb_conv_h3_launch.restype = ctypes.c_int
+        lib.rnb_conv_h3_affine_ok.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        lib.rnb_conv_h3_affine_ok.restype = ctypes.c_int
+        lib.rnb_conv_h3_config_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                                ctypes.POINTER(ctypes.c_int)]
         lib.rnb_preprocess_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
                                            ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_float), ctypes.c_void_p]
@@ -344,6 +354,11 @@ class Kernels:
             p, c = ctypes.c_int(), ctypes.c_int()
             lib.rnb_conv_x6_config_info(i, ctypes.byref(p), ctypes.byref(c))
             self.x6_configs.append((p.value, c.value))
+        self.h3_configs = []       # (pixel tile, channel tile) per h3 direct config
+        for i in range(lib.rnb_conv_h3_num_configs()):
+            p, c = ctypes.c_int(), ctypes.c_int()
+            lib.rnb_conv_h3_config_info(i, ctypes.byref(p), ctypes.byref(c))
+            self.h3_configs.append((p.value, c.value))
         self.configs = []          # (pixel tile, channel tile) per config id
         self.stages = []           # LDS staging depth per config id
         for i in range(lib.rnb_conv_num_configs()):
@@ -370,6 +385,24 @@ class Kernels:
                                                   sums or None, clip_seg or None, stats_c,
                                                   ksplit, ws or None),
                "conv_x6 (config %d, ksplit %d)" % (config_id, ksplit))
+
+    def conv_h3(self, params: ConvParams, config_id: int, stream: int, in_scale: float,
+                out_scale: float, sums: int = 0, clip_seg: int = 0, stats_c: int = 0,
+                ksplit: int = 1, ws: int = 0, in_ss: int = 0, in_seg: int = 0) -> None:
+        """h3 direct conv (fp32 products as fp16 hi/lo products, csrc/conv_h3.hip):
+        ``params.w`` = split weights scaled by 2^sw, ``in_scale`` = 2^sa applied
+        to the activations, ``out_scale`` = 2^-(sa + sw); sums / ksplit / ws as
+        ``conv_x6``; ``in_ss`` (fp32 [nseg][2][Cin_p] scale/shift) with
+        ``in_seg`` (int32 [N] video per clip): the input's BatchNorm + ReLU
+        applied on load."""
+        _check(self.lib.rnb_conv_h3_launch(ctypes.byref(params), config_id, stream,
+                                           sums or None, clip_seg or None, stats_c, ksplit,
+                                           ws or None, in_scale, out_scale, in_ss or None,
+                                           in_seg or None),
+               "conv_h3 (config %d, ksplit %d)" % (config_id, ksplit))
+
+    def conv_h3_affine_ok(self, config_id: int, cin_p: int, rows_per_clip: int) -> bool:
+        return bool(self.lib.rnb_conv_h3_affine_ok(config_id, cin_p, rows_per_clip))
 
     def conv_x6r(self, params: ConvParams, variant: int, stream: int, sums: int = 0,
                  clip_seg: int = 0, stats_c: int = 0) -> None:
@@ -563,11 +596,27 @@ class Runtime:
         lib.rnb_can_access_peer.argtypes = [ctypes.c_int, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_int)]
         lib.rnb_mem_get_info.argtypes = [ctypes.POINTER(sz), ctypes.POINTER(sz)]
+        lib.rnb_stream_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+        lib.rnb_stream_destroy.argtypes = [vp]
+        lib.rnb_spin.argtypes = [vp, ctypes.c_longlong]
         self.handle_size = lib.rnb_ipc_handle_size()
         self.event_handle_size = lib.rnb_ipc_event_handle_size()
 
     def set_device(self, dev: int) -> None:
         _check(self.lib.rnb_set_device(dev), "hipSetDevice")
+
+    def stream_create(self, nonblocking: bool = True, priority: int = 0) -> int:
+        s = ctypes.c_void_p()
+        _check(self.lib.rnb_stream_create(int(nonblocking), priority, ctypes.byref(s)),
+               "hipStreamCreateWithPriority")
+        return s.value
+
+    def stream_destroy(self, stream: int) -> None:
+        _check(self.lib.rnb_stream_destroy(stream), "hipStreamDestroy")
+
+    def spin(self, stream: int, cycles: int) -> None:
+        """Busy-wait kernel of ~``cycles`` GPU clocks on ``stream``."""
+        _check(self.lib.rnb_spin(stream, cycles), "spin kernel")
 
     def ipc_malloc(self, nbytes: int) -> int:
         p = ctypes.c_void_p()

@@ -16,10 +16,15 @@ bridges that with a *claim handshake* (SURVEY.md §7.4 item 3):
 
 A consumer that gathers several items into one model call posts all their
 claims first and launches all their ``irecv``s as ONE ``batch_isend_irecv``
-group (``flush_recvs``, called by the runner once per call); on RCCL the
-receives are ordered on the consumer's stream (no host synchronisation),
-and the process group's timeout is the watchdog. The producer may decode
-straight into a send slot (``slot_views`` / ``commit``, runner direct_out).
+group (``flush_recvs``, called by the runner once per call). The receives of
+a call live in a list the runner owns for that call (``read_into(...,
+pending=ops)``), never in module state, and the runner drops it if the call
+fails before the flush. On RCCL the receives are ordered on the consumer's
+stream (no host synchronisation), so the only watchdog of a stuck sender is
+the process group's timeout (``RNB_RCCL_TIMEOUT_S`` at
+``init_process_group``); on gloo (CPU) ``flush_recvs`` waits on the host with
+that timeout. The producer may decode straight into a send slot
+(``slot_views`` / ``commit``, runner direct_out).
 
 Per (src, dst) pair the claims are served in the order the consumer posted
 them, so sends and receives match. All participating runners form one
@@ -93,22 +98,18 @@ def _timeout():
     return timedelta(seconds=float(os.environ.get(RCCL_TIMEOUT_ENV, "120")))
 
 
-# receives posted by RcclRing.read_into in this process, launched together by
-# flush_recvs (one batch_isend_irecv group per model call)
-_pending_recvs = []
-
-
-def flush_recvs() -> int:
-    """Launch every receive ``read_into`` posted since the last flush as one
-    group. RCCL: the current stream waits for them (ordered on the GPU, the
-    host does not block; a stuck sender trips the group timeout). gloo (CPU):
-    wait on the host, raising TimeoutError after RNB_RCCL_TIMEOUT_S. Returns
-    the number of receives."""
-    if not _pending_recvs:
+def flush_recvs(pending: list) -> int:
+    """Launch the receives ``read_into`` appended to ``pending`` (the runner's
+    list for one model call) as one group and empty the list. RCCL: the
+    current stream waits for them (ordered on the GPU, the host does not
+    block; a stuck sender trips the process group's timeout). gloo (CPU): wait
+    on the host, raising TimeoutError after RNB_RCCL_TIMEOUT_S. Returns the
+    number of receives."""
+    if not pending:
         return 0
     import torch.distributed as dist
-    ops = list(_pending_recvs)
-    _pending_recvs.clear()
+    ops = list(pending)
+    pending.clear()
     works = dist.batch_isend_irecv(ops)
     if _state["backend"] == "nccl":
         for w in works:
@@ -137,11 +138,17 @@ class RcclRing(RingBase):
       sends as one ``batch_isend_irecv`` group (one NCCL group launch); each
       completion is awaited with a timeout (``RNB_RCCL_TIMEOUT_S``, default
       120 s) and the slot is freed only after its send completed.
-    * The consumer posts its claim and its ``irecv``s together and waits with
-      the same timeout: a dead or stuck sender makes the consumer raise (the
-      launcher's watchdog then aborts the job with CHILD_FAILED) instead of
-      hanging in ``recv``. A sender-side failure is reported on the producer's
-      next ``write`` and by ``raise_if_failed``.
+    * The consumer posts its claim and queues its ``irecv``s in the call's
+      ``pending`` list; ``flush_recvs`` launches them. On gloo the host waits
+      with the same timeout and raises, so the launcher's watchdog aborts the
+      job with CHILD_FAILED. On RCCL the receive is stream-ordered and the
+      host returns at once: a dead or stuck sender is caught by the process
+      group's timeout (set to RNB_RCCL_TIMEOUT_S at init), not by the runner.
+      A sender-side failure is reported on the producer's next ``write`` and
+      by ``raise_if_failed``.
+    * ``verify(.., "after pull")`` and ``release`` are no-ops: the data moves
+      only when the call's receives are flushed, and the slot is freed by the
+      sender thread once its send completed.
     """
 
     kind = "rccl"
@@ -288,18 +295,23 @@ class RcclRing(RingBase):
             print("[ring %s] rccl edge gpu %d -> gpu %d, peer access %s"
                   % (self.name, self.producer_gpu, device.index, ok), flush=True)
 
-    def read_into(self, idx, placeholders, descriptor=None):
-        """Claim slot ``idx`` and post its receives into ``placeholders``
-        (rows [0, b)); they are launched by ``flush_recvs`` together with the
-        other items of the call, so the views are valid only after it."""
+    def read_into(self, idx, placeholders, descriptor=None, pending=None):
+        """Claim slot ``idx`` and append its receives into ``placeholders``
+        (rows [0, b)) to ``pending``, the caller's list for this model call;
+        ``flush_recvs(pending)`` launches them together with the other items
+        of the call, so the views are valid only after it. Without a list the
+        receives are launched at once."""
         import torch.distributed as dist
         src = self.producer_rank if descriptor is None else descriptor
+        ops = [] if pending is None else pending
         out = []
         for ph, rows in zip(placeholders, self.valid_rows(idx)):
             if rows:
-                _pending_recvs.append(dist.P2POp(dist.irecv, ph[:rows], src))
+                ops.append(dist.P2POp(dist.irecv, ph[:rows], src))
             out.append(ph[:rows])
         self.claims.put((idx, my_rank()))
+        if pending is None:
+            flush_recvs(ops)
         return out
 
     def release(self, idx):

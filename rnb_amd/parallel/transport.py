@@ -15,12 +15,14 @@ Backends (chosen per edge by ``make_ring``):
 
 ``HostRing``  shared-memory CPU tensors; used whenever the producer or any
               consumer runs on the CPU (``gpus: [-1]``) or there is no GPU.
-``IpcRing``   producer-owned HBM buffers allocated with ``hipMalloc`` by the
-              native runtime and exported with ``hipIpcGetMemHandle``; the
-              handles travel inside each ``Signal`` so consumers open them
-              lazily; pulls are ``hipMemcpyAsync`` (peer copy over xGMI when
-              the consumer sits on another GPU, an on-device copy otherwise),
-              ordered on the GPU by interprocess events (no host syncs).
+``IpcRing``   producer-owned HBM: ONE ``hipMalloc`` per ring (slots are
+              offsets into it) exported with one ``hipIpcGetMemHandle``;
+              consumers open it once, on their first pull from that
+              producer; pulls are ``hipMemcpyAsync`` (peer copy over xGMI
+              when the consumer sits on another GPU, an on-device copy
+              otherwise), ordered on the GPU by interprocess events (no host
+              syncs). Events are opened / created per slot on first use, so a
+              consumer holds handles only for the slots it actually pulled.
 
 The RCCL send/recv channel for static 1:1 edges lives in
 ``parallel/rccl_channel.py``.
@@ -246,6 +248,14 @@ class IpcRing(RingBase):
     def __init__(self, ctx, shapes, dtypes, num_slots, name, producer_gpu):
         super().__init__(ctx, shapes, dtypes, num_slots, name, producer_gpu)
         self._ptrs = None          # producer: [slot][tensor] device pointers
+        self._base = None          # producer: the ring's single allocation
+        # slot layout inside the allocation: tensor t of slot i at
+        # i * slot_stride + tensor_offsets[t] (256-B aligned)
+        offs, o = [], 0
+        for sh, d in zip(self.shapes, self.dtypes):
+            offs.append(o)
+            o += (max(_nbytes(sh, d), 256) + 255) // 256 * 256
+        self.tensor_offsets, self.slot_stride = tuple(offs), o
         self._desc = None
         self._opened: Dict[Tuple, List[List[int]]] = {}
         self.consumers: List[Tuple[int, int, int]] = []   # (step, group, instance)
@@ -265,8 +275,13 @@ class IpcRing(RingBase):
         self._rel_open: Dict[int, List[Optional[int]]] = {}   # producer: cid -> events
         self._cid = None           # consumer id of this process
         self._rev = None           # consumer: own release events [slot]
-        self._wopen: Dict[Tuple, List[int]] = {}              # consumer: opened written events
+        self._wopen: Dict[Tuple, List[Optional[int]]] = {}    # consumer: opened written events
+        self._whandles: Dict[Tuple, tuple] = {}               # consumer: their handles
+        self._opened_base: Dict[Tuple, int] = {}              # consumer: opened allocations
+        self.events_opened = 0
+        self.events_created = 0
         self.stale_event_waits = 0      # stream waits ROCm refused on completed events
+        self.gpu_waits = 0              # stream waits ordered on the GPU
         self._dev = None
         self._views = None
         self._token = None
@@ -277,17 +292,23 @@ class IpcRing(RingBase):
         n = max(1, len(self.consumers))
         self.rel_handles = self._ctx.Array("c", n * self.num_slots * EVENT_HANDLE_BYTES,
                                            lock=False)
-        self.rel_ready = self._ctx.Array("i", n, lock=False)
+        # per (consumer, slot): 1 once that consumer's release event of the
+        # slot is created and its handle published (consumers create them
+        # on their first release of the slot)
+        self.rel_ready = self._ctx.Array("b", n * self.num_slots, lock=False)
 
     def __getstate__(self):
         st = dict(self.__dict__)
         st["_ptrs"] = None
+        st["_base"] = None
         st["_opened"] = {}
         st["_ctx"] = None
         st["_wev"] = None
         st["_rel_open"] = {}
         st["_rev"] = None
         st["_wopen"] = {}
+        st["_whandles"] = {}
+        st["_opened_base"] = {}
         st["_cid"] = None
         st["_views"] = None
         st["_token"] = None
@@ -303,15 +324,11 @@ class IpcRing(RingBase):
         rt = native.runtime()
         rt.set_device(device.index)
         self._dev = device
-        self._ptrs, handles = [], []
-        for _ in range(self.num_slots):
-            row_ptrs, row_h = [], []
-            for s, d in zip(self.shapes, self.dtypes):
-                ptr = rt.ipc_malloc(max(_nbytes(s, d), 256))
-                row_ptrs.append(ptr)
-                row_h.append(rt.ipc_get_handle(ptr))
-            self._ptrs.append(row_ptrs)
-            handles.append(tuple(row_h))
+        # one allocation and one IPC memory handle for the whole ring
+        self._base = rt.ipc_malloc(self.num_slots * self.slot_stride)
+        handle = rt.ipc_get_handle(self._base)
+        self._ptrs = [[self._base + i * self.slot_stride + o for o in self.tensor_offsets]
+                      for i in range(self.num_slots)]
         wh = ()
         if self.gpu_ordered:
             if rt.event_handle_size > EVENT_HANDLE_BYTES:
@@ -319,7 +336,7 @@ class IpcRing(RingBase):
                                    % (rt.event_handle_size, EVENT_HANDLE_BYTES))
             self._wev = [rt.event_create_ipc() for _ in range(self.num_slots)]
             wh = tuple(rt.event_get_handle(e) for e in self._wev)
-        self._desc = (self.name, os.getpid(), device.index, tuple(handles), wh)
+        self._desc = (self.name, os.getpid(), device.index, handle, wh)
         import pickle
         blob = pickle.dumps(self._desc, protocol=pickle.HIGHEST_PROTOCOL)
         if len(blob) > self._desc_cap:
@@ -348,9 +365,9 @@ class IpcRing(RingBase):
         if evs is None:
             evs = self._rel_open[cid] = [None] * self.num_slots
         if evs[idx] is None:
-            if not self.rel_ready[cid]:
-                raise RuntimeError("ring %s: consumer %d released a slot before "
-                                   "publishing its events" % (self.name, cid))
+            if not self.rel_ready[cid * self.num_slots + idx]:
+                raise RuntimeError("ring %s: consumer %d released slot %d before "
+                                   "publishing its event" % (self.name, cid, idx))
             off = (cid * self.num_slots + idx) * EVENT_HANDLE_BYTES
             h = bytes(self.rel_handles[off:off + EVENT_HANDLE_BYTES])
             evs[idx] = native.runtime().event_open_handle(h)
@@ -378,6 +395,7 @@ class IpcRing(RingBase):
         rt = native.runtime()
         rc = rt.try_stream_wait_event(stream.cuda_stream, ev)
         if rc == 0:
+            self.gpu_waits += 1
             return
         rt.clear_last_error()        # else the next kernel launch check reports it
         q = rt.event_query(ev)
@@ -444,12 +462,7 @@ class IpcRing(RingBase):
         if key is None or tuple(key) not in self.consumers:
             raise RuntimeError("ring %s: consumer %s was not declared" % (self.name, key))
         self._cid = self.consumers.index(tuple(key))
-        self._rev = [rt.event_create_ipc() for _ in range(self.num_slots)]
-        for i, e in enumerate(self._rev):
-            h = rt.event_get_handle(e)
-            off = (self._cid * self.num_slots + i) * EVENT_HANDLE_BYTES
-            self.rel_handles[off:off + len(h)] = h
-        self.rel_ready[self._cid] = 1
+        self._rev = [None] * self.num_slots       # created on first release of a slot
 
     def _open(self, token):
         from ..ops import native
@@ -463,11 +476,23 @@ class IpcRing(RingBase):
                 raise RuntimeError("ring %s: no published descriptor for producer %s"
                                    % (self.name, key))
             rt = native.runtime()
-            ptrs = [[rt.ipc_open_handle(h) for h in row] for row in desc[3]]
+            base = rt.ipc_open_handle(desc[3])
+            ptrs = [[base + i * self.slot_stride + o for o in self.tensor_offsets]
+                    for i in range(self.num_slots)]
             self._opened[key] = ptrs
+            self._opened_base[key] = base
             if self.gpu_ordered and len(desc) > 4 and desc[4]:
-                self._wopen[key] = [rt.event_open_handle(h) for h in desc[4]]
+                self._whandles[key] = desc[4]
+                self._wopen[key] = [None] * self.num_slots    # opened on first pull
         return ptrs
+
+    def _written_event(self, key, idx: int) -> int:
+        evs = self._wopen[key]
+        if evs[idx] is None:
+            from ..ops import native
+            evs[idx] = native.runtime().event_open_handle(self._whandles[key][idx])
+            self.events_opened += 1
+        return evs[idx]
 
     def rows_of(self, idx: int) -> int:
         return self.valid_rows(idx)[0]
@@ -488,7 +513,8 @@ class IpcRing(RingBase):
         if gpu:
             stream = torch.cuda.current_stream(dev)
             if self.gpu_ordered:
-                self._wait_ipc_event(stream, self._wopen[tuple(descriptor[:2])][idx], idx)
+                self._wait_ipc_event(stream, self._written_event(tuple(descriptor[:2]), idx),
+                                     idx)
         for t, (ph, b) in enumerate(zip(placeholders, self.valid_rows(idx))):
             if b:
                 if b > ph.shape[0] or not ph.is_contiguous():
@@ -507,27 +533,44 @@ class IpcRing(RingBase):
     def release(self, idx: int) -> None:
         if self.gpu_ordered and self._rev is not None:
             from ..ops import native
+            rt = native.runtime()
+            if self._rev[idx] is None:
+                # first release of this slot by this consumer: create its
+                # event and publish the handle before naming itself below
+                ev = rt.event_create_ipc()
+                h = rt.event_get_handle(ev)
+                off = (self._cid * self.num_slots + idx) * EVENT_HANDLE_BYTES
+                self.rel_handles[off:off + len(h)] = h
+                self.rel_ready[self._cid * self.num_slots + idx] = 1
+                self._rev[idx] = ev
+                self.events_created += 1
             stream = torch.cuda.current_stream(self.consumer_device)
-            native.runtime().event_record(self._rev[idx], stream.cuda_stream)
+            rt.event_record(self._rev[idx], stream.cuda_stream)
             self.released_by[idx] = self._cid
         super().release(idx)
+
+    def handle_stats(self) -> dict:
+        """IPC resources this process holds for the ring (stress test, stats)."""
+        return {"mem_handles_opened": len(self._opened),
+                "events_opened": self.events_opened,
+                "events_created": self.events_created,
+                "gpu_ordered_waits": self.gpu_waits,
+                "host_fallback_waits": self.stale_event_waits}
 
     def close(self):
         from ..ops import native
         if self._ptrs is None and not self._opened and self._rev is None:
             return
         rt = native.runtime()
-        for ptrs in self._opened.values():
-            for row in ptrs:
-                for p in row:
-                    rt.ipc_close_handle(p)
+        for base in self._opened_base.values():
+            rt.ipc_close_handle(base)
         self._opened = {}
+        self._opened_base = {}
         if self._ptrs is not None:
             torch.cuda.synchronize(self._dev)
             self._views = None
-            for row in self._ptrs:
-                for p in row:
-                    rt.free(p)
+            rt.free(self._base)
+            self._base = None
             self._ptrs = None
 
 

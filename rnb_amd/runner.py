@@ -32,6 +32,18 @@ QUEUE_POLL_S = 0.1
 # batching keeps gathering at most this
 # long while the replica's previous batch still runs on the GPU
 INFLIGHT_GATHER_S = float(os.environ.get("RNB_INFLIGHT_GATHER_MS", "50")) / 1000.0
+# latency regime: with fewer than this many items queued, a replica whose
+# previous batch still runs on the GPU neither dequeues nor keeps gathering
+# until that batch completes, so queued requests go to idle replicas instead
+# of waiting behind a busy one (RNB_LATENCY_BACKLOG=0: always gather)
+LATENCY_BACKLOG = int(os.environ.get("RNB_LATENCY_BACKLOG", "8"))
+# a non-blocking mp.Queue read fails whenever another replica holds the
+# queue's read lock, even with items waiting; when the queue's count says
+# items are there the gather blocks this long for the next one instead
+CONTENDED_GET_S = float(os.environ.get("RNB_CONTENDED_GET_MS", "5")) / 1000.0
+# why a consumer-side gather ended (runner stats, BENCH JSON)
+GATHER_ENDS = ("item_cap", "row_cap", "empty", "empty_backlog", "busy_timeout", "wait_timeout",
+               "other_class")
 
 
 def _set_flag(flag, value, only_if_unset=True):
@@ -274,9 +286,12 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 # must catch the producer's overwrite
                 ring.release(signal.tensor_idx)
                 time.sleep(0.3)
-            out = ring.read_into(signal.tensor_idx, dst, signal.ring)
             if getattr(ring, "deferred_reads", False):
-                deferred["rccl"] = True     # receives launched by flush_reads()
+                # RCCL: receives queue in this call's list, flush_reads() launches them
+                out = ring.read_into(signal.tensor_idx, dst, signal.ring,
+                                     pending=call_recvs)
+            else:
+                out = ring.read_into(signal.tensor_idx, dst, signal.ring)
             if fault != "early_release":
                 ring.verify(signal.tensor_idx, signal.gen, "after pull")
             elif signal.gen is not None and ring.gen[signal.tensor_idx] != signal.gen:
@@ -286,14 +301,15 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             ring.release(signal.tensor_idx)
             return out
 
-        deferred = {"rccl": False}
+        # receives the RCCL input rings queued for the current model call
+        # (launched as one group by flush_reads; dropped if the call fails)
+        call_recvs = []
 
         def flush_reads():
             """RCCL input rings post receives per item; launch them as one group."""
-            if deferred["rccl"]:
+            if call_recvs:
                 from .parallel.rccl_channel import flush_recvs
-                deferred["rccl"] = False
-                flush_recvs()
+                flush_recvs(call_recvs)
 
         def rows_of(signal):
             return shared_input_rings[signal.group_idx][signal.instance_idx].rows_of(
@@ -304,7 +320,34 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
 
         pending = []                  # items taken out of the queue but not run yet
         group_key = getattr(selector, "group_key", None)
-        gstats = {"calls": 0, "items": 0, "rows": 0}
+        # gather counters per phase of the launcher run (request ids: warm-up,
+        # timed bulk phase, latency phases after it; RNB_PHASE_IDS = "warm,videos")
+        try:
+            warm_ids, bulk_ids = (int(v) for v in
+                                  os.environ.get("RNB_PHASE_IDS", "0,0").split(","))
+        except ValueError:
+            warm_ids, bulk_ids = 0, 0
+
+        def phase_of(card_id):
+            if bulk_ids <= 0:
+                return "all"
+            if card_id <= warm_ids:
+                return "warmup"
+            return "bulk" if card_id <= warm_ids + bulk_ids else "latency"
+        gstats = {}
+
+        def gstat(phase):
+            st = gstats.get(phase)
+            if st is None:
+                st = gstats[phase] = dict({"calls": 0, "items": 0, "rows": 0},
+                                          **{"end_" + k: 0 for k in GATHER_ENDS})
+            return st
+
+        def backlog():
+            try:
+                return input_queue.qsize()
+            except (NotImplementedError, AttributeError, OSError):
+                return 0
         # RNB_PROFILE_STAGES=1: where this runner's host time goes (seconds per
         # phase: queue wait, slot pulls, model call, output publish)
         prof = {} if os.environ.get("RNB_PROFILE_STAGES") == "1" else None
@@ -316,8 +359,14 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 prof[name] = prof.get(name, 0.0) + now - pclock[0]
                 pclock[0] = now
         while termination_flag.value == TerminationFlag.UNSET:
+            if (gather is not None and inflight is not None and LATENCY_BACKLOG > 0
+                    and not pending and backlog() < LATENCY_BACKLOG and not inflight.query()):
+                # little queued: take the next request only once this replica
+                # is idle (another, idle replica serves it sooner)
+                inflight.synchronize()
+                tick("inflight_wait")
             if pending:
-                tpl = pending.pop()
+                tpl = pending.pop(0)
             else:
                 try:
                     tpl = input_queue.get(timeout=QUEUE_POLL_S)
@@ -336,6 +385,7 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 else:
                     continue
             tick("queue")
+            call_recvs.clear()      # never launch a failed call's receives later
             signal, non_tensor_inputs, time_card = tpl
             time_card.add_gpu(g_idx)
             time_card.record("runner%d_start" % step_idx)
@@ -364,32 +414,55 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                     nxt[2].record("runner%d_start" % step_idx)
                     items.append(nxt)
                     rows += rows_of(nxt[0])
-                while len(items) < max_items and rows < max_rows:
+                end = "item_cap"
+                while True:
+                    if len(items) >= max_items:
+                        end = "item_cap"
+                        break
+                    if rows >= max_rows:
+                        end = "row_cap"
+                        break
                     # while this replica's previous batch is still running on
                     # the GPU, a launch now would only queue behind it: keep
                     # gathering (bounded), so batches grow with the load
                     busy = (inflight is not None and not inflight.query()
-                            and time.time() - t0 < INFLIGHT_GATHER_S)
+                            and time.time() - t0 < INFLIGHT_GATHER_S
+                            and (LATENCY_BACKLOG <= 0 or backlog() >= LATENCY_BACKLOG))
+                    wait = deadline - time.time()
                     try:
-                        wait = deadline - time.time()
                         if busy:
                             nxt = input_queue.get(timeout=max(wait, 0.0005))
+                        elif wait > 0:
+                            nxt = input_queue.get(timeout=wait)
                         else:
-                            nxt = input_queue.get_nowait() if wait <= 0 else \
-                                input_queue.get(timeout=wait)
+                            nxt = input_queue.get_nowait()
                     except Empty:
                         if busy:
                             continue
-                        break
+                        if backlog() > 0:
+                            # items are queued but the read lost the lock race
+                            # (or the pipe is between two items): wait briefly
+                            try:
+                                nxt = input_queue.get(timeout=CONTENDED_GET_S)
+                            except Empty:
+                                end = "empty_backlog"
+                                break
+                        else:
+                            end = ("busy_timeout" if inflight is not None
+                                   and time.time() - t0 >= INFLIGHT_GATHER_S else
+                                   "wait_timeout" if max_wait_s > 0 else "empty")
+                            break
                     if nxt is None:
                         continue            # end-of-stream wake-up marker
                     if key is not None and nxt[0] is not None and group_key(nxt[2]) != key:
-                        pending.insert(0, nxt)      # other routing class: a later call
-                        if len(pending) > 4 * max_items:
-                            break
-                        continue
+                        # other routing class: it starts a later call (one item
+                        # is parked per call, so `pending` stays bounded and FIFO)
+                        pending.append(nxt)
+                        end = "other_class"
+                        break
                     if nxt[0] is None or rows + rows_of(nxt[0]) > max_rows:
                         pending.append(nxt)
+                        end = "row_cap"
                         break
                     nxt[2].add_gpu(g_idx)
                     nxt[2].record("runner%d_start" % step_idx)
@@ -418,9 +491,11 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 flush_reads()
                 tensor_inputs = tuple(d[:rows] for d in dst)
                 time_card = TimeCardList(cards, item_rows)
-                gstats["calls"] += 1
-                gstats["items"] += len(items)
-                gstats["rows"] += rows
+                st = gstat(phase_of(cards[0].id) if cards else "all")
+                st["calls"] += 1
+                st["items"] += len(items)
+                st["rows"] += rows
+                st["end_" + end] += 1
                 non_tensor_inputs = nts
             elif signal is not None:
                 tensor_inputs = pull(signal, placeholders)
@@ -478,11 +553,15 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                      ", ".join("%s %.0f us" % (k, 1e6 * v / max(1, count["items"]))
                                for k, v in sorted(prof.items(), key=lambda kv: -kv[1]))),
                   flush=True)
-        if gstats["calls"]:
-            print("[runner %d/%d/%d gpu %d] %d batched calls: %.1f items, %.1f rows per call"
-                  % (step_idx, group_idx, instance_idx, g_idx, gstats["calls"],
-                     gstats["items"] / gstats["calls"], gstats["rows"] / gstats["calls"]),
-                  flush=True)
+        for ph, st in sorted(gstats.items()):
+            if st["calls"]:
+                print("[runner %d/%d/%d gpu %d] %s: %d batched calls: %.1f items, %.1f rows per "
+                      "call; ended by %s"
+                      % (step_idx, group_idx, instance_idx, g_idx, ph, st["calls"],
+                         st["items"] / st["calls"], st["rows"] / st["calls"],
+                         ", ".join("%s %d" % (k, st["end_" + k]) for k in GATHER_ENDS
+                                   if st["end_" + k])),
+                      flush=True)
         def _rings(x):
             if isinstance(x, dict):
                 x = list(x.values())
@@ -499,9 +578,20 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                   "events: %d on input rings, %d on the output ring"
                   % (step_idx, group_idx, instance_idx, g_idx, stale, stale_out), flush=True)
         if result_queue is not None:
-            # per-runner transport counters for the launcher's JSON
-            result_queue.put(("ring_stats", step_idx, group_idx, instance_idx,
-                              {"stale_event_waits": int(stale) + int(stale_out)}))
+            # per-runner transport counters for the launcher's JSON; IPC event
+            # waits per edge kind: ordered on the GPU or host fallback
+            stats = {"stale_event_waits": int(stale) + int(stale_out)}
+            for r in _rings(shared_input_rings):
+                hs = getattr(r, "handle_stats", None)
+                if hs is None:
+                    continue
+                edge = "same_gpu" if r.producer_gpu == g_idx else "cross_gpu"
+                for k, v in hs().items():
+                    stats["ipc.%s.%s" % (edge, k)] = stats.get("ipc.%s.%s" % (edge, k), 0) + v
+            for ph, st in gstats.items():
+                for k, v in st.items():
+                    stats["gather.%s.%s" % (ph, k)] = v
+            result_queue.put(("ring_stats", step_idx, group_idx, instance_idx, stats))
         # ---- shutdown
         if not is_final_step:
             try:

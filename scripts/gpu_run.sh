@@ -3,7 +3,7 @@
 # its own time limit and a crash / abort / timeout (rc not 0 or 1) stops the
 # script. Logs go to gpurun_out/<step>.log.
 #
-#   bash scripts/gpu_run.sh tests bench:20 layers:128 x6exp pmc:conv2.blocks.0.conv1.spatial:1018,1050
+#   bash scripts/gpu_run.sh tests bench:20 layers:128 pmc:conv2.blocks.0.conv1.spatial:1018,1050
 #
 # steps:
 #   build                 python -m rnb_amd.build
@@ -13,13 +13,14 @@
 #   benchargs:ARGS        bench.py with extra arguments (commas -> spaces)
 #   layers[:CLIPS]        per-conv table of the fp32 R(2+1)D-34 forward (autotuned)
 #   wino[:CLIPS]          every Winograd variant per layer shape (fp32)
-#   x6exp                 x6 Winograd bottleneck experiments (scripts/x6_exp.py)
-#   x6dexp                x6 direct-conv bottleneck experiments (scripts/x6d_exp.py)
+#   compare[:CLIPS]       per conv: the best config of each kernel family (fp32 / wino / x6 / h3)
 #   bnbreak[:CLIPS]       kernel breakdown of one graphed batch-BN forward (rocprofv3)
 #   pmc:LAYER:CFGS        per-dispatch PMC passes of one conv (scripts/gpu_pmc_conv.sh)
 #   fold:N                bench.py --gpus N through torchrun, all ranks folded onto GPU 0
 #   mfma                  MFMA rate / split-bf16 numerics microbenchmark
 #   repro[:ROUNDS]        interprocess-event wait reproducer (csrc/bench/ipc_event_repro.cpp)
+#   ipcmatrix[:ROUNDS]    which factor decides the IPC-event wait (scripts/ipc_event_matrix.py)
+#   ipcscale              16 rings x 386 slots in one consumer (tests/test_gpu_ipc_scale.py)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -54,10 +55,8 @@ for step in "$@"; do
               --dtype fp32 --autotune ;;
     wino) run wino 400 python scripts/profile_layers.py --depth 34 --clips "${arg:-128}" \
             --dtype fp32 --list-wino --reps 5 ;;
-    x6exp) run x6exp 300 python -u scripts/x6_exp.py run ;;
-    x6dexp) run x6dexp 300 python -u scripts/x6d_exp.py run ;;
-    x6dsweep) run x6dsweep 300 python -u scripts/x6d_exp.py sweep ;;
-    x6dsmall) run x6dsmall 300 python -u scripts/x6d_exp.py small ;;
+    compare) run compare 600 python scripts/profile_layers.py --depth 34 --clips "${arg:-128}" \
+               --dtype fp32 --compare --reps 5 ;;
     bnbreak)
       rm -rf gpurun_out/bnbreak
       run bnbreak 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/bnbreak -o run \
@@ -84,6 +83,10 @@ for step in "$@"; do
             --loaders 1 --json-out gpurun_out/foldl$n.json
           unset RNB_FOLD_GPUS ;;
     repro) run repro 150 bash scripts/ipc_event_repro.sh "${arg:-2000}" ;;
+    ipcmatrix) run ipcmatrix 400 python -u scripts/ipc_event_matrix.py --rounds "${arg:-200}" \
+                 --out gpurun_out/ipc_event_matrix.txt ;;
+    ipcscale) run ipcscale 300 python -u -m pytest tests/test_gpu_ipc_scale.py -v -s \
+                -p no:cacheprovider --timeout 240 --timeout-method thread ;;
     mfma) run mfma 120 python -u scripts/mfma_split.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

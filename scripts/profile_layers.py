@@ -35,7 +35,13 @@ def tile_name(cid, f32=False):
         if cid in WINO_TC:
             return "wino%d%s" % (16 * WINO_TC[cid], "s" if cid in WINO_SPLIT else "")
         from rnb_amd.ops.conv_f32 import (X6D_BASE, X6R_BASE, X6K_BASE, X6K_CONFIGS, is_x6d,
-                                          is_x6r, is_x6k)
+                                          is_x6r, is_x6k, H3D_BASE, H3K_BASE, H3K_CONFIGS,
+                                          is_h3, is_h3k)
+        if is_h3k(cid):
+            return "h3k_%dx%d" % k.h3_configs[H3K_CONFIGS[cid - H3K_BASE]]
+        if is_h3(cid):
+            return "h3_%dx%d%s" % (k.h3_configs[cid - H3D_BASE] +
+                                   ("p4" if cid - H3D_BASE >= 11 else "",))
         if is_x6r(cid):
             return "x6r_%d" % (cid - X6R_BASE)
         if is_x6k(cid):
@@ -47,6 +53,22 @@ def tile_name(cid, f32=False):
         from rnb_amd.ops.conv import SPECIAL_NAMES
         return SPECIAL_NAMES.get(cid, str(cid))
     return "%dx%d%s" % (k.configs[cid] + ("s3" if k.stages[cid] == 3 else "",))
+
+
+def family(cid, f32):
+    """Kernel family of a config id (--compare reports the best of each)."""
+    if not f32:
+        return "best"
+    from rnb_amd.ops.conv_f32 import WINO_X6, WINO_ALL, is_h3, is_x6d
+    if is_h3(cid):
+        return "h3"
+    if is_x6d(cid):
+        return "x6d"
+    if cid in WINO_X6:
+        return "x6wino"
+    if cid in WINO_ALL:
+        return "wino"
+    return "f32"
 
 
 def main():
@@ -156,7 +178,7 @@ def main():
                 e.record()
                 e.synchronize()
                 t = s.elapsed_time(e) / args.reps
-                fam = "best"
+                fam = family(c, f32)
                 if fam not in best or t < best[fam][1]:
                     best[fam] = (c, t)
             rows[-1]["best"] = {k: (tile_name(v[0], f32), v[1]) for k, v in best.items()}

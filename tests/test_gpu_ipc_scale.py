@@ -1,0 +1,119 @@
+"""HIP-IPC slot rings at the 8-GPU ``global`` scale, on one GPU.
+
+At ``bench.py --gpus 8`` with the defaults every runner consumes from the
+rings of 16 loader processes and ``plan_ring_depths`` gives 386 slots per
+ring. A ring is ONE allocation with ONE memory handle (slots are offsets) and
+a consumer opens a producer's "written" event, or creates its own "released"
+event, only on its first use of that slot. This test opens 16 rings x 386
+slots in one consumer process (two producer processes of 8 rings each), pulls
+every slot twice (the second round exercises the producers' waits on the
+consumer's release events), checks every value, and prints the open / pull
+times and the handles the consumer holds.
+"""
+import time
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RINGS, SLOTS, PER_PRODUCER = 16, 386, 8
+
+
+def _producer(rings, q, base, rounds, go):
+    import torch
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(dev)
+    t0 = time.time()
+    with torch.cuda.stream(s):
+        for r in rings:
+            r.producer_attach(dev)
+        q.put(("attached", base, time.time() - t0))
+        for rnd in range(rounds):
+            for k, r in enumerate(rings):
+                for idx in range(SLOTS):
+                    if not r.wait_free(idx):
+                        raise RuntimeError("aborted")
+                    r.begin_write(idx, s)
+                    view = r.slot_views(idx)[0]
+                    view.fill_(float((base + k) * 1000 + idx + rnd * 0.5))
+                    r.commit(idx, [view.shape[0]], s)
+                    q.put((base + k, idx, rnd, r.descriptor()))
+        q.put(("done", base, 0.0))
+        s.synchronize()
+        go.wait(300)            # keep the allocations alive until the consumer is done
+        for r in rings:
+            r.close()
+
+
+def test_ipc_rings_at_8gpu_global_counts():
+    import multiprocessing as mp
+    import torch
+    from rnb_amd.parallel.transport import IpcRing
+    ctx = mp.get_context("spawn")
+    rings = [IpcRing(ctx, ((4, 1024),), (torch.float32,), SLOTS, "scale%d" % i, 0)
+             for i in range(RINGS)]
+    for r in rings:
+        r.set_consumers([(1, 0, 0)])
+    q, go = ctx.Queue(), ctx.Event()
+    rounds = 2
+    procs = [ctx.Process(target=_producer,
+                         args=(rings[b:b + PER_PRODUCER], q, b, rounds, go))
+             for b in range(0, RINGS, PER_PRODUCER)]
+    for p in procs:
+        p.start()
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(dev)
+    out = torch.empty((SLOTS * RINGS * rounds, 4, 1024), device=dev)
+    want = []
+    attach_s, done = [], 0
+    t_first = t0 = None
+    with torch.cuda.stream(s):
+        ta = time.time()
+        for r in rings:
+            r.consumer_attach(dev, (1, 0, 0))
+        consumer_attach_s = time.time() - ta
+        n = 0
+        while done < len(procs):
+            m = q.get(timeout=240)
+            if m[0] == "attached":
+                attach_s.append(m[2])
+                continue
+            if m[0] == "done":
+                done += 1
+                continue
+            ring_i, idx, rnd, desc = m
+            if t0 is None:
+                t0 = time.time()
+            r = rings[ring_i]
+            r.read_into(idx, [out[n]], desc)
+            r.release(idx)
+            want.append(ring_i * 1000 + idx + rnd * 0.5)
+            n += 1
+            if n == RINGS * SLOTS and t_first is None:
+                t_first = time.time() - t0
+        s.synchronize()
+    pull_s = time.time() - t0
+    go.set()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert n == RINGS * SLOTS * rounds
+    got = out[:, 0, 0].cpu()
+    assert torch.equal(got, torch.tensor(want, dtype=torch.float32))
+    assert torch.equal(out.amax(dim=(1, 2)).cpu(), got)
+    stats = {}
+    for r in rings:
+        for k, v in r.handle_stats().items():
+            stats[k] = stats.get(k, 0) + v
+        r.close()
+    # one memory handle per ring; events only for slots actually pulled
+    assert stats["mem_handles_opened"] == RINGS
+    assert stats["events_opened"] == RINGS * SLOTS
+    assert stats["events_created"] == RINGS * SLOTS
+    print("\n[ipc-scale] %d rings x %d slots, %d pulls: producer attach %.2f / %.2f s, "
+          "consumer attach %.3f s, first round (opens + creates) %.2f s, both rounds %.2f s "
+          "(%.0f us per pull); consumer holds %s"
+          % (RINGS, SLOTS, n, attach_s[0], attach_s[-1], consumer_attach_s, t_first, pull_s,
+             1e6 * pull_s / n, stats), flush=True)

@@ -64,8 +64,10 @@ def _rccl_timeout_rank(rank, store_path, ring, out_q):
             ph = [torch.zeros((1, 2))]
             try:
                 from rnb_amd.parallel.rccl_channel import flush_recvs
-                ring.read_into(0, ph, 0)
-                flush_recvs()
+                pending = []
+                ring.read_into(0, ph, 0, pending=pending)
+                assert len(pending) == 1          # queued for the call, not launched
+                flush_recvs(pending)
                 out_q.put(("consumer", "returned"))
             except Exception as err:          # the timeout, not a hang
                 out_q.put(("consumer", type(err).__name__))
