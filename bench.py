@@ -152,6 +152,10 @@ def parse_args(argv=None):
                          "(loader GPU 0 -> runner GPUs over xGMI) and two-stage (RCCL) runs "
                          "reported under cross_gpu")
     ap.add_argument("--cross-gpu-steps", type=int, default=4)
+    ap.add_argument("--time-budget", type=float, default=540.0,
+                    help="seconds the whole bench.py run should stay within: the cross-GPU "
+                         "and literal extras get only what the headline run left (minus "
+                         "30 s for the numerics check and the JSON line)")
     ap.add_argument("--cross-gpu-timeout", type=float, default=330.0,
                     help="total seconds for the cross-GPU extras (all topologies); the "
                          "headline line is printed after them, so keep this bounded")
@@ -276,6 +280,14 @@ def run_pipeline(args, world: int) -> dict:
     res["wall_s"] = time.time() - t0
     res["config_path"] = os.path.relpath(cfg_path, root)
     return res
+
+
+_T_START = time.time()
+
+
+def _budget_left(args) -> float:
+    """Seconds left of --time-budget for extras (30 s kept for the rest)."""
+    return args.time_budget - (time.time() - _T_START) - 30.0
 
 
 def main(argv=None) -> int:
@@ -414,7 +426,7 @@ def run_cross_gpu_extras(args) -> dict:
     # #4 as the reference wires it (loader GPU 0 -> runners on GPUs 1..N-1 ->
     # CPU aggregator); two-stage: RCCL pairs (BASELINE config #3)
     topologies = ["global", "segment-literal"] + (["two-stage"] if args.gpus % 2 == 0 else [])
-    deadline = time.time() + args.cross_gpu_timeout
+    deadline = time.time() + min(args.cross_gpu_timeout, _budget_left(args))
     for topo in topologies:
         budget = deadline - time.time()
         if budget < 45:
@@ -523,7 +535,7 @@ def run_literal_extras(args) -> dict:
                                  "--steps", "2", "--warmup", "1", "--videos-per-step", "128",
                                  "--latency-seconds", "0"])]
     out = {}
-    deadline = time.time() + args.literal_timeout
+    deadline = time.time() + min(args.literal_timeout, _budget_left(args))
     for key, extra in runs:
         budget = deadline - time.time()
         if budget < 30:

@@ -358,6 +358,206 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
                                        NS * BUF);
 }
 
+// ===========================================================================
+// Row-band halo h3 kernel for the stride-1 1x3x3 convs (pad 1), the h3 form of
+// conv_x6r_kernel: a block owns R full output rows of one frame (P = NW * TP
+// * 16 >= R * W pixels) x TC * 16 output channels. Per 32-channel input chunk
+// the (R + 2) x (W + 2) patch is loaded ONCE (optionally normalised by the
+// producer's BatchNorm + ReLU, padding kept at zero), split into fp16 hi / lo
+// and stored as ready-made MFMA B operands: per pixel and channel quad q the
+// 16-B slots [H0 H1] (2 q) and [L0 L1] (2 q + 1), 128 B per pixel, slots
+// permuted by x6r_swz. The 9 taps are 9 GEMM steps on shifted patch pixels
+// with the weights streamed per tap group (LDS-DMA, double-buffered): the
+// gathered activation traffic of the direct kernel drops 9x and the split
+// runs once per input value instead of once per tap.
+template <int NW, int TP, int TC, int HALO_PX, int G, bool ST, bool AFF>
+__global__ __launch_bounds__(64 * NW, 1)
+void conv_h3r_kernel(const ConvF32Params p, const X6DStats st) {
+  constexpr int P_TILE = NW * TP * 16, C_TILE = TC * 16;
+  constexpr int HALO_BYTES = HALO_PX * 128;
+  constexpr int W_BYTES = C_TILE * 128;
+  constexpr int W_TOTAL = C_TILE / 8;
+  constexpr int W_INSTR = (W_TOTAL + NW - 1) / NW;
+  constexpr int NT = 64 * NW;
+  constexpr int ITEMS = (HALO_PX * 4 + NT - 1) / NT;     // (pixel, quad) items per lane
+  static_assert(NT % 4 == 0, "a lane keeps one channel quad");
+  __shared__ __attribute__((aligned(16))) char lds[HALO_BYTES + 2 * G * W_BYTES];
+  char* const wbuf = lds + HALO_BYTES;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int frow = lane & 15, fq = lane >> 4;
+  const int W = p.W, H = p.H, W2 = p.W + 2;
+  const int R = p.ST;                        // rows per band (host: stride field reused)
+  const int bands = (H + R - 1) / R;
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int ctile = wgid % p.n_ctiles;
+  const int band = wgid / p.n_ctiles;
+  const int f = band / bands, r0 = (band - f * bands) * R;
+  const int c0 = ctile * C_TILE;
+  const int p0 = (f * H + r0) * W;                       // first output row (NDHWC)
+  const int m_end = p0 + min(R, H - r0) * W;             // valid rows of this band
+  const int nck = p.Cin_p / 32;
+
+  const x6d_u32x4 wr = x6d_rsrc(p.w, (uint32_t)(p.K_pad / 32) * (uint32_t)p.w_rows * 128u);
+  auto issue_w = [&](int s, int buf) {
+    const uint32_t wbase = ((uint32_t)s * (uint32_t)p.w_rows + (uint32_t)c0) * 128u;
+#pragma unroll
+    for (int j = 0; j < W_INSTR; ++j) {
+      const int instr = (W_TOTAL % NW == 0) ? wave + NW * j : min(wave + NW * j, W_TOTAL - 1);
+      x6d_dma16(wr, wbase + (uint32_t)(instr * 1024 + lane * 16),
+                wbuf + buf * W_BYTES + instr * 1024);
+    }
+  };
+
+  // patch staging: item i = 4 q + quad of the (R + 2) x (W + 2) patch; the
+  // lane's quad is threadIdx.x & 3 for every item (NT % 4 == 0)
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+  const int npx = (R + 2) * W2;
+  const int qd = threadIdx.x & 3;
+  uint32_t src[ITEMS];
+  int dst[ITEMS];
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const int it = threadIdx.x + i * NT;
+    const int q = it >> 2;
+    const int hy = q / W2, hx = q - hy * W2;
+    const int y = r0 - 1 + hy, x = hx - 1;
+    const bool ok = it < 4 * npx && y >= 0 && y < H && x >= 0 && x < W;
+    src[i] = ok ? (uint32_t)((((f * H + y) * W + x) * p.Cin_p + qd * 4) * 4) : X6D_INVALID;
+    dst[i] = it < 4 * npx ? q * 128 : -1;
+  }
+  const float* ssv = nullptr;                // AFF: this frame's video's scale / shift
+  if constexpr (AFF) ssv = st.in_ss + (size_t)st.in_seg[f / p.T] * 2 * p.Cin_p + qd * 4;
+  const float in_scale = st.in_scale;
+  // items in batches of SB (the AFF form keeps the scale / shift live too)
+  constexpr int SB = AFF ? (NW > 8 ? 1 : 2) : ITEMS;
+  auto stage = [&](int chunk) {
+    x6f32x4 sc0, sh0, sc1, sh1;
+    if constexpr (AFF) {
+      const float* ss = ssv + chunk * 32;
+      sc0 = *(const x6f32x4*)ss;
+      sc1 = *(const x6f32x4*)(ss + 16);
+      sh0 = *(const x6f32x4*)(ss + p.Cin_p);
+      sh1 = *(const x6f32x4*)(ss + p.Cin_p + 16);
+    }
+#pragma unroll
+    for (int i0 = 0; i0 < ITEMS; i0 += SB) {
+    x6f32x4 v0[SB], v1[SB];
+#pragma unroll
+    for (int k = 0; k < SB; ++k) {
+      const int i = min(i0 + k, ITEMS - 1);
+      const uint32_t o = src[i] == X6D_INVALID ? X6D_INVALID : src[i] + (uint32_t)(chunk * 128);
+      v0[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0);
+      v1[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, o == X6D_INVALID ? o : o + 64u, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < SB; ++k) {
+      const int i = i0 + k;
+      if (i >= ITEMS || dst[i] < 0) continue;
+      const int q = dst[i] >> 7;
+      x6f32x4 a0 = v0[k], a1 = v1[k];
+      if constexpr (AFF) {
+        const float m = src[i] == X6D_INVALID ? 0.f : in_scale;      // padding stays zero
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a0[j] = fmaxf(fmaf(a0[j], sc0[j], sh0[j]), 0.f) * m;
+          a1[j] = fmaxf(fmaf(a1[j], sc1[j], sh1[j]), 0.f) * m;
+        }
+      } else {
+        a0 *= in_scale;
+        a1 *= in_scale;
+      }
+      uint32_t h[4], l[4];
+      h3_split4(a0, h, l);
+      h3_split4(a1, h + 2, l + 2);
+      char* base = lds + dst[i];
+      *(wu32x4*)(base + (x6r_swz(2 * qd, q) << 4)) = (wu32x4){h[0], h[1], h[2], h[3]};
+      *(wu32x4*)(base + (x6r_swz(2 * qd + 1, q) << 4)) = (wu32x4){l[0], l[1], l[2], l[3]};
+    }
+    }
+  };
+
+  // this lane's output pixel of tile tp -> patch pixel at tap (0, 0)
+  int pq[TP];
+#pragma unroll
+  for (int tp = 0; tp < TP; ++tp) {
+    const int pp = (wave * TP + tp) * 16 + frow;
+    const int py = pp / W;
+    pq[tp] = pp < R * W ? py * W2 + (pp - py * W) : 0;     // past the band: never stored
+  }
+
+  x6f32x4 acc[TP][TC];
+#pragma unroll
+  for (int b = 0; b < TC; ++b) {
+    const int c = c0 + b * 16 + 4 * fq;
+    const float4 b4 = *(const float4*)(p.bias + c);
+    const x6f32x4 bv = (x6f32x4){b4.x, b4.y, b4.z, b4.w} * st.acc_scale;
+#pragma unroll
+    for (int a = 0; a < TP; ++a) acc[a][b] = bv;
+  }
+  const int w_hh = x6_chunk(2 * fq, frow) << 4, w_ll = x6_chunk(2 * fq + 1, frow) << 4;
+
+  // steps in (chunk, tap) order, weight step s = tap * nck + chunk, in sync
+  // groups of G taps: one wait + barrier per group (conv_x6r_kernel)
+  constexpr int NG = (9 + G - 1) / G;
+  auto issue_group = [&](int c, int g, int half) {
+    for (int j = 0; j < G && g * G + j < 9; ++j) issue_w((g * G + j) * nck + c, half * G + j);
+  };
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  issue_group(0, 0, 0);
+  int half = 0;
+  for (int c = 0; c < nck; ++c) {
+    stage(c);
+    x6d_wait_vm<0>();
+    x6d_barrier();
+#pragma unroll 1
+    for (int g = 0; g < NG; ++g) {
+      if (g + 1 < NG) issue_group(c, g + 1, half ^ 1);
+      else if (c + 1 < nck) issue_group(c + 1, 0, half ^ 1);
+      for (int j = 0; j < G && g * G + j < 9; ++j) {
+        const int t = g * G + j;
+        const int toff = (t / 3) * W2 + (t % 3);
+        H3B bf[TP];
+#pragma unroll
+        for (int tp = 0; tp < TP; ++tp) {
+          const int q = pq[tp] + toff;
+          const char* base = lds + q * 128;
+          bf[tp].h = *(const wu32x4*)(base + (x6r_swz(2 * fq, q) << 4));
+          bf[tp].l = *(const wu32x4*)(base + (x6r_swz(2 * fq + 1, q) << 4));
+        }
+        const char* wb = wbuf + (half * G + j) * W_BYTES;
+#pragma unroll
+        for (int tc = 0; tc < TC; ++tc) {
+          const char* wrow = wb + (tc * 16 + frow) * 128;
+          const wu32x4 ah = *(const wu32x4*)(wrow + w_hh);
+          const wu32x4 al = *(const wu32x4*)(wrow + w_ll);
+#pragma unroll
+          for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(al, bf[tp].h, acc[tp][tc]);
+#pragma unroll
+          for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(ah, bf[tp].l, acc[tp][tc]);
+#pragma unroll
+          for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(ah, bf[tp].h, acc[tp][tc]);
+        }
+      }
+      x6d_wait_vm<0>();             // the next group's weights landed (this wave) ...
+      x6d_barrier();                // ... in every wave; this group's LDS reads are done
+      half ^= 1;
+    }
+  }
+  const float out_scale = st.out_scale;
+#pragma unroll
+  for (int tp = 0; tp < TP; ++tp)
+#pragma unroll
+    for (int tc = 0; tc < TC; ++tc) acc[tp][tc] *= out_scale;
+  x6d_epilogue<TP, TC, NW, C_TILE, ST>(p, st, acc, p0, m_end, p0 + P_TILE, c0, wave, 0, lane,
+                                       lds, HALO_BYTES + 2 * G * W_BYTES);
+}
+
 // ---------------------------------------------------------------------------
 // host side: config table + launcher (C ABI, ctypes)
 // ---------------------------------------------------------------------------
@@ -474,6 +674,85 @@ int rnb_conv_h3_launch(const ConvF32Params* pp, int config_id, hipStream_t strea
   hipLaunchKernelGGL(aff ? (sums ? cfg.kernel_aff_st : cfg.kernel_aff)
                          : (sums ? cfg.kernel_st : cfg.kernel),
                      dim3((unsigned)blocks), dim3(cfg.threads), 0, stream, p, st);
+  return (int)hipGetLastError();
+}
+
+// Row-band halo h3 kernel (conv_h3r_kernel): 1x3x3 stride 1 pad 1 with
+// Cin_p % 32 == 0. Variants as rnb_conv_x6r_launch: 0 = 7 waves x 4 tiles
+// (448 px), 1 = 14 waves x 2 tiles, 2 = 7 waves x 3 tiles (336 px), 3 / 4 / 5
+// = 0 / 1 / 2 with 2 taps per barrier; 144 channels per block.
+struct ConvH3RConfig {
+  int nw, tp, halo_px;
+  void (*kernel)(const ConvF32Params, const X6DStats);
+  void (*kernel_st)(const ConvF32Params, const X6DStats);
+  void (*kernel_aff)(const ConvF32Params, const X6DStats);
+  void (*kernel_aff_st)(const ConvF32Params, const X6DStats);
+};
+#define H3RCFG(NW, TP, HALO, G)                                                    \
+  {NW, TP, HALO, conv_h3r_kernel<NW, TP, 9, HALO, G, false, false>,                \
+   conv_h3r_kernel<NW, TP, 9, HALO, G, true, false>,                               \
+   conv_h3r_kernel<NW, TP, 9, HALO, G, false, true>,                               \
+   conv_h3r_kernel<NW, TP, 9, HALO, G, true, true>}
+static const ConvH3RConfig kH3RConfigs[] = {
+    H3RCFG(7, 4, 600, 1), H3RCFG(14, 2, 600, 1), H3RCFG(7, 3, 480, 1),
+    H3RCFG(7, 4, 600, 2), H3RCFG(14, 2, 600, 2), H3RCFG(7, 3, 480, 2),
+};
+
+int rnb_conv_h3r_num_variants() { return (int)(sizeof(kH3RConfigs) / sizeof(kH3RConfigs[0])); }
+
+// band rows of a variant for frame width W (0: the variant cannot run it)
+static int h3r_rows(const ConvH3RConfig& cfg, int H, int W) {
+  const int R = cfg.nw * cfg.tp * 16 / W;
+  return (R >= 1 && (R + 2) * (W + 2) <= cfg.halo_px) ? R : 0;
+}
+
+int rnb_conv_h3r_launch(const ConvF32Params* pp, int variant, hipStream_t stream, double* sums,
+                        const int* clip_seg, int stats_c, float in_scale, float out_scale,
+                        const float* in_ss, const int* in_seg) {
+  if (variant < 0 || variant >= rnb_conv_h3r_num_variants()) return -1;
+  ConvF32Params p = *pp;
+  const ConvH3RConfig& cfg = kH3RConfigs[variant];
+  if (p.KT != 1 || p.KH != 3 || p.KW != 3 || p.PH != 1 || p.PW != 1 || p.PT != 0) return -2;
+  if (p.SH != 1 || p.SW != 1 || p.ST != 1 || p.Cin_p % 32 != 0 || p.Cout_p % 4 != 0) return -2;
+  if (p.K_pad < 9 * p.Cin_p || p.K_pad % 32 != 0) return -3;
+  if (p.M <= 0) return 0;
+  if (p.y_stride < p.Cout_p || p.y_stride % 4 != 0 || (p.res && (p.res_stride < p.Cout_p ||
+                                                               p.res_stride % 4 != 0)))
+    return -4;
+  const long long xb = (long long)p.N * p.T * p.H * p.W * p.Cin_p * 4;
+  if (xb > 0x7FFFFF00LL || (long long)p.M * p.y_stride * 4 > 0x7FFFFF00LL) return -5;
+  if (p.res && (long long)p.M * p.res_stride * 4 > 0x7FFFFF00LL) return -6;
+  const int R = h3r_rows(cfg, p.H, p.W);
+  if (R == 0) return -13;
+  if ((long long)(p.K_pad / 32) * p.w_rows * 128 > 0x7FFFFF00LL) return -11;
+  if (!(in_scale > 0.f) || !(out_scale > 0.f)) return -15;
+  if (in_ss && !in_seg) return -16;
+  p.x_bytes = (uint32_t)xb;
+  f32_magic_div((uint32_t)p.Wo, &p.mWo, &p.sWo);
+  f32_magic_div((uint32_t)p.Ho, &p.mHo, &p.sHo);
+  f32_magic_div((uint32_t)p.To, &p.mTo, &p.sTo);
+  p.ST = R;                                    // rows per band (read by the kernel)
+  const int bands = (p.H + R - 1) / R;
+  p.n_ctiles = (p.Cout_p + 143) / 144;
+  if (p.n_ctiles * 144 > p.w_rows) return -8;
+  const long long blocks = (long long)p.N * p.T * bands * p.n_ctiles;
+  if (blocks > 0x7FFFFFFF) return -7;
+  if (sums && (!clip_seg || stats_c < p.Cout_p)) return -12;
+  X6DStats st;
+  st.sums = sums;
+  st.clip_seg = clip_seg;
+  st.stats_c = stats_c;
+  st.ksplit = 1;
+  st.ws = nullptr;
+  st.in_scale = in_scale;
+  st.out_scale = out_scale;
+  st.acc_scale = 1.f / out_scale;
+  st.in_ss = in_ss;
+  st.in_seg = in_seg;
+  const bool aff = in_ss != nullptr;
+  hipLaunchKernelGGL(aff ? (sums ? cfg.kernel_aff_st : cfg.kernel_aff)
+                         : (sums ? cfg.kernel_st : cfg.kernel),
+                     dim3((unsigned)blocks), dim3(64 * cfg.nw), 0, stream, p, st);
   return (int)hipGetLastError();
 }
 

@@ -356,9 +356,6 @@ __global__ __launch_bounds__(512) void x6d_splitk_reduce_kernel(const ConvF32Par
 // step (LDS-DMA, double-buffered, counted vmcnt + raw barrier).
 // Patch pixel q's 16-B slots are XOR-permuted by g(q) = [5,6,4,1,0,7,3,0][q & 7]
 // (searched: conflict-free ds_read_b128 for any 16 consecutive pixels).
-static __device__ __forceinline__ int x6r_swz(int slot, int q) {
-  return slot ^ ((0x03701465 >> (4 * (q & 7))) & 7);
-}
 
 template <int NW, int TP, int TC, int HALO_PX, int G, bool ST>
 __global__ __launch_bounds__(64 * NW, 1)

@@ -66,6 +66,13 @@ struct X6DStats {
   const int* in_seg;
 };
 
+// 16-B slot permutation of row-band halo patch pixels (conv_x6r_kernel,
+// conv_h3r_kernel): pixel q's slots XOR g(q) = [5,6,4,1,0,7,3,0][q & 7]
+// (searched: conflict-free ds_read_b128 for any 16 consecutive pixels)
+static __device__ __forceinline__ int x6r_swz(int slot, int q) {
+  return slot ^ ((0x03701465 >> (4 * (q & 7))) & 7);
+}
+
 // split-K finish (conv_x6.hip): the ksplit raw partials in st.ws + bias (+
 // residual) (ReLU) -> p.y, plus the BN sums; shared by the x6 and h3 kernels
 extern "C" int rnb_x6d_splitk_reduce(const ConvF32Params* p, const X6DStats* st,

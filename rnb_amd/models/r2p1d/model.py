@@ -327,15 +327,18 @@ class R2P1DLoader(RunnerModel):
         if device.type == "cuda":
             torch.cuda.current_stream(device).synchronize()
 
-    def load(self, path: str, out: Optional[torch.Tensor] = None, time_card=None):
+    def _sample(self, path: str, time_card=None):
+        """(video id, clip start frames) of ``path``; tags sampled requests
+        with what a numerics check needs to decode the same clips again."""
         vid, length = self.decoder.probe(path)
-        starts = self.sampler.sample(length) or []
-        if len(starts) > self.max_clips:
-            starts = starts[:self.max_clips]
+        starts = (self.sampler.sample(length) or [])[:self.max_clips]
         if time_card is not None and (time_card.id % CHECK_EVERY == 0 or (
                 len(starts) >= 15 and time_card.id % CHECK_EVERY_LARGE == 0)):
-            # what a numerics check needs to decode the same clips again
             time_card.extra["clip_src"] = (int(vid), [int(s) for s in starts])
+        return vid, starts
+
+    def load(self, path: str, out: Optional[torch.Tensor] = None, time_card=None):
+        vid, starts = self._sample(path, time_card)
         return self.decoder.decode(vid, starts, out=None if out is None else
                                    out[:len(starts)])
 
@@ -350,6 +353,24 @@ class R2P1DLoader(RunnerModel):
         frames = self.load(non_tensors, out=out[0], time_card=time_card)
         time_card.num_clips = int(frames.shape[0])
         return (frames,), None, time_card
+
+    def call_into_segments(self, tensors, non_tensors, time_card, outs):
+        """Segment-parallel producer (``num_segments`` = len(outs)): decode
+        each segment's clips (the reference's row split, runner.py:149-151)
+        straight into its own output slot ``outs[k][0]``; returns the rows per
+        segment (runner.py direct_seg: no staging tensor, no slot copy;
+        SURVEY.md K31). The synthetic decoder renders a clip from (video,
+        start frame) only, so the segments equal the split of one decode."""
+        from ...control import segment_bounds
+        vid, starts = self._sample(non_tensors, time_card)
+        rows = []
+        for k, out in enumerate(outs):
+            a, b = segment_bounds(len(starts), len(outs), k)
+            if b > a:
+                self.decoder.decode(vid, starts[a:b], out=out[0][:b - a])
+            rows.append(b - a)
+        time_card.num_clips = len(starts)
+        return rows, None, time_card
 
     def input_shape(self):
         return None

@@ -137,6 +137,9 @@ def is_x6k(cid: int) -> bool:
 H3D_BASE = 1300
 H3K_BASE = 1350
 H3K_CONFIGS = (2, 4, 5, 9, 10)
+# row-band halo h3 kernel (csrc/conv_h3.hip conv_h3r_kernel): 1x3x3 stride 1
+# pad 1 with Cin_p % 32 == 0, variant H3R_BASE + v of rnb_conv_h3r_launch
+H3R_BASE = 1380
 # activations are split after scaling by 2^H3_IN_LOG2: fp16 lo parts stay
 # normal for |a| >= 2^-9 and inputs up to 2^10 stay in the fp16 range
 H3_IN_LOG2 = 6
@@ -147,7 +150,12 @@ H3_W_TOP_LOG2 = 13
 def is_h3(cid: int) -> bool:
     from .native import kernels
     return ((H3D_BASE <= cid < H3D_BASE + len(kernels().h3_configs))
-            or H3K_BASE <= cid < H3K_BASE + len(H3K_CONFIGS))
+            or H3K_BASE <= cid < H3K_BASE + len(H3K_CONFIGS) or is_h3r(cid))
+
+
+def is_h3r(cid: int) -> bool:
+    from .native import kernels
+    return H3R_BASE <= cid < H3R_BASE + kernels().h3r_variants
 
 
 def is_h3k(cid: int) -> bool:
@@ -465,6 +473,9 @@ class ConvLayerF32:
                       if self.ksplit_for(X6K_BASE + j, x_shape) > 1]
         if h3_enabled():
             c += [H3D_BASE + i for i in range(len(kernels().h3_configs))]
+            if self.h3r_ok(x_shape):
+                c += [H3R_BASE + i for i in range(kernels().h3r_variants)
+                      if self.h3r_fits(i, x_shape)]
             if x_shape is not None and os.environ.get("RNB_X6K", "1") != "0":
                 c += [H3K_BASE + j for j in range(len(H3K_CONFIGS))
                       if self.ksplit_for(H3K_BASE + j, x_shape) > 1]
@@ -672,9 +683,27 @@ class ConvLayerF32:
             self._config[key] = cid
         return cid
 
+    def h3r_ok(self, x_shape=None) -> bool:
+        """The row-band h3 kernel takes 1x3x3 stride-1 pad-1 convs over
+        32-channel chunks."""
+        return self.wino_ok and self.geom.cin_p % 32 == 0
+
+    def h3r_fits(self, variant: int, x_shape, efficient: bool = True) -> bool:
+        """Whether variant ``variant``'s band (P pixels // W rows, halo of
+        (rows + 2) x (W + 2) pixels) fits frames of width W, and (when
+        ``efficient``) its band uses at least half of the block's pixels."""
+        if x_shape is None:
+            return True
+        _, T, H, W, _ = x_shape
+        nw, tp, halo = ((7, 4, 600), (14, 2, 600), (7, 3, 480))[variant % 3]
+        rows = nw * tp * 16 // W
+        if rows < 1 or (rows + 2) * (W + 2) > halo:
+            return False
+        return not efficient or 2 * min(rows, H) * W >= nw * tp * 16
+
     def affine_ok(self, cid: int, x_shape) -> bool:
         """Whether config ``cid`` can apply the input's BN + ReLU on load."""
-        if cid in WINO_TEMPORAL:
+        if cid in WINO_TEMPORAL or is_h3r(cid):
             return True
         if not is_h3(cid):
             return False
@@ -727,7 +756,17 @@ class ConvLayerF32:
         h3 = is_h3(cid)
         for n0 in range(0, N, step):
             p = self.params(x, y, residual, n0, min(N, n0 + step), x6=x6 and not h3, h3=h3)
-            if h3:
+            if is_h3r(cid):
+                _, _, s_in, s_out = self.h3d_buffers()
+                aff = ((in_affine[0].data_ptr(), in_affine[1].data_ptr() + 4 * n0)
+                       if in_affine is not None else (0, 0))
+                if out_stats is not None:
+                    k.conv_h3r(p, cid - H3R_BASE, stream.cuda_stream, s_in, s_out,
+                               out_stats[0].data_ptr(), out_stats[1].data_ptr() + 4 * n0,
+                               out_stats[0].shape[2], *aff)
+                else:
+                    k.conv_h3r(p, cid - H3R_BASE, stream.cuda_stream, s_in, s_out, 0, 0, 0, *aff)
+            elif h3:
                 _, _, s_in, s_out = self.h3d_buffers()
                 ks, ws = 1, None
                 conf = cid - H3D_BASE

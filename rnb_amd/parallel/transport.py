@@ -183,6 +183,23 @@ class HostRing(RingBase):
         self._set_valid(idx, rows)
         return self._publish(idx)
 
+    @property
+    def direct_writes(self) -> bool:
+        """A CPU producer may write its output into the slot itself
+        (``slot_views`` / ``commit``); a GPU producer's kernels cannot write
+        host shared memory, so it goes through ``write``."""
+        return self.producer_gpu < 0
+
+    def slot_views(self, idx: int):
+        return self.slots[idx]
+
+    def begin_write(self, idx: int, stream=None) -> None:
+        pass
+
+    def commit(self, idx: int, rows, stream=None) -> int:
+        self._set_valid(idx, rows)
+        return self._publish(idx)
+
     def read_into(self, idx, placeholders, descriptor=None):
         out = []
         for ph, src, b in zip(placeholders, self.slots[idx], self.valid_rows(idx)):

@@ -155,9 +155,15 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         adaptive_gather = os.environ.get("RNB_ADAPTIVE_GATHER", "1") == "1"
         inflight = None             # completion event of this replica's last batch
         # producer writes straight into its output slot (no staging copy)
-        direct_out = (shared_output_ring is not None and num_segments == 1
-                      and callable(getattr(model, "call_into", None))
-                      and callable(getattr(shared_output_ring, "slot_views", None)))
+        direct_ok = (shared_output_ring is not None
+                     and callable(getattr(shared_output_ring, "slot_views", None))
+                     and getattr(shared_output_ring, "direct_writes", True))
+        direct_out = (direct_ok and num_segments == 1
+                      and callable(getattr(model, "call_into", None)))
+        # segment-parallel producer writing each segment straight into its own
+        # slot (RunnerModel.call_into_segments: no staging tensor, no copy)
+        direct_seg = (direct_ok and num_segments > 1
+                      and callable(getattr(model, "call_into_segments", None)))
 
         placeholders = None
         if shared_input_rings is not None:
@@ -198,15 +204,18 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         sync_each = is_final_step or shared_output_ring is None or \
             not shared_output_ring.gpu_ordered or os.environ.get("RNB_STAGE_SYNC") == "1"
 
-        def emit(outputs, slot=None):
+        def emit(outputs, slot=None, seg_slots=None):
             """Route one model output; False means stop the runner loop.
-            ``slot``: the output slot the model already wrote (direct_out)."""
+            ``slot``: the output slot the model already wrote (direct_out);
+            ``seg_slots``: [(slot, rows)] of the segments it wrote (direct_seg)."""
             tensor_outputs, non_tensor_outputs, time_card = outputs
             if stream is not None and sync_each:
                 stream.synchronize()
             if time_card is None:
                 if slot is not None:
                     shared_output_ring.release(slot)    # nothing written
+                for sl, _ in seg_slots or ():
+                    shared_output_ring.release(sl)
                 return True
             time_card.record("inference%d_finish" % step_idx)
             if is_final_step:
@@ -235,6 +244,12 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             out_q = output_queues[selector.select(tensor_outputs, non_tensor_outputs,
                                                   time_card)]
             msgs = []
+            for seg, (sl, rows) in enumerate(seg_slots or ()):
+                # segments the model already wrote into their slots
+                gen = shared_output_ring.commit(sl, [rows] * len(shared_output_ring.shapes))
+                signal_out = Signal(group_idx, instance_idx, sl, shared_output_ring.descriptor(),
+                                    gen if shared_output_ring.check else None)
+                msgs.append((signal_out, non_tensor_outputs, time_card.fork(seg)))
             if slot is not None:
                 gen = shared_output_ring.commit(slot, [t.shape[0] for t in tensor_outputs])
                 state["out_counter"] = (state["out_counter"] + 1) % len(shared_output_ring)
@@ -242,7 +257,7 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                                     shared_output_ring.descriptor(),
                                     gen if shared_output_ring.check else None)
                 msgs.append((signal_out, non_tensor_outputs, time_card))
-            for seg in range(num_segments if slot is None else 0):
+            for seg in range(num_segments if slot is None and seg_slots is None else 0):
                 signal_out = None
                 if shared_output_ring is not None:
                     seg_tensors = []
@@ -518,6 +533,26 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 if stream is not None and adaptive_gather:
                     inflight = torch.cuda.Event()
                     inflight.record(stream)
+                tick("emit")
+                continue
+            if direct_seg:
+                slots = []
+                for _ in range(num_segments):
+                    sl = state["out_counter"] % len(shared_output_ring)
+                    if not shared_output_ring.wait_free(sl, aborted):
+                        break
+                    shared_output_ring.begin_write(sl, stream)
+                    slots.append(sl)
+                    state["out_counter"] = (state["out_counter"] + 1) % len(shared_output_ring)
+                if len(slots) < num_segments:
+                    break
+                tick("slot_wait")
+                rows, nts, tc = model.call_into_segments(
+                    tensor_inputs, non_tensor_inputs, time_card,
+                    [shared_output_ring.slot_views(sl) for sl in slots])
+                tick("model")
+                if not emit((None, nts, tc), seg_slots=list(zip(slots, rows))):
+                    break
                 tick("emit")
                 continue
             if direct_out:

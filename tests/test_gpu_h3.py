@@ -196,3 +196,72 @@ def test_h3_input_bn_on_load_matches_separate_apply(k, s, p, thw, cin, n):
             torch.cuda.synchronize()
             err = (y[..., :144].double().cpu() - ref).abs().max().item()
             assert err <= 1e-5 * scale, (cid, ost is not None, err, scale)
+
+
+def _h3r_ids():
+    from rnb_amd.ops.conv_f32 import H3R_BASE
+    from rnb_amd.ops.native import kernels
+    return [H3R_BASE + i for i in range(kernels().h3r_variants)]
+
+
+@pytest.mark.parametrize("thw", [(2, 15, 13), (3, 56, 56), (2, 28, 28), (1, 7, 7)])
+def test_h3_rowband_exact_integers_stats_and_affine(thw):
+    """Row-band halo h3 kernel (conv_h3r_kernel): bit-exact on small integers
+    (bands of whole rows, partial last band, 3x3 padding at frame edges,
+    residual + ReLU epilogue) for every variant whose band fits the frame;
+    epilogue BN sums vs fp64; the input BN + ReLU on load (one video per
+    frame, padding kept at zero) within 1e-5 of the fp64 conv of the
+    applied input."""
+    layer = _layer(64, 150, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=True, integer=True)
+    x = _input(2, thw, 64, 64, integer=True)
+    res = _input(2, thw, layer.geom.cout_p, 150, integer=True, seed=3)
+    ref = _ref64(layer, x, res).float()
+    ids = [c for c in _h3r_ids() if layer.h3r_fits(c - _h3r_ids()[0], x.shape, efficient=False)]
+    if not ids:
+        pytest.skip("no row-band variant fits %s" % (thw,))
+    for cid in ids:
+        y = layer.forward_hip(x, res, config=cid)
+        torch.cuda.synchronize()
+        assert torch.equal(y[..., :150].cpu(), ref), cid
+    lay2 = _layer(64, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False)
+    xf = _input(3, thw, 64, 64)
+    seg = torch.tensor([0, 2, 2], dtype=torch.int32, device=DEV)
+    g = torch.Generator().manual_seed(9)
+    ss = torch.empty((3, 2, 64), dtype=torch.float32)
+    ss[:, 0] = torch.rand((3, 64), generator=g) + 0.5
+    ss[:, 1] = torch.randn((3, 64), generator=g) * 0.5
+    ss = ss.to(DEV)
+    xa = torch.relu(xf * ss[seg.long(), 0][:, None, None, None, :] +
+                    ss[seg.long(), 1][:, None, None, None, :])
+    ref_a = _ref64(lay2, xa)
+    scale = ref_a.abs().max().item()
+    for cid in ids:
+        sums = torch.zeros((3, 2, lay2.geom.cout_p), dtype=torch.float64, device=DEV)
+        y = lay2.forward_hip(xf, config=cid, out_stats=(sums, seg))
+        torch.cuda.synchronize()
+        yd = y[..., :144].double().cpu()
+        for v, (a, b) in enumerate([(0, 1), (1, 1), (1, 3)]):
+            part = yd[a:b].reshape(-1, 144)
+            got = sums[v, :, :144].cpu()
+            assert ((got[0] - part.sum(0)).abs() <= 1e-6 * part.abs().sum(0) + 1e-9).all()
+            assert torch.allclose(got[1], (part * part).sum(0), rtol=1e-6, atol=1e-9)
+        ya = lay2.forward_hip(xf, config=cid, in_affine=(ss, seg))
+        torch.cuda.synchronize()
+        err = (ya[..., :144].double().cpu() - ref_a).abs().max().item()
+        assert err <= 1e-5 * scale, (cid, err, scale)
+
+
+@pytest.mark.parametrize("case", [c for c in F32_CASES if c[2] == (1, 3, 3) and c[3] == (1, 1, 1)],
+                         ids=lambda c: "%dx%d" % (c[0], c[1]))
+def test_h3_rowband_matches_fp64(case):
+    cin, cout, k, s, p, thw = case
+    layer = _layer(cin, cout, k, s, p)
+    x = _input(2, thw, layer.geom.cin_p, cin)
+    ref = _ref64(layer, x)
+    scale = ref.abs().max().item()
+    ids = [c for c in _h3r_ids() if layer.h3r_fits(c - _h3r_ids()[0], x.shape)]
+    for cid in ids:
+        y = layer.forward_hip(x, config=cid)
+        torch.cuda.synchronize()
+        err = (y[..., :cout].double().cpu() - ref).abs().max().item()
+        assert err <= 1e-5 * scale, (cid, err, scale)
