@@ -84,6 +84,13 @@ def parse_args(argv=None):
                          "replicas per GPU with a queue per GPU -- at 1 GPU the same "
                          "topology as global (one shared queue), at N GPUs no slot "
                          "crosses xGMI; global shares one queue across all GPUs")
+    ap.add_argument("--route", default="none", choices=["none", "large-small"],
+                    help="(aggressive) large-small: the reference's content routing "
+                         "(config/rnb.json, models/r2p1d/model.py:288-296) -- 15-clip videos "
+                         "go to their own queue and runner replica per GPU "
+                         "(--large-replicas), the others batch among themselves")
+    ap.add_argument("--large-replicas", type=int, default=1,
+                    help="(--route large-small) runner replicas per GPU for 15-clip videos")
     ap.add_argument("--segments", type=int, default=None,
                     help="(segment) segments per video (default min(4, GPUs), >= 2)")
     ap.add_argument("--segment-layout", default="spread", choices=["spread", "literal"],
@@ -180,6 +187,17 @@ def pipeline_config(args, n_gpus: int) -> dict:
     if args.pipeline == "global":
         steps = [{"model": LOADER, "queue_groups": [{"gpus": loader_gpus, "out_queues": [0]}]},
                  dict(runner, queue_groups=[{"gpus": runner_gpus, "in_queue": 0}])]
+    elif args.pipeline == "aggressive" and args.route == "large-small":
+        # per GPU: queue 2g (1-clip videos, batched) and 2g + 1 (15-clip videos)
+        nl = max(1, min(args.large_replicas, args.replicas - 1))
+        steps = [{"model": LOADER,
+                  "queue_groups": [{"gpus": [g] * args.loaders, "out_queues": [2 * g, 2 * g + 1],
+                                    "queue_selector":
+                                        "rnb_amd.models.r2p1d.model.LargeSmallSelector"}
+                                   for g in gpus]},
+                 dict(runner, queue_groups=[q for g in gpus for q in (
+                     {"gpus": [g] * (args.replicas - nl), "in_queue": 2 * g},
+                     {"gpus": [g] * nl, "in_queue": 2 * g + 1})])]
     elif args.pipeline == "aggressive":
         steps = [{"model": LOADER,
                   "queue_groups": [{"gpus": [g] * args.loaders, "out_queues": [g]}
@@ -354,6 +372,7 @@ def main(argv=None) -> int:
                        "parallelism": "rnb pipeline: %d loader + %d runner processes per GPU"
                                       % (args.loaders, args.replicas),
                        "pipeline": args.pipeline, "launcher_config": res.get("config_path"),
+                       "route": args.route,
                        "bn": ("eval (folded into the convs in fp64)" if args.bn == "eval" else
                               "batch (training-mode BN as the reference, per-video "
                               "statistics)"),

@@ -20,6 +20,15 @@
 //
 //   hipcc --offload-arch=gfx950 -O2 csrc/bench/ipc_event_repro.cpp -o ipc_event_repro
 //   ./ipc_event_repro [rounds]        (scripts/ipc_event_repro.sh)
+//
+// Finding (round 4, scripts/ipc_event_matrix.py, profiles/r4_ipc_event_matrix.txt):
+// the waits this program sees accepted are exactly the event's first 32
+// records ("done": 32 of 2000; "pending"/"burst" run after them: 0). The
+// process start method, stream kind, torch context and an IPC event of the
+// waiting process's own change nothing. The slot rings record each slot's
+// event only a few times per run, which is why they never saw a refusal;
+// they now replace every slot event after 30 records
+// (parallel/transport.py EVENT_ROTATE) so long runs stay GPU-ordered too.
 #include <hip/hip_runtime.h>
 #include <sys/wait.h>
 #include <unistd.h>

@@ -237,6 +237,12 @@ def device_view(ptr: int, shape, dtype, device) -> torch.Tensor:
 
 
 HIP_ERROR_NOT_READY = 600
+# records per interprocess event before it is replaced: ROCm accepts
+# hipStreamWaitEvent on an opened IPC event only for the event's first 32
+# records (scripts/ipc_event_matrix.py, profiles/r4_ipc_event_matrix.txt:
+# exactly 32 of 200 accepted in every process / stream / context variant), so
+# every slot event is recreated (and its handle republished) after this many
+EVENT_ROTATE = int(os.environ.get("RNB_IPC_EVENT_ROTATE", "30"))
 
 
 class IpcRing(RingBase):
@@ -258,6 +264,13 @@ class IpcRing(RingBase):
     The host flags only carry "who may touch the slot next"; the data
     dependencies are GPU-to-GPU waits, so neither side blocks on the other's
     kernels. ``RNB_RING_ORDER=host`` restores host-synchronised copies.
+
+    ROCm refuses stream waits on an opened IPC event after its 32nd record,
+    so both kinds of event are replaced every EVENT_ROTATE records: the owner
+    creates a new event, writes its handle into the slot's shared-memory
+    entry and bumps the slot's epoch before the record that the other side
+    will wait on; the other side re-opens the handle when the epoch changed.
+    A refused wait still falls back to the host (``_wait_ipc_event``).
     """
 
     kind = "ipc"
@@ -279,6 +292,9 @@ class IpcRing(RingBase):
         self._ctx = ctx
         self.released_by = ctx.Array("i", [-1] * self.num_slots, lock=False)
         self.rel_handles = None    # set by set_consumers (before spawn)
+        # "written" event handle and epoch per slot (producer-owned, rotated)
+        self.wev_handles = ctx.Array("c", self.num_slots * EVENT_HANDLE_BYTES, lock=False)
+        self.wev_epoch = ctx.Array("i", self.num_slots, lock=False)
         # the producer's import descriptor (mem + event handles of every slot,
         # ~25 KB for a deep ring) is published once in shared memory; queue
         # signals carry only the small token (name, producer pid)
@@ -289,11 +305,12 @@ class IpcRing(RingBase):
         self.order = os.environ.get(ORDER_ENV, "event")
         # per process
         self._wev = None           # producer: written events [slot]
+        self._wrec = None          # producer: records of each written event
+        self._rrec = None          # consumer: records of each release event
         self._rel_open: Dict[int, List[Optional[int]]] = {}   # producer: cid -> events
         self._cid = None           # consumer id of this process
         self._rev = None           # consumer: own release events [slot]
         self._wopen: Dict[Tuple, List[Optional[int]]] = {}    # consumer: opened written events
-        self._whandles: Dict[Tuple, tuple] = {}               # consumer: their handles
         self._opened_base: Dict[Tuple, int] = {}              # consumer: opened allocations
         self.events_opened = 0
         self.events_created = 0
@@ -309,10 +326,10 @@ class IpcRing(RingBase):
         n = max(1, len(self.consumers))
         self.rel_handles = self._ctx.Array("c", n * self.num_slots * EVENT_HANDLE_BYTES,
                                            lock=False)
-        # per (consumer, slot): 1 once that consumer's release event of the
-        # slot is created and its handle published (consumers create them
-        # on their first release of the slot)
-        self.rel_ready = self._ctx.Array("b", n * self.num_slots, lock=False)
+        # per (consumer, slot): epoch of that consumer's release event of the
+        # slot (0 = none yet; created on its first release, replaced every
+        # EVENT_ROTATE records), the handle in rel_handles
+        self.rel_epoch = self._ctx.Array("i", n * self.num_slots, lock=False)
 
     def __getstate__(self):
         st = dict(self.__dict__)
@@ -321,10 +338,11 @@ class IpcRing(RingBase):
         st["_opened"] = {}
         st["_ctx"] = None
         st["_wev"] = None
+        st["_wrec"] = None
+        st["_rrec"] = None
         st["_rel_open"] = {}
         st["_rev"] = None
         st["_wopen"] = {}
-        st["_whandles"] = {}
         st["_opened_base"] = {}
         st["_cid"] = None
         st["_views"] = None
@@ -351,8 +369,10 @@ class IpcRing(RingBase):
             if rt.event_handle_size > EVENT_HANDLE_BYTES:
                 raise RuntimeError("hipIpcEventHandle_t is %d bytes (> %d)"
                                    % (rt.event_handle_size, EVENT_HANDLE_BYTES))
-            self._wev = [rt.event_create_ipc() for _ in range(self.num_slots)]
-            wh = tuple(rt.event_get_handle(e) for e in self._wev)
+            self._wev = [None] * self.num_slots
+            self._wrec = [0] * self.num_slots
+            for i in range(self.num_slots):
+                self._new_written_event(i)
         self._desc = (self.name, os.getpid(), device.index, handle, wh)
         import pickle
         blob = pickle.dumps(self._desc, protocol=pickle.HIGHEST_PROTOCOL)
@@ -376,19 +396,35 @@ class IpcRing(RingBase):
                            for row in self._ptrs]
         return self._views[idx]
 
+    def _new_written_event(self, idx: int) -> None:
+        """(Re)create slot ``idx``'s "written" event and publish its handle
+        (before the slot is published to consumers)."""
+        from ..ops import native
+        rt = native.runtime()
+        ev = rt.event_create_ipc()
+        h = rt.event_get_handle(ev)
+        off = idx * EVENT_HANDLE_BYTES
+        self.wev_handles[off:off + len(h)] = h
+        self.wev_epoch[idx] += 1
+        self._wev[idx] = ev          # the old one stays alive: a consumer may still wait on it
+        self._wrec[idx] = 0
+        self.events_created += 1
+
     def _release_event(self, cid: int, idx: int) -> int:
         from ..ops import native
         evs = self._rel_open.get(cid)
         if evs is None:
             evs = self._rel_open[cid] = [None] * self.num_slots
-        if evs[idx] is None:
-            if not self.rel_ready[cid * self.num_slots + idx]:
-                raise RuntimeError("ring %s: consumer %d released slot %d before "
-                                   "publishing its event" % (self.name, cid, idx))
+        epoch = self.rel_epoch[cid * self.num_slots + idx]
+        if epoch == 0:
+            raise RuntimeError("ring %s: consumer %d released slot %d before "
+                               "publishing its event" % (self.name, cid, idx))
+        if evs[idx] is None or evs[idx][1] != epoch:
             off = (cid * self.num_slots + idx) * EVENT_HANDLE_BYTES
             h = bytes(self.rel_handles[off:off + EVENT_HANDLE_BYTES])
-            evs[idx] = native.runtime().event_open_handle(h)
-        return evs[idx]
+            evs[idx] = (native.runtime().event_open_handle(h), epoch)
+            self.events_opened += 1
+        return evs[idx][0]
 
     def begin_write(self, idx: int, stream=None) -> None:
         """Order the producer stream after the last consumer's pull of ``idx``
@@ -430,7 +466,10 @@ class IpcRing(RingBase):
         from ..ops import native
         stream = stream or torch.cuda.current_stream(self._dev)
         if self.gpu_ordered:
+            if self._wrec[idx] >= EVENT_ROTATE:
+                self._new_written_event(idx)
             native.runtime().event_record(self._wev[idx], stream.cuda_stream)
+            self._wrec[idx] += 1
         else:
             stream.synchronize()   # push completes before the slot is marked full
         self._set_valid(idx, rows)
@@ -480,6 +519,7 @@ class IpcRing(RingBase):
             raise RuntimeError("ring %s: consumer %s was not declared" % (self.name, key))
         self._cid = self.consumers.index(tuple(key))
         self._rev = [None] * self.num_slots       # created on first release of a slot
+        self._rrec = [0] * self.num_slots
 
     def _open(self, token):
         from ..ops import native
@@ -498,18 +538,22 @@ class IpcRing(RingBase):
                     for i in range(self.num_slots)]
             self._opened[key] = ptrs
             self._opened_base[key] = base
-            if self.gpu_ordered and len(desc) > 4 and desc[4]:
-                self._whandles[key] = desc[4]
+            if self.gpu_ordered:
                 self._wopen[key] = [None] * self.num_slots    # opened on first pull
         return ptrs
 
     def _written_event(self, key, idx: int) -> int:
+        """The producer's current "written" event of slot ``idx`` (opened on
+        first use and again whenever the producer rotated it)."""
         evs = self._wopen[key]
-        if evs[idx] is None:
+        epoch = self.wev_epoch[idx]
+        if evs[idx] is None or evs[idx][1] != epoch:
             from ..ops import native
-            evs[idx] = native.runtime().event_open_handle(self._whandles[key][idx])
+            off = idx * EVENT_HANDLE_BYTES
+            h = bytes(self.wev_handles[off:off + EVENT_HANDLE_BYTES])
+            evs[idx] = (native.runtime().event_open_handle(h), epoch)
             self.events_opened += 1
-        return evs[idx]
+        return evs[idx][0]
 
     def rows_of(self, idx: int) -> int:
         return self.valid_rows(idx)[0]
@@ -551,18 +595,21 @@ class IpcRing(RingBase):
         if self.gpu_ordered and self._rev is not None:
             from ..ops import native
             rt = native.runtime()
-            if self._rev[idx] is None:
-                # first release of this slot by this consumer: create its
-                # event and publish the handle before naming itself below
+            if self._rev[idx] is None or self._rrec[idx] >= EVENT_ROTATE:
+                # first release of this slot by this consumer, or the event
+                # reached its record budget: a new event, its handle published
+                # (epoch bumped) before naming this consumer below
                 ev = rt.event_create_ipc()
                 h = rt.event_get_handle(ev)
                 off = (self._cid * self.num_slots + idx) * EVENT_HANDLE_BYTES
                 self.rel_handles[off:off + len(h)] = h
-                self.rel_ready[self._cid * self.num_slots + idx] = 1
+                self.rel_epoch[self._cid * self.num_slots + idx] += 1
                 self._rev[idx] = ev
+                self._rrec[idx] = 0
                 self.events_created += 1
             stream = torch.cuda.current_stream(self.consumer_device)
             rt.event_record(self._rev[idx], stream.cuda_stream)
+            self._rrec[idx] += 1
             self.released_by[idx] = self._cid
         super().release(idx)
 

@@ -204,11 +204,35 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         sync_each = is_final_step or shared_output_ring is None or \
             not shared_output_ring.gpu_ordered or os.environ.get("RNB_STAGE_SYNC") == "1"
 
+        # final step on a GPU: keep up to FINAL_INFLIGHT model calls in flight
+        # while the next request is prepared, completing (finish time, count)
+        # each when its event is observed done; drained before the runner
+        # blocks on an empty queue, so a completion is never held back by an
+        # idle queue (RNB_FINAL_INFLIGHT=0: synchronise every call)
+        final_depth = (int(os.environ.get("RNB_FINAL_INFLIGHT", "1"))
+                       if is_final_step and stream is not None else 0)
+        final_pending = []
+
+        def complete_final(limit: int) -> bool:
+            """Complete in-flight final-step calls until at most ``limit`` are
+            left; False means stop the runner loop."""
+            ok = True
+            while len(final_pending) > limit:
+                ev, tc = final_pending.pop(0)
+                ev.synchronize()
+                ok = finish_final(tc) and ok
+            return ok
+
         def emit(outputs, slot=None, seg_slots=None):
             """Route one model output; False means stop the runner loop.
             ``slot``: the output slot the model already wrote (direct_out);
             ``seg_slots``: [(slot, rows)] of the segments it wrote (direct_seg)."""
             tensor_outputs, non_tensor_outputs, time_card = outputs
+            if final_depth > 0 and time_card is not None:
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                final_pending.append((ev, time_card))
+                return complete_final(final_depth)
             if stream is not None and sync_each:
                 stream.synchronize()
             if time_card is None:
@@ -217,29 +241,38 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 for sl, _ in seg_slots or ():
                     shared_output_ring.release(sl)
                 return True
-            time_card.record("inference%d_finish" % step_idx)
             if is_final_step:
-                n_inf = len(time_card.time_cards) if isinstance(time_card, TimeCardList) else 1
-                with global_inference_counter.get_lock():
-                    prev = global_inference_counter.value
-                    global_inference_counter.value = prev + n_inf
-                    now = global_inference_counter.value
-                goal = num_videos.value if hasattr(num_videos, "value") else num_videos
-                if now >= goal:
-                    if prev < goal:
-                        print("Finished processing %d videos" % goal, flush=True)
-                        _set_flag(termination_flag,
-                                  TerminationFlag.TARGET_NUM_VIDEOS_REACHED)
-                    else:
-                        return False
-                if progress is not None and now > state["last_count"]:
-                    progress.update(min(now, goal) - min(state["last_count"], goal))
-                    state["last_count"] = now
-                cards = time_card.time_cards if isinstance(time_card, TimeCardList) \
-                    else [time_card]
-                for tc in cards:
-                    summary.register(tc)
-                return True
+                return finish_final(time_card)
+            time_card.record("inference%d_finish" % step_idx)
+            return route(tensor_outputs, non_tensor_outputs, time_card, slot, seg_slots)
+
+        def finish_final(time_card) -> bool:
+            """Final step: completion time, global count, summary; False when
+            the target was already reached before this call."""
+            time_card.record("inference%d_finish" % step_idx)
+            n_inf = len(time_card.time_cards) if isinstance(time_card, TimeCardList) else 1
+            with global_inference_counter.get_lock():
+                prev = global_inference_counter.value
+                global_inference_counter.value = prev + n_inf
+                now = global_inference_counter.value
+            goal = num_videos.value if hasattr(num_videos, "value") else num_videos
+            if now >= goal:
+                if prev < goal:
+                    print("Finished processing %d videos" % goal, flush=True)
+                    _set_flag(termination_flag,
+                              TerminationFlag.TARGET_NUM_VIDEOS_REACHED)
+                else:
+                    return False
+            if progress is not None and now > state["last_count"]:
+                progress.update(min(now, goal) - min(state["last_count"], goal))
+                state["last_count"] = now
+            cards = time_card.time_cards if isinstance(time_card, TimeCardList) \
+                else [time_card]
+            for tc in cards:
+                summary.register(tc)
+            return True
+
+        def route(tensor_outputs, non_tensor_outputs, time_card, slot, seg_slots) -> bool:
             # non-final step: push segments into slots, enqueue signals
             out_q = output_queues[selector.select(tensor_outputs, non_tensor_outputs,
                                                   time_card)]
@@ -374,6 +407,10 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 prof[name] = prof.get(name, 0.0) + now - pclock[0]
                 pclock[0] = now
         while termination_flag.value == TerminationFlag.UNSET:
+            if final_pending and not pending and backlog() == 0:
+                # nothing queued: complete the calls in flight before blocking
+                if not complete_final(0):
+                    break
             if (gather is not None and inflight is not None and LATENCY_BACKLOG > 0
                     and not pending and backlog() < LATENCY_BACKLOG and not inflight.query()):
                 # little queued: take the next request only once this replica
@@ -574,6 +611,7 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             if not emit(outputs):
                 break
             tick("emit")
+        complete_final(0)
         if termination_flag.value == TerminationFlag.UNSET and hasattr(model, "flush"):
             # natural end of stream: let batching/aggregating stages emit what
             # they still hold (the reference's Batcher would hold it forever)

@@ -19,6 +19,12 @@ from collections import defaultdict
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 FAMILIES = (
+    ("h3 row-band", r"conv_h3r_kernel"),
+    ("h3 direct", r"conv_h3_kernel"),
+    ("x6 row-band", r"conv_x6r_kernel"),
+    ("x6 direct", r"conv_x6_kernel"),
+    ("x6 wino temporal", r"conv_winot_x6_kernel"),
+    ("x6 wino spatial", r"conv_wino_x6"),
     ("wino spatial", r"conv_wino_f32_kernel"),
     ("wino temporal", r"conv_winot_f32_kernel"),
     ("conv direct", r"conv_f32_kernel"),

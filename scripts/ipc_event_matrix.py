@@ -19,8 +19,14 @@ and changes ONE factor at a time from the ring configuration:
   torch_ctx  the waiting process initialised torch's CUDA context first
 
 Per variant two patterns, as the C++ repro: ``done`` (record completed and
-synchronised before the wait) and ``pending`` (record behind a ~50 us spin).
-Prints the accepted-wait fraction per variant and pattern.
+synchronised before the wait) and ``pending`` (record behind a ~50 us spin),
+one event re-recorded every round. Prints the accepted-wait fraction per
+variant and pattern. Result (profiles/r4_ipc_event_matrix.txt): no factor
+matters; ROCm accepts waits on an IPC event for its first 32 records only,
+which the C++ reproducer (2000 records of one event: 32 accepted) and the
+rings (each slot's event recorded a few times per run: all accepted) both
+show. ``rotate=30`` (a new event every 30 records, as the rings now do)
+keeps every wait on the GPU.
 """
 import argparse
 import multiprocessing as mp
@@ -40,7 +46,7 @@ def _stream(kind, rt):
     return rt.stream_create(nonblocking=(kind == "raw"), priority=0)
 
 
-def producer(q_h, q_go, q_ack, rounds, stream_kind):
+def producer(q_h, q_go, q_ack, rounds, stream_kind, rotate=0):
     from rnb_amd.ops import native
     rt = native.runtime()
     rt.set_device(0)
@@ -50,14 +56,22 @@ def producer(q_h, q_go, q_ack, rounds, stream_kind):
     ev = rt.event_create_ipc()
     q_h.put(rt.event_get_handle(ev))
     s = _stream(stream_kind, rt)
+    records = 0
     for pat in PATTERNS:
         for _ in range(rounds):
+            msg = 1
+            if rotate and records == rotate:
+                # a fresh event after `rotate` records (transport.EVENT_ROTATE)
+                ev = rt.event_create_ipc()
+                msg = rt.event_get_handle(ev)
+                records = 0
             if pat == "pending":
                 rt.spin(s, 100000)
             rt.event_record(ev, s)
+            records += 1
             if pat == "done":
                 rt.stream_synchronize(s)
-            q_go.put(1)
+            q_go.put(msg)
             q_ack.get(timeout=60)
     rt.stream_synchronize(s)
 
@@ -80,7 +94,9 @@ def consumer(q_h, q_go, q_ack, q_out, rounds, stream_kind, own_event, torch_ctx)
         ok = 0
         codes = {}
         for _ in range(rounds):
-            q_go.get(timeout=60)
+            msg = q_go.get(timeout=60)
+            if isinstance(msg, bytes):             # the producer rotated its event
+                ev = rt.event_open_handle(msg)
             rc = rt.try_stream_wait_event(s, ev)
             if rc == 0:
                 ok += 1
@@ -94,12 +110,12 @@ def consumer(q_h, q_go, q_ack, q_out, rounds, stream_kind, own_event, torch_ctx)
     q_out.put(res)
 
 
-def run_variant(start, stream, own_event, torch_ctx, rounds):
+def run_variant(start, stream, own_event, torch_ctx, rounds, rotate=0):
     ctx = mp.get_context(start)
     q_h, q_go, q_ack, q_out = ctx.Queue(), ctx.Queue(), ctx.Queue(), ctx.Queue()
     c = ctx.Process(target=consumer, args=(q_h, q_go, q_ack, q_out, rounds, stream, own_event,
                                            torch_ctx))
-    p = ctx.Process(target=producer, args=(q_h, q_go, q_ack, rounds, stream))
+    p = ctx.Process(target=producer, args=(q_h, q_go, q_ack, rounds, stream, rotate))
     c.start()
     p.start()
     try:
@@ -129,6 +145,8 @@ def main():
     # event before the first wait)
     variants.append({"start": "fork", "stream": "raw", "own_event": False, "torch_ctx": False})
     variants.append({"start": "spawn", "stream": "torch", "own_event": False, "torch_ctx": True})
+    # the rings' fix: a new event (handle republished) every 30 records
+    variants.append(dict(base, rotate=30))
     lines = ["# scripts/ipc_event_matrix.py: accepted hipStreamWaitEvent on an opened IPC "
              "event, %d rounds per pattern" % args.rounds]
     for v in variants:
@@ -138,14 +156,15 @@ def main():
             pass
         try:
             res = run_variant(v["start"], v["stream"], v["own_event"], v["torch_ctx"],
-                              args.rounds)
+                              args.rounds, v.get("rotate", 0))
             cells = ["%s %d/%d%s" % (pat, ok, args.rounds,
                                      (" refused rc %s" % codes) if codes else "")
                      for pat, (ok, codes) in res.items()]
         except Exception as err:
             cells = ["error %s: %s" % (type(err).__name__, err)]
-        line = "start=%-5s stream=%-6s own_event=%-5s torch_ctx=%-5s | %s" % (
-            v["start"], v["stream"], v["own_event"], v["torch_ctx"], " | ".join(cells))
+        line = "start=%-5s stream=%-6s own_event=%-5s torch_ctx=%-5s rotate=%-3d | %s" % (
+            v["start"], v["stream"], v["own_event"], v["torch_ctx"], v.get("rotate", 0),
+            " | ".join(cells))
         print(line, flush=True)
         lines.append(line)
     if args.out:

@@ -117,3 +117,75 @@ def test_ipc_rings_at_8gpu_global_counts():
           "(%.0f us per pull); consumer holds %s"
           % (RINGS, SLOTS, n, attach_s[0], attach_s[-1], consumer_attach_s, t_first, pull_s,
              1e6 * pull_s / n, stats), flush=True)
+
+
+def _reuse_producer(ring, q, n, out_q):
+    import torch
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        ring.producer_attach(dev)
+        for i in range(n):
+            idx = i % len(ring)
+            if not ring.wait_free(idx):
+                raise RuntimeError("aborted")
+            ring.begin_write(idx, s)
+            view = ring.slot_views(idx)[0]
+            if i % 3 == 0:
+                torch.cuda._sleep(200_000)          # the fill lands late on the GPU
+            view.fill_(float(i))
+            ring.commit(idx, [view.shape[0]], s)
+            q.put((idx, i, ring.descriptor()))
+        q.put(None)
+        s.synchronize()
+        out_q.put((ring.gpu_waits, ring.stale_event_waits, ring.events_created))
+        time.sleep(2.0)
+        ring.close()
+
+
+def test_ipc_slot_events_past_32_records_stay_gpu_ordered():
+    """ROCm accepts a stream wait on an opened interprocess event only for
+    its first 32 records (profiles/r4_ipc_event_matrix.txt); IpcRing replaces
+    each slot's events every EVENT_ROTATE records and republishes the handle.
+    Two slots reused 60 times each: every pull must see its value and every
+    wait, on both sides, must stay on the GPU (no host fallback)."""
+    import multiprocessing as mp
+    import torch
+    from rnb_amd.parallel.transport import EVENT_ROTATE, IpcRing
+    ctx = mp.get_context("spawn")
+    ring = IpcRing(ctx, ((4, 1024),), (torch.float32,), 2, "rotate", 0)
+    ring.set_consumers([(1, 0, 0)])
+    q, out_q = ctx.Queue(), ctx.Queue()
+    n = 120
+    p = ctx.Process(target=_reuse_producer, args=(ring, q, n, out_q))
+    p.start()
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(dev)
+    outs = torch.empty((n, 4, 1024), device=dev)
+    with torch.cuda.stream(s):
+        ring.consumer_attach(dev, (1, 0, 0))
+        while True:
+            m = q.get(timeout=120)
+            if m is None:
+                break
+            idx, i, desc = m
+            if i % 4 == 1:
+                torch.cuda._sleep(200_000)           # the pull lands late on the GPU
+            ring.read_into(idx, [outs[i]], desc)
+            ring.release(idx)
+        s.synchronize()
+    prod = out_q.get(timeout=60)
+    p.join(60)
+    assert p.exitcode == 0
+    assert torch.equal(outs[:, 0, 0].cpu(), torch.arange(n, dtype=torch.float32))
+    assert torch.equal(outs.amin(dim=(1, 2)).cpu(), torch.arange(n, dtype=torch.float32))
+    st = ring.handle_stats()
+    ring.close()
+    assert st["host_fallback_waits"] == 0 and st["gpu_ordered_waits"] == n, st
+    assert prod[1] == 0, prod                      # producer: no host fallback either
+    rotations = -(-(n // 2) // EVENT_ROTATE)
+    assert st["events_created"] == 2 * rotations, st
+    print("\n[ipc-rotate] %d pulls over 2 slots: consumer %s, producer gpu waits %d, host "
+          "fallbacks %d, events created %d" % (n, st, prod[0], prod[1], prod[2]), flush=True)
