@@ -293,6 +293,7 @@ def run_pipeline(args, world: int) -> dict:
         os.environ["RNB_CHECK_DIR"] = check_dir
     t0 = time.time()
     res = launcher.run(launcher.build_parser().parse_args(largv))
+    res["t_launch"] = t0
     os.environ.pop("RNB_CHECK_DIR", None)
     res["check_dir"] = check_dir
     res["wall_s"] = time.time() - t0
@@ -385,18 +386,31 @@ def main(argv=None) -> int:
         }
         # extra runs first: the numerics check opens the GPU in this process,
         # and the extras' launchers bring their own loader/runner processes
+        timeline = {"start_to_launch": round(res.get("t_launch", _T_START) - _T_START, 2)}
+        timeline.update({"headline." + k: v for k, v in (res.get("timeline_s") or {}).items()})
+        timeline["headline_total"] = round(res.get("wall_s", 0.0), 2)
+        t_x = time.time()
         if args.gpus > 1 and args.cross_gpu_extras and args.pipeline == "aggressive":
             rec["cross_gpu"] = run_cross_gpu_extras(args)
+            timeline["cross_gpu_extras"] = round(time.time() - t_x, 2)
+        t_x = time.time()
         if args.gpus == 1 and args.literal and args.pipeline == "aggressive":
             rec["literal"] = run_literal_extras(args)
+            timeline["literal_extras"] = round(time.time() - t_x, 2)
+        t_x = time.time()
         if res.get("check_dir"):
             rec["numerics"] = check_numerics(args, res["check_dir"])
+            timeline["numerics_check"] = round(time.time() - t_x, 2)
             seg = ((rec.get("literal") or {}).get("config4_segment") or {}).get("numerics")
             strata = rec["numerics"].get("strata")
             if strata is not None and seg and "aggregate" in (seg.get("strata") or {}):
                 # literal config #4's re-joined segment videos (its own run)
                 strata["segment_rejoined"] = dict(seg["strata"]["aggregate"],
                                                   run="literal config4_segment")
+        # the whole job against --time-budget (the driver's 600 s limit)
+        timeline["total"] = round(time.time() - _T_START, 2)
+        timeline["budget"] = args.time_budget
+        rec["timeline_s"] = timeline
         line = json.dumps(rec)
     if store is not None:
         # every rank waits for rank 0's run (its launcher drives all GPUs)

@@ -298,6 +298,7 @@ def run(args) -> dict:
                 procs.append((p.name, p))
     # request-id ranges of the phases, for the runners' per-phase gather stats
     os.environ["RNB_PHASE_IDS"] = "%d,%d" % (warm, args.videos)
+    t_spawn = time.time()
     for _, p in procs:
         p.start()
     dog = Watchdog(procs, flag, [sta_bar, fin_bar])
@@ -357,6 +358,7 @@ def run(args) -> dict:
             p.terminate()
             p.join(5.0)
     dog.stop.set()
+    t_exit = time.time()
 
     result = {"job_id": job_id, "config": os.path.basename(args.config_file_path),
               "termination_flag": TerminationFlag.NAMES.get(flag.value, flag.value),
@@ -371,6 +373,7 @@ def run(args) -> dict:
               # GPU-ordered vs host fallback, plus handles held by consumers
               "ipc_edges": ipc_summary(ring_stats)}
     if time_start is not None and time_end is not None:
+        sta_time = time_start
         if warm and phase_start[0] > 0:
             time_start = phase_start[0]          # timed window starts after warm-up
         total = time_end - time_start
@@ -410,6 +413,14 @@ def run(args) -> dict:
                                            phases[0])
         if lat_s:
             total = window      # the barrier also waits for the latency phase
+        # where the job's wall time went (bench.py's time-budget table):
+        # process start + model build + autotune + graph capture up to the
+        # start barrier, warm-up, timed window, latency phases + drain, shutdown
+        result["timeline_s"] = {
+            "setup": round(sta_time - t_spawn, 2), "warmup": round(time_start - sta_time, 2),
+            "timed": round(window, 2),
+            "latency_and_drain": round(time_end - time_start - window, 2),
+            "shutdown": round(t_exit - time_end, 2)}
         result.update({"time_s": total, "videos_per_s": done / total if total > 0 else 0.0,
                        "window_s": window,
                        "videos_per_s_window": done / window if window > 0 else 0.0,

@@ -58,13 +58,14 @@ for step in "$@"; do
     compare) run compare 600 python scripts/profile_layers.py --depth 34 --clips "${arg:-128}" \
                --dtype fp32 --compare --reps 5 ;;
     bnbreak)
-      rm -rf gpurun_out/bnbreak
-      run bnbreak 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/bnbreak -o run \
-        -- python3 scripts/bn_breakdown.py run --mode batch --clips "${arg:-128}"
-      trace=$(ls gpurun_out/bnbreak/*/*/run_kernel_trace.csv gpurun_out/bnbreak/*/run_kernel_trace.csv \
-                 gpurun_out/bnbreak/run_kernel_trace.csv 2>/dev/null | tail -1)
-      [ -n "$trace" ] && python3 scripts/bn_breakdown.py parse "$trace" --kernels 12 \
-        > gpurun_out/bnbreak.txt && head -n 40 gpurun_out/bnbreak.txt ;;
+      c=${arg:-128}
+      rm -rf gpurun_out/bnbreak_$c
+      run bnbreak 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/bnbreak_$c -o run \
+        -- python3 scripts/bn_breakdown.py run --mode batch --clips "$c"
+      trace=$(ls gpurun_out/bnbreak_$c/*/*/run_kernel_trace.csv gpurun_out/bnbreak_$c/*/run_kernel_trace.csv \
+                 gpurun_out/bnbreak_$c/run_kernel_trace.csv 2>/dev/null | tail -1)
+      [ -n "$trace" ] && python3 scripts/bn_breakdown.py parse "$trace" --kernels 40 \
+        > gpurun_out/bnbreak_$c.txt && head -n 60 gpurun_out/bnbreak_$c.txt ;;
     pmc) layer=${arg%%:*}; cfgs=${arg#*:}
          LAYER=$layer CFGS="${cfgs//,/ }" run pmc 900 bash scripts/gpu_pmc_conv.sh ;;
     fold) n=${arg:-2}
