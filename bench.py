@@ -130,6 +130,9 @@ def parse_args(argv=None):
                          "a 256-clip R(2+1)D-34 runner holds ~19 GB)")
     ap.add_argument("--bucket-step", type=int, default=4,
                     help="HIP-graph clip buckets every this many clips")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="graphed engines per runner process, calls rotating over their "
+                         "streams (R2P1DRunner lanes: one-video calls overlap on the GPU)")
     ap.add_argument("--batch-wait-ms", type=float, default=0.0,
                     help="how long a runner waits for more queued videos to batch")
     ap.add_argument("--slots", type=int, default=None,
@@ -145,7 +148,7 @@ def parse_args(argv=None):
                     help="skip recomputing sampled served logits with the fp32 nn.Module")
     ap.add_argument("--no-literal", dest="literal", action="store_false",
                     help="at 1 GPU, skip the short literal BASELINE config #2 / #4 runs")
-    ap.add_argument("--literal-timeout", type=float, default=150.0,
+    ap.add_argument("--literal-timeout", type=float, default=200.0,
                     help="total seconds for the literal-config runs")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-autotune", action="store_true")
@@ -180,6 +183,8 @@ def pipeline_config(args, n_gpus: int) -> dict:
     runner = {"model": RUNNER, "start_index": 1, "end_index": 5,
               "max_clips": args.clips_per_batch, "bucket_step": args.bucket_step,
               "max_batch_videos": args.video_batch, "batch_wait_ms": args.batch_wait_ms}
+    if args.lanes > 1:
+        runner["lanes"] = args.lanes
     loader_gpus = [g for g in gpus for _ in range(args.loaders)]
     runner_gpus = [g for g in gpus for _ in range(args.replicas)]
     defaults = {"depth": args.depth, "dtype": args.dtype,
@@ -373,7 +378,7 @@ def main(argv=None) -> int:
                        "parallelism": "rnb pipeline: %d loader + %d runner processes per GPU"
                                       % (args.loaders, args.replicas),
                        "pipeline": args.pipeline, "launcher_config": res.get("config_path"),
-                       "route": args.route,
+                       "route": args.route, "lanes": args.lanes,
                        "bn": ("eval (folded into the convs in fp64)" if args.bn == "eval" else
                               "batch (training-mode BN as the reference, per-video "
                               "statistics)"),
@@ -559,10 +564,13 @@ def run_literal_extras(args) -> dict:
     (each video split into 3 segments, runners on the GPU, re-joined by the
     CPU aggregator, reference config/r2p1d-segment.json)."""
     root = os.path.dirname(os.path.abspath(__file__))
-    runs = [("config2_whole", ["--pipeline", "whole", "--replicas", "1", "--loaders", "1",
-                               "--steps", "2", "--warmup", "1", "--videos-per-step", "128",
-                               "--latency-mi", "90", "--latency-load", "0",
-                               "--latency-seconds", "4", "--no-check"]),
+    whole = ["--pipeline", "whole", "--replicas", "1", "--loaders", "1",
+             "--steps", "2", "--warmup", "1", "--videos-per-step", "128",
+             "--latency-mi", "90", "--latency-load", "0", "--latency-seconds", "4", "--no-check"]
+    runs = [("config2_whole", whole),
+            # the same processes (1 loader + 1 runner, one video per model
+            # call); the runner keeps two calls in flight on two streams
+            ("config2_whole_lanes2", whole + ["--lanes", "2"]),
             # its numerics (re-joined segment videos) join the headline's strata
             ("config4_segment", ["--pipeline", "segment", "--segments", "3",
                                  "--steps", "2", "--warmup", "1", "--videos-per-step", "128",
@@ -583,6 +591,7 @@ def run_literal_extras(args) -> dict:
             mi = sub.get("latency_mi10") or {}
             out[key] = {"videos_per_s": sub.get("value"), "ms_per_step": sub.get("ms_per_step"),
                         "parallelism": sub["config"]["parallelism"],
+                        "lanes": sub["config"].get("lanes", 1),
                         "pipeline": sub["config"]["pipeline"],
                         "launcher_config": sub["config"]["launcher_config"],
                         "wall_s": round(time.time() - t0, 1)}

@@ -146,7 +146,8 @@ class R2P1DRunner(RunnerModel):
                  layer_sizes=None, depth=None, block_type=None, backend="auto",
                  bn_mode=None, seed=0, ckpt_path=None, max_clips=DEFAULT_MAX_CLIPS,
                  warmup=3, use_graphs=True, autotune=True, dtype=None,
-                 max_batch_videos=1, batch_wait_ms=0.0, bucket_step=None, **unused):
+                 max_batch_videos=1, batch_wait_ms=0.0, bucket_step=None, lanes=1,
+                 **unused):
         super().__init__(device)
         if start_index < 1:
             raise ValueError("Wrong layer index for the starting layer! The start_index "
@@ -167,8 +168,29 @@ class R2P1DRunner(RunnerModel):
         self.engine = build_engine(device, start_index, end_index, num_classes,
                                    layer_sizes, depth, backend, bn_mode, seed, ckpt_path,
                                    self.max_clips, use_graphs, autotune, self.dtype, buckets)
-        if isinstance(self.engine, GraphedEngine):
-            self.engine.prepare()
+        # lanes > 1: that many graphed engines (own weights copy, BN buffers and
+        # graph pool each; the same seed / checkpoint, so identical outputs) on
+        # their own streams, calls rotating over them. One-video calls leave
+        # most of the chip idle and are ~220 short dispatches: two in flight on
+        # two streams overlap (scripts/lanes_probe.py: 1-clip calls 2.28 ->
+        # 1.33 ms each, 16-clip 6.87 -> 5.69 ms; profiles/r4_lanes_probe.txt).
+        # Each lane keeps its own BatchNorm running statistics.
+        self.lanes = max(1, int(lanes)) if (isinstance(self.engine, GraphedEngine)
+                                             and device.type == "cuda") else 1
+        self._lane_engines = [self.engine]
+        for _ in range(self.lanes - 1):
+            self._lane_engines.append(build_engine(
+                device, start_index, end_index, num_classes, layer_sizes, depth, backend,
+                bn_mode, seed, ckpt_path, self.max_clips, use_graphs, autotune, self.dtype,
+                buckets))
+        self._lane_streams = ([torch.cuda.Stream(device) for _ in range(self.lanes)]
+                              if self.lanes > 1 else None)
+        self._lane_done = [None] * self.lanes     # completion event of each lane's last call
+        self._lane = 0                             # lane of the next call
+        self.last_event = None                     # completion event of the last call
+        for eng in self._lane_engines:
+            if isinstance(eng, GraphedEngine):
+                eng.prepare()
             if device.type == "cuda" and os.environ.get("RNB_REPORT_MEMORY") == "1":
                 print("[runner gpu %d] %d graph buckets, capture %.1f s, %.1f GB allocated, "
                       "%.1f GB reserved" % (device.index or 0, len(self.engine.graphs),
@@ -194,9 +216,24 @@ class R2P1DRunner(RunnerModel):
             return None
         return (max(1, self.max_batch_videos), self.max_clips, self.batch_wait_s)
 
+    def completion_event(self):
+        """lanes > 1: the event that completes the last call (it ran on a lane
+        stream, not on the runner's); None otherwise."""
+        return self.last_event if self.lanes > 1 else None
+
+    def inflight_calls(self) -> int:
+        """Calls the final-step runner should keep in flight (runner.py)."""
+        return self.lanes - 1
+
     def gather_buffers(self, rows: int):
-        if isinstance(self.engine, GraphedEngine) and rows > 0:
-            static_in, _ = self.engine.input_buffer(rows)
+        if self.lanes > 1:
+            ev = self._lane_done[self._lane]
+            if ev is not None:
+                # the lane's previous call must be done reading its static input
+                torch.cuda.current_stream(self.device).wait_event(ev)
+        eng = self._lane_engines[self._lane]
+        if isinstance(eng, GraphedEngine) and rows > 0:
+            static_in, _ = eng.input_buffer(rows)
         else:
             if self._gather_buf is None:
                 self._gather_buf = torch.empty(
@@ -261,6 +298,8 @@ class R2P1DRunner(RunnerModel):
                 stratum = stratum_of("runner", n, call_rows)
                 if self._checked.get(stratum, 0) < CHECK_MAX:
                     self._checked[stratum] = self._checked.get(stratum, 0) + 1
+                    if self.lanes > 1:          # y was written on a lane stream
+                        torch.cuda.current_stream(self.device).wait_event(self.last_event)
                     write_sample(self._check_dir, tc.id, "runner", src[0], src[1],
                                  y[off:off + n].float().cpu().numpy(), self.bn_mode,
                                  str(self.dtype), call_rows=call_rows)
@@ -273,22 +312,34 @@ class R2P1DRunner(RunnerModel):
         return out
 
     def _call(self, tensors, non_tensors, time_card):
-        x = tensors[0]
+        if self.lanes == 1:
+            return (self._run(self.engine, tensors[0], time_card),), non_tensors, time_card
+        lane = self._lane
+        self._lane = (lane + 1) % self.lanes
+        cur = torch.cuda.current_stream(self.device)
+        ls = self._lane_streams[lane]
+        ls.wait_stream(cur)                        # the input rows were pulled on `cur`
+        with torch.cuda.stream(ls):
+            y = self._run(self._lane_engines[lane], tensors[0], time_card)
+            ev = torch.cuda.Event()
+            ev.record(ls)
+        self._lane_done[lane] = ev
+        self.last_event = ev
+        return (y,), non_tensors, time_card
+
+    def _run(self, eng, x, time_card):
         offs = (self._clip_offsets(time_card, x.shape[0]) if self.bn_mode == "batch"
                 else None)
         if (self._gather_ptr is not None and x.data_ptr() == self._gather_ptr
-                and isinstance(self.engine, GraphedEngine) and x.shape[0] > 0):
+                and isinstance(eng, GraphedEngine) and x.shape[0] > 0):
             # rows already sit in the bucket graph's static input: replay only
             self._gather_ptr = None
-            y = self.engine.replay(x.shape[0], clip_offsets=offs)
-        else:
-            self._gather_ptr = None
-            x = _to_boundary(x, self.start_index, self.dtype)
-            if self.bn_mode == "batch" and x.shape[0] > 0:
-                y = self.engine.forward(x, clip_offsets=offs)
-            else:
-                y = self.engine(x)
-        return (y,), non_tensors, time_card
+            return eng.replay(x.shape[0], clip_offsets=offs)
+        self._gather_ptr = None
+        x = _to_boundary(x, self.start_index, self.dtype)
+        if self.bn_mode == "batch" and x.shape[0] > 0:
+            return eng.forward(x, clip_offsets=offs)
+        return eng(x)
 
 
 class R2P1DVideoPathIterator(VideoPathIterator):

@@ -204,13 +204,24 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         sync_each = is_final_step or shared_output_ring is None or \
             not shared_output_ring.gpu_ordered or os.environ.get("RNB_STAGE_SYNC") == "1"
 
-        # final step on a GPU: keep up to FINAL_INFLIGHT model calls in flight
-        # while the next request is prepared, completing (finish time, count)
-        # each when its event is observed done; drained before the runner
-        # blocks on an empty queue, so a completion is never held back by an
-        # idle queue (RNB_FINAL_INFLIGHT=0: synchronise every call)
-        final_depth = (int(os.environ.get("RNB_FINAL_INFLIGHT", "1"))
+        # final step on a GPU: RNB_FINAL_INFLIGHT=k keeps up to k model calls
+        # in flight while the next request is prepared, completing (finish
+        # time, count) each when its event is observed done; drained before the
+        # runner blocks on an empty queue. Default 0 (synchronise every call):
+        # on one stream in-flight calls only queue behind each other, and
+        # interleaved A/B runs measured 1 no better for the headline and worse
+        # for one-video calls (literal config #2: 310 vs 351 videos/s,
+        # profiles/r4_ab_literal2_final_inflight.txt)
+        final_depth = (int(os.environ.get("RNB_FINAL_INFLIGHT", "0"))
                        if is_final_step and stream is not None else 0)
+        # a model running calls on streams of its own (R2P1DRunner lanes) says
+        # how many to keep in flight, and which event completes each call
+        lane_inflight = getattr(model, "inflight_calls", None)
+        if is_final_step and stream is not None and callable(lane_inflight):
+            final_depth = max(final_depth, int(lane_inflight()))
+        model_event = getattr(model, "completion_event", None)
+        if not callable(model_event):
+            model_event = None
         final_pending = []
 
         def complete_final(limit: int) -> bool:
@@ -228,11 +239,16 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             ``slot``: the output slot the model already wrote (direct_out);
             ``seg_slots``: [(slot, rows)] of the segments it wrote (direct_seg)."""
             tensor_outputs, non_tensor_outputs, time_card = outputs
+            mev = model_event() if model_event is not None else None
             if final_depth > 0 and time_card is not None:
-                ev = torch.cuda.Event()
-                ev.record(stream)
+                ev = mev
+                if ev is None:
+                    ev = torch.cuda.Event()
+                    ev.record(stream)
                 final_pending.append((ev, time_card))
                 return complete_final(final_depth)
+            if mev is not None and stream is not None:
+                stream.wait_event(mev)      # outputs written on the model's stream
             if stream is not None and sync_each:
                 stream.synchronize()
             if time_card is None:
@@ -568,8 +584,10 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 if not emit(outputs, gslot):
                     break
                 if stream is not None and adaptive_gather:
-                    inflight = torch.cuda.Event()
-                    inflight.record(stream)
+                    inflight = model_event() if model_event is not None else None
+                    if inflight is None:
+                        inflight = torch.cuda.Event()
+                        inflight.record(stream)
                 tick("emit")
                 continue
             if direct_seg:

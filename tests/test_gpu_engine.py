@@ -318,3 +318,35 @@ def test_batch_bn_fp32_error_vs_fp64():
     e_mod = (ym - y64).abs().max().item() / scale
     print("batch-BN fp32 vs fp64: HIP %.2e, PyTorch fp32 module %.2e" % (e_hip, e_mod))
     assert e_hip <= 3 * e_mod + 1e-6, (e_hip, e_mod)
+
+
+def test_runner_lanes_match_one_lane():
+    """R2P1DRunner(lanes=2): calls alternate over two graphed engines on two
+    streams (inputs pulled on the caller's stream, outputs complete on
+    ``completion_event()``); every output equals the one-lane runner's."""
+    from rnb_amd.models.r2p1d.model import R2P1DRunner
+    kw = dict(depth=10, bn_mode="batch", dtype="fp32", warmup=0, max_clips=4,
+              bucket_step=1, autotune=False)
+    one = R2P1DRunner(DEV, lanes=1, **kw)
+    two = R2P1DRunner(DEV, lanes=2, **kw)
+    assert two.lanes == 2 and two.inflight_calls() == 1
+    g = torch.Generator(device=DEV).manual_seed(5)
+    xs = [torch.randn(one.input_shape()[0][1:], device=DEV, generator=g)
+          .unsqueeze(0).repeat(n, 1, 1, 1, 1) * (1 + 0.1 * i)
+          for i, n in enumerate((1, 3, 2, 4, 1, 2))]
+    outs = {}
+    for name, r in (("one", one), ("two", two)):
+        cur = torch.cuda.current_stream(DEV)
+        res = []
+        for x in xs:
+            dst = r.gather_buffers(x.shape[0])[0]
+            dst[:x.shape[0]].copy_(x)
+            y = r((dst[:x.shape[0]],), None, None)[0][0]
+            ev = r.completion_event()
+            if ev is not None:
+                cur.wait_event(ev)
+            res.append(y.clone())
+        torch.cuda.synchronize()
+        outs[name] = res
+    for a, b in zip(outs["one"], outs["two"]):
+        assert torch.equal(a, b)
