@@ -130,6 +130,9 @@ def parse_args(argv=None):
                          "a 256-clip R(2+1)D-34 runner holds ~19 GB)")
     ap.add_argument("--bucket-step", type=int, default=4,
                     help="HIP-graph clip buckets every this many clips")
+    ap.add_argument("--large-priority", action="store_true",
+                    help="(--route large-small) the 15-clip-video replicas run on "
+                         "high-priority streams")
     ap.add_argument("--lanes", type=int, default=1,
                     help="graphed engines per runner process, calls rotating over their "
                          "streams (R2P1DRunner lanes: one-video calls overlap on the GPU)")
@@ -202,7 +205,9 @@ def pipeline_config(args, n_gpus: int) -> dict:
                                    for g in gpus]},
                  dict(runner, queue_groups=[q for g in gpus for q in (
                      {"gpus": [g] * (args.replicas - nl), "in_queue": 2 * g},
-                     {"gpus": [g] * nl, "in_queue": 2 * g + 1})])]
+                     {"gpus": [g] * nl, "in_queue": 2 * g + 1})],
+                      **({"group_stream_priority": [0, -1] * n_gpus}
+                         if args.large_priority else {}))]
     elif args.pipeline == "aggressive":
         steps = [{"model": LOADER,
                   "queue_groups": [{"gpus": [g] * args.loaders, "out_queues": [g]}

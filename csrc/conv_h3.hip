@@ -513,13 +513,209 @@ void conv_h3r_kernel(const ConvF32Params p, const X6DStats st) {
       half ^= 1;
     }
   }
-  const float out_scale = st.out_scale;
-#pragma unroll
-  for (int tp = 0; tp < TP; ++tp)
-#pragma unroll
-    for (int tc = 0; tc < TC; ++tc) acc[tp][tc] *= out_scale;
   x6d_epilogue<TP, TC, NW, C_TILE, ST>(p, st, acc, p0, m_end, p0 + P_TILE, c0, wave, 0, lane,
-                                       lds, HALO_BYTES + 2 * G * W_BYTES);
+                                       lds, HALO_BYTES + 2 * G * W_BYTES, st.out_scale);
+}
+
+// ---------------------------------------------------------------------------
+// Row-band halo conv with one wave per SIMD ("h3q"): 4 waves x TP = 7 tiles
+// = 448 output pixels x 144 channels per block. conv_h3r_kernel's 7 waves
+// put two waves on three SIMDs and one on the fourth (at most 7/8 of the
+// matrix cores), and each tap waited for its fragment reads right before
+// the MFMAs using them (lgkmcnt(0) per channel tile: 46 % MFMA-busy on
+// conv2, profiles/pmc/r4_h3r_conv2_spatial.txt). Here each wave owns a SIMD,
+// its 7 x 9 accumulator tiles (252 registers) sit in AGPRs, and the
+// fragment reads are software-pipelined: a channel tile's MFMAs run while
+// the next tile's weights and one of the next tap's activation fragments
+// are read (double-buffered registers, one scheduling region per tile).
+template <int NW, int TP, int HALO_PX, int G, int MINB, bool ST, bool AFF>
+__global__ __launch_bounds__(64 * NW, MINB)
+void conv_h3q_kernel(const ConvF32Params p, const X6DStats st) {
+  constexpr int TC = 9;
+  constexpr int P_TILE = NW * TP * 16, C_TILE = TC * 16;
+  constexpr int HALO_BYTES = HALO_PX * 128;
+  constexpr int W_BYTES = C_TILE * 128;
+  constexpr int W_TOTAL = C_TILE / 8;
+  constexpr int W_INSTR = (W_TOTAL + NW - 1) / NW;
+  constexpr int NT = 64 * NW;
+  constexpr int ITEMS = (HALO_PX * 4 + NT - 1) / NT;     // (pixel, quad) items per lane
+  static_assert(TP <= TC - 1, "next-tap fragments are read during channel tiles 1..TP");
+  __shared__ __attribute__((aligned(16))) char lds[HALO_BYTES + 2 * G * W_BYTES];
+  char* const wbuf = lds + HALO_BYTES;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int frow = lane & 15, fq = lane >> 4;
+  const int W = p.W, H = p.H, W2 = p.W + 2;
+  const int R = p.ST;                        // rows per band (host: stride field reused)
+  const int bands = (H + R - 1) / R;
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int ctile = wgid % p.n_ctiles;
+  const int band = wgid / p.n_ctiles;
+  const int f = band / bands, r0 = (band - f * bands) * R;
+  const int c0 = ctile * C_TILE;
+  const int p0 = (f * H + r0) * W;
+  const int m_end = p0 + min(R, H - r0) * W;
+  const int nck = p.Cin_p / 32;
+
+  const x6d_u32x4 wr = x6d_rsrc(p.w, (uint32_t)(p.K_pad / 32) * (uint32_t)p.w_rows * 128u);
+  auto issue_w = [&](int s, int buf) {
+    const uint32_t wbase = ((uint32_t)s * (uint32_t)p.w_rows + (uint32_t)c0) * 128u;
+#pragma unroll
+    for (int j = 0; j < W_INSTR; ++j) {
+      const int instr = (W_TOTAL % NW == 0) ? wave + NW * j : min(wave + NW * j, W_TOTAL - 1);
+      x6d_dma16(wr, wbase + (uint32_t)(instr * 1024 + lane * 16),
+                wbuf + buf * W_BYTES + instr * 1024);
+    }
+  };
+
+  // patch staging as conv_h3r_kernel
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+  const int npx = (R + 2) * W2;
+  const int qd = threadIdx.x & 3;
+  uint32_t src[ITEMS];
+  int dst[ITEMS];
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const int it = threadIdx.x + i * NT;
+    const int q = it >> 2;
+    const int hy = q / W2, hx = q - hy * W2;
+    const int y = r0 - 1 + hy, x = hx - 1;
+    const bool ok = it < 4 * npx && y >= 0 && y < H && x >= 0 && x < W;
+    src[i] = ok ? (uint32_t)((((f * H + y) * W + x) * p.Cin_p + qd * 4) * 4) : X6D_INVALID;
+    dst[i] = it < 4 * npx ? q * 128 : -1;
+  }
+  const float* ssv = nullptr;
+  if constexpr (AFF) ssv = st.in_ss + (size_t)st.in_seg[f / p.T] * 2 * p.Cin_p + qd * 4;
+  const float in_scale = st.in_scale;
+  constexpr int SB = AFF ? 2 : 5;
+  auto stage = [&](int chunk) {
+    x6f32x4 sc0, sh0, sc1, sh1;
+    if constexpr (AFF) {
+      const float* ss = ssv + chunk * 32;
+      sc0 = *(const x6f32x4*)ss;
+      sc1 = *(const x6f32x4*)(ss + 16);
+      sh0 = *(const x6f32x4*)(ss + p.Cin_p);
+      sh1 = *(const x6f32x4*)(ss + p.Cin_p + 16);
+    }
+#pragma unroll
+    for (int i0 = 0; i0 < ITEMS; i0 += SB) {
+      x6f32x4 v0[SB], v1[SB];
+#pragma unroll
+      for (int k = 0; k < SB; ++k) {
+        const int i = min(i0 + k, ITEMS - 1);
+        const uint32_t o = src[i] == X6D_INVALID ? X6D_INVALID : src[i] + (uint32_t)(chunk * 128);
+        v0[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0);
+        v1[k] = __builtin_amdgcn_raw_buffer_load_b128(xr, o == X6D_INVALID ? o : o + 64u, 0, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < SB; ++k) {
+        const int i = i0 + k;
+        if (i >= ITEMS || dst[i] < 0) continue;
+        const int q = dst[i] >> 7;
+        x6f32x4 a0 = v0[k], a1 = v1[k];
+        if constexpr (AFF) {
+          const float m = src[i] == X6D_INVALID ? 0.f : in_scale;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            a0[j] = fmaxf(fmaf(a0[j], sc0[j], sh0[j]), 0.f) * m;
+            a1[j] = fmaxf(fmaf(a1[j], sc1[j], sh1[j]), 0.f) * m;
+          }
+        } else {
+          a0 *= in_scale;
+          a1 *= in_scale;
+        }
+        uint32_t h[4], l[4];
+        h3_split4(a0, h, l);
+        h3_split4(a1, h + 2, l + 2);
+        char* base = lds + dst[i];
+        *(wu32x4*)(base + (x6r_swz(2 * qd, q) << 4)) = (wu32x4){h[0], h[1], h[2], h[3]};
+        *(wu32x4*)(base + (x6r_swz(2 * qd + 1, q) << 4)) = (wu32x4){l[0], l[1], l[2], l[3]};
+      }
+    }
+  };
+
+  int pq[TP];
+#pragma unroll
+  for (int tp = 0; tp < TP; ++tp) {
+    const int pp = (wave * TP + tp) * 16 + frow;
+    const int py = pp / W;
+    pq[tp] = pp < R * W ? py * W2 + (pp - py * W) : 0;
+  }
+
+  x6f32x4 acc[TP][TC];
+#pragma unroll
+  for (int b = 0; b < TC; ++b) {
+    const int c = c0 + b * 16 + 4 * fq;
+    const float4 b4 = *(const float4*)(p.bias + c);
+    const x6f32x4 bv = (x6f32x4){b4.x, b4.y, b4.z, b4.w} * st.acc_scale;
+#pragma unroll
+    for (int a = 0; a < TP; ++a) acc[a][b] = bv;
+  }
+  const int w_hh = x6_chunk(2 * fq, frow) << 4, w_ll = x6_chunk(2 * fq + 1, frow) << 4;
+  auto rd_bf = [&](H3B& b, int tap, int tp) {
+    const int q = pq[tp] + (tap / 3) * W2 + (tap % 3);
+    const char* base = lds + q * 128;
+    b.h = *(const wu32x4*)(base + (x6r_swz(2 * fq, q) << 4));
+    b.l = *(const wu32x4*)(base + (x6r_swz(2 * fq + 1, q) << 4));
+  };
+  auto rd_w = [&](wu32x4& ah, wu32x4& al, int jslot, int tc) {
+    const char* wrow = wbuf + jslot * W_BYTES + (tc * 16 + frow) * 128;
+    ah = *(const wu32x4*)(wrow + w_hh);
+    al = *(const wu32x4*)(wrow + w_ll);
+  };
+
+  constexpr int NG = (9 + G - 1) / G;
+  auto issue_group = [&](int c, int g, int half) {
+    for (int j = 0; j < G && g * G + j < 9; ++j) issue_w((g * G + j) * nck + c, half * G + j);
+  };
+  issue_group(0, 0, 0);
+  int half = 0;
+  for (int c = 0; c < nck; ++c) {
+    stage(c);
+    x6d_wait_vm<0>();
+    x6d_barrier();
+#pragma unroll 1
+    for (int g = 0; g < NG; ++g) {
+      if (g + 1 < NG) issue_group(c, g + 1, half ^ 1);
+      else if (c + 1 < nck) issue_group(c + 1, 0, half ^ 1);
+      const int t0 = g * G;
+      H3B bf[2][TP];
+      wu32x4 wh[2], wl[2];
+#pragma unroll
+      for (int tp = 0; tp < TP; ++tp) rd_bf(bf[0][tp], t0, tp);
+      rd_w(wh[0], wl[0], half * G, 0);
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        if (t0 + j >= 9) break;                      // uniform
+        const bool more = j + 1 < G && t0 + j + 1 < 9;
+#pragma unroll
+        for (int tc = 0; tc < TC; ++tc) {
+          const int cs = (j * TC + tc) & 1;
+          if (tc + 1 < TC) rd_w(wh[cs ^ 1], wl[cs ^ 1], half * G + j, tc + 1);
+          else if (more) rd_w(wh[cs ^ 1], wl[cs ^ 1], half * G + j + 1, 0);
+          if (more && tc >= 1 && tc <= TP) rd_bf(bf[(j + 1) & 1][tc - 1], t0 + j + 1, tc - 1);
+          const H3B (&b)[TP] = bf[j & 1];
+#pragma unroll
+          for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(wl[cs], b[tp].h, acc[tp][tc]);
+#pragma unroll
+          for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(wh[cs], b[tp].l, acc[tp][tc]);
+#pragma unroll
+          for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(wh[cs], b[tp].h, acc[tp][tc]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      x6d_wait_vm<0>();             // the next group's weights landed (this wave) ...
+      x6d_barrier();                // ... in every wave; this group's LDS reads are done
+      half ^= 1;
+    }
+  }
+  x6d_epilogue<TP, TC, NW, C_TILE, ST>(p, st, acc, p0, m_end, p0 + P_TILE, c0, wave, 0, lane,
+                                       lds, HALO_BYTES + 2 * G * W_BYTES, st.out_scale);
 }
 
 // ---------------------------------------------------------------------------
@@ -644,7 +840,9 @@ int rnb_conv_h3_launch(const ConvF32Params* pp, int config_id, hipStream_t strea
 // Row-band halo h3 kernel (conv_h3r_kernel): 1x3x3 stride 1 pad 1 with
 // Cin_p % 32 == 0. Variants as rnb_conv_x6r_launch: 0 = 7 waves x 4 tiles
 // (448 px), 1 = 14 waves x 2 tiles, 2 = 7 waves x 3 tiles (336 px), 3 / 4 / 5
-// = 0 / 1 / 2 with 2 taps per barrier; 144 channels per block.
+// = 0 / 1 / 2 with 2 taps per barrier, 6 = conv_h3q_kernel (4 waves x 7
+// tiles, 448 px), 7 = conv_h3q_kernel (4 waves x 4 tiles, 256 px, two blocks
+// per CU); 144 channels per block.
 struct ConvH3RConfig {
   int nw, tp, halo_px;
   void (*kernel)(const ConvF32Params, const X6DStats);
@@ -657,9 +855,23 @@ struct ConvH3RConfig {
    conv_h3r_kernel<NW, TP, 9, HALO, G, true, false>,                               \
    conv_h3r_kernel<NW, TP, 9, HALO, G, false, true>,                               \
    conv_h3r_kernel<NW, TP, 9, HALO, G, true, true>}
+// one wave per SIMD (conv_h3q_kernel): 4 waves x TP tiles
+#define H3QCFG(NW, TP, HALO, G, MINB)                                             \
+  {NW, TP, HALO, conv_h3q_kernel<NW, TP, HALO, G, MINB, false, false>,             \
+   conv_h3q_kernel<NW, TP, HALO, G, MINB, true, false>,                            \
+   conv_h3q_kernel<NW, TP, HALO, G, MINB, false, true>,                            \
+   conv_h3q_kernel<NW, TP, HALO, G, MINB, true, true>}
 static const ConvH3RConfig kH3RConfigs[] = {
     H3RCFG(7, 4, 600, 1), H3RCFG(14, 2, 600, 1), H3RCFG(7, 3, 480, 1),
     H3RCFG(7, 4, 600, 2), H3RCFG(14, 2, 600, 2), H3RCFG(7, 3, 480, 2),
+    H3QCFG(4, 7, 600, 2, 1),  // 6: 448 px, one block (one wave per SIMD) per CU
+    // 7: 256 px, 1 tap per barrier, 80 KB of LDS: two blocks per CU, so one
+    // block's patch staging and epilogue (HBM-bound phases) overlap the
+    // other's MFMAs
+    H3QCFG(4, 4, 352, 1, 2),
+    // 8: 8 waves x 4 tiles = 512 px (two waves per SIMD: one wave issues an
+    // MFMA every ~16.5 cycles, two together every ~8.5, profiles/r3_mfma_split.txt)
+    H3QCFG(8, 4, 640, 2, 1),
 };
 
 int rnb_conv_h3r_num_variants() { return (int)(sizeof(kH3RConfigs) / sizeof(kH3RConfigs[0])); }

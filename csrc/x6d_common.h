@@ -101,11 +101,14 @@ static __device__ __forceinline__ float x6d_row16_sum(float v) {
 // Epilogue of the x6 direct kernels: (+ residual) (+ ReLU) -> fp32 stores,
 // one 16-B store per tile, and (ST) the per-video BN sums. Rows m < m_end of
 // [p0, p_hi) are valid; `lds` (lds_bytes) is free scratch (no DMA in flight).
+// acc_mul scales the accumulators as they are read (h3: out_scale; one tile
+// at a time, so accumulators held in AGPRs move to VGPRs tile by tile)
 template <int TP, int TC, int NW, int CT_ALL, bool ST>
 static __device__ __forceinline__ void x6d_epilogue(const ConvF32Params& p, const X6DStats& st,
                                                     x6f32x4 (&acc)[TP][TC], int p0, int m_end,
                                                     int p_hi, int c0, int wp, int wc, int lane,
-                                                    char* lds, int lds_bytes) {
+                                                    char* lds, int lds_bytes,
+                                                    float acc_mul = 1.f) {
   const int frow = lane & 15, fq = lane >> 4;
   // ---- epilogue: (+ residual) (+ ReLU) -> fp32, one 16-B store per tile ----
   const uint32_t y_bytes = (uint32_t)p.M * (uint32_t)p.y_stride * 4u;
@@ -132,7 +135,7 @@ static __device__ __forceinline__ void x6d_epilogue(const ConvF32Params& p, cons
       for (int tc = 0; tc < TC; ++tc) {
         const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
         const bool ok = m < m_end && c < p.Cout_p;
-        x6f32x4 v = acc[tp][tc] + r[tc];
+        x6f32x4 v = acc[tp][tc] * acc_mul + r[tc];
         if (p.relu) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
@@ -145,9 +148,12 @@ static __device__ __forceinline__ void x6d_epilogue(const ConvF32Params& p, cons
     // channel tiles outer (one tile's sums live at a time). Rows are
     // clip-major, so a block's videos are the contiguous range seg_lo ..
     // seg_hi. One video (the common case): each lane sums its TP rows, the 16
-    // lanes of a channel quad reduce by shuffles, one LDS add per channel and
-    // wave. Several videos: LDS adds per row into per-video slots. Then one
-    // fp64 atomic per video, channel and statistic per block.
+    // lanes of a channel quad reduce by DPP, one LDS add per channel and
+    // wave. Several videos (tiles across a video boundary, rare): after the
+    // stores, the block reads its tile back (L2, glc) in a runtime loop and
+    // adds per row into per-video slots -- kept out of the unrolled tile loop,
+    // whose full unroll (and the accumulators' registers) it would otherwise
+    // break. Then one fp64 atomic per video, channel and statistic per block.
     constexpr int NT = 64 * NW;
     int na, nz, t_, h_, w_;
     f32_decode_row(p, p0, na, t_, h_, w_);
@@ -174,14 +180,14 @@ static __device__ __forceinline__ void x6d_epilogue(const ConvF32Params& p, cons
                               rr, ok ? (uint32_t)(m * p.res_stride + c) * 4u : X6D_INVALID, 0, 0)
                         : (x6f32x4){0.f, 0.f, 0.f, 0.f};
       }
-      // lane partials over its TP rows in fp32 (<= 4 values), the 16-lane
-      // reduction in fp32 by DPP, everything after in fp64
+      // lane partials over its TP rows in fp32, the 16-lane reduction in
+      // fp32 by DPP, everything after in fp64
       float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int tp = 0; tp < TP; ++tp) {
         const int m = p0 + (wp * TP + tp) * 16 + frow;
         const bool ok = m < m_end && c < p.Cout_p;
-        x6f32x4 v = acc[tp][tc] + r[tp];
+        x6f32x4 v = acc[tp][tc] * acc_mul + r[tp];
         if (p.relu) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
@@ -189,27 +195,10 @@ static __device__ __forceinline__ void x6d_epilogue(const ConvF32Params& p, cons
         __builtin_amdgcn_raw_buffer_store_b128(
             v, yr, ok ? (uint32_t)(m * p.y_stride + c) * 4u : X6D_INVALID, 0, 0);
         if (!ok) continue;
-        if (uni) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            s1[j] += v[j];
-            s2[j] = fmaf(v[j], v[j], s2[j]);
-          }
-        } else {
-          int n, tt, hh, ww;
-          f32_decode_row(p, m, n, tt, hh, ww);
-          const int sg = st.clip_seg[n];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const double a = (double)v[j], b = (double)v[j] * (double)v[j];
-            if (in_lds) {
-              atomicAdd(red + ((size_t)(sg - seg_lo) * CT_ALL + cl + j) * 2, a);
-              atomicAdd(red + ((size_t)(sg - seg_lo) * CT_ALL + cl + j) * 2 + 1, b);
-            } else {
-              atomicAdd(st.sums + ((size_t)sg * 2) * st.stats_c + c + j, a);
-              atomicAdd(st.sums + ((size_t)sg * 2 + 1) * st.stats_c + c + j, b);
-            }
-          }
+        for (int j = 0; j < 4; ++j) {
+          s1[j] += v[j];
+          s2[j] = fmaf(v[j], v[j], s2[j]);
         }
       }
       if (uni) {
@@ -223,6 +212,34 @@ static __device__ __forceinline__ void x6d_epilogue(const ConvF32Params& p, cons
           for (int j = 0; j < 4; ++j) {
             atomicAdd(red + (cl + j) * 2, (double)s1[j]);
             atomicAdd(red + (cl + j) * 2 + 1, (double)s2[j]);
+          }
+        }
+      }
+    }
+    if (!uni) {
+      // the block's stored tile, back from L2 (glc: not this CU's L1)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int rows = min(p_hi, m_end) - p0;
+      const int cq = CT_ALL / 4;
+#pragma unroll 1
+      for (int i = threadIdx.x; i < rows * cq; i += NT) {
+        const int m = p0 + i / cq, cl = (i % cq) * 4, c = c0 + cl;
+        if (c >= p.Cout_p) continue;
+        const x6f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+            yr, (uint32_t)(m * p.y_stride + c) * 4u, 0, 1);
+        int n, tt, hh, ww;
+        f32_decode_row(p, m, n, tt, hh, ww);
+        const int sg = st.clip_seg[n];
+#pragma unroll 1
+        for (int j = 0; j < 4; ++j) {
+          const double a = (double)v[j], b = (double)v[j] * (double)v[j];
+          if (in_lds) {
+            atomicAdd(red + ((size_t)(sg - seg_lo) * CT_ALL + cl + j) * 2, a);
+            atomicAdd(red + ((size_t)(sg - seg_lo) * CT_ALL + cl + j) * 2 + 1, b);
+          } else {
+            atomicAdd(st.sums + ((size_t)sg * 2) * st.stats_c + c + j, a);
+            atomicAdd(st.sums + ((size_t)sg * 2 + 1) * st.stats_c + c + j, b);
           }
         }
       }

@@ -695,7 +695,10 @@ class ConvLayerF32:
         if x_shape is None:
             return True
         _, T, H, W, _ = x_shape
-        nw, tp, halo = ((7, 4, 600), (14, 2, 600), (7, 3, 480))[variant % 3]
+        # csrc/conv_h3.hip kH3RConfigs: 0-5 conv_h3r_kernel (x 2 barrier
+        # groupings), 6 / 7 conv_h3q_kernel (4 waves x 7 / 4 tiles)
+        nw, tp, halo = ((7, 4, 600), (14, 2, 600), (7, 3, 480))[variant % 3] if variant < 6 \
+            else ((4, 7, 600), (4, 4, 352), (8, 4, 640))[variant - 6]
         rows = nw * tp * 16 // W
         if rows < 1 or (rows + 2) * (W + 2) > halo:
             return False

@@ -106,6 +106,10 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         raise RuntimeError("injected fault in runner%d init" % step_idx)
 
     use_gpu = g_idx >= 0
+    # per queue group stream priority (step kwarg ``group_stream_priority``:
+    # a list indexed by queue group, lower = higher), e.g. the 15-clip-video
+    # replicas of the large-small routing ahead of the 1-clip batches
+    group_prio = model_kwargs.pop("group_stream_priority", None)
     if use_gpu:
         torch.cuda.set_device(g_idx)
         device = torch.device("cuda:%d" % g_idx)
@@ -113,6 +117,8 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         # high-priority stream (RunnerModel.stream_priority, lower = higher)
         from .utils.class_utils import load_class as _lc
         prio = int(getattr(_lc(model_module_path), "stream_priority", 0))
+        if group_prio is not None and group_idx < len(group_prio):
+            prio = int(group_prio[group_idx])
         stream = torch.cuda.Stream(device=device, priority=prio)
         stream_ctx = torch.cuda.stream(stream)
     else:
