@@ -46,6 +46,27 @@
 
 #include "h3_common.h"
 
+// Phase timing for experiments (csrc/bench/h3_phase.hip defines
+// H3_PHASE_TIMING): thread 0 of a block stores s_memtime at phase k of the
+// row-band kernels (vector store); empty in the product build.
+#ifdef H3_PHASE_TIMING
+__device__ unsigned long long* h3_phase_buf;
+#define H3_PHASE(k)                                                                   \
+  do {                                                                                \
+    if (threadIdx.x == 0 && (k) < 16) {                                               \
+      h3_phase_buf[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime();     \
+      if ((k) == 0) {                                                                 \
+        unsigned hw, xcc;                                                             \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));              \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));            \
+        h3_phase_buf[(size_t)blockIdx.x * 16 + 14] = ((unsigned long long)xcc << 32) | hw; \
+      }                                                                               \
+    }                                                                                 \
+  } while (0)
+#else
+#define H3_PHASE(k) do {} while (0)
+#endif
+
 // input BatchNorm on load (AFF): per stage, the scale / shift of the step's
 // 32 channels for each clip the tile touches, [clip][sub][scale, shift][16]
 // (256 B per clip), DMA'd with the step's activations
@@ -473,12 +494,14 @@ void conv_h3r_kernel(const ConvF32Params p, const X6DStats st) {
     for (int j = 0; j < G && g * G + j < 9; ++j) issue_w((g * G + j) * nck + c, half * G + j);
   };
   if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  H3_PHASE(0);
   issue_group(0, 0, 0);
   int half = 0;
   for (int c = 0; c < nck; ++c) {
     stage(c);
     x6d_wait_vm<0>();
     x6d_barrier();
+    H3_PHASE(1 + 2 * c);
 #pragma unroll 1
     for (int g = 0; g < NG; ++g) {
       if (g + 1 < NG) issue_group(c, g + 1, half ^ 1);
@@ -512,9 +535,11 @@ void conv_h3r_kernel(const ConvF32Params p, const X6DStats st) {
       x6d_barrier();                // ... in every wave; this group's LDS reads are done
       half ^= 1;
     }
+    H3_PHASE(2 + 2 * c);
   }
   x6d_epilogue<TP, TC, NW, C_TILE, ST>(p, st, acc, p0, m_end, p0 + P_TILE, c0, wave, 0, lane,
                                        lds, HALO_BYTES + 2 * G * W_BYTES, st.out_scale);
+  H3_PHASE(15);
 }
 
 // ---------------------------------------------------------------------------
@@ -546,7 +571,9 @@ void conv_h3q_kernel(const ConvF32Params p, const X6DStats st) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int frow = lane & 15, fq = lane >> 4;
-  const int W = p.W, H = p.H, W2 = p.W + 2;
+  // patch rows of W + 1 entries: one zero column serves as the right pad of
+  // a row and the left pad of the next (plus one zero entry at the end)
+  const int W = p.W, H = p.H, W2 = p.W + 1;
   const int R = p.ST;                        // rows per band (host: stride field reused)
   const int bands = (H + R - 1) / R;
 
@@ -575,7 +602,7 @@ void conv_h3q_kernel(const ConvF32Params p, const X6DStats st) {
   // patch staging as conv_h3r_kernel
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
-  const int npx = (R + 2) * W2;
+  const int npx = (R + 2) * W2 + 1;
   const int qd = threadIdx.x & 3;
   uint32_t src[ITEMS];
   int dst[ITEMS];
@@ -673,12 +700,14 @@ void conv_h3q_kernel(const ConvF32Params p, const X6DStats st) {
   auto issue_group = [&](int c, int g, int half) {
     for (int j = 0; j < G && g * G + j < 9; ++j) issue_w((g * G + j) * nck + c, half * G + j);
   };
+  H3_PHASE(0);
   issue_group(0, 0, 0);
   int half = 0;
   for (int c = 0; c < nck; ++c) {
     stage(c);
     x6d_wait_vm<0>();
     x6d_barrier();
+    H3_PHASE(1 + 2 * c);
 #pragma unroll 1
     for (int g = 0; g < NG; ++g) {
       if (g + 1 < NG) issue_group(c, g + 1, half ^ 1);
@@ -713,9 +742,288 @@ void conv_h3q_kernel(const ConvF32Params p, const X6DStats st) {
       x6d_barrier();                // ... in every wave; this group's LDS reads are done
       half ^= 1;
     }
+    H3_PHASE(2 + 2 * c);
   }
   x6d_epilogue<TP, TC, NW, C_TILE, ST>(p, st, acc, p0, m_end, p0 + P_TILE, c0, wave, 0, lane,
                                        lds, HALO_BYTES + 2 * G * W_BYTES, st.out_scale);
+  H3_PHASE(15);
+}
+
+// ---------------------------------------------------------------------------
+// Temporal frame-band conv ("h3t"): the 3x1x1 stride-1 temporal convs. A
+// block owns P pixels of one clip over all T frames (T x P = NW x TP x 16
+// output rows, frame-major) and C_TILE output channels. Per 32-channel chunk
+// the (T + 2) x P input patch (zero frames at both ends) is staged once,
+// pre-split into fp16 hi / lo as conv_h3r_kernel's patch, and the 3 taps read
+// it at frame offsets 0, P, 2P: every input value is loaded and split once
+// per chunk instead of once per tap (conv_h3_kernel's gather: 3 loads and 3
+// splits per value, VALU-bound at 6.5 VALU per MFMA on conv2,
+// profiles/pmc/r4_h3_conv2_temporal.txt). The next chunk's patch loads and
+// weight DMA are issued before the current chunk's MFMAs (registers /
+// second weight buffer), so HBM stays busy through the MFMA phase. Cin_p %
+// 16 == 0: a chunk whose upper 16 channels are past Cin_p loads zeros there
+// (the host pads each tap's weights to 32-channel chunks).
+template <int NW, int TP, int TC, int HALO, bool ST, bool AFF>
+__global__ __launch_bounds__(64 * NW, 1)
+void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
+  constexpr int ROWS = NW * TP * 16, C_TILE = TC * 16;
+  constexpr int HALO_BYTES = HALO * 128;
+  constexpr int TAP_BYTES = C_TILE * 128;            // one tap's weights of a chunk
+  constexpr int W_BYTES = 3 * TAP_BYTES;
+  constexpr int W_TOTAL = W_BYTES / 1024;
+  constexpr int W_INSTR = (W_TOTAL + NW - 1) / NW;
+  constexpr int NT = 64 * NW;
+  constexpr int ITEMS = (HALO * 4 + NT - 1) / NT;    // (entry, quad) items per lane
+  static_assert(NT % 4 == 0 && TAP_BYTES % 1024 == 0, "staging / DMA split");
+  static_assert(TP <= TC * 3 - 1, "next-tap fragments are read during the channel tiles");
+  __shared__ __attribute__((aligned(16))) char lds[HALO_BYTES + 2 * W_BYTES];
+  char* const wbuf = lds + HALO_BYTES;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int frow = lane & 15, fq = lane >> 4;
+  const int T = p.T, HW = p.H * p.W, P = p.ngroups;     // host: P = ROWS / T
+  const int nck = (p.Cin_p + 31) / 32;
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int ctile = wgid % p.n_ctiles;
+  const int rest = wgid / p.n_ctiles;
+  const int ptile = rest % p.n_ptiles;
+  const int n = rest / p.n_ptiles;
+  const int c0 = ctile * C_TILE, hw0 = ptile * P;
+
+  const x6d_u32x4 wr = x6d_rsrc(p.w, (uint32_t)(p.K_pad / 32) * (uint32_t)p.w_rows * 128u);
+  auto issue_w = [&](int c, int buf) {                // the 3 taps of chunk c
+#pragma unroll
+    for (int j = 0; j < W_INSTR; ++j) {
+      const int instr = (W_TOTAL % NW == 0) ? wave + NW * j : min(wave + NW * j, W_TOTAL - 1);
+      const int k = instr / (TAP_BYTES / 1024), part = instr % (TAP_BYTES / 1024);
+      const uint32_t s = (uint32_t)(k * nck + c);
+      x6d_dma16(wr, (s * (uint32_t)p.w_rows + (uint32_t)c0) * 128u +
+                        (uint32_t)(part * 1024 + lane * 16),
+                wbuf + buf * W_BYTES + instr * 1024);
+    }
+  };
+
+  // staging items: entry e = (frame + 1) * P + pixel, quad qd
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+  const int nent = (T + 2) * P;
+  const int qd = threadIdx.x & 3;
+  uint32_t src[ITEMS];
+  int dst[ITEMS];
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const int it = threadIdx.x + i * NT;
+    const int e = it >> 2;
+    const int fr = e / P - 1, px = e - (fr + 1) * P;
+    const bool ok = it < 4 * nent && fr >= 0 && fr < T && hw0 + px < HW;
+    src[i] = ok ? (uint32_t)((((n * T + fr) * HW + hw0 + px) * p.Cin_p + qd * 4) * 4) : X6D_INVALID;
+    dst[i] = it < 4 * nent ? e * 128 : -1;
+  }
+  const float* ssv = nullptr;
+  if constexpr (AFF) ssv = st.in_ss + (size_t)st.in_seg[n] * 2 * p.Cin_p + qd * 4;
+  const float in_scale = st.in_scale;
+  x6f32x4 raw0[ITEMS], raw1[ITEMS];
+  auto load_chunk = [&](int c) {
+    const bool hi_ok = c * 32 + 16 < p.Cin_p;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const uint32_t o = src[i] == X6D_INVALID ? X6D_INVALID : src[i] + (uint32_t)(c * 128);
+      raw0[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0);
+      raw1[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, (o == X6D_INVALID || !hi_ok) ? X6D_INVALID
+                                                                                  : o + 64u, 0, 0);
+    }
+  };
+  auto store_chunk = [&](int c) {
+    x6f32x4 sc0, sh0, sc1, sh1;
+    if constexpr (AFF) {
+      const bool hi_ok = c * 32 + 16 < p.Cin_p;
+      const float* ss = ssv + c * 32;
+      sc0 = *(const x6f32x4*)ss;
+      sh0 = *(const x6f32x4*)(ss + p.Cin_p);
+      sc1 = hi_ok ? *(const x6f32x4*)(ss + 16) : (x6f32x4){0.f, 0.f, 0.f, 0.f};
+      sh1 = hi_ok ? *(const x6f32x4*)(ss + p.Cin_p + 16) : (x6f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      if (dst[i] < 0) continue;
+      const int e = dst[i] >> 7;
+      x6f32x4 a0 = raw0[i], a1 = raw1[i];
+      if constexpr (AFF) {
+        const float m = src[i] == X6D_INVALID ? 0.f : in_scale;      // padding stays zero
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a0[j] = fmaxf(fmaf(a0[j], sc0[j], sh0[j]), 0.f) * m;
+          a1[j] = fmaxf(fmaf(a1[j], sc1[j], sh1[j]), 0.f) * m;
+        }
+      } else {
+        a0 *= in_scale;
+        a1 *= in_scale;
+      }
+      uint32_t h[4], l[4];
+      h3_split4(a0, h, l);
+      h3_split4(a1, h + 2, l + 2);
+      char* base = lds + dst[i];
+      *(wu32x4*)(base + (x6r_swz(2 * qd, e) << 4)) = (wu32x4){h[0], h[1], h[2], h[3]};
+      *(wu32x4*)(base + (x6r_swz(2 * qd + 1, e) << 4)) = (wu32x4){l[0], l[1], l[2], l[3]};
+    }
+  };
+
+  // the lane's rows: tile (wave, tp) = rows r0 .. r0 + 15 of one frame
+  int pe[TP];                                        // patch entry at tap 0
+#pragma unroll
+  for (int tp = 0; tp < TP; ++tp) {
+    const int r = (wave * TP + tp) * 16 + frow;
+    const int fr = r / P;
+    pe[tp] = fr * P + (r - fr * P);                  // frame fr + tap k - 1 -> entry + k P
+  }
+
+  x6f32x4 acc[TP][TC];
+#pragma unroll
+  for (int b = 0; b < TC; ++b) {
+    const int c = c0 + b * 16 + 4 * fq;
+    const float4 b4 = *(const float4*)(p.bias + c);
+    const x6f32x4 bv = (x6f32x4){b4.x, b4.y, b4.z, b4.w} * st.acc_scale;
+#pragma unroll
+    for (int a = 0; a < TP; ++a) acc[a][b] = bv;
+  }
+  const int w_hh = x6_chunk(2 * fq, frow) << 4, w_ll = x6_chunk(2 * fq + 1, frow) << 4;
+  auto rd_bf = [&](H3B& b, int k, int tp) {
+    const int e = pe[tp] + k * P;
+    const char* base = lds + e * 128;
+    b.h = *(const wu32x4*)(base + (x6r_swz(2 * fq, e) << 4));
+    b.l = *(const wu32x4*)(base + (x6r_swz(2 * fq + 1, e) << 4));
+  };
+  auto rd_w = [&](wu32x4& ah, wu32x4& al, int buf, int k, int tc) {
+    const char* wrow = wbuf + buf * W_BYTES + k * TAP_BYTES + (tc * 16 + frow) * 128;
+    ah = *(const wu32x4*)(wrow + w_hh);
+    al = *(const wu32x4*)(wrow + w_ll);
+  };
+
+  issue_w(0, 0);
+  load_chunk(0);
+  for (int c = 0; c < nck; ++c) {
+    if (c > 0) x6d_barrier();                        // every wave is done with chunk c - 1
+    store_chunk(c);
+    x6d_wait_vm<0>();                                // chunk c's weights landed (this wave) ...
+    x6d_barrier();                                   // ... the patch and weights in every wave
+    if (c + 1 < nck) {
+      issue_w(c + 1, (c + 1) & 1);                   // DMA first, then the patch loads
+      load_chunk(c + 1);
+    }
+    const int buf = c & 1;
+    H3B bf[2][TP];
+    wu32x4 wh[2], wl[2];
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp) rd_bf(bf[0][tp], 0, tp);
+    rd_w(wh[0], wl[0], buf, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+      for (int tc = 0; tc < TC; ++tc) {
+        const int cs = (k * TC + tc) & 1;
+        if (tc + 1 < TC) rd_w(wh[cs ^ 1], wl[cs ^ 1], buf, k, tc + 1);
+        else if (k + 1 < 3) rd_w(wh[cs ^ 1], wl[cs ^ 1], buf, k + 1, 0);
+        // the next tap's fragments, one tile per channel tile (TP <= 3 TC - 1)
+        if (k + 1 < 3) {
+#pragma unroll
+          for (int tp = 0; tp < TP; ++tp)
+            if (tp * TC / TP == tc && tp < TP) rd_bf(bf[(k + 1) & 1][tp], k + 1, tp);
+        }
+        const H3B (&b)[TP] = bf[k & 1];
+#pragma unroll
+        for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(wl[cs], b[tp].h, acc[tp][tc]);
+#pragma unroll
+        for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(wh[cs], b[tp].l, acc[tp][tc]);
+#pragma unroll
+        for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(wh[cs], b[tp].h, acc[tp][tc]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+
+  // ---- epilogue: rows (frame, pixel) of clip n, one video (ST) ----
+  const float out_scale = st.out_scale;
+  const uint32_t y_bytes = (uint32_t)p.M * (uint32_t)p.y_stride * 4u;
+  const __amdgpu_buffer_rsrc_t yr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.y, (short)0, y_bytes, 0x00020000);
+  const bool has_res = p.res != nullptr;
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(has_res ? p.res : p.y), (short)0,
+      has_res ? (uint32_t)p.M * (uint32_t)p.res_stride * 4u : 0u, 0x00020000);
+  int mrow[TP];
+#pragma unroll
+  for (int tp = 0; tp < TP; ++tp) {
+    const int r = (wave * TP + tp) * 16 + frow;
+    const int fr = r / P, px = r - fr * P;
+    mrow[tp] = hw0 + px < HW ? (n * T + fr) * HW + hw0 + px : -1;
+  }
+  double* red = (double*)lds;                        // [C_TILE][2] (patch no longer read)
+  if constexpr (ST) {
+    x6d_barrier();
+    for (int i = threadIdx.x; i < C_TILE * 2; i += NT) red[i] = 0.0;
+    __syncthreads();
+  }
+#pragma unroll
+  for (int tc = 0; tc < TC; ++tc) {
+    const int cl = tc * 16 + 4 * fq, c = c0 + cl;
+    x6f32x4 rv[TP];
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp) {
+      const bool ok = has_res && mrow[tp] >= 0 && c < p.Cout_p;
+      rv[tp] = has_res ? __builtin_amdgcn_raw_buffer_load_b128(
+                             rr, ok ? (uint32_t)(mrow[tp] * p.res_stride + c) * 4u : X6D_INVALID,
+                             0, 0)
+                       : (x6f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp) {
+      const bool ok = mrow[tp] >= 0 && c < p.Cout_p;
+      x6f32x4 v = acc[tp][tc] * out_scale + rv[tp];
+      if (p.relu) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(
+          v, yr, ok ? (uint32_t)(mrow[tp] * p.y_stride + c) * 4u : X6D_INVALID, 0, 0);
+      if (ST && ok) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s1[j] += v[j];
+          s2[j] = fmaf(v[j], v[j], s2[j]);
+        }
+      }
+    }
+    if constexpr (ST) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s1[j] = x6d_row16_sum(s1[j]);
+        s2[j] = x6d_row16_sum(s2[j]);
+      }
+      if (frow == 0 && c < p.Cout_p) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          atomicAdd(red + (cl + j) * 2, (double)s1[j]);
+          atomicAdd(red + (cl + j) * 2 + 1, (double)s2[j]);
+        }
+      }
+    }
+  }
+  if constexpr (ST) {
+    __syncthreads();
+    const int sg = st.clip_seg[n];
+    for (int i = threadIdx.x; i < C_TILE; i += NT) {
+      const int c = c0 + i;
+      if (c < p.Cout_p) {
+        atomicAdd(st.sums + ((size_t)sg * 2) * st.stats_c + c, red[i * 2]);
+        atomicAdd(st.sums + ((size_t)sg * 2 + 1) * st.stats_c + c, red[i * 2 + 1]);
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -844,20 +1152,20 @@ int rnb_conv_h3_launch(const ConvF32Params* pp, int config_id, hipStream_t strea
 // tiles, 448 px), 7 = conv_h3q_kernel (4 waves x 4 tiles, 256 px, two blocks
 // per CU); 144 channels per block.
 struct ConvH3RConfig {
-  int nw, tp, halo_px;
+  int nw, tp, halo_px, q;        // q: conv_h3q_kernel patch layout
   void (*kernel)(const ConvF32Params, const X6DStats);
   void (*kernel_st)(const ConvF32Params, const X6DStats);
   void (*kernel_aff)(const ConvF32Params, const X6DStats);
   void (*kernel_aff_st)(const ConvF32Params, const X6DStats);
 };
 #define H3RCFG(NW, TP, HALO, G)                                                    \
-  {NW, TP, HALO, conv_h3r_kernel<NW, TP, 9, HALO, G, false, false>,                \
+  {NW, TP, HALO, 0, conv_h3r_kernel<NW, TP, 9, HALO, G, false, false>,             \
    conv_h3r_kernel<NW, TP, 9, HALO, G, true, false>,                               \
    conv_h3r_kernel<NW, TP, 9, HALO, G, false, true>,                               \
    conv_h3r_kernel<NW, TP, 9, HALO, G, true, true>}
 // one wave per SIMD (conv_h3q_kernel): 4 waves x TP tiles
 #define H3QCFG(NW, TP, HALO, G, MINB)                                             \
-  {NW, TP, HALO, conv_h3q_kernel<NW, TP, HALO, G, MINB, false, false>,             \
+  {NW, TP, HALO, 1, conv_h3q_kernel<NW, TP, HALO, G, MINB, false, false>,          \
    conv_h3q_kernel<NW, TP, HALO, G, MINB, true, false>,                            \
    conv_h3q_kernel<NW, TP, HALO, G, MINB, false, true>,                            \
    conv_h3q_kernel<NW, TP, HALO, G, MINB, true, true>}
@@ -865,10 +1173,10 @@ static const ConvH3RConfig kH3RConfigs[] = {
     H3RCFG(7, 4, 600, 1), H3RCFG(14, 2, 600, 1), H3RCFG(7, 3, 480, 1),
     H3RCFG(7, 4, 600, 2), H3RCFG(14, 2, 600, 2), H3RCFG(7, 3, 480, 2),
     H3QCFG(4, 7, 600, 2, 1),  // 6: 448 px, one block (one wave per SIMD) per CU
-    // 7: 256 px, 1 tap per barrier, 80 KB of LDS: two blocks per CU, so one
+    // 7: 256 px, 1 tap per barrier, 79 KB of LDS: two blocks per CU, so one
     // block's patch staging and epilogue (HBM-bound phases) overlap the
     // other's MFMAs
-    H3QCFG(4, 4, 352, 1, 2),
+    H3QCFG(4, 4, 344, 1, 2),
     // 8: 8 waves x 4 tiles = 512 px (two waves per SIMD: one wave issues an
     // MFMA every ~16.5 cycles, two together every ~8.5, profiles/r3_mfma_split.txt)
     H3QCFG(8, 4, 640, 2, 1),
@@ -879,7 +1187,9 @@ int rnb_conv_h3r_num_variants() { return (int)(sizeof(kH3RConfigs) / sizeof(kH3R
 // band rows of a variant for frame width W (0: the variant cannot run it)
 static int h3r_rows(const ConvH3RConfig& cfg, int H, int W) {
   const int R = cfg.nw * cfg.tp * 16 / W;
-  return (R >= 1 && (R + 2) * (W + 2) <= cfg.halo_px) ? R : 0;
+  // conv_h3r_kernel: rows of W + 2 entries; conv_h3q_kernel: W + 1 plus one
+  const int entries = cfg.q ? (R + 2) * (W + 1) + 1 : (R + 2) * (W + 2);
+  return (R >= 1 && entries <= cfg.halo_px) ? R : 0;
 }
 
 int rnb_conv_h3r_launch(const ConvF32Params* pp, int variant, hipStream_t stream, double* sums,
@@ -929,6 +1239,88 @@ int rnb_conv_h3r_launch(const ConvF32Params* pp, int variant, hipStream_t stream
   hipLaunchKernelGGL(aff ? (sums ? cfg.kernel_aff_st : cfg.kernel_aff)
                          : (sums ? cfg.kernel_st : cfg.kernel),
                      dim3((unsigned)blocks), dim3(64 * cfg.nw), 0, stream, p, st);
+  return (int)hipGetLastError();
+}
+
+// Temporal frame-band h3 kernel (conv_h3t_kernel): 3x1x1 stride 1 pad
+// (1, 0, 0), Cin_p % 16 == 0, T >= 2. Variants: 0 = 8 waves x 4 tiles (512
+// rows: P = 512 / T pixels) x 64 channels, 1 = 8 waves x 2 tiles (256 rows) x
+// 64 channels, 2 = 8 waves x 2 tiles x 128 channels. p.w = split weights with
+// every tap padded to whole 32-channel chunks: step s = tap * ceil(Cin_p / 32)
+// + chunk (p.K_pad = 3 * 32 * ceil(Cin_p / 32)).
+struct ConvH3TConfig {
+  int rows, c_tile, halo;
+  void (*kernel)(const ConvF32Params, const X6DStats);
+  void (*kernel_st)(const ConvF32Params, const X6DStats);
+  void (*kernel_aff)(const ConvF32Params, const X6DStats);
+  void (*kernel_aff_st)(const ConvF32Params, const X6DStats);
+};
+#define H3TCFG(NW, TP, TC, HALO)                                                   \
+  {NW * TP * 16, TC * 16, HALO, conv_h3t_kernel<NW, TP, TC, HALO, false, false>,   \
+   conv_h3t_kernel<NW, TP, TC, HALO, true, false>,                                 \
+   conv_h3t_kernel<NW, TP, TC, HALO, false, true>,                                 \
+   conv_h3t_kernel<NW, TP, TC, HALO, true, true>}
+static const ConvH3TConfig kH3TConfigs[] = {
+    H3TCFG(8, 4, 4, 768), H3TCFG(8, 2, 4, 512), H3TCFG(8, 2, 8, 512),
+};
+
+int rnb_conv_h3t_num_variants() { return (int)(sizeof(kH3TConfigs) / sizeof(kH3TConfigs[0])); }
+
+// pixels per block of a variant for T frames (0: the variant cannot run it)
+int rnb_conv_h3t_pixels(int variant, int T) {
+  if (variant < 0 || variant >= rnb_conv_h3t_num_variants() || T < 2) return 0;
+  const ConvH3TConfig& cfg = kH3TConfigs[variant];
+  if (cfg.rows % T) return 0;
+  const int P = cfg.rows / T;
+  return (P % 16 == 0 && (T + 2) * P <= cfg.halo) ? P : 0;
+}
+
+int rnb_conv_h3t_launch(const ConvF32Params* pp, int variant, hipStream_t stream, double* sums,
+                        const int* clip_seg, int stats_c, float in_scale, float out_scale,
+                        const float* in_ss, const int* in_seg) {
+  if (variant < 0 || variant >= rnb_conv_h3t_num_variants()) return -1;
+  ConvF32Params p = *pp;
+  const ConvH3TConfig& cfg = kH3TConfigs[variant];
+  if (p.KT != 3 || p.KH != 1 || p.KW != 1 || p.PT != 1 || p.PH != 0 || p.PW != 0) return -2;
+  if (p.ST != 1 || p.SH != 1 || p.SW != 1 || p.Cin_p % 16 != 0 || p.Cout_p % 4 != 0) return -2;
+  const int nck = (p.Cin_p + 31) / 32;
+  if (p.K_pad != 3 * 32 * nck) return -3;
+  if (p.M <= 0) return 0;
+  if (p.M != p.N * p.T * p.H * p.W) return -3;
+  if (p.y_stride < p.Cout_p || p.y_stride % 4 != 0 || (p.res && (p.res_stride < p.Cout_p ||
+                                                               p.res_stride % 4 != 0)))
+    return -4;
+  const long long xb = (long long)p.N * p.T * p.H * p.W * p.Cin_p * 4;
+  if (xb > 0x7FFFFF00LL || (long long)p.M * p.y_stride * 4 > 0x7FFFFF00LL) return -5;
+  if (p.res && (long long)p.M * p.res_stride * 4 > 0x7FFFFF00LL) return -6;
+  const int P = rnb_conv_h3t_pixels(variant, p.T);
+  if (P == 0) return -13;
+  if ((long long)(p.K_pad / 32) * p.w_rows * 128 > 0x7FFFFF00LL) return -11;
+  if (!(in_scale > 0.f) || !(out_scale > 0.f)) return -15;
+  if (in_ss && !in_seg) return -16;
+  p.x_bytes = (uint32_t)xb;
+  p.ngroups = P;
+  p.n_ptiles = (p.H * p.W + P - 1) / P;
+  p.n_ctiles = (p.Cout_p + cfg.c_tile - 1) / cfg.c_tile;
+  if (p.n_ctiles * cfg.c_tile > p.w_rows) return -8;
+  const long long blocks = (long long)p.N * p.n_ptiles * p.n_ctiles;
+  if (blocks > 0x7FFFFFFF) return -7;
+  if (sums && (!clip_seg || stats_c < p.Cout_p)) return -12;
+  X6DStats st;
+  st.sums = sums;
+  st.clip_seg = clip_seg;
+  st.stats_c = stats_c;
+  st.ksplit = 1;
+  st.ws = nullptr;
+  st.in_scale = in_scale;
+  st.out_scale = out_scale;
+  st.acc_scale = 1.f / out_scale;
+  st.in_ss = in_ss;
+  st.in_seg = in_seg;
+  const bool aff = in_ss != nullptr;
+  hipLaunchKernelGGL(aff ? (sums ? cfg.kernel_aff_st : cfg.kernel_aff)
+                         : (sums ? cfg.kernel_st : cfg.kernel),
+                     dim3((unsigned)blocks), dim3(512), 0, stream, p, st);
   return (int)hipGetLastError();
 }
 

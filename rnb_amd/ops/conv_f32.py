@@ -140,6 +140,9 @@ H3K_CONFIGS = (2, 4, 5, 9, 10)
 # row-band halo h3 kernel (csrc/conv_h3.hip conv_h3r_kernel): 1x3x3 stride 1
 # pad 1 with Cin_p % 32 == 0, variant H3R_BASE + v of rnb_conv_h3r_launch
 H3R_BASE = 1380
+# temporal frame-band h3 kernel (conv_h3t_kernel): 3x1x1 stride 1 pad (1, 0, 0)
+# with T >= 2, variant H3T_BASE + v of rnb_conv_h3t_launch
+H3T_BASE = 1395
 # activations are split after scaling by 2^H3_IN_LOG2: fp16 lo parts stay
 # normal for |a| >= 2^-9 and inputs up to 2^10 stay in the fp16 range
 H3_IN_LOG2 = 6
@@ -150,7 +153,13 @@ H3_W_TOP_LOG2 = 13
 def is_h3(cid: int) -> bool:
     from .native import kernels
     return ((H3D_BASE <= cid < H3D_BASE + len(kernels().h3_configs))
-            or H3K_BASE <= cid < H3K_BASE + len(H3K_CONFIGS) or is_h3r(cid))
+            or H3K_BASE <= cid < H3K_BASE + len(H3K_CONFIGS) or is_h3r(cid)
+            or is_h3t(cid))
+
+
+def is_h3t(cid: int) -> bool:
+    from .native import kernels
+    return H3T_BASE <= cid < H3T_BASE + kernels().h3t_variants
 
 
 def is_h3r(cid: int) -> bool:
@@ -367,6 +376,7 @@ class ConvLayerF32:
         self.tune_with_affine = False
         self._x6d = None                     # (split weights, bias) for the x6 direct kernel
         self._h3d = None                     # (weights, bias, in_scale, out_scale) for h3
+        self._h3t = None                     # h3d_buffers in the per-tap padded K layout (h3t)
         self._x6k_ws: Dict[int, torch.Tensor] = {}
 
     def ksplit_for(self, cid: int, x_shape) -> int:
@@ -417,6 +427,41 @@ class ConvLayerF32:
             self._h3d = (h3_direct_weights(w, sw).to(self.device), b.to(self.device),
                          float(2.0 ** H3_IN_LOG2), float(2.0 ** -(H3_IN_LOG2 + sw)))
         return self._h3d
+
+    @property
+    def h3t_k_pad(self) -> int:
+        """K of the h3t weight layout: every tap padded to 32-channel chunks."""
+        return 3 * 32 * ((self.geom.cin_p + 31) // 32)
+
+    def h3t_buffers(self):
+        """h3d_buffers() with the K layout of the temporal frame-band kernel:
+        tap k's channels at [k * 32 * ceil(Cin_p / 32), ...) (zero padding up
+        to the next 32-channel chunk; the same matrix as h3d when Cin_p % 32
+        == 0)."""
+        if self.geom.cin_p % 32 == 0:
+            return self.h3d_buffers()
+        if self._h3t is None:
+            rows, cin, kp = self.geom.cout_p + X6_ROW_SLACK, self.geom.cin_p, self.h3t_k_pad
+            w = torch.zeros(rows, kp, dtype=torch.float32)
+            tap = kp // 3
+            src = self.wmat[:self.geom.cout, :self.k_total].cpu()
+            for k in range(3):
+                w[:self.geom.cout, k * tap:k * tap + cin] = src[:, k * cin:(k + 1) * cin]
+            b = torch.zeros(rows, dtype=torch.float32)
+            b[:self.geom.cout] = self.bias[:self.geom.cout].cpu()
+            sw = h3_weight_scale_log2(w)
+            self._h3t = (h3_direct_weights(w, sw).to(self.device), b.to(self.device),
+                         float(2.0 ** H3_IN_LOG2), float(2.0 ** -(H3_IN_LOG2 + sw)))
+        return self._h3t
+
+    def h3t_ok(self, x_shape=None) -> bool:
+        """The temporal frame-band h3 kernel: 3x1x1 stride 1 pad (1, 0, 0), T >= 2."""
+        return (self.winot_ok and self.geom.cin_p % 16 == 0
+                and (x_shape is None or x_shape[1] >= 2))
+
+    def h3t_fits(self, variant: int, x_shape) -> bool:
+        from .native import kernels
+        return x_shape is None or kernels().conv_h3t_pixels(variant, x_shape[1]) > 0
 
     def wino_u(self, tc: int, m: int = 2, co0: int = 0, nco: Optional[int] = None,
                x6: bool = False) -> torch.Tensor:
@@ -476,6 +521,9 @@ class ConvLayerF32:
             if self.h3r_ok(x_shape):
                 c += [H3R_BASE + i for i in range(kernels().h3r_variants)
                       if self.h3r_fits(i, x_shape)]
+            if self.h3t_ok(x_shape):
+                c += [H3T_BASE + i for i in range(kernels().h3t_variants)
+                      if self.h3t_fits(i, x_shape)]
             if x_shape is not None and os.environ.get("RNB_X6K", "1") != "0":
                 c += [H3K_BASE + j for j in range(len(H3K_CONFIGS))
                       if self.ksplit_for(H3K_BASE + j, x_shape) > 1]
@@ -579,7 +627,8 @@ class ConvLayerF32:
         return tab
 
     def params(self, x: torch.Tensor, y: torch.Tensor, residual: Optional[torch.Tensor],
-               n0: int = 0, n1: Optional[int] = None, x6: bool = False, h3: bool = False):
+               n0: int = 0, n1: Optional[int] = None, x6: bool = False, h3: bool = False,
+               h3t: bool = False):
         """Launch parameters for clips [n0, n1) of the batch (``x6``: for the
         x6 direct kernel: split weights, K rounded to 16; ``h3``: for the h3
         kernel: split fp16 weights, K rounded to 32)."""
@@ -613,7 +662,11 @@ class ConvLayerF32:
         p.w_rows = self.wmat.shape[0]
         p.ktab = self.ktab(T, H, W, x.device).data_ptr()
         p.row_mode = 0
-        if h3:
+        if h3t:
+            wx, bx, _, _ = self.h3t_buffers()
+            p.w, p.bias = wx.data_ptr(), bx.data_ptr()
+            p.K_pad, p.w_rows = self.h3t_k_pad, bx.shape[0]
+        elif h3:
             wx, bx, _, _ = self.h3d_buffers()
             p.w, p.bias = wx.data_ptr(), bx.data_ptr()
             p.K_pad, p.w_rows = self.k_pad, bx.shape[0]
@@ -698,15 +751,17 @@ class ConvLayerF32:
         # csrc/conv_h3.hip kH3RConfigs: 0-5 conv_h3r_kernel (x 2 barrier
         # groupings), 6 / 7 conv_h3q_kernel (4 waves x 7 / 4 tiles)
         nw, tp, halo = ((7, 4, 600), (14, 2, 600), (7, 3, 480))[variant % 3] if variant < 6 \
-            else ((4, 7, 600), (4, 4, 352), (8, 4, 640))[variant - 6]
+            else ((4, 7, 600), (4, 4, 344), (8, 4, 640))[variant - 6]
         rows = nw * tp * 16 // W
-        if rows < 1 or (rows + 2) * (W + 2) > halo:
+        # conv_h3q_kernel rows hold W + 1 entries (one shared zero column) + 1
+        entries = (rows + 2) * (W + 2) if variant < 6 else (rows + 2) * (W + 1) + 1
+        if rows < 1 or entries > halo:
             return False
         return not efficient or 2 * min(rows, H) * W >= nw * tp * 16
 
     def affine_ok(self, cid: int, x_shape) -> bool:
         """Whether config ``cid`` can apply the input's BN + ReLU on load."""
-        if cid in WINO_TEMPORAL or is_h3r(cid):
+        if cid in WINO_TEMPORAL or is_h3r(cid) or is_h3t(cid):
             return True
         if not is_h3(cid):
             return False
@@ -757,9 +812,21 @@ class ConvLayerF32:
         step = self.chunk_clips(x.shape, y.shape,
                                 residual.shape[-1] if residual is not None else 0)
         h3 = is_h3(cid)
+        h3t = is_h3t(cid)
         for n0 in range(0, N, step):
-            p = self.params(x, y, residual, n0, min(N, n0 + step), x6=x6 and not h3, h3=h3)
-            if is_h3r(cid):
+            p = self.params(x, y, residual, n0, min(N, n0 + step), x6=x6 and not h3, h3=h3,
+                            h3t=h3t)
+            if h3t:
+                _, _, s_in, s_out = self.h3t_buffers()
+                aff = ((in_affine[0].data_ptr(), in_affine[1].data_ptr() + 4 * n0)
+                       if in_affine is not None else (0, 0))
+                if out_stats is not None:
+                    k.conv_h3t(p, cid - H3T_BASE, stream.cuda_stream, s_in, s_out,
+                               out_stats[0].data_ptr(), out_stats[1].data_ptr() + 4 * n0,
+                               out_stats[0].shape[2], *aff)
+                else:
+                    k.conv_h3t(p, cid - H3T_BASE, stream.cuda_stream, s_in, s_out, 0, 0, 0, *aff)
+            elif is_h3r(cid):
                 _, _, s_in, s_out = self.h3d_buffers()
                 aff = ((in_affine[0].data_ptr(), in_affine[1].data_ptr() + 4 * n0)
                        if in_affine is not None else (0, 0))

@@ -325,6 +325,10 @@ class Kernels:
                                             ctypes.c_int, ctypes.c_float, ctypes.c_float,
                                             ctypes.c_void_p, ctypes.c_void_p]
         lib.rnb_conv_h3r_launch.restype = ctypes.c_int
+        lib.rnb_conv_h3t_launch.argtypes = lib.rnb_conv_h3r_launch.argtypes
+        lib.rnb_conv_h3t_launch.restype = ctypes.c_int
+        lib.rnb_conv_h3t_pixels.argtypes = [ctypes.c_int, ctypes.c_int]
+        lib.rnb_conv_h3t_pixels.restype = ctypes.c_int
         lib.rnb_conv_h3_config_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                                 ctypes.POINTER(ctypes.c_int)]
         lib.rnb_preprocess_f32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
@@ -355,6 +359,7 @@ class Kernels:
         self.f32_max_bytes = lib.rnb_conv_f32_max_bytes()
         self.x6r_variants = lib.rnb_conv_x6r_num_variants()
         self.h3r_variants = lib.rnb_conv_h3r_num_variants()
+        self.h3t_variants = lib.rnb_conv_h3t_num_variants()
         self.x6_configs = []       # (pixel tile, channel tile) per x6 direct config
         for i in range(lib.rnb_conv_x6_num_configs()):
             p, c = ctypes.c_int(), ctypes.c_int()
@@ -416,6 +421,20 @@ class Kernels:
                                             sums or None, clip_seg or None, stats_c, in_scale,
                                             out_scale, in_ss or None, in_seg or None),
                "conv_h3r (variant %d)" % variant)
+
+    def conv_h3t(self, params: ConvParams, variant: int, stream: int, in_scale: float,
+                 out_scale: float, sums: int = 0, clip_seg: int = 0, stats_c: int = 0,
+                 in_ss: int = 0, in_seg: int = 0) -> None:
+        """h3 temporal frame-band conv (3x1x1 stride 1 pad (1, 0, 0), weights
+        padded per tap to 32-channel chunks); the arguments as ``conv_h3``."""
+        _check(self.lib.rnb_conv_h3t_launch(ctypes.byref(params), variant, stream,
+                                            sums or None, clip_seg or None, stats_c, in_scale,
+                                            out_scale, in_ss or None, in_seg or None),
+               "conv_h3t (variant %d)" % variant)
+
+    def conv_h3t_pixels(self, variant: int, T: int) -> int:
+        """Pixels per block of h3t variant ``variant`` for T frames (0: cannot run)."""
+        return int(self.lib.rnb_conv_h3t_pixels(variant, T))
 
     def conv_h3_affine_ok(self, config_id: int, cin_p: int, rows_per_clip: int) -> bool:
         return bool(self.lib.rnb_conv_h3_affine_ok(config_id, cin_p, rows_per_clip))

@@ -265,3 +265,79 @@ def test_h3_rowband_matches_fp64(case):
         torch.cuda.synchronize()
         err = (y[..., :cout].double().cpu() - ref).abs().max().item()
         assert err <= 1e-5 * scale, (cid, err, scale)
+
+
+def _h3t_ids():
+    from rnb_amd.ops.conv_f32 import H3T_BASE
+    from rnb_amd.ops.native import kernels
+    return [H3T_BASE + i for i in range(kernels().h3t_variants)]
+
+
+@pytest.mark.parametrize("thw,cin,cout", [((8, 9, 7), 80, 72), ((4, 14, 14), 64, 150),
+                                          ((2, 7, 7), 144, 64), ((8, 8, 8), 48, 130)])
+def test_h3_temporal_band_exact_integers_stats_and_affine(thw, cin, cout):
+    """Temporal frame-band h3 kernel (conv_h3t_kernel): bit-exact on small
+    integers (zero frames at both clip ends, a partial last pixel block,
+    Cin_p % 32 == 16: the last chunk's upper half zero-padded per tap,
+    residual + ReLU epilogue) for every variant that fits T; epilogue BN
+    sums per video vs fp64 sums of the output; the input BN + ReLU on load
+    within 1e-5 of the fp64 conv of the applied input."""
+    layer = _layer(cin, cout, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=True, integer=True)
+    x = _input(3, thw, layer.geom.cin_p, cin, integer=True)
+    res = _input(3, thw, layer.geom.cout_p, cout, integer=True, seed=3)
+    ref = _ref64(layer, x, res).float()
+    assert layer.h3t_ok(x.shape)
+    ids = [c for c in _h3t_ids() if layer.h3t_fits(c - _h3t_ids()[0], x.shape)]
+    assert ids, thw
+    for cid in ids:
+        y = layer.forward_hip(x, res, config=cid)
+        torch.cuda.synchronize()
+        assert torch.equal(y[..., :cout].cpu(), ref), cid
+        assert torch.all(y[..., cout:] == 0), cid
+    lay2 = _layer(cin, cout, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=False)
+    xf = _input(3, thw, lay2.geom.cin_p, cin)
+    seg = torch.tensor([0, 2, 2], dtype=torch.int32, device=DEV)
+    g = torch.Generator().manual_seed(11)
+    cp = lay2.geom.cin_p
+    ss = torch.empty((3, 2, cp), dtype=torch.float32)
+    ss[:, 0] = torch.rand((3, cp), generator=g) + 0.5
+    ss[:, 1] = torch.randn((3, cp), generator=g) * 0.5
+    ss = ss.to(DEV)
+    xa = torch.relu(xf * ss[seg.long(), 0][:, None, None, None, :] +
+                    ss[seg.long(), 1][:, None, None, None, :])
+    ref_a = _ref64(lay2, xa)
+    scale = ref_a.abs().max().item()
+    for cid in ids:
+        sums = torch.zeros((3, 2, lay2.geom.cout_p), dtype=torch.float64, device=DEV)
+        y = lay2.forward_hip(xf, config=cid, out_stats=(sums, seg))
+        torch.cuda.synchronize()
+        yd = y[..., :cout].double().cpu()
+        for v, (a, b) in enumerate([(0, 1), (1, 1), (1, 3)]):
+            part = yd[a:b].reshape(-1, cout)
+            got = sums[v, :, :cout].cpu()
+            assert ((got[0] - part.sum(0)).abs() <= 1e-6 * part.abs().sum(0) + 1e-9).all(), cid
+            assert torch.allclose(got[1], (part * part).sum(0), rtol=1e-6, atol=1e-9), cid
+        for ost in (None, (torch.zeros_like(sums), seg)):
+            ya = lay2.forward_hip(xf, config=cid, in_affine=(ss, seg), out_stats=ost)
+            torch.cuda.synchronize()
+            err = (ya[..., :cout].double().cpu() - ref_a).abs().max().item()
+            assert err <= 1e-5 * scale, (cid, err, scale)
+
+
+@pytest.mark.parametrize("case", [c for c in F32_CASES if c[2] == (3, 1, 1) and c[3] == (1, 1, 1)],
+                         ids=lambda c: "%dx%d" % (c[0], c[1]))
+def test_h3_temporal_band_matches_fp64(case):
+    cin, cout, k, s, p, thw = case
+    layer = _layer(cin, cout, k, s, p)
+    x = _input(2, thw, layer.geom.cin_p, cin)
+    ref = _ref64(layer, x)
+    scale = ref.abs().max().item()
+    ids = [c for c in _h3t_ids() if layer.h3t_ok(x.shape)
+           and layer.h3t_fits(c - _h3t_ids()[0], x.shape)]
+    if not ids:
+        pytest.skip("no frame-band variant for T=%d" % thw[0])
+    for cid in ids:
+        y = layer.forward_hip(x, config=cid)
+        torch.cuda.synchronize()
+        err = (y[..., :cout].double().cpu() - ref).abs().max().item()
+        assert err <= 1e-5 * scale, (cid, err, scale)
