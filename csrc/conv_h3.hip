@@ -763,8 +763,10 @@ void conv_h3q_kernel(const ConvF32Params p, const X6DStats st) {
 // second weight buffer), so HBM stays busy through the MFMA phase. Cin_p %
 // 16 == 0: a chunk whose upper 16 channels are past Cin_p loads zeros there
 // (the host pads each tap's weights to 32-channel chunks).
-template <int NW, int TP, int TC, int HALO, bool ST, bool AFF>
-__global__ __launch_bounds__(64 * NW, 1)
+// WB = weight buffers: 2 = the next chunk's weights DMA'd during this
+// chunk's MFMAs; 1 = after them (smaller LDS: two blocks per CU cover it).
+template <int NW, int TP, int TC, int HALO, int WB, int MINB, bool ST, bool AFF>
+__global__ __launch_bounds__(64 * NW, MINB)
 void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
   constexpr int ROWS = NW * TP * 16, C_TILE = TC * 16;
   constexpr int HALO_BYTES = HALO * 128;
@@ -776,7 +778,7 @@ void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
   constexpr int ITEMS = (HALO * 4 + NT - 1) / NT;    // (entry, quad) items per lane
   static_assert(NT % 4 == 0 && TAP_BYTES % 1024 == 0, "staging / DMA split");
   static_assert(TP <= TC * 3 - 1, "next-tap fragments are read during the channel tiles");
-  __shared__ __attribute__((aligned(16))) char lds[HALO_BYTES + 2 * W_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[HALO_BYTES + WB * W_BYTES];
   char* const wbuf = lds + HALO_BYTES;
 
   const int lane = threadIdx.x & 63;
@@ -907,14 +909,15 @@ void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
   load_chunk(0);
   for (int c = 0; c < nck; ++c) {
     if (c > 0) x6d_barrier();                        // every wave is done with chunk c - 1
+    if (WB == 1 && c > 0) issue_w(c, 0);             // the only buffer is free now
     store_chunk(c);
     x6d_wait_vm<0>();                                // chunk c's weights landed (this wave) ...
     x6d_barrier();                                   // ... the patch and weights in every wave
     if (c + 1 < nck) {
-      issue_w(c + 1, (c + 1) & 1);                   // DMA first, then the patch loads
+      if (WB == 2) issue_w(c + 1, (c + 1) & 1);      // DMA first, then the patch loads
       load_chunk(c + 1);
     }
-    const int buf = c & 1;
+    const int buf = WB == 2 ? (c & 1) : 0;
     H3B bf[2][TP];
     wu32x4 wh[2], wl[2];
 #pragma unroll
@@ -1245,23 +1248,27 @@ int rnb_conv_h3r_launch(const ConvF32Params* pp, int variant, hipStream_t stream
 // Temporal frame-band h3 kernel (conv_h3t_kernel): 3x1x1 stride 1 pad
 // (1, 0, 0), Cin_p % 16 == 0, T >= 2. Variants: 0 = 8 waves x 4 tiles (512
 // rows: P = 512 / T pixels) x 64 channels, 1 = 8 waves x 2 tiles (256 rows) x
-// 64 channels, 2 = 8 waves x 2 tiles x 128 channels. p.w = split weights with
+// 64 channels, 2 = 8 waves x 2 tiles x 128 channels, 3 = 4 waves x 4 tiles
+// (256 rows) x 64 channels with one weight buffer (two blocks per CU). p.w = split weights with
 // every tap padded to whole 32-channel chunks: step s = tap * ceil(Cin_p / 32)
 // + chunk (p.K_pad = 3 * 32 * ceil(Cin_p / 32)).
 struct ConvH3TConfig {
-  int rows, c_tile, halo;
+  int rows, c_tile, halo, nw;
   void (*kernel)(const ConvF32Params, const X6DStats);
   void (*kernel_st)(const ConvF32Params, const X6DStats);
   void (*kernel_aff)(const ConvF32Params, const X6DStats);
   void (*kernel_aff_st)(const ConvF32Params, const X6DStats);
 };
-#define H3TCFG(NW, TP, TC, HALO)                                                   \
-  {NW * TP * 16, TC * 16, HALO, conv_h3t_kernel<NW, TP, TC, HALO, false, false>,   \
-   conv_h3t_kernel<NW, TP, TC, HALO, true, false>,                                 \
-   conv_h3t_kernel<NW, TP, TC, HALO, false, true>,                                 \
-   conv_h3t_kernel<NW, TP, TC, HALO, true, true>}
+#define H3TCFG(NW, TP, TC, HALO, WB, MINB)                                         \
+  {NW * TP * 16, TC * 16, HALO, NW,                                                  \
+   conv_h3t_kernel<NW, TP, TC, HALO, WB, MINB, false, false>,                       \
+   conv_h3t_kernel<NW, TP, TC, HALO, WB, MINB, true, false>,                        \
+   conv_h3t_kernel<NW, TP, TC, HALO, WB, MINB, false, true>,                        \
+   conv_h3t_kernel<NW, TP, TC, HALO, WB, MINB, true, true>}
 static const ConvH3TConfig kH3TConfigs[] = {
-    H3TCFG(8, 4, 4, 768), H3TCFG(8, 2, 4, 512), H3TCFG(8, 2, 8, 512),
+    H3TCFG(8, 4, 4, 768, 2, 1), H3TCFG(8, 2, 4, 512, 2, 1), H3TCFG(8, 2, 8, 512, 2, 1),
+    // 3: 4 waves x 4 tiles x 64 channels, one weight buffer, 72 KB: two blocks per CU
+    H3TCFG(4, 4, 4, 384, 1, 2),
 };
 
 int rnb_conv_h3t_num_variants() { return (int)(sizeof(kH3TConfigs) / sizeof(kH3TConfigs[0])); }
@@ -1320,7 +1327,7 @@ int rnb_conv_h3t_launch(const ConvF32Params* pp, int variant, hipStream_t stream
   const bool aff = in_ss != nullptr;
   hipLaunchKernelGGL(aff ? (sums ? cfg.kernel_aff_st : cfg.kernel_aff)
                          : (sums ? cfg.kernel_st : cfg.kernel),
-                     dim3((unsigned)blocks), dim3(512), 0, stream, p, st);
+                     dim3((unsigned)blocks), dim3(64 * cfg.nw), 0, stream, p, st);
   return (int)hipGetLastError();
 }
 
