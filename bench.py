@@ -486,6 +486,9 @@ def run_cross_gpu_extras(args) -> dict:
                "--warmup", "1", "--dtype", args.dtype, "--bn", args.bn,
                "--depth", str(args.depth), "--latency-seconds", "2",
                "--loaders", str(args.loaders), "--replicas", str(args.replicas),
+               # 16-clip graph buckets: a quarter of the headline's graph
+               # captures in each extra's setup (4 short steps, padding cost small)
+               "--bucket-step", str(max(args.bucket_step, 16)),
                "--no-check", "--no-cross-gpu-extras", "--json-out", path]
         env = {k: v for k, v in os.environ.items()
                if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",

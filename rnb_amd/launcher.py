@@ -307,14 +307,30 @@ def run(args) -> dict:
     from threading import BrokenBarrierError
     time_start = time_end = None
     broken = False
+    # setup heartbeat: model build, autotune and graph capture of every
+    # process can take minutes (N runners folded onto one device: many), and
+    # a silent launcher looks hung to whoever watches its output
+    setup_done = threading.Event()
+
+    def heartbeat():
+        while not setup_done.wait(30.0):
+            try:
+                ready = sta_bar.n_waiting
+            except Exception:
+                ready = -1
+            print("[launcher] setup: %d of %d processes ready after %.0f s"
+                  % (ready, sta_bar.parties - 1, time.time() - t_spawn), flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     try:
         sta_bar.wait(args.barrier_timeout)
+        setup_done.set()
         time_start = time.time()
         print("START! %f" % time_start, flush=True)
         fin_bar.wait(args.barrier_timeout)
         time_end = time.time()
         print("FINISH! %f" % time_end, flush=True)
     except BrokenBarrierError:
+        setup_done.set()
         broken = True
         with flag.get_lock():
             if flag.value == TerminationFlag.UNSET:
