@@ -84,11 +84,14 @@ def parse_args(argv=None):
                          "replicas per GPU with a queue per GPU -- at 1 GPU the same "
                          "topology as global (one shared queue), at N GPUs no slot "
                          "crosses xGMI; global shares one queue across all GPUs")
-    ap.add_argument("--route", default="none", choices=["none", "large-small"],
-                    help="(aggressive) large-small: the reference's content routing "
-                         "(config/rnb.json, models/r2p1d/model.py:288-296) -- 15-clip videos "
-                         "go to their own queue and runner replica per GPU "
-                         "(--large-replicas), the others batch among themselves")
+    ap.add_argument("--route", default="large-small", choices=["none", "large-small"],
+                    help="(aggressive) large-small (default since round 4): the reference's "
+                         "content routing (config/rnb.json, models/r2p1d/model.py:288-296) -- "
+                         "15-clip videos go to their own queue and runner replica per GPU "
+                         "(--large-replicas) on a high-priority stream, the others batch among "
+                         "themselves. Interleaved A/B, 3 rounds: 1597 vs 1572 videos/s, Poisson "
+                         "p99/p50 3.26 vs 3.62 at half load and 3.35 vs 3.73 at mi = 10 "
+                         "(profiles/r4_ab_route_priority.txt); none = one queue per GPU")
     ap.add_argument("--large-replicas", type=int, default=1,
                     help="(--route large-small) runner replicas per GPU for 15-clip videos")
     ap.add_argument("--segments", type=int, default=None,
@@ -130,9 +133,9 @@ def parse_args(argv=None):
                          "a 256-clip R(2+1)D-34 runner holds ~19 GB)")
     ap.add_argument("--bucket-step", type=int, default=4,
                     help="HIP-graph clip buckets every this many clips")
-    ap.add_argument("--large-priority", action="store_true",
-                    help="(--route large-small) the 15-clip-video replicas run on "
-                         "high-priority streams")
+    ap.add_argument("--no-large-priority", dest="large_priority", action="store_false",
+                    help="(--route large-small) keep the 15-clip-video replicas on "
+                         "normal-priority streams")
     ap.add_argument("--lanes", type=int, default=1,
                     help="graphed engines per runner process, calls rotating over their "
                          "streams (R2P1DRunner lanes: one-video calls overlap on the GPU)")
@@ -195,7 +198,8 @@ def pipeline_config(args, n_gpus: int) -> dict:
     if args.pipeline == "global":
         steps = [{"model": LOADER, "queue_groups": [{"gpus": loader_gpus, "out_queues": [0]}]},
                  dict(runner, queue_groups=[{"gpus": runner_gpus, "in_queue": 0}])]
-    elif args.pipeline == "aggressive" and args.route == "large-small":
+    elif args.pipeline == "aggressive" and args.route == "large-small" and args.replicas >= 2:
+        # (one replica per GPU: nothing to split, one queue per GPU below)
         # per GPU: queue 2g (1-clip videos, batched) and 2g + 1 (15-clip videos)
         nl = max(1, min(args.large_replicas, args.replicas - 1))
         steps = [{"model": LOADER,
