@@ -382,17 +382,24 @@ def test_bench_pipeline_configs_parse():
 
 
 def test_bench_default_topology_is_per_gpu():
-    """bench.py's default pipeline (aggressive): at 1 GPU the same topology as
-    global, at N GPUs every runner queue is fed only by loaders on its own GPU
-    (no slot crosses xGMI in the driver's scaling runs)."""
+    """bench.py's default pipeline (aggressive): at 1 GPU without routing the
+    same topology as global; by default LargeSmall routing per GPU (15-clip
+    videos to their own queue and high-priority replica); at N GPUs every
+    runner queue is fed only by loaders on its own GPU (no slot crosses xGMI
+    in the driver's scaling runs)."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    a1 = bench.pipeline_config(bench.parse_args([]), 1)
+    a1 = bench.pipeline_config(bench.parse_args(["--route", "none"]), 1)
     g1 = bench.pipeline_config(bench.parse_args(["--pipeline", "global"]), 1)
     assert bench.parse_args([]).pipeline == "aggressive"
     assert a1 == g1
+    d1 = bench.pipeline_config(bench.parse_args([]), 1)
+    loader, runner = d1["pipeline"]
+    assert loader["queue_groups"][0]["out_queues"] == [0, 1]
+    assert [g["gpus"] for g in runner["queue_groups"]] == [[0, 0], [0]]
+    assert runner["group_stream_priority"] == [0, -1]
     cfg = bench.pipeline_config(bench.parse_args(["--gpus", "8"]), 8)
     loader, runner = cfg["pipeline"]
     feeds = {}
