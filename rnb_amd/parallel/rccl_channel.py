@@ -35,6 +35,7 @@ transport on edges whose producer and consumers sit on different GPUs.
 """
 from __future__ import annotations
 
+import collections
 import os
 import queue
 import threading
@@ -135,9 +136,11 @@ class RcclRing(RingBase):
       model's direct write) is followed by a "written" event; the sender
       thread's stream waits on that event, so the producer never blocks.
     * The sender thread drains up to 16 claims at a time and issues their
-      sends as one ``batch_isend_irecv`` group (one NCCL group launch); each
-      completion is awaited with a timeout (``RNB_RCCL_TIMEOUT_S``, default
-      120 s) and the slot is freed only after its send completed.
+      sends as one ``batch_isend_irecv`` group (one NCCL group launch). A
+      batch's completion is an event on the sender stream: its slots are
+      freed once the event has completed, while the thread keeps serving
+      later claims (no host synchronisation per batch); on gloo each send is
+      awaited with a timeout (``RNB_RCCL_TIMEOUT_S``, default 120 s).
     * The consumer posts its claim and queues its ``irecv``s in the call's
       ``pending`` list; ``flush_recvs`` launches them. On gloo the host waits
       with the same timeout and raises, so the launcher's watchdog aborts the
@@ -191,10 +194,22 @@ class RcclRing(RingBase):
             torch.cuda.set_device(self.device)
         stream = torch.cuda.Stream(self.device) if cuda else None
         ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
+        # sent batches whose buffers are still in use on the GPU: (completion
+        # event, slots); a slot is freed once its batch's event has completed,
+        # while the thread keeps serving claims (no host sync per batch)
+        inflight = collections.deque()
+
+        def retire(block: bool = False) -> None:
+            while inflight and (block or inflight[0][0].query()):
+                ev, slots = inflight.popleft()
+                ev.synchronize()
+                for i in slots:
+                    self.events[i].set()
         with ctx:
             while not self._stop.is_set():
+                retire()
                 try:
-                    claim = self.claims.get(timeout=0.1)
+                    claim = self.claims.get(timeout=0.001 if inflight else 0.1)
                 except queue.Empty:
                     continue
                 if claim is None:
@@ -219,14 +234,19 @@ class RcclRing(RingBase):
                                 ops.append(dist.P2POp(dist.isend, t[:rows], dst))
                     works = dist.batch_isend_irecv(ops) if ops else []
                     for w in works:
-                        w.wait(_timeout())
+                        w.wait(_timeout())   # gloo: done; nccl: this stream waits on the sends
                     if stream is not None:
-                        stream.synchronize()     # send buffers free for reuse
+                        ev = torch.cuda.Event()
+                        ev.record(stream)         # send buffers free for reuse after this
+                        inflight.append((ev, [idx for idx, _ in batch]))
+                        continue
                 except Exception as err:  # surfaced on the producer's next write
                     self._error = err
                     break
                 for idx, _ in batch:
                     self.events[idx].set()
+            if self._error is None:
+                retire(block=True)
 
     def raise_if_failed(self):
         if self._error is not None:
