@@ -349,7 +349,7 @@ __global__ __launch_bounds__(64) void bn_seg_sums_walk_f32_kernel(BnSegParams p,
 // instead of two.
 #define BN_FR_CH 64
 #define BN_FR_SL 16
-#define BN_FR_MAX_SEG 32
+#define BN_FR_MAX_SEG 256
 // FROM_SUMS: moments from a producer epilogue's fp64 sums [nseg][2][sums_c]
 // (re-armed to zero here), as bn_seg_finalize_sums_f32_kernel.
 template <bool FROM_SUMS>
@@ -638,8 +638,12 @@ extern "C" {
 // one-video forwards). A split sized to fill the chip from (nseg, C, M)
 // measured the same (13.4 ms per 24-clip forward, 60.2 ms per 128).
 static int g_bn_fixed_bps = 0;     // > 0: override (experiments)
-static int g_bn_fused_finalize = 1;  // 0: separate finalize + running kernels (A/B)
-void rnb_bn_seg_set_fused_finalize(int on) { g_bn_fused_finalize = on; }
+// fused finalize + running kernel up to this many segments (larger: separate
+// finalize + running kernels); 0 = never (A/B)
+static int g_bn_fused_finalize = 32;
+void rnb_bn_seg_set_fused_finalize(int max_seg) {
+  g_bn_fused_finalize = max_seg < 0 ? 0 : (max_seg > BN_FR_MAX_SEG ? BN_FR_MAX_SEG : max_seg);
+}
 void rnb_bn_seg_set_bps(int bps) { g_bn_fixed_bps = bps > BN_SEG_MAX_BPS ? BN_SEG_MAX_BPS : bps; }
 
 int rnb_bn_seg_bps(int nseg, int C, long long M) {
@@ -674,7 +678,7 @@ int rnb_bn_seg_stats_f32(const float* y, const int* coffs, int nseg, int rpc, lo
   p.channels = channels; p.running_mean = running_mean; p.running_var = running_var;
   p.mean = mean; p.var = var; p.ss = ss;
   hipLaunchKernelGGL(bn_seg_sums_f32_kernel, dim3(p.bps, nseg), dim3(256), 0, stream, p);
-  if (g_bn_fused_finalize && nseg <= BN_FR_MAX_SEG) {
+  if (nseg <= g_bn_fused_finalize) {
     hipLaunchKernelGGL(bn_seg_finalize_running_f32_kernel<false>,
                        dim3((C + BN_FR_CH - 1) / BN_FR_CH), dim3(BN_FR_CH * BN_FR_SL), 0, stream,
                        p, (double*)nullptr, 0);
@@ -702,7 +706,7 @@ int rnb_bn_seg_stats_from_sums_f32(double* sums, int sums_c, const int* coffs, i
   p.run_acc = run_acc; p.gamma = gamma; p.beta = beta; p.eps = eps; p.momentum = momentum;
   p.channels = channels; p.running_mean = running_mean; p.running_var = running_var;
   p.mean = mean; p.var = var; p.ss = ss;
-  if (g_bn_fused_finalize && nseg > BN_WALK_MAX_SEG && nseg <= BN_FR_MAX_SEG) {
+  if (nseg > BN_WALK_MAX_SEG && nseg <= g_bn_fused_finalize) {
     hipLaunchKernelGGL(bn_seg_finalize_running_f32_kernel<true>,
                        dim3((C + BN_FR_CH - 1) / BN_FR_CH), dim3(BN_FR_CH * BN_FR_SL), 0, stream,
                        p, sums, sums_c);

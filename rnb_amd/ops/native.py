@@ -235,7 +235,8 @@ class Kernels:
             lib.rnb_bn_seg_set_bps(int(os.environ["RNB_BN_BPS"]))
         lib.rnb_bn_seg_set_fused_finalize.argtypes = [ctypes.c_int]
         if os.environ.get("RNB_BN_FUSED_FINALIZE"):
-            # 0: separate finalize + running-update kernels (A/B)
+            # fused finalize + running-update kernel up to this many videos
+            # per launch (default 32; 0: separate kernels, A/B)
             lib.rnb_bn_seg_set_fused_finalize(int(os.environ["RNB_BN_FUSED_FINALIZE"]))
         lib.rnb_bn_seg_scratch_floats.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_longlong]
         lib.rnb_bn_seg_scratch_floats.restype = ctypes.c_longlong

@@ -228,6 +228,12 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         model_event = getattr(model, "completion_event", None)
         if not callable(model_event):
             model_event = None
+        if callable(lane_inflight) and int(lane_inflight()) > 0:
+            # calls overlap on the model's lanes: "wait while the previous call
+            # runs" (adaptive gathering, the latency backlog rule) would
+            # serialise them again (--pipeline whole, 2 replicas x 2 lanes:
+            # 345 videos/s against 559 for one runner with two lanes)
+            adaptive_gather = False
         final_pending = []
 
         def complete_final(limit: int) -> bool:

@@ -649,13 +649,14 @@ def test_deferred_batch_bn_into_temporal_winograd_matches_separate_apply(monkeyp
 
 
 @pytest.mark.parametrize("source,nseg", [("pass", 14), ("pass", 28), ("pass", 41),
-                                         ("sums", 14), ("sums", 28), ("sums", 41)])
+                                         ("pass", 130), ("sums", 14), ("sums", 28),
+                                         ("sums", 41), ("sums", 130)])
 def test_bn_fused_finalize_running_matches_split_kernels_and_torch(source, nseg):
     """BN statistics per video, every finalize path against the others and an
-    fp64 torch reference: statistics pass with <= 32 segments (the fused
-    finalize + running-update kernel, 16 segment waves, vs the separate
-    kernels), > 32 segments (separate kernels), epilogue sums (in-order walk
-    <= 16, fused kernel 17..32, separate kernels above). Per-segment mean / var / scale / shift, the running statistics
+    fp64 torch reference: the fused finalize + running-update kernel (16
+    segment waves, up to 256 segments) vs the separate kernels, from a
+    statistics pass and from epilogue sums (in-order walk <= 16 segments).
+    Per-segment mean / var / scale / shift, the running statistics
     (segments with < 2 rows skipped), 88 channels (a partial 64-channel
     block), empty and one-row segments; epilogue sums re-armed to zero."""
     from rnb_amd.ops.bn import BatchNormBatch
@@ -678,7 +679,7 @@ def test_bn_fused_finalize_running_matches_split_kernels_and_torch(source, nseg)
     y = (torch.randn((M, C), generator=g) * 2 + 0.5).to(DEV)
     seg = torch.tensor(offs, dtype=torch.int32, device=DEV)
     outs = []
-    for fused in (1, 0):
+    for fused in (256, 0):               # fused finalize + running up to 256 segments / never
         op = BatchNormBatch(bn, C, DEV)
         sums = None
         if source == "sums":
@@ -692,7 +693,7 @@ def test_bn_fused_finalize_running_matches_split_kernels_and_torch(source, nseg)
         try:
             mean, var, ss = op._stats_ss(y.view(M, 1, 1, 1, C), seg, sums, 1)
         finally:
-            k.lib.rnb_bn_seg_set_fused_finalize(1)
+            k.lib.rnb_bn_seg_set_fused_finalize(32)
         torch.cuda.synchronize()
         if sums is not None:
             assert float(sums.abs().sum()) == 0.0, "epilogue sums must be re-armed"
