@@ -37,9 +37,11 @@ def tile_name(cid, f32=False):
         from rnb_amd.ops.conv_f32 import (X6D_BASE, X6R_BASE, X6K_BASE, X6K_CONFIGS, is_x6d,
                                           is_x6r, is_x6k, H3D_BASE, H3K_BASE, H3K_CONFIGS,
                                           is_h3, is_h3k)
-        from rnb_amd.ops.conv_f32 import H3R_BASE, is_h3r
+        from rnb_amd.ops.conv_f32 import H3R_BASE, H3T_BASE, is_h3r, is_h3t
         if is_h3r(cid):
             return "h3r_%d" % (cid - H3R_BASE)
+        if is_h3t(cid):
+            return "h3t_%d" % (cid - H3T_BASE)
         if is_h3k(cid):
             return "h3k_%dx%d" % k.h3_configs[H3K_CONFIGS[cid - H3K_BASE]]
         if is_h3(cid):
