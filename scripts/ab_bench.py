@@ -29,14 +29,20 @@ def run(name, env, extra, timeout, idx):
     e.update(env)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + BASE + extra + ["--json-out", out]
     t0 = time.time()
+    # the child's output goes to a log under gpurun_out/ as it runs (the
+    # launcher's setup heartbeat keeps it growing: a GPU box kills commands
+    # that write nothing for minutes)
+    log = out[:-5] + ".log"
     try:
-        p = subprocess.run(cmd, env=e, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
-                           timeout=timeout, start_new_session=True)
+        with open(log, "w") as f:
+            p = subprocess.run(cmd, env=e, stdout=f, stderr=subprocess.STDOUT,
+                               timeout=timeout, start_new_session=True)
         rc = p.returncode
     except subprocess.TimeoutExpired:
         rc = "timeout"
     if rc != 0 or not os.path.exists(out):
-        tail = p.stderr.decode(errors="replace").strip().splitlines()[-2:] if rc != "timeout" else []
+        with open(log) as f:
+            tail = f.read().strip().splitlines()[-2:]
         return {"name": name, "rc": rc, "wall_s": round(time.time() - t0, 1), "stderr": tail}
     d = json.load(open(out))
     mi = d.get("latency_mi10") or {}
