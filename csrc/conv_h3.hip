@@ -419,8 +419,12 @@ void conv_h3r_kernel(const ConvF32Params p, const X6DStats st) {
   const float* ssv = nullptr;                // AFF: this frame's video's scale / shift
   if constexpr (AFF) ssv = st.in_ss + (size_t)st.in_seg[f / p.T] * 2 * p.Cin_p + qd * 4;
   const float in_scale = st.in_scale;
-  // items in batches of SB (the AFF form keeps the scale / shift live too)
-  constexpr int SB = AFF ? (NW > 8 ? 1 : 2) : ITEMS;
+  // items in batches of SB (the AFF form keeps the scale / shift live too;
+  // 2 items per batch left the AFF staging latency-bound: conv2's second
+  // spatial conv ran 1.68-1.85 ms with BN on load vs 1.40 ms without)
+  // (AFF: 3 items' loads in flight at 4 tiles per wave, every item at 3:
+  // the largest batches that compile without scratch)
+  constexpr int SB = AFF ? (NW > 8 ? 1 : (TP >= 4 ? 3 : ITEMS)) : ITEMS;
   auto stage = [&](int chunk) {
     x6f32x4 sc0, sh0, sc1, sh1;
     if constexpr (AFF) {
@@ -619,7 +623,7 @@ void conv_h3q_kernel(const ConvF32Params p, const X6DStats st) {
   const float* ssv = nullptr;
   if constexpr (AFF) ssv = st.in_ss + (size_t)st.in_seg[f / p.T] * 2 * p.Cin_p + qd * 4;
   const float in_scale = st.in_scale;
-  constexpr int SB = AFF ? 2 : 5;
+  constexpr int SB = AFF ? (NW == 4 && MINB == 1 ? 5 : 2) : 5;
   auto stage = [&](int chunk) {
     x6f32x4 sc0, sh0, sc1, sh1;
     if constexpr (AFF) {

@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--clips", type=int, default=128)
     ap.add_argument("--configs", type=int, nargs="+", default=[1383, 1386, 1388])
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--affine", action="store_true", help="input BN + ReLU on load (AFF)")
+    ap.add_argument("--stats", action="store_true", help="epilogue BN sums (ST)")
     args = ap.parse_args()
     if args.build_only or not os.path.exists(OUT):
         build()
@@ -78,16 +80,26 @@ def main():
         if op.layer.name != args.layer:
             bufs[op.dst] = y
             continue
+        kw = {}
+        N = src.shape[0]
+        seg = torch.zeros(N, dtype=torch.int32, device=dev)
+        if args.affine:
+            ss = torch.ones((1, 2, src.shape[-1]), dtype=torch.float32, device=dev)
+            ss[:, 1] = 0.0
+            kw["in_affine"] = (ss, seg)
+        if args.stats:
+            kw["out_stats"] = (torch.zeros((1, 2, op.layer.geom.cout_p), dtype=torch.float64,
+                                           device=dev), seg)
         for cfg in args.configs:
             real = k.lib
             try:
                 k.lib = _Proxy(real, exp)
-                op.layer.forward_hip(src, res, out=y, config=cfg)      # warm
+                op.layer.forward_hip(src, res, out=y, config=cfg, **kw)      # warm
                 torch.cuda.synchronize()
                 buf.zero_()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
-                op.layer.forward_hip(src, res, out=y, config=cfg)
+                op.layer.forward_hip(src, res, out=y, config=cfg, **kw)
                 e.record()
                 e.synchronize()
             finally:
