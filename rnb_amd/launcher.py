@@ -312,6 +312,8 @@ def run(args) -> dict:
     # a silent launcher looks hung to whoever watches its output
     setup_done = threading.Event()
 
+    run_done = threading.Event()
+
     def heartbeat():
         while not setup_done.wait(30.0):
             try:
@@ -320,6 +322,11 @@ def run(args) -> dict:
                 ready = -1
             print("[launcher] setup: %d of %d processes ready after %.0f s"
                   % (ready, sta_bar.parties - 1, time.time() - t_spawn), flush=True)
+        # then the run: completed requests every 30 s (a stalled run shows)
+        t_run = time.time()
+        while not run_done.wait(30.0):
+            print("[launcher] run: %d of %d requests done after %.0f s"
+                  % (counter.value, warm + args.videos, time.time() - t_run), flush=True)
     threading.Thread(target=heartbeat, daemon=True).start()
     try:
         sta_bar.wait(args.barrier_timeout)
@@ -327,10 +334,12 @@ def run(args) -> dict:
         time_start = time.time()
         print("START! %f" % time_start, flush=True)
         fin_bar.wait(args.barrier_timeout)
+        run_done.set()
         time_end = time.time()
         print("FINISH! %f" % time_end, flush=True)
     except BrokenBarrierError:
         setup_done.set()
+        run_done.set()
         broken = True
         with flag.get_lock():
             if flag.value == TerminationFlag.UNSET:
