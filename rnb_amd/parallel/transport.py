@@ -243,6 +243,8 @@ HIP_ERROR_NOT_READY = 600
 # exactly 32 of 200 accepted in every process / stream / context variant), so
 # every slot event is recreated (and its handle republished) after this many
 EVENT_ROTATE = int(os.environ.get("RNB_IPC_EVENT_ROTATE", "30"))
+# largest single IPC allocation of a slot ring (RNB_IPC_CHUNK_MB, default 2048)
+IPC_CHUNK_BYTES = int(os.environ.get("RNB_IPC_CHUNK_MB", "2048")) << 20
 
 
 class IpcRing(RingBase):
@@ -265,6 +267,10 @@ class IpcRing(RingBase):
     dependencies are GPU-to-GPU waits, so neither side blocks on the other's
     kernels. ``RNB_RING_ORDER=host`` restores host-synchronised copies.
 
+    Memory: the slots are offsets in a few allocations of at most
+    ``IPC_CHUNK_BYTES`` (2 GB), one IPC memory handle each, opened by a
+    consumer on its first pull from the producer.
+
     ROCm refuses stream waits on an opened IPC event after its 32nd record,
     so both kinds of event are replaced every EVENT_ROTATE records: the owner
     creates a new event, writes its handle into the slot's shared-memory
@@ -278,7 +284,7 @@ class IpcRing(RingBase):
     def __init__(self, ctx, shapes, dtypes, num_slots, name, producer_gpu):
         super().__init__(ctx, shapes, dtypes, num_slots, name, producer_gpu)
         self._ptrs = None          # producer: [slot][tensor] device pointers
-        self._base = None          # producer: the ring's single allocation
+        self._base = None          # producer: the ring's allocations (IPC_CHUNK_BYTES each)
         # slot layout inside the allocation: tensor t of slot i at
         # i * slot_stride + tensor_offsets[t] (256-B aligned)
         offs, o = [], 0
@@ -286,6 +292,12 @@ class IpcRing(RingBase):
             offs.append(o)
             o += (max(_nbytes(sh, d), 256) + 255) // 256 * 256
         self.tensor_offsets, self.slot_stride = tuple(offs), o
+        # the ring's slots live in allocations of at most IPC_CHUNK_BYTES (one
+        # IPC memory handle each): opening one 12 GB handle (514 slots of a
+        # 4-replica, 256-clip consumer plan) never returned in the consumers,
+        # while 9 GB opened fine; slot i is slot i % spc of allocation i // spc
+        self.slots_per_chunk = max(1, IPC_CHUNK_BYTES // self.slot_stride)
+        self.num_chunks = -(-self.num_slots // self.slots_per_chunk)
         self._desc = None
         self._opened: Dict[Tuple, List[List[int]]] = {}
         self.consumers: List[Tuple[int, int, int]] = []   # (step, group, instance)
@@ -311,7 +323,7 @@ class IpcRing(RingBase):
         self._cid = None           # consumer id of this process
         self._rev = None           # consumer: own release events [slot]
         self._wopen: Dict[Tuple, List[Optional[int]]] = {}    # consumer: opened written events
-        self._opened_base: Dict[Tuple, int] = {}              # consumer: opened allocations
+        self._opened_base: Dict[Tuple, List[int]] = {}        # consumer: opened allocations
         self.events_opened = 0
         self.events_created = 0
         self.stale_event_waits = 0      # stream waits ROCm refused on completed events
@@ -359,11 +371,13 @@ class IpcRing(RingBase):
         rt = native.runtime()
         rt.set_device(device.index)
         self._dev = device
-        # one allocation and one IPC memory handle for the whole ring
-        self._base = rt.ipc_malloc(self.num_slots * self.slot_stride)
-        handle = rt.ipc_get_handle(self._base)
-        self._ptrs = [[self._base + i * self.slot_stride + o for o in self.tensor_offsets]
-                      for i in range(self.num_slots)]
+        # a few allocations (IPC memory handles) for the whole ring
+        spc = self.slots_per_chunk
+        self._base = [rt.ipc_malloc(min(spc, self.num_slots - c * spc) * self.slot_stride)
+                      for c in range(self.num_chunks)]
+        handle = tuple(rt.ipc_get_handle(b) for b in self._base)
+        self._ptrs = [[self._base[i // spc] + (i % spc) * self.slot_stride + o
+                       for o in self.tensor_offsets] for i in range(self.num_slots)]
         wh = ()
         if self.gpu_ordered:
             if rt.event_handle_size > EVENT_HANDLE_BYTES:
@@ -533,9 +547,10 @@ class IpcRing(RingBase):
                 raise RuntimeError("ring %s: no published descriptor for producer %s"
                                    % (self.name, key))
             rt = native.runtime()
-            base = rt.ipc_open_handle(desc[3])
-            ptrs = [[base + i * self.slot_stride + o for o in self.tensor_offsets]
-                    for i in range(self.num_slots)]
+            base = [rt.ipc_open_handle(h) for h in desc[3]]
+            spc = self.slots_per_chunk
+            ptrs = [[base[i // spc] + (i % spc) * self.slot_stride + o
+                     for o in self.tensor_offsets] for i in range(self.num_slots)]
             self._opened[key] = ptrs
             self._opened_base[key] = base
             if self.gpu_ordered:
@@ -615,7 +630,7 @@ class IpcRing(RingBase):
 
     def handle_stats(self) -> dict:
         """IPC resources this process holds for the ring (stress test, stats)."""
-        return {"mem_handles_opened": len(self._opened),
+        return {"mem_handles_opened": sum(len(b) for b in self._opened_base.values()),
                 "events_opened": self.events_opened,
                 "events_created": self.events_created,
                 "gpu_ordered_waits": self.gpu_waits,
@@ -626,14 +641,16 @@ class IpcRing(RingBase):
         if self._ptrs is None and not self._opened and self._rev is None:
             return
         rt = native.runtime()
-        for base in self._opened_base.values():
-            rt.ipc_close_handle(base)
+        for bases in self._opened_base.values():
+            for base in bases:
+                rt.ipc_close_handle(base)
         self._opened = {}
         self._opened_base = {}
         if self._ptrs is not None:
             torch.cuda.synchronize(self._dev)
             self._views = None
-            rt.free(self._base)
+            for base in self._base:
+                rt.free(base)
             self._base = None
             self._ptrs = None
 

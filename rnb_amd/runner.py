@@ -192,6 +192,11 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             return termination_flag.value != TerminationFlag.UNSET
 
         sta_bar.wait(barrier_timeout)
+        if os.environ.get("RNB_DUMP_STACKS_S"):
+            # diagnostics: every thread's Python stack after this many seconds
+            import faulthandler
+            faulthandler.dump_traceback_later(float(os.environ["RNB_DUMP_STACKS_S"]),
+                                              exit=False)
         progress = None
         if print_summary and os.environ.get("RNB_NO_TQDM") != "1":
             try:

@@ -2,7 +2,8 @@
 
 At ``bench.py --gpus 8`` with the defaults every runner consumes from the
 rings of 16 loader processes and ``plan_ring_depths`` gives 386 slots per
-ring. A ring is ONE allocation with ONE memory handle (slots are offsets) and
+ring. A ring is a few allocations of at most 2 GB (one memory handle each;
+slots are offsets; these 16 KB slots fit one) and
 a consumer opens a producer's "written" event, or creates its own "released"
 event, only on its first use of that slot. This test opens 16 rings x 386
 slots in one consumer process (two producer processes of 8 rings each), pulls
