@@ -110,6 +110,12 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
     # a list indexed by queue group, lower = higher), e.g. the 15-clip-video
     # replicas of the large-small routing ahead of the 1-clip batches
     group_prio = model_kwargs.pop("group_stream_priority", None)
+    # per queue group model lanes (``group_lanes``, a list like the above),
+    # e.g. two lanes for the 15-clip replica so a second large video need not
+    # wait for the first
+    group_lanes = model_kwargs.pop("group_lanes", None)
+    if group_lanes is not None and group_idx < len(group_lanes):
+        model_kwargs["lanes"] = int(group_lanes[group_idx])
     if use_gpu:
         torch.cuda.set_device(g_idx)
         device = torch.device("cuda:%d" % g_idx)
