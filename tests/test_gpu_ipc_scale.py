@@ -190,3 +190,50 @@ def test_ipc_slot_events_past_32_records_stay_gpu_ordered():
     assert st["events_created"] == 2 * rotations, st
     print("\n[ipc-rotate] %d pulls over 2 slots: consumer %s, producer gpu waits %d, host "
           "fallbacks %d, events created %d" % (n, st, prod[0], prod[1], prod[2]), flush=True)
+
+
+def test_ipc_ring_split_into_chunks():
+    """A ring larger than IPC_CHUNK_BYTES lives in several allocations (one
+    IPC memory handle each; a single 12 GB handle never opened in a
+    consumer): 10 slots, 3 per allocation -> 4 handles; every slot's data
+    arrives through the right allocation."""
+    import multiprocessing as mp
+    import torch
+    from rnb_amd.parallel import transport
+    from rnb_amd.parallel.transport import IpcRing
+    ctx = mp.get_context("spawn")
+    saved = transport.IPC_CHUNK_BYTES
+    try:
+        probe = IpcRing(ctx, ((4, 1024),), (torch.float32,), 10, "chunkprobe", 0)
+        transport.IPC_CHUNK_BYTES = 3 * probe.slot_stride
+        ring = IpcRing(ctx, ((4, 1024),), (torch.float32,), 10, "chunks", 0)
+    finally:
+        transport.IPC_CHUNK_BYTES = saved
+    assert ring.slots_per_chunk == 3 and ring.num_chunks == 4
+    ring.set_consumers([(1, 0, 0)])
+    q, out_q = ctx.Queue(), ctx.Queue()
+    n = 20
+    p = ctx.Process(target=_reuse_producer, args=(ring, q, n, out_q))
+    p.start()
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(dev)
+    outs = torch.empty((n, 4, 1024), device=dev)
+    with torch.cuda.stream(s):
+        ring.consumer_attach(dev, (1, 0, 0))
+        while True:
+            m = q.get(timeout=120)
+            if m is None:
+                break
+            idx, i, desc = m
+            ring.read_into(idx, [outs[i]], desc)
+            ring.release(idx)
+        s.synchronize()
+    out_q.get(timeout=60)
+    p.join(60)
+    assert p.exitcode == 0
+    assert torch.equal(outs.amin(dim=(1, 2)).cpu(), torch.arange(n, dtype=torch.float32))
+    assert torch.equal(outs.amax(dim=(1, 2)).cpu(), torch.arange(n, dtype=torch.float32))
+    st = ring.handle_stats()
+    ring.close()
+    assert st["mem_handles_opened"] == 4, st
