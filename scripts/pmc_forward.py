@@ -23,8 +23,18 @@ import sys
 
 PEAK_TF = 157.3
 FLOP_PER_MFMA = 2048
+# 16-bit MFMA kernels: v_mfma_f32_16x16x32_{f16,bf16} = 16384 FLOP of matrix-
+# core work, dense peak ~2.5 PF (the h3 / x6 kernels issue 3 of them per 32
+# (h3) or 16 (x6) channels of fp32 work)
+PEAK16_TF = 2516.6
+FLOP16 = 16384
 
 FAMILIES = (
+    ("h3 temporal band", r"conv_h3t_kernel"),
+    ("h3 row-band 4w", r"conv_h3q_kernel"),
+    ("h3 row-band", r"conv_h3r_kernel"),
+    ("h3 direct", r"conv_h3_kernel"),
+    ("x6", r"conv_x6|conv_wino_x6|conv_winot_x6"),
     ("wino spatial", r"conv_wino_f32_kernel"),
     ("wino temporal", r"conv_winot_f32_kernel"),
     ("conv direct", r"conv_f32_kernel"),
@@ -66,7 +76,8 @@ def main(root):
         mf = c.get("SQ_INSTS_MFMA", 0.0)
         clk = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0 * 1024
         busy = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / clk if clk else 0.0
-        tf = mf * FLOP_PER_MFMA / (us * 1e-6) / 1e12 if us > 0 else 0.0
+        fl = FLOP16 if re.search(r"h3|x6", name) else FLOP_PER_MFMA
+        tf = mf * fl / (us * 1e-6) / 1e12 if us > 0 else 0.0
         short = re.sub(r"\(.*\)$", "", name)[:44]
         print("%-4d %-44s %9.1f %10.2f %7.1f%% %8.1f" % (i, short, us, mf / 1e6, 100 * busy, tf))
         key = next((k for k, p in FAMILIES if re.search(p, name)), "other")
@@ -76,18 +87,21 @@ def main(root):
         a[2] += mf
         a[3] += c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
         a[4] += clk
+        a.append(fl)
     tot_us = sum(a[1] for a in fam.values())
     print("\n%-16s %5s %10s %6s %10s %8s %8s" % ("family", "n", "ms", "share", "MFMA busy",
                                                   "TF/s", "% peak"))
-    for k, (n, us, mf, b, clk) in sorted(fam.items(), key=lambda kv: -kv[1][1]):
-        tf = mf * FLOP_PER_MFMA / (us * 1e-6) / 1e12 if us else 0.0
+    for k, a in sorted(fam.items(), key=lambda kv: -kv[1][1]):
+        n, us, mf, b, clk = a[:5]
+        fl = a[5] if len(a) > 5 else FLOP_PER_MFMA
+        peak = PEAK16_TF if fl == FLOP16 else PEAK_TF
+        tf = mf * fl / (us * 1e-6) / 1e12 if us else 0.0
         print("%-16s %5d %10.3f %5.1f%% %9.1f%% %8.1f %7.1f%%"
               % (k, n, us / 1e3, 100 * us / tot_us, 100 * b / clk if clk else 0.0, tf,
-                 100 * tf / PEAK_TF))
-    mf_all = sum(a[2] for a in fam.values())
-    print("\nwhole forward: %.3f ms, %.1f TF/s fp32 MFMA (%.1f%% of %.0f)"
-          % (tot_us / 1e3, mf_all * FLOP_PER_MFMA / (tot_us * 1e-6) / 1e12,
-             100 * mf_all * FLOP_PER_MFMA / (tot_us * 1e-6) / 1e12 / PEAK_TF, PEAK_TF))
+                 100 * tf / peak))
+    print("\n(TF/s = matrix-core FLOP rate of the MFMAs issued; %% peak against %.0f TF/s for "
+          "fp32 MFMA, %.0f for the 16-bit 16x16x32 forms)" % (PEAK_TF, PEAK16_TF))
+    print("whole forward: %.3f ms" % (tot_us / 1e3))
 
 
 if __name__ == "__main__":
