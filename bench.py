@@ -486,6 +486,11 @@ def run_cross_gpu_extras(args) -> dict:
         if budget < 45:
             out[topo] = {"skipped": "cross-GPU time budget spent (%.0f s left)" % budget}
             continue
+        if topo == "two-stage" and os.environ.get("RNB_FOLD_GPUS"):
+            # folded rehearsal: every logical GPU is the same card, and RCCL
+            # refuses send/recv between two ranks of one device
+            out[topo] = {"skipped": "RNB_FOLD_GPUS: RCCL edges need distinct GPUs"}
+            continue
         path = os.path.join(root, "logs", "bench", "cross-%s-%dgpu.json" % (topo, args.gpus))
         if os.path.exists(path):
             os.remove(path)                     # never report a previous run's record
