@@ -141,9 +141,12 @@ def parse_args(argv=None):
     ap.add_argument("--no-large-priority", dest="large_priority", action="store_false",
                     help="(--route large-small) keep the 15-clip-video replicas on "
                          "normal-priority streams")
-    ap.add_argument("--lanes", type=int, default=1,
+    ap.add_argument("--lanes", type=int, default=None,
                     help="graphed engines per runner process, calls rotating over their "
-                         "streams (R2P1DRunner lanes: one-video calls overlap on the GPU)")
+                         "streams (R2P1DRunner lanes: one-video calls overlap on the GPU). "
+                         "Default: 2 when a GPU hosts one runner replica (literal config #2: "
+                         "356 -> 554-566 videos/s, profiles/r4_ab_literal2_lanes.txt), else 1 "
+                         "(with several replicas lanes lose, r4_ab_whole_pipeline_lanes.txt)")
     ap.add_argument("--batch-wait-ms", type=float, default=0.0,
                     help="how long a runner waits for more queued videos to batch")
     ap.add_argument("--slots", type=int, default=None,
@@ -185,6 +188,8 @@ def parse_args(argv=None):
     args = ap.parse_args(argv)
     if args.replicas is None:
         args.replicas = 4 if args.pipeline == "whole" else 3
+    if args.lanes is None:
+        args.lanes = 2 if args.replicas == 1 else 1
     return args
 
 
@@ -591,10 +596,11 @@ def run_literal_extras(args) -> dict:
     whole = ["--pipeline", "whole", "--replicas", "1", "--loaders", "1",
              "--steps", "2", "--warmup", "1", "--videos-per-step", "128",
              "--latency-mi", "90", "--latency-load", "0", "--latency-seconds", "4", "--no-check"]
+    # (1 loader + 1 runner, one video per model call; the runner's default
+    # two lanes keep two calls in flight on two streams; the one-lane run is
+    # the round-3 form, kept for comparison)
     runs = [("config2_whole", whole),
-            # the same processes (1 loader + 1 runner, one video per model
-            # call); the runner keeps two calls in flight on two streams
-            ("config2_whole_lanes2", whole + ["--lanes", "2"]),
+            ("config2_whole_one_lane", whole + ["--lanes", "1"]),
             # its numerics (re-joined segment videos) join the headline's strata
             ("config4_segment", ["--pipeline", "segment", "--segments", "3",
                                  "--steps", "2", "--warmup", "1", "--videos-per-step", "128",
