@@ -15,8 +15,15 @@ one or more processes per GPU itself, as the reference does).
 
 Precision and numerics: ``--dtype fp32`` (default) is the reference's
 precision (reference models/r2p1d/model.py:149,225): fp32 activations and
-weights, fp32-accurate products (fp32 MFMA, or the split-bf16 x6 Winograd
-kernels where the autotuner picks them; both within 1e-5 of an fp64 conv).
+weights, fp32-accurate products. The autotuner picks per layer among the
+fp32-MFMA kernels, the split-bf16 "x6" kernels (six bf16 products per fp32
+product) and -- what the headline mostly runs since round 4 -- the "h3"
+kernels: each fp32 operand split into an fp16 hi/lo pair after a
+power-of-two scale, three fp16 MFMA products per fp32 product. Every one is
+held to 1e-5 of an fp64 conv (tests/test_gpu_h3.py, test_gpu_f32.py). h3's
+exponent range is narrower than fp32's, so its kernels flag any non-finite
+output and the runner re-runs such a call on full-range kernels
+(``h3_range_fallbacks`` in the JSON line; tests/test_gpu_range_guard.py).
 ``--bn batch`` (default) is the reference's BatchNorm: it never calls
 ``.eval()``, so every BatchNorm normalises with the statistics of the video
 being served (per-video segments when a runner batches videos).
@@ -131,8 +138,11 @@ def parse_args(argv=None):
                          "256 clips / 128 videos beat 128 / 64 by 4.8%% in interleaved "
                          "runs (1090 vs 1040 videos/s, profiles/r3_bench_batch_sweep.txt; "
                          "a 256-clip R(2+1)D-34 runner holds ~19 GB)")
-    ap.add_argument("--bucket-step", type=int, default=4,
-                    help="HIP-graph clip buckets every this many clips")
+    ap.add_argument("--bucket-step", default="geo",
+                    help="HIP-graph clip buckets: every this many clips, or 'geo' (default: "
+                         "1..8, then ~12.5%% apart; a gathering runner ends a bulk call at a "
+                         "bucket boundary instead of padding: 30 graphs per engine instead of "
+                         "65 at 256 clips)")
     ap.add_argument("--large-lanes", type=int, default=2,
                     help="(--route large-small) runner lanes of the 15-clip-video replicas: "
                          "two (default) let a second large video start while the first runs; "
@@ -193,6 +203,9 @@ def parse_args(argv=None):
     return args
 
 
+LARGE_CLIPS = 15        # the sampler's large videos (reference sampler.py: [1, 15])
+
+
 def pipeline_config(args, n_gpus: int) -> dict:
     """The pipeline JSON (benchmark.py format) for ``--pipeline``."""
     gpus = list(range(n_gpus))
@@ -219,7 +232,9 @@ def pipeline_config(args, n_gpus: int) -> dict:
                                    for g in gpus]},
                  dict(runner, queue_groups=[q for g in gpus for q in (
                      {"gpus": [g] * (args.replicas - nl), "in_queue": 2 * g},
-                     {"gpus": [g] * nl, "in_queue": 2 * g + 1})],
+                     # 15-clip videos only: buckets of whole videos (19 graphs)
+                     {"gpus": [g] * nl, "in_queue": 2 * g + 1,
+                      "bucket_step": LARGE_CLIPS})],
                       **({"group_stream_priority": [0, -1] * n_gpus}
                          if args.large_priority else {}),
                       **({"group_lanes": [args.lanes, args.large_lanes] * n_gpus}
@@ -390,6 +405,12 @@ def main(argv=None) -> int:
             # why each gather ended (runner.py GATHER_ENDS)
             "gather": res.get("gather"),
             "ipc_edges": res.get("ipc_edges"),
+            # h3 range guard: calls re-run on full-range kernels (rnb_amd/ops/
+            # conv_f32.RangeGuard), summed over the runners
+            "h3_range_fallbacks": (res.get("model_counters") or {}).get("h3_range_fallbacks", 0),
+            "model_counters": res.get("model_counters"),
+            "rccl_world": res.get("rccl_world") or None,
+            "rccl_edges": res.get("rccl_edges") or None,
             "bulk_p50_ms": round(res.get("latency", {}).get("p50_ms", float("nan")), 3),
             "bulk_p99_ms": round(res.get("latency", {}).get("p99_ms", float("nan")), 3),
             "barrier_videos_per_s": round(res.get("videos_per_s", 0.0), 2),
@@ -403,6 +424,13 @@ def main(argv=None) -> int:
                        "bn": ("eval (folded into the convs in fp64)" if args.bn == "eval" else
                               "batch (training-mode BN as the reference, per-video "
                               "statistics)"),
+                       "products": ("fp32 activations and weights; products on the matrix "
+                                    "cores as the autotuner picks per layer: h3 (fp16 hi/lo "
+                                    "split, 3 fp16 MFMA products per fp32 product), x6 (3-way "
+                                    "bf16 split, 6 products) or fp32 MFMA; each held to 1e-5 "
+                                    "of an fp64 conv; h3 calls with a non-finite output re-run "
+                                    "on full-range kernels" if args.dtype == "fp32" else
+                                    "bf16 activations and weights, fp32 accumulation"),
                        "clip": "8x112x112",
                        "clips_dist": "1 w.p. 10/11, 15 w.p. 1/11",
                        "max_batch_videos": args.video_batch,
@@ -509,7 +537,8 @@ def run_cross_gpu_extras(args) -> dict:
                "--loaders", str(args.loaders), "--replicas", str(args.replicas),
                # 16-clip graph buckets: a quarter of the headline's graph
                # captures in each extra's setup (4 short steps, padding cost small)
-               "--bucket-step", str(max(args.bucket_step, 16)),
+               "--bucket-step", ("geo" if args.bucket_step == "geo"
+                                 else str(max(int(args.bucket_step), 16))),
                "--no-check", "--no-cross-gpu-extras", "--json-out", path]
         env = {k: v for k, v in os.environ.items()
                if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
@@ -534,7 +563,12 @@ def run_cross_gpu_extras(args) -> dict:
                 sub = json.loads(f.read())
             out[topo] = {"videos_per_s": sub.get("value"), "p50_ms": sub.get("p50_ms"),
                          "p99_ms": sub.get("p99_ms"), "steps": args.cross_gpu_steps,
-                         "rc": r.returncode, "wall_s": round(time.time() - t0, 1)}
+                         "rc": r.returncode, "wall_s": round(time.time() - t0, 1),
+                         # the RCCL ranks / pair groups formed and the consumers'
+                         # peer-access state per edge (two-stage), the IPC edges
+                         "rccl_world": sub.get("rccl_world"),
+                         "rccl_edges": sub.get("rccl_edges"),
+                         "ipc_edges": sub.get("ipc_edges")}
         except Exception as e:          # reported, never fatal for the headline
             tail = ""
             if r is not None and r.stderr:
@@ -732,7 +766,7 @@ def run_fused(args) -> int:
     # graph buckets every --bucket-step clips: a batch pads to the next
     # bucket (every 8 clips with arrival-order packing: 2.3 % of the clips
     # padded vs 6.2 % with power-of-two-ish buckets on the reference clip mix)
-    bstep = max(1, args.bucket_step)
+    bstep = 8 if args.bucket_step == "geo" else max(1, int(args.bucket_step))
     buckets = sorted(set(range(bstep, args.clips_per_batch + 1, bstep))
                      | {args.clips_per_batch, max_clips})
     eng = FusedR2P1D(device, depth=args.depth, replicas=args.fused_replicas,

@@ -587,7 +587,12 @@ __global__ __launch_bounds__(256) void bn_seg_running_f32_kernel(BnSegParams p) 
 __global__ __launch_bounds__(256) void bn_seg_apply_f32_kernel(
     const float* __restrict__ y, float* __restrict__ z, const float* __restrict__ res,
     const int* __restrict__ coffs, int nseg, int rpc, const float* __restrict__ ss, int relu,
-    long long M, int C, int y_stride, int z_stride, int res_stride) {
+    long long M, int C, int y_stride, int z_stride, int res_stride,
+    float* const* __restrict__ zind) {
+  // zind (nullable): the destination read from device memory, so a graph
+  // captured once can write each replay's output where the host pointed it
+  // (a pipeline stage's IPC output slot: no staging copy)
+  if (zind != nullptr) z = *zind;
   const int cq = C / 4;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   const long long groups = (M + BN_APPLY_RPT - 1) / BN_APPLY_RPT;
@@ -753,17 +758,27 @@ int rnb_bn_seg_walk_apply_f32(double* sums, int sums_c, int* ticket, const int* 
   return (int)hipGetLastError();
 }
 
-int rnb_bn_seg_apply_f32(const float* y, float* z, const float* res, const int* coffs, int nseg,
-                         int rpc, const float* ss, int relu, long long M, int C, int y_stride,
-                         int z_stride, int res_stride, hipStream_t stream) {
+// zind (nullable): device address of a pointer that replaces z at run time
+int rnb_bn_seg_apply_f32_ind(const float* y, float* z, const float* res, const int* coffs,
+                             int nseg, int rpc, const float* ss, int relu, long long M, int C,
+                             int y_stride, int z_stride, int res_stride, float* const* zind,
+                             hipStream_t stream) {
   if (M <= 0 || C <= 0 || nseg <= 0) return 0;
   if (C % 4 || y_stride % 4 || z_stride % 4 || (res && res_stride % 4) || rpc <= 0) return -2;
+  if (zind != nullptr && ((uintptr_t)zind % 8) != 0) return -2;
   const long long n = (M + BN_APPLY_RPT - 1) / BN_APPLY_RPT * (C / 4);
   if (M > 0x7FFFFFFFLL) return -3;
   hipLaunchKernelGGL(bn_seg_apply_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      stream, y, z, res, coffs, nseg, rpc, ss, relu, M, C, y_stride, z_stride,
-                     res_stride);
+                     res_stride, zind);
   return (int)hipGetLastError();
+}
+
+int rnb_bn_seg_apply_f32(const float* y, float* z, const float* res, const int* coffs, int nseg,
+                         int rpc, const float* ss, int relu, long long M, int C, int y_stride,
+                         int z_stride, int res_stride, hipStream_t stream) {
+  return rnb_bn_seg_apply_f32_ind(y, z, res, coffs, nseg, rpc, ss, relu, M, C, y_stride, z_stride,
+                                  res_stride, nullptr, stream);
 }
 
 // Scratch floats rnb_bn_stats needs for (M, C).

@@ -969,6 +969,7 @@ void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
     mrow[tp] = hw0 + px < HW ? (n * T + fr) * HW + hw0 + px : -1;
   }
   double* red = (double*)lds;                        // [C_TILE][2] (patch no longer read)
+  bool bad = false;                                  // range guard (st.oflag)
   if constexpr (ST) {
     x6d_barrier();
     for (int i = threadIdx.x; i < C_TILE * 2; i += NT) red[i] = 0.0;
@@ -991,6 +992,7 @@ void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
     for (int tp = 0; tp < TP; ++tp) {
       const bool ok = mrow[tp] >= 0 && c < p.Cout_p;
       x6f32x4 v = acc[tp][tc] * out_scale + rv[tp];
+      if (st.oflag != nullptr && ok) bad |= x6d_nonfinite(v);
       if (p.relu) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
@@ -1031,6 +1033,7 @@ void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
       }
     }
   }
+  if (bad) *st.oflag = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -1068,7 +1071,13 @@ static const ConvH3Config kH3Configs[] = {
 };
 static const int kNumH3Configs = sizeof(kH3Configs) / sizeof(kH3Configs[0]);
 
+// range-guard flag of the launches that follow (X6DStats.oflag): host-coherent
+// memory of the engine being run or captured (rnb_h3_set_range_flag), or null
+static int* g_h3_range_flag = nullptr;
+
 extern "C" {
+
+void rnb_h3_set_range_flag(int* flag) { g_h3_range_flag = flag; }
 
 int rnb_conv_h3_num_configs() { return kNumH3Configs; }
 
@@ -1135,6 +1144,7 @@ int rnb_conv_h3_launch(const ConvF32Params* pp, int config_id, hipStream_t strea
   st.acc_scale = 1.f / out_scale;            // exact: powers of two
   st.in_ss = in_ss;
   st.in_seg = in_seg;
+  st.oflag = g_h3_range_flag;
   const bool aff = in_ss != nullptr;
   if (aff && (!in_seg || !rnb_conv_h3_affine_ok(config_id, p.Cin_p, p.To * p.Ho * p.Wo)))
     return -16;
@@ -1242,6 +1252,7 @@ int rnb_conv_h3r_launch(const ConvF32Params* pp, int variant, hipStream_t stream
   st.acc_scale = 1.f / out_scale;
   st.in_ss = in_ss;
   st.in_seg = in_seg;
+  st.oflag = g_h3_range_flag;
   const bool aff = in_ss != nullptr;
   hipLaunchKernelGGL(aff ? (sums ? cfg.kernel_aff_st : cfg.kernel_aff)
                          : (sums ? cfg.kernel_st : cfg.kernel),
@@ -1328,6 +1339,7 @@ int rnb_conv_h3t_launch(const ConvF32Params* pp, int variant, hipStream_t stream
   st.acc_scale = 1.f / out_scale;
   st.in_ss = in_ss;
   st.in_seg = in_seg;
+  st.oflag = g_h3_range_flag;
   const bool aff = in_ss != nullptr;
   hipLaunchKernelGGL(aff ? (sums ? cfg.kernel_aff_st : cfg.kernel_aff)
                          : (sums ? cfg.kernel_st : cfg.kernel),

@@ -301,6 +301,7 @@ __global__ __launch_bounds__(512) void x6d_splitk_reduce_kernel(const ConvF32Par
 #pragma unroll
     for (int k = 0; k < 16; ++k) v += part[k];
     if (p.res) v += *(const x6f32x4*)(p.res + (size_t)m * p.res_stride + c);
+    if (st.oflag != nullptr && x6d_nonfinite(v)) *st.oflag = 1;     // h3 range guard
     if (p.relu) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);

@@ -27,6 +27,17 @@ int rnb_malloc(void** ptr, size_t bytes) { return (int)hipMalloc(ptr, bytes); }
 
 int rnb_free(void* ptr) { return (int)hipFree(ptr); }
 
+// host-coherent, device-mapped memory (a flag the GPU writes and the host
+// reads after the work completes, with no copy): *host and *dev address it
+int rnb_host_alloc_mapped(size_t bytes, void** host, void** dev) {
+  hipError_t e = hipHostMalloc(host, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return (int)e;
+  std::memset(*host, 0, bytes);
+  return (int)hipHostGetDevicePointer(dev, *host, 0);
+}
+
+int rnb_host_free(void* host) { return (int)hipHostFree(host); }
+
 int rnb_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
 
 int rnb_ipc_get_mem_handle(void* ptr, void* out_handle) {

@@ -64,7 +64,19 @@ struct X6DStats {
   // fp32, in_seg [N] video of each clip); padding taps stay zero
   const float* in_ss;
   const int* in_seg;
+  // conv_h3.hip only (null elsewhere): range guard. An h3 input with
+  // |x| * in_scale past the fp16 range (65504) splits into inf / -inf and its
+  // products into inf - inf = NaN; any non-finite output value (checked before
+  // the ReLU, which would hide a NaN) sets *oflag = 1 (a plain vector store to
+  // host-coherent memory; the host re-runs the call on full-range kernels)
+  int* oflag = nullptr;
 };
+
+// true when any element of v is +-inf or NaN (v_cmp_class: sNaN, qNaN, -inf, +inf)
+static __device__ __forceinline__ bool x6d_nonfinite(const x6f32x4& v) {
+  return __builtin_amdgcn_classf(v[0], 0x207) | __builtin_amdgcn_classf(v[1], 0x207) |
+         __builtin_amdgcn_classf(v[2], 0x207) | __builtin_amdgcn_classf(v[3], 0x207);
+}
 
 // 16-B slot permutation of row-band halo patch pixels (conv_x6r_kernel,
 // conv_h3r_kernel): pixel q's slots XOR g(q) = [5,6,4,1,0,7,3,0][q & 7]
@@ -118,6 +130,7 @@ static __device__ __forceinline__ void x6d_epilogue(const ConvF32Params& p, cons
   const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(has_res ? p.res : p.y), (short)0,
       has_res ? (uint32_t)p.M * (uint32_t)p.res_stride * 4u : 0u, 0x00020000);
+  bool bad = false;                                   // range guard (st.oflag)
   if constexpr (!ST) {
 #pragma unroll
     for (int tp = 0; tp < TP; ++tp) {
@@ -136,6 +149,7 @@ static __device__ __forceinline__ void x6d_epilogue(const ConvF32Params& p, cons
         const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
         const bool ok = m < m_end && c < p.Cout_p;
         x6f32x4 v = acc[tp][tc] * acc_mul + r[tc];
+        if (st.oflag != nullptr && ok) bad |= x6d_nonfinite(v);
         if (p.relu) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
@@ -188,6 +202,7 @@ static __device__ __forceinline__ void x6d_epilogue(const ConvF32Params& p, cons
         const int m = p0 + (wp * TP + tp) * 16 + frow;
         const bool ok = m < m_end && c < p.Cout_p;
         x6f32x4 v = acc[tp][tc] * acc_mul + r[tp];
+        if (st.oflag != nullptr && ok) bad |= x6d_nonfinite(v);
         if (p.relu) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
@@ -255,4 +270,5 @@ static __device__ __forceinline__ void x6d_epilogue(const ConvF32Params& p, cons
       }
     }
   }
+  if (bad) *st.oflag = 1;
 }

@@ -142,7 +142,13 @@ class Watchdog(threading.Thread):
 
 
 def _assign_rccl_ranks(spec, qt, job_id):
-    """One torch.distributed world for every runner touching an RCCL ring."""
+    """One torch.distributed world for every runner touching an RCCL ring, and
+    one 2-rank group per (producer, consumer) pair of each RCCL edge (traffic
+    runs only on those: rccl_channel.init_dist). Refused before anything is
+    spawned: a pair whose two ends share a GPU (RCCL cannot hold two ranks of
+    one communicator on one device; use 'ipc' for same-GPU edges) and, on
+    'nccl', a CPU end. Several consumer replicas (or producers) on one GPU are
+    fine: each pair has its own communicator."""
     import tempfile
     from .config import ConfigError
     from .parallel.rccl_channel import DistInfo
@@ -156,7 +162,10 @@ def _assign_rccl_ranks(spec, qt, job_id):
         return {}
     backend = os.environ.get("RNB_RCCL_BACKEND", "nccl")
     members = set(rccl)
+    edges = []                       # (producer key, consumer key)
+    gpu_of = {}
     for (s, g, i), ring in rccl.items():
+        gpu_of[(s, g, i)] = spec.steps[s].groups[g].gpus[i]
         outs = set(spec.steps[s].groups[g].out_queues)
         for cg, grp in enumerate(spec.steps[s + 1].groups):
             if grp.in_queue in outs:
@@ -167,15 +176,37 @@ def _assign_rccl_ranks(spec, qt, job_id):
                             "GPUs (step %d group %d gpu %d -> gpu %d); use 'ipc' for "
                             "same-GPU edges" % (s, g, ring.producer_gpu, gpu))
                     members.add((s + 1, cg, ci))
+                    gpu_of[(s + 1, cg, ci)] = gpu
+                    edges.append(((s, g, i), (s + 1, cg, ci)))
     order = sorted(members)
+    rank = {key: r for r, key in enumerate(order)}
+    pairs = sorted({tuple(sorted((rank[a], rank[b]))) for a, b in edges})
+    if backend == "nccl":
+        for a, b in pairs:           # (a pair on one GPU was refused above)
+            assert gpu_of[order[a]] != gpu_of[order[b]]
     store = os.path.join(tempfile.gettempdir(), "rnb-rccl-%s-%d" % (job_id, os.getpid()))
     if os.path.exists(store):
         os.remove(store)
-    infos = {key: DistInfo(rank, len(order), store, backend)
-             for rank, key in enumerate(order)}
+    gpus = {r: gpu_of[key] for r, key in enumerate(order)}
+    infos = {key: DistInfo(r, len(order), store, backend,
+                           pairs=[p for p in pairs if r in p], gpus=gpus)
+             for r, key in enumerate(order)}
     for key, ring in rccl.items():
         ring.producer_rank = infos[key].rank
     return infos
+
+
+def rccl_world_summary(infos) -> dict:
+    """The RCCL world the launcher formed (for the result JSON): every rank's
+    (step, group, instance) and GPU, and the 2-rank pair groups."""
+    if not infos:
+        return {}
+    any_info = next(iter(infos.values()))
+    pairs = sorted({tuple(p) for i in infos.values() for p in i.pairs})
+    return {"backend": any_info.backend, "world_size": any_info.world_size,
+            "ranks": {str(i.rank): {"runner": list(key), "gpu": any_info.gpus.get(i.rank)}
+                      for key, i in sorted(infos.items(), key=lambda kv: kv[1].rank)},
+            "pair_groups": [list(p) for p in pairs]}
 
 
 def _client_main(fn, *args, **kwargs):
@@ -396,7 +427,15 @@ def run(args) -> dict:
               "gather": gather_summary(ring_stats),
               # IPC slot-ring event waits per edge kind (same / cross GPU):
               # GPU-ordered vs host fallback, plus handles held by consumers
-              "ipc_edges": ipc_summary(ring_stats)}
+              "ipc_edges": ipc_summary(ring_stats),
+              # model counters summed over runners ("model.<key>", RunnerModel
+              # runtime_stats: e.g. h3 range-guard re-runs)
+              "model_counters": {k[6:]: v for k, v in sorted(ring_stats.items())
+                                 if k.startswith("model.")},
+              # RCCL edges: the world and pair groups formed, and the consumers'
+              # peer-access state per edge kind
+              "rccl_world": rccl_world_summary(dist_infos),
+              "rccl_edges": ipc_summary(ring_stats, "rccl.")}
     if time_start is not None and time_end is not None:
         sta_time = time_start
         if warm and phase_start[0] > 0:
@@ -487,10 +526,10 @@ def gather_summary(stats: dict) -> dict:
     return out
 
 
-def ipc_summary(stats: dict) -> dict:
+def ipc_summary(stats: dict, prefix: str = "ipc.") -> dict:
     out = {}
     for k, v in stats.items():
-        if k.startswith("ipc."):
+        if k.startswith(prefix):
             _, edge, key = k.split(".", 2)
             out.setdefault(edge, {})[key] = v
     return out

@@ -43,7 +43,8 @@ import torch
 from ...ops.bn import BatchNormBatch
 from ...ops.conv import ConvGeom, ConvLayer, StemConv, fold_bn, pad_to, CH_ALIGN
 from ...ops.conv21 import FusedSTConv
-from ...ops.conv_f32 import F32_ALIGN, WINOT_MIN_T, ConvLayerF32, h3_enabled
+from ...ops.conv_f32 import (F32_ALIGN, WINOT_MIN_T, ConvLayerF32, RangeGuard, full_range,
+                              h3_enabled)
 from ...ops.video import (Head, IN_CHANNELS_P, ndhwc_to_ncdhw, ncdhw_to_ndhwc,
                           packed_input_shape)
 from .network import (LAYER_CHANNELS, LAYER_INPUT_CTHW, LAYER_OUTPUT_CTHW,
@@ -51,6 +52,22 @@ from .network import (LAYER_CHANNELS, LAYER_INPUT_CTHW, LAYER_OUTPUT_CTHW,
 
 DEFAULT_BUCKETS = (1, 2, 3, 4, 5, 6, 8, 10, 12, 15, 16, 20, 24, 30, 32, 40, 45, 48,
                    60, 64, 80, 96, 128)
+
+
+def geometric_buckets(max_clips: int, ratio: float = 1.125, dense: int = 8,
+                      align: int = 4) -> List[int]:
+    """Clip buckets 1..``dense`` one by one, then growing by ``ratio`` (rounded
+    up to multiples of ``align``) to ``max_clips``: 30 graphs instead of 65 at
+    256 clips with 4-clip steps. A gathering runner trims a call to a bucket
+    boundary when padding would cost more than a few percent
+    (R2P1DRunner.gather_fit), so the coarser spacing defers clips to the next
+    call instead of computing padding rows."""
+    out = list(range(1, min(dense, max_clips) + 1))
+    s = dense
+    while s < max_clips:
+        s = min(max_clips, max(s + align, -(-int(s * ratio) // align) * align))
+        out.append(s)
+    return sorted(set(out) | {max_clips})
 
 
 def boundary_channels_p(layer_idx: int, dtype=torch.bfloat16) -> int:
@@ -114,6 +131,10 @@ class R2P1DEngine:
             self._build(net.res2plus1d)
             if self.end_idx == 5:
                 self.head = Head(net.linear, device)
+        # h3 range guard (fp32 hip engines whose convs may pick h3 configs):
+        # the launches of this engine write its flag on a non-finite output
+        self.range_guard = (RangeGuard() if backend == "hip" and self.f32 and h3_enabled()
+                            and device.type == "cuda" else None)
 
     # ---------------------------------------------------------------- build
     def _name(self) -> str:
@@ -297,9 +318,19 @@ class R2P1DEngine:
         return [op.layer for op in self.ops if op.kind == "conv"]
 
     # -------------------------------------------------------------- forward
+    @property
+    def supports_out_indirect(self) -> bool:
+        """An intermediate stage (end_index < 5) of the fp32 batch-BN hip
+        engine ends in a BatchNorm apply, which can write its output through a
+        device-held pointer (``forward(out_indirect=...)``): a graph captured
+        once then writes each call straight into the stage's output slot."""
+        return (self.backend == "hip" and self.f32 and self.bn_mode == "batch"
+                and self.end_idx < 5 and bool(self.ops) and self.ops[-1].bn is not None)
+
     def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
                 packed: bool = False, clip_offsets=None,
-                clip_offsets_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
+                clip_offsets_dev: Optional[torch.Tensor] = None,
+                out_indirect: Optional[torch.Tensor] = None) -> torch.Tensor:
         """x: NDHWC boundary tensor (or NCDHW fp32 for backend=module); with
         ``packed``, the stem's pair-packed input (``input_shape(n, True)``).
         ``clip_offsets`` (bn_mode='batch'): clip ranges of the videos in the
@@ -308,7 +339,10 @@ class R2P1DEngine:
         (default: the whole batch is one video). ``clip_offsets_dev``: the same
         as a device int32 tensor, possibly padded with trailing repeats of its
         last offset (empty videos); nothing is read back to the host, so the
-        forward can be captured in a HIP graph."""
+        forward can be captured in a HIP graph.
+        ``out_indirect`` (``supports_out_indirect`` engines): device int64 [1]
+        holding the address the final BatchNorm apply writes to (rows of the
+        returned tensor's shape) -- read when the kernel runs, not here."""
         if packed and not self.accepts_packed_input:
             raise ValueError("this engine's first op does not take a packed input")
         if self.backend == "module":
@@ -324,6 +358,8 @@ class R2P1DEngine:
             return torch.zeros(self.output_shape(0), dtype=self.output_dtype(),
                                device=x.device)
         hip = self.backend == "hip"
+        if hip and self.range_guard is not None:
+            self.range_guard.activate()       # this engine's h3 launches flag into it
         bufs: Dict[str, torch.Tensor] = {"x": x}
         coffs = None
         defer = os.environ.get("RNB_BN_DEFER", "1") != "0"
@@ -392,8 +428,9 @@ class R2P1DEngine:
                             clip_seg = self._clip_segments(coffs, x.shape[0], x.device)
                         pending = (op.bn.scale_shift_f32(y, coffs, sums, rpc=thw), clip_seg)
                     else:
+                        ind = out_indirect if i == len(self.ops) - 1 else None
                         y = op.bn.forward_hip(y, res, op.bn_relu, out=y, segments=coffs,
-                                              sums=sums, rpc=thw)
+                                              sums=sums, rpc=thw, out_ind=ind)
                 else:
                     y = op.layer.forward_torch(src, None, out_dtype=self.dtype)
                     y = op.bn.forward_torch(y, res, op.bn_relu, out_dtype=self.dtype,
@@ -422,6 +459,33 @@ class R2P1DEngine:
         return y
 
     __call__ = forward
+
+    def forward_checked(self, x: torch.Tensor, out: Optional[torch.Tensor] = None,
+                        clip_offsets=None) -> torch.Tensor:
+        """Eager forward that honours the h3 range guard: waits for the call,
+        and when an h3 conv produced a non-finite value re-runs it on
+        full-range kernels (``range_fallback``)."""
+        y = self.forward(x, out=out, clip_offsets=clip_offsets)
+        if self.range_guard is not None:
+            torch.cuda.current_stream(self.device).synchronize()
+            self.range_fallback(x, y, clip_offsets)
+        return y
+
+    def range_fallback(self, x: torch.Tensor, y: torch.Tensor, clip_offsets=None) -> bool:
+        """After a completed call on input ``x`` with output ``y``: if this
+        engine's h3 range guard tripped, recompute ``y`` in place with every
+        conv on a full-range (non-h3) config and count it; True if it did."""
+        g = self.range_guard
+        if g is None or not g.tripped():
+            return False
+        g.reset()
+        with full_range():
+            z = self.forward(x, clip_offsets=clip_offsets)
+        y.copy_(z)
+        torch.cuda.current_stream(self.device).synchronize()
+        g.reset()
+        g.fallbacks += 1
+        return True
 
     @staticmethod
     def _clip_segments(coffs: Optional[torch.Tensor], n: int, device) -> torch.Tensor:
@@ -501,7 +565,7 @@ class GraphedEngine:
 
     def __init__(self, engine: R2P1DEngine, max_clips: int,
                  buckets: Sequence[int] = DEFAULT_BUCKETS, autotune: bool = True,
-                 warmup: int = 2):
+                 warmup: int = 1):
         assert engine.backend == "hip"
         if engine.bn_mode == "batch" and not engine.f32:
             raise ValueError("graphed bn_mode='batch' (per-video statistics) is fp32 only")
@@ -523,6 +587,39 @@ class GraphedEngine:
         self.graphs: Dict[int, Tuple[torch.cuda.CUDAGraph, torch.Tensor, torch.Tensor]] = {}
         self.pool = None
         self.capture_s = 0.0
+        self._last = None           # (bucket, n, clip offsets) of the last replay
+        # intermediate stages: each bucket graph's final BN apply writes through
+        # a device-held pointer (int64 [1] per bucket), so a replay can target
+        # an output slot (replay(out=...)); default: the bucket's static output
+        self.indirect_out = engine.supports_out_indirect and torch.cuda.is_available()
+        self._dst: Dict[int, torch.Tensor] = {}
+        self._dst_val: Dict[int, int] = {}
+        self._pinned_dst = [torch.zeros(1, dtype=torch.int64).pin_memory()
+                            if self.indirect_out else None for _ in range(4)]
+        self._pinned_dst_ev = [None] * 4
+        self._pinned_dst_i = 0
+
+    @property
+    def range_guard(self):
+        return self.engine.range_guard
+
+    def range_fallback(self, out: Optional[torch.Tensor] = None) -> bool:
+        """After the last replay completed: if the engine's h3 range guard
+        tripped, recompute that call's rows eagerly on full-range kernels (its
+        input still sits in the bucket's static input) into the bucket's
+        output, or into ``out`` (where the caller copied it); True if it did."""
+        g = self.engine.range_guard
+        if g is None or not g.tripped() or self._last is None:
+            return False
+        b, n, offs = self._last
+        _, static_in, static_out = self.graphs[b]
+        return self.engine.range_fallback(static_in[:n], static_out[:n] if out is None else out,
+                                          offs)
+
+    def bucket_floor(self, n: int) -> int:
+        """Largest bucket <= n (0 if none)."""
+        i = bisect.bisect_right(self.buckets, n)
+        return self.buckets[i - 1] if i else 0
 
     def bucket_for(self, n: int) -> int:
         i = bisect.bisect_left(self.buckets, n)
@@ -564,10 +661,18 @@ class GraphedEngine:
         torch.cuda.synchronize(self.device)
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
+        if self.indirect_out:
+            self._dst[b] = torch.zeros(1, dtype=torch.int64, device=self.device)
+            kw["out_indirect"] = self._dst[b]
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=self.pool):
             static_out = eng.forward(static_in, **kw)
         torch.cuda.synchronize(self.device)
+        if self.indirect_out:
+            # captured, not run: point the final apply at the static output
+            self._dst[b].fill_(static_out.data_ptr())
+            self._dst_val[b] = static_out.data_ptr()
+            torch.cuda.synchronize(self.device)
         self.graphs[b] = (g, static_in, static_out)
         self.capture_s += time.time() - t0
         return self.graphs[b]
@@ -612,18 +717,50 @@ class GraphedEngine:
         ev.record(torch.cuda.current_stream(self.device))
         self._pinned_ev[i] = ev
 
-    def replay(self, n: int, clip_offsets=None) -> torch.Tensor:
+    def _set_dst(self, b: int, ptr: int) -> None:
+        """Stage the final apply's destination address for bucket b (pinned
+        ring, stream-ordered, as _set_offsets)."""
+        if self._dst_val.get(b) == ptr:
+            return
+        i = self._pinned_dst_i
+        self._pinned_dst_i = (i + 1) % len(self._pinned_dst)
+        if self._pinned_dst_ev[i] is not None:
+            self._pinned_dst_ev[i].synchronize()
+        host = self._pinned_dst[i]
+        host[0] = ptr
+        self._dst[b].copy_(host, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._pinned_dst_ev[i] = ev
+        self._dst_val[b] = ptr
+
+    def replay(self, n: int, clip_offsets=None, out: Optional[torch.Tensor] = None
+               ) -> torch.Tensor:
         """Replay the bucket graph whose input was filled via input_buffer;
-        ``clip_offsets`` (bn_mode='batch'): the videos' clip ranges."""
+        ``clip_offsets`` (bn_mode='batch'): the videos' clip ranges. ``out``
+        (``indirect_out`` engines): write the n output rows straight into it
+        (e.g. an IPC output slot) instead of the bucket's static output."""
         b = self.bucket_for(n)
         g, static_in, static_out = self.graphs[b]
+        if out is not None:
+            if not self.indirect_out:
+                raise ValueError("replay(out=...) needs an intermediate fp32 batch-BN engine")
+            if (out.dtype != static_out.dtype or not out.is_contiguous()
+                    or tuple(out.shape[1:]) != tuple(static_out.shape[1:]) or out.shape[0] < b
+                    or out.device != static_out.device):
+                raise ValueError("replay output %s %s does not hold %d rows of %s %s"
+                                 % (tuple(out.shape), out.dtype, b,
+                                    tuple(static_out.shape[1:]), static_out.dtype))
+        if self.indirect_out:
+            self._set_dst(b, (out if out is not None else static_out).data_ptr())
         if self.batch_bn:
             self._set_offsets(b, n, clip_offsets)
+        self._last = (b, n, None if clip_offsets is None else [int(o) for o in clip_offsets])
         # rows >= n hold stale (finite) inputs; in eval mode clip rows are
         # independent, in batch mode they sit outside every video's segment:
         # their outputs are simply not returned
         g.replay()
-        return static_out[:n]
+        return static_out[:n] if out is None else out[:n]
 
     def forward(self, x: torch.Tensor, clip_offsets=None) -> torch.Tensor:
         n = x.shape[0]

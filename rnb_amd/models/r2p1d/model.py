@@ -46,7 +46,8 @@ from ...timecard import TimeCard, TimeCardList
 from ...video_path_provider import (DirectoryVideoPathIterator,
                                     SyntheticVideoPathIterator, VideoPathIterator)
 from .decoder import make_decoder
-from .engine import (GraphedEngine, R2P1DEngine, boundary_channels_p, boundary_shape)
+from .engine import (GraphedEngine, R2P1DEngine, boundary_channels_p, boundary_shape,
+                     geometric_buckets)
 from .network import (LAYER_INPUT_CTHW, R2Plus1DLayerWrapper, init_random_,
                       load_reference_state_dict, normalize_layer_sizes)
 from .sampler import R2P1DSampler
@@ -147,7 +148,7 @@ class R2P1DRunner(RunnerModel):
                  bn_mode=None, seed=0, ckpt_path=None, max_clips=DEFAULT_MAX_CLIPS,
                  warmup=3, use_graphs=True, autotune=True, dtype=None,
                  max_batch_videos=1, batch_wait_ms=0.0, bucket_step=None, lanes=1,
-                 **unused):
+                 stream_priority=0, **unused):
         super().__init__(device)
         if start_index < 1:
             raise ValueError("Wrong layer index for the starting layer! The start_index "
@@ -162,7 +163,10 @@ class R2P1DRunner(RunnerModel):
         self.max_batch_videos = int(max_batch_videos)
         self.batch_wait_s = float(batch_wait_ms) / 1000.0
         buckets = None
-        if bucket_step:
+        if bucket_step == "geo":
+            # geometric spacing + bucket-aligned gathering (gather_fit)
+            buckets = geometric_buckets(self.max_clips)
+        elif bucket_step:
             step = int(bucket_step)
             buckets = sorted(set(range(step, self.max_clips + 1, step)) | {1, self.max_clips})
         self.engine = build_engine(device, start_index, end_index, num_classes,
@@ -183,8 +187,10 @@ class R2P1DRunner(RunnerModel):
                 device, start_index, end_index, num_classes, layer_sizes, depth, backend,
                 bn_mode, seed, ckpt_path, self.max_clips, use_graphs, autotune, self.dtype,
                 buckets))
-        self._lane_streams = ([torch.cuda.Stream(device) for _ in range(self.lanes)]
-                              if self.lanes > 1 else None)
+        # lane streams at the runner's stream priority (runner.py passes the
+        # queue group's, e.g. the high-priority 15-clip replica's)
+        self._lane_streams = ([torch.cuda.Stream(device, priority=int(stream_priority))
+                               for _ in range(self.lanes)] if self.lanes > 1 else None)
         self._lane_done = [None] * self.lanes     # completion event of each lane's last call
         self._lane = 0                             # lane of the next call
         self.last_event = None                     # completion event of the last call
@@ -208,6 +214,63 @@ class R2P1DRunner(RunnerModel):
         self._gather_buf = None
         self._check_dir = os.environ.get("RNB_CHECK_DIR") or None
         self._checked = {}               # samples written per stratum
+        # h3 range guard (ops/conv_f32.RangeGuard): graphed calls are checked
+        # when the runner sees them complete (on_complete), in call order
+        self.range_guarded = any(getattr(e, "range_guard", None) is not None
+                                 for e in self._lane_engines)
+        self._guard_calls = []           # (graphed engine, output) per call in flight
+        self.range_fallbacks = 0
+        self._direct_calls = self._staged_calls = 0     # intermediate-stage outputs
+
+    def on_complete(self, outputs) -> None:
+        """runner.py: the oldest call in flight has completed. If an h3 conv of
+        it produced a non-finite value (an input past the fp16 range of the h3
+        split), recompute its output on full-range kernels before it is used."""
+        if not self._guard_calls:
+            return
+        eng, out = self._guard_calls.pop(0)
+        if eng.range_fallback(out):
+            self.range_fallbacks += 1
+            print("[runner] h3 range guard: call of %d rows re-run on full-range kernels "
+                  "(%d so far)" % (out.shape[0], self.range_fallbacks), flush=True)
+
+    def runtime_stats(self) -> dict:
+        st = {"h3_range_fallbacks": self.range_fallbacks} if self.range_guarded else {}
+        if self.end_index < 5:
+            st.update(direct_slot_calls=self._direct_calls, staged_slot_calls=self._staged_calls)
+        return st
+
+    def call_into(self, tensors, non_tensors, time_card, out):
+        """Intermediate stage (end_index < 5; runner.py direct_out): write the
+        boundary activation straight into the output slot ``out[0]``. The
+        fp32 batch-BN graphs end in a BatchNorm apply that writes through a
+        device-held pointer, so the replay targets the slot itself and no
+        staging copy runs (the reference copies each output
+        into its slot, runner.py:156-173). Other engines compute into their
+        own buffer and copy the rows into the slot."""
+        x = tensors[0]
+        eng = self.engine
+        slot = out[0]
+        if (self.lanes == 1 and isinstance(eng, GraphedEngine) and eng.indirect_out
+                and x.shape[0] > 0 and self._gather_ptr is not None
+                and x.data_ptr() == self._gather_ptr):
+            self._gather_ptr = None
+            offs = self._clip_offsets(time_card, x.shape[0])
+            y = eng.replay(x.shape[0], clip_offsets=offs, out=slot)
+            if eng.range_guard is not None:
+                self._guard_calls.append((eng, y))
+            self._direct_calls += 1
+            return (y,), non_tensors, time_card
+        (y,), nts, tc = self._call(tensors, non_tensors, time_card)
+        if self.lanes > 1 and self.last_event is not None:
+            torch.cuda.current_stream(self.device).wait_event(self.last_event)
+        if y.shape[0]:
+            slot[:y.shape[0]].copy_(y)
+        if self._guard_calls and self._guard_calls[-1][1] is y:
+            # a guard re-run of this call must land in the slot
+            self._guard_calls[-1] = (self._guard_calls[-1][0], slot[:y.shape[0]])
+        self._staged_calls += 1
+        return (slot[:y.shape[0]],), nts, tc
 
     # consumer-side batching (runner.py): up to max_batch_videos queued
     # videos per call, their rows pulled into the graph's static input
@@ -215,6 +278,22 @@ class R2P1DRunner(RunnerModel):
         if self.max_batch_videos <= 1 and not isinstance(self.engine, GraphedEngine):
             return None
         return (max(1, self.max_batch_videos), self.max_clips, self.batch_wait_s)
+
+    # trim a gathered call to a bucket boundary when padding up to the next
+    # bucket would add more than this fraction of rows (runner.py gather)
+    FIT_PAD_FRAC = 0.03
+
+    def gather_fit(self, rows: int) -> int:
+        """Rows a gathered call of ``rows`` should keep: ``rows`` when padding
+        to its graph bucket is cheap, else the largest bucket below (runner.py
+        defers the trailing items to the next call)."""
+        eng = self.engine
+        if not isinstance(eng, GraphedEngine) or rows <= 1:
+            return rows
+        up = eng.bucket_for(rows)
+        if up - rows <= self.FIT_PAD_FRAC * rows:
+            return rows
+        return eng.bucket_floor(rows) or rows
 
     def completion_event(self):
         """lanes > 1: the event that completes the last call (it ran on a lane
@@ -334,9 +413,23 @@ class R2P1DRunner(RunnerModel):
                 and isinstance(eng, GraphedEngine) and x.shape[0] > 0):
             # rows already sit in the bucket graph's static input: replay only
             self._gather_ptr = None
-            return eng.replay(x.shape[0], clip_offsets=offs)
+            y = eng.replay(x.shape[0], clip_offsets=offs)
+            if eng.range_guard is not None:
+                self._guard_calls.append((eng, y))
+            return y
         self._gather_ptr = None
         x = _to_boundary(x, self.start_index, self.dtype)
+        if isinstance(eng, GraphedEngine) and x.shape[0] > 0:
+            y = eng.forward(x, clip_offsets=offs) if self.bn_mode == "batch" else eng(x)
+            if eng.range_guard is not None:
+                self._guard_calls.append((eng, y))
+            return y
+        if getattr(eng, "range_guard", None) is not None and x.shape[0] > 0:
+            # eager hip engine: checked right here (waits for the call)
+            before = eng.range_guard.fallbacks
+            y = eng.forward_checked(x, clip_offsets=offs)
+            self.range_fallbacks += eng.range_guard.fallbacks - before
+            return y
         if self.bn_mode == "batch" and x.shape[0] > 0:
             return eng.forward(x, clip_offsets=offs)
         return eng(x)
@@ -457,6 +550,16 @@ class R2P1DSingleStep(RunnerModel):
                                   max_clips=max_clips, warmup=warmup,
                                   use_graphs=use_graphs, autotune=autotune, dtype=dtype)
 
+    @property
+    def range_guarded(self) -> bool:
+        return self.runner.range_guarded
+
+    def on_complete(self, outputs) -> None:
+        self.runner.on_complete(outputs)
+
+    def runtime_stats(self) -> dict:
+        return self.runner.runtime_stats()
+
     def __call__(self, tensors, non_tensors, time_card):
         eng = self.runner.engine
         if isinstance(eng, GraphedEngine) and self.runner.device.type == "cuda":
@@ -467,7 +570,10 @@ class R2P1DSingleStep(RunnerModel):
             if starts:
                 static_in, _ = eng.input_buffer(len(starts))
                 self.loader.decoder.decode(vid, starts, out=static_in[:len(starts)])
-                return (eng.replay(len(starts)),), None, time_card
+                y = eng.replay(len(starts))
+                if eng.range_guard is not None:
+                    self.runner._guard_calls.append((eng, y))
+                return (y,), None, time_card
             frames = self.loader.decoder.empty()
             (logits,), _, _ = self.runner((frames,), None, time_card)
             return (logits,), None, time_card

@@ -88,11 +88,13 @@ class BatchNormBatch:
     def forward_hip_f32(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,
                         out: Optional[torch.Tensor] = None,
                         segments: Optional[torch.Tensor] = None,
-                        seg_rows=None, sums=None, rpc: int = 1) -> torch.Tensor:
+                        seg_rows=None, sums=None, rpc: int = 1,
+                        out_ind: Optional[torch.Tensor] = None) -> torch.Tensor:
         """fp32 tensor; ``segments``: device int32 [nseg+1] offsets in units of
         ``rpc`` rows (clip offsets with rpc = T*H*W, or row offsets with rpc =
         1): each segment -- one video -- gets its own statistics; default one
-        segment."""
+        segment. ``out_ind``: device memory holding the address the apply
+        writes to at run time (instead of ``out``, whose shape it must have)."""
         from .native import kernels
         k = kernels()
         N, T, H, W, Cs = y.shape
@@ -103,7 +105,7 @@ class BatchNormBatch:
         if segments is None:
             segments, rpc = self._whole(M, y.device), 1
         nseg = segments.numel() - 1
-        if (sums is not None and nseg <= WALK_APPLY_MAX_SEG and C <= 512
+        if (sums is not None and nseg <= WALK_APPLY_MAX_SEG and C <= 512 and out_ind is None
                 and os.environ.get("RNB_BN_WALK_APPLY", "0") == "1"):
             return self._walk_apply_f32(y, residual, relu, z, segments, sums, rpc)
         # statistics, scale / shift and the running update (three small
@@ -114,7 +116,8 @@ class BatchNormBatch:
                            residual.data_ptr() if residual is not None else None,
                            segments.data_ptr(), nseg, rpc, ss.data_ptr(), 1 if relu else 0,
                            M, C, Cs, z.shape[-1],
-                           residual.shape[-1] if residual is not None else 0, stream)
+                           residual.shape[-1] if residual is not None else 0, stream,
+                           out_ind.data_ptr() if out_ind is not None else None)
         return z
 
     def _walk_apply_f32(self, y, residual, relu, z, segments, sums, rpc):
@@ -245,9 +248,12 @@ class BatchNormBatch:
 
     def forward_hip(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,
                     out: Optional[torch.Tensor] = None, segments=None,
-                    seg_rows=None, sums=None, rpc: int = 1) -> torch.Tensor:
+                    seg_rows=None, sums=None, rpc: int = 1, out_ind=None) -> torch.Tensor:
         if y.dtype == torch.float32:
-            return self.forward_hip_f32(y, residual, relu, out, segments, seg_rows, sums, rpc)
+            return self.forward_hip_f32(y, residual, relu, out, segments, seg_rows, sums, rpc,
+                                        out_ind=out_ind)
+        if out_ind is not None:
+            raise NotImplementedError("indirect BN output is fp32 only")
         if segments is not None and segments.numel() > 2:
             raise NotImplementedError("per-video BN statistics are fp32 only")
         from .native import kernels

@@ -176,6 +176,52 @@ def h3_enabled() -> bool:
     return os.environ.get("RNB_H3", "1") != "0"
 
 
+class RangeGuard:
+    """h3 range guard of one engine (reference precision is cuDNN
+    fp32 with full range, models/r2p1d/model.py:82-84). The h3 kernels split
+    each activation after scaling it by 2^H3_IN_LOG2, so an input with
+    |x| >= 65504 / 2^6 (~1024) would become fp16 inf and its products NaN.
+    Their epilogues (and the split-K reduce) check every output value before
+    the ReLU and write 1 into this guard's flag, a word of host-coherent
+    memory, when one is non-finite: the host reads it after the call completed
+    without a copy. ``activate()`` points the launches that follow (eager or
+    captured into a HIP graph) at this flag; the engine then re-runs a tripped
+    call on full-range kernels (``full_range()``: fp32 MFMA / Winograd / x6,
+    which keep fp32's exponent range) and counts it."""
+
+    def __init__(self):
+        from .native import runtime
+        self._host, self.dev_ptr = runtime().host_alloc_mapped(64)
+        import ctypes
+        self._word = ctypes.c_int.from_address(self._host)
+        self.fallbacks = 0
+
+    def activate(self) -> None:
+        from .native import kernels
+        kernels().h3_set_range_flag(self.dev_ptr)
+
+    def tripped(self) -> bool:
+        return self._word.value != 0
+
+    def reset(self) -> None:
+        self._word.value = 0
+
+
+_FULL_RANGE = [0]      # > 0 inside full_range(): no h3 configs
+
+
+class full_range:
+    """Context: every fp32 conv picks a non-h3 config (the guard's re-run)."""
+
+    def __enter__(self):
+        _FULL_RANGE[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _FULL_RANGE[0] -= 1
+        return False
+
+
 def h3_weight_scale_log2(wmat: torch.Tensor) -> int:
     """Power-of-two exponent sw that puts max |w| * 2^sw in [2^13, 2^14)."""
     m = float(wmat.abs().max()) if wmat.numel() else 0.0
@@ -706,7 +752,21 @@ class ConvLayerF32:
     def config_for(self, x_shape) -> int:
         """Tile config for this input shape: tuned (this layer, or any layer of
         the same geometry via the tuning cache), else the nearest tuned batch
-        of the same geometry, else the cost heuristic."""
+        of the same geometry, else the cost heuristic. Inside ``full_range()``
+        an h3 choice is replaced by the heuristic's full-range config."""
+        cid = self._config_for(x_shape)
+        if _FULL_RANGE[0] and is_h3(cid):
+            N, T, H, W, _ = x_shape
+            To, Ho, Wo = self.geom.out_thw(T, H, W)
+            cid = self.heuristic_config(N * To * Ho * Wo)
+            if os.environ.get("RNB_WINOGRAD", "1") != "0":
+                if self.wino_ok:
+                    cid = wino_default(False)
+                elif self.winot_ok and T >= WINOT_MIN_T:
+                    cid = wino_default(True)
+        return cid
+
+    def _config_for(self, x_shape) -> int:
         key = tuple(x_shape[:4])
         cid = self._config.get(key)
         if cid is None:

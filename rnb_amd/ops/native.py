@@ -255,6 +255,8 @@ class Kernels:
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
             ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_int,
             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        lib.rnb_bn_seg_apply_f32_ind.argtypes = (lib.rnb_bn_seg_apply_f32.argtypes[:-1]
+                                                 + [ctypes.c_void_p, ctypes.c_void_p])
         lib.rnb_bn_seg_walk_apply_f32.argtypes = [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
             ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
@@ -329,6 +331,8 @@ class Kernels:
         lib.rnb_conv_h3t_launch.argtypes = lib.rnb_conv_h3r_launch.argtypes
         lib.rnb_conv_h3t_launch.restype = ctypes.c_int
         lib.rnb_conv_h3t_pixels.argtypes = [ctypes.c_int, ctypes.c_int]
+        lib.rnb_h3_set_range_flag.argtypes = [ctypes.c_void_p]
+        lib.rnb_h3_set_range_flag.restype = None
         lib.rnb_conv_h3t_pixels.restype = ctypes.c_int
         lib.rnb_conv_h3_config_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                                 ctypes.POINTER(ctypes.c_int)]
@@ -412,6 +416,11 @@ class Kernels:
                                            ws or None, in_scale, out_scale, in_ss or None,
                                            in_seg or None),
                "conv_h3 (config %d, ksplit %d)" % (config_id, ksplit))
+
+    def h3_set_range_flag(self, dev_ptr: int) -> None:
+        """Range-guard flag (device address of host-coherent memory, 0 = none)
+        written by the h3 launches that follow when an output is non-finite."""
+        self.lib.rnb_h3_set_range_flag(dev_ptr or None)
 
     def conv_h3r(self, params: ConvParams, variant: int, stream: int, in_scale: float,
                  out_scale: float, sums: int = 0, clip_seg: int = 0, stats_c: int = 0,
@@ -539,10 +548,13 @@ class Kernels:
             "bn_seg_stats_from_sums_f32")
 
     def bn_seg_apply_f32(self, y_ptr, z_ptr, res_ptr, coffs_ptr, nseg, rpc, ss_ptr, relu, M, C,
-                         y_stride, z_stride, res_stride, stream):
-        _check(self.lib.rnb_bn_seg_apply_f32(y_ptr, z_ptr, res_ptr, coffs_ptr, nseg, rpc,
-                                             ss_ptr, relu, M, C, y_stride, z_stride, res_stride,
-                                             stream), "bn_seg_apply_f32")
+                         y_stride, z_stride, res_stride, stream, zind_ptr=None):
+        """``zind_ptr``: device address of an 8-byte pointer the kernel reads
+        as its destination instead of ``z_ptr`` (graphs writing into a slot)."""
+        _check(self.lib.rnb_bn_seg_apply_f32_ind(y_ptr, z_ptr, res_ptr, coffs_ptr, nseg, rpc,
+                                                 ss_ptr, relu, M, C, y_stride, z_stride,
+                                                 res_stride, zind_ptr or None, stream),
+               "bn_seg_apply_f32")
 
     def bn_seg_walk_apply_f32(self, sums_ptr, sums_c, ticket_ptr, coffs_ptr, nseg, rpc, C,
                               gamma_ptr, beta_ptr, eps, momentum, channels, rmean_ptr, rvar_ptr,
@@ -613,6 +625,8 @@ class Runtime:
         lib.rnb_error_string.restype = ctypes.c_char_p
         lib.rnb_malloc.argtypes = [ctypes.POINTER(vp), sz]
         lib.rnb_free.argtypes = [vp]
+        lib.rnb_host_alloc_mapped.argtypes = [sz, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        lib.rnb_host_free.argtypes = [vp]
         lib.rnb_ipc_get_mem_handle.argtypes = [vp, vp]
         lib.rnb_ipc_open_mem_handle.argtypes = [vp, ctypes.POINTER(vp)]
         lib.rnb_ipc_close_mem_handle.argtypes = [vp]
@@ -661,6 +675,17 @@ class Runtime:
 
     def free(self, ptr: int) -> None:
         _check(self.lib.rnb_free(ptr), "hipFree")
+
+    def host_alloc_mapped(self, nbytes: int):
+        """(host pointer, device pointer) of zeroed host-coherent memory the
+        GPU can write (hipHostMalloc mapped | coherent)."""
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        _check(self.lib.rnb_host_alloc_mapped(nbytes, ctypes.byref(h), ctypes.byref(d)),
+               "hipHostMalloc(%d)" % nbytes)
+        return h.value, d.value
+
+    def host_free(self, host: int) -> None:
+        _check(self.lib.rnb_host_free(host), "hipHostFree")
 
     def ipc_get_handle(self, ptr: int) -> bytes:
         buf = ctypes.create_string_buffer(self.handle_size)
@@ -712,6 +737,11 @@ class Runtime:
 
     def event_query(self, ev: int) -> int:
         return int(self.lib.rnb_event_query(ev))
+
+    def event_destroy(self, ev: int) -> None:
+        """hipEventDestroy: frees an event this process created, or closes an
+        interprocess event it opened with ``event_open_handle``."""
+        _check(self.lib.rnb_event_destroy(ev), "hipEventDestroy")
 
     def memcpy_async(self, dst: int, src: int, nbytes: int, stream: int) -> None:
         _check(self.lib.rnb_memcpy_async(dst, src, nbytes, stream), "hipMemcpyAsync")

@@ -27,11 +27,26 @@ that timeout. The producer may decode straight into a send slot
 (``slot_views`` / ``commit``, runner direct_out).
 
 Per (src, dst) pair the claims are served in the order the consumer posted
-them, so sends and receives match. All participating runners form one
-``torch.distributed`` world (backend ``nccl`` = RCCL on ROCm; ``gloo`` for the
-CPU tests) created by the launcher-assigned ``DistInfo``. RCCL cannot put two
-ranks of one communicator on the same GPU, so the launcher only allows this
-transport on edges whose producer and consumers sit on different GPUs.
+them, so sends and receives match. The participating runners form one world
+(ranks from the launcher-assigned ``DistInfo``, rendezvous on a file store),
+but there is no world communicator: every (producer, consumer) pair of an RCCL
+edge gets its own 2-rank process-group backend (``ProcessGroupNCCL`` = RCCL on
+ROCm, ``ProcessGroupGloo`` for the CPU tests) under its own store prefix,
+created by the two members in one global order (no creation deadlock), and a
+call's sends or receives are launched per pair communicator. Hence
+
+* RCCL never sees two ranks of one communicator on one GPU, even when a GPU
+  hosts several consumer replicas or producers of an edge (the launcher only
+  refuses a pair whose two ends share a GPU, ``_assign_rccl_ranks``);
+* a process that both consumes one RCCL edge and produces the next (a middle
+  stage) drives disjoint communicators from its main thread (receives) and
+  its sender thread (sends);
+* the world's start barrier runs on the rendezvous store, not as an RCCL
+  collective over the whole world.
+
+(``torch.distributed.new_group(use_local_synchronization=True)`` was the
+first design; with gloo a rank's second pair group never finished its
+rendezvous, so the backends are built directly.)
 """
 from __future__ import annotations
 
@@ -46,42 +61,124 @@ import torch
 
 from .transport import RingBase
 
-_state = {"rank": None, "world": None, "backend": None}
+_state = {"rank": None, "world": None, "backend": None, "pairs": {}, "device": None}
 
 
 class DistInfo:
-    """Picklable description of this process's place in the RCCL world."""
+    """Picklable description of this process's place in the RCCL world:
+    its rank, and the (producer rank, consumer rank) pairs of the RCCL edges
+    it is an end of (one 2-rank communicator each; none given: one per other
+    rank); ``gpus`` maps every rank to its GPU (reporting)."""
 
-    def __init__(self, rank: int, world_size: int, store_path: str, backend: str):
+    def __init__(self, rank: int, world_size: int, store_path: str, backend: str,
+                 pairs=(), gpus=None):
         self.rank, self.world_size = rank, world_size
         self.store_path, self.backend = store_path, backend
+        self.pairs = sorted(tuple(sorted(p)) for p in pairs)
+        self.gpus = dict(gpus or {})
+
+
+def _store_barrier(store, key: str, n: int) -> None:
+    """Every rank of the world passes ``key`` (on the rendezvous store; an
+    RCCL collective over the world would need one GPU per rank)."""
+    store.add(key, 1)
+    deadline = time.time() + _timeout().total_seconds()
+    while store.add(key, 0) < n:
+        if time.time() > deadline:
+            raise TimeoutError("RCCL world barrier %s: %d of %d ranks after %s s"
+                               % (key, store.add(key, 0), n, _timeout().total_seconds()))
+        time.sleep(0.01)
 
 
 def init_dist(info: Optional[DistInfo], device: torch.device) -> None:
+    """Join the RCCL world: one 2-rank process-group backend per pair this
+    rank belongs to (``ProcessGroupNCCL`` = RCCL, or ``ProcessGroupGloo``),
+    each rendezvousing under its own prefix of the launcher's file store, in
+    one global pair order (so creation cannot deadlock); then a store barrier
+    over the world. There is no world communicator: no RCCL communicator ever
+    holds two ranks of one GPU, and a middle stage's receives (main thread)
+    and sends (sender thread) run on different communicators."""
     if info is None or _state["rank"] is not None:
         return
     import torch.distributed as dist
     store = dist.FileStore(info.store_path, info.world_size)
-    kwargs = {}
-    if info.backend == "nccl":
-        kwargs["device_id"] = device
-    # the group timeout is the watchdog of stream-ordered RCCL receives
-    dist.init_process_group(info.backend, store=store, rank=info.rank,
-                            world_size=info.world_size, timeout=_timeout(), **kwargs)
-    # one collective first: batched point-to-point groups may then involve
-    # only the two peers of an edge (torch.distributed.batch_isend_irecv)
-    dist.barrier()
-    _state.update(rank=info.rank, world=info.world_size, backend=info.backend)
+    pairs = info.pairs or sorted(tuple(sorted((info.rank, o)))
+                                 for o in range(info.world_size) if o != info.rank)
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    comms = {}
+    for pair in pairs:
+        if info.rank not in pair:
+            continue
+        me = pair.index(info.rank)
+        ps = dist.PrefixStore("rnb_pair_%d_%d/" % pair, store)
+        if info.backend == "nccl":
+            opts = dist.ProcessGroupNCCL.Options()
+            opts._timeout = _timeout()
+            pg = dist.ProcessGroupNCCL(ps, me, 2, opts)
+        elif info.backend == "gloo":
+            pg = dist.ProcessGroupGloo(ps, me, 2, _timeout())
+        else:
+            raise ValueError("RCCL world backend must be 'nccl' or 'gloo', got %r"
+                             % info.backend)
+        comms[pair[1 - me]] = (pg, 1 - me)         # peer global rank -> (pg, its rank)
+    _store_barrier(store, "rnb_rccl_world_up", info.world_size)
+    _state.update(rank=info.rank, world=info.world_size, backend=info.backend,
+                  pairs=comms, device=device)
+
+
+def _pair(peer: int):
+    comm = _state["pairs"].get(int(peer))
+    if comm is None:
+        raise RuntimeError("RCCL: rank %s has no communicator with rank %d (peers %s)"
+                           % (_state["rank"], peer, sorted(_state["pairs"])))
+    return comm
+
+
+class P2P:
+    """One point-to-point transfer (``kind`` "send" or "recv") with the peer's
+    global rank, launched by ``launch_p2p`` on that pair's communicator."""
+    __slots__ = ("kind", "tensor", "peer")
+
+    def __init__(self, kind: str, tensor: torch.Tensor, peer: int):
+        self.kind, self.tensor, self.peer = kind, tensor, int(peer)
+
+
+def launch_p2p(ops) -> list:
+    """Launch transfers in order, per pair communicator (one NCCL group per
+    pair when the backend coalesces); returns their works."""
+    by = collections.OrderedDict()
+    for op in ops:
+        by.setdefault(op.peer, []).append(op)
+    works = []
+    for peer, lst in by.items():
+        pg, pr = _pair(peer)
+        co = (_state["backend"] == "nccl" and len(lst) > 1
+              and getattr(pg, "supports_coalescing", False))
+        dev = lst[0].tensor.device
+        if co:
+            pg._start_coalescing(dev)
+        ws = [pg.send([op.tensor], pr, 0) if op.kind == "send" else pg.recv([op.tensor], pr, 0)
+              for op in lst]
+        if co:
+            ws = [pg._end_coalescing(dev)]
+        works += ws
+    return works
 
 
 def shutdown_dist() -> None:
     if _state["rank"] is None:
         return
-    import torch.distributed as dist
     try:
-        dist.destroy_process_group()
+        for pg, _ in _state["pairs"].values():
+            shut = getattr(pg, "shutdown", None) or getattr(pg, "_shutdown", None)
+            if callable(shut):
+                try:
+                    shut()
+                except Exception:
+                    pass
     finally:
-        _state.update(rank=None, world=None, backend=None)
+        _state.update(rank=None, world=None, backend=None, pairs={}, device=None)
 
 
 def my_rank() -> int:
@@ -101,17 +198,16 @@ def _timeout():
 
 def flush_recvs(pending: list) -> int:
     """Launch the receives ``read_into`` appended to ``pending`` (the runner's
-    list for one model call) as one group and empty the list. RCCL: the
-    current stream waits for them (ordered on the GPU, the host does not
-    block; a stuck sender trips the process group's timeout). gloo (CPU): wait
+    list for one model call) per pair communicator and empty the list. RCCL:
+    the current stream waits for them (ordered on the GPU, the host does not
+    block; a stuck sender trips the communicator's timeout). gloo (CPU): wait
     on the host, raising TimeoutError after RNB_RCCL_TIMEOUT_S. Returns the
     number of receives."""
     if not pending:
         return 0
-    import torch.distributed as dist
     ops = list(pending)
     pending.clear()
-    works = dist.batch_isend_irecv(ops)
+    works = launch_p2p(ops)
     if _state["backend"] == "nccl":
         for w in works:
             w.wait()
@@ -188,7 +284,6 @@ class RcclRing(RingBase):
         self._thread.start()
 
     def _serve(self):
-        import torch.distributed as dist
         cuda = self.device.type == "cuda"
         if cuda:
             torch.cuda.set_device(self.device)
@@ -231,8 +326,8 @@ class RcclRing(RingBase):
                             stream.wait_event(self._written[idx])
                         for t, rows in zip(self._slots[idx], self.valid_rows(idx)):
                             if rows:
-                                ops.append(dist.P2POp(dist.isend, t[:rows], dst))
-                    works = dist.batch_isend_irecv(ops) if ops else []
+                                ops.append(P2P("send", t[:rows], dst))
+                    works = launch_p2p(ops) if ops else []
                     for w in works:
                         w.wait(_timeout())   # gloo: done; nccl: this stream waits on the sends
                     if stream is not None:
@@ -312,8 +407,17 @@ class RcclRing(RingBase):
                 ok = native.runtime().can_access_peer(device.index, self.producer_gpu)
             except Exception as err:           # logged, not fatal
                 ok = "unknown (%s)" % err
+            self._peer_access = ok
             print("[ring %s] rccl edge gpu %d -> gpu %d, peer access %s"
                   % (self.name, self.producer_gpu, device.index, ok), flush=True)
+
+    def handle_stats(self) -> dict:
+        """Consumer side, for the result JSON: edges attached and their
+        peer-access state (cross-GPU edges)."""
+        pa = getattr(self, "_peer_access", None)
+        return {"edges": 1, "peer_access_yes": int(pa is True),
+                "peer_access_no": int(pa is False),
+                "peer_access_unknown": int(isinstance(pa, str))}
 
     def read_into(self, idx, placeholders, descriptor=None, pending=None):
         """Claim slot ``idx`` and append its receives into ``placeholders``
@@ -321,13 +425,12 @@ class RcclRing(RingBase):
         ``flush_recvs(pending)`` launches them together with the other items
         of the call, so the views are valid only after it. Without a list the
         receives are launched at once."""
-        import torch.distributed as dist
         src = self.producer_rank if descriptor is None else descriptor
         ops = [] if pending is None else pending
         out = []
         for ph, rows in zip(placeholders, self.valid_rows(idx)):
             if rows:
-                ops.append(dist.P2POp(dist.irecv, ph[:rows], src))
+                ops.append(P2P("recv", ph[:rows], src))
             out.append(ph[:rows])
         self.claims.put((idx, my_rank()))
         if pending is None:

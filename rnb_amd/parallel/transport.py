@@ -245,6 +245,9 @@ HIP_ERROR_NOT_READY = 600
 EVENT_ROTATE = int(os.environ.get("RNB_IPC_EVENT_ROTATE", "30"))
 # largest single IPC allocation of a slot ring (RNB_IPC_CHUNK_MB, default 2048)
 IPC_CHUNK_BYTES = int(os.environ.get("RNB_IPC_CHUNK_MB", "2048")) << 20
+# superseded interprocess events a process keeps waiting for their marker
+# before it synchronises the oldest one (IpcRing._retire)
+RETIRE_MAX = 64
 
 
 class IpcRing(RingBase):
@@ -277,6 +280,19 @@ class IpcRing(RingBase):
     entry and bumps the slot's epoch before the record that the other side
     will wait on; the other side re-opens the handle when the epoch changed.
     A refused wait still falls back to the host (``_wait_ipc_event``).
+
+    Event lifecycle (bounded; the reference keeps a fixed set of per-slot
+    events, control.py:19-46). A superseded event -- a "written" or
+    "released" event its owner replaced, or a handle a peer re-opened for a
+    new epoch -- is handed to ``_retire`` together with a marker recorded on
+    the stream right after the first use of its replacement. The use chain
+    makes the marker a safe point for every process: the owner's new record
+    (or the peer's new wait) is ordered after the other side's last use of the
+    old event through the slot's write -> pull -> release cycle. Once the
+    marker completes, the old event is destroyed (owner) or closed (peer).
+    At most RETIRE_MAX events wait per process; past that the oldest marker
+    is synchronised. ``handle_stats()["events_live"]`` counts what a process
+    holds, and ``close`` frees every remaining event.
     """
 
     kind = "ipc"
@@ -326,6 +342,8 @@ class IpcRing(RingBase):
         self._opened_base: Dict[Tuple, List[int]] = {}        # consumer: opened allocations
         self.events_opened = 0
         self.events_created = 0
+        self.events_destroyed = 0       # created or opened events freed again
+        self._retiring = None           # [(marker, event)] awaiting destruction
         self.stale_event_waits = 0      # stream waits ROCm refused on completed events
         self.gpu_waits = 0              # stream waits ordered on the GPU
         self._dev = None
@@ -359,6 +377,7 @@ class IpcRing(RingBase):
         st["_cid"] = None
         st["_views"] = None
         st["_token"] = None
+        st["_retiring"] = None
         return st
 
     @property
@@ -420,11 +439,46 @@ class IpcRing(RingBase):
         off = idx * EVENT_HANDLE_BYTES
         self.wev_handles[off:off + len(h)] = h
         self.wev_epoch[idx] += 1
-        self._wev[idx] = ev          # the old one stays alive: a consumer may still wait on it
+        old, self._wev[idx] = self._wev[idx], ev
         self._wrec[idx] = 0
         self.events_created += 1
+        return old
 
-    def _release_event(self, cid: int, idx: int) -> int:
+    def _retire(self, ev, stream) -> None:
+        """Free interprocess event ``ev`` (created or opened by this process)
+        once the work enqueued on ``stream`` so far has completed; call right
+        after the first use of its replacement (see the class docstring)."""
+        if ev is None:
+            return
+        if self._retiring is None:
+            self._retiring = []
+        marker = torch.cuda.Event()
+        marker.record(stream)
+        self._retiring.append((marker, ev))
+        self._reap()
+
+    def _reap(self, wait_all: bool = False) -> None:
+        """Destroy retired events whose marker completed (all of them, waiting
+        if needed, with ``wait_all``; the oldest when over RETIRE_MAX)."""
+        if not self._retiring:
+            return
+        from ..ops import native
+        rt = native.runtime()
+        keep = []
+        over = len(self._retiring) - RETIRE_MAX
+        for k, (marker, ev) in enumerate(self._retiring):
+            if wait_all or k < over:
+                marker.synchronize()
+            elif not marker.query():
+                keep.append((marker, ev))
+                continue
+            rt.event_destroy(ev)
+            self.events_destroyed += 1
+        self._retiring = keep
+
+    def _release_event(self, cid: int, idx: int):
+        """(event, superseded opened event or None) of consumer ``cid``'s
+        current release event of slot ``idx``."""
         from ..ops import native
         evs = self._rel_open.get(cid)
         if evs is None:
@@ -433,12 +487,15 @@ class IpcRing(RingBase):
         if epoch == 0:
             raise RuntimeError("ring %s: consumer %d released slot %d before "
                                "publishing its event" % (self.name, cid, idx))
+        old = None
         if evs[idx] is None or evs[idx][1] != epoch:
             off = (cid * self.num_slots + idx) * EVENT_HANDLE_BYTES
             h = bytes(self.rel_handles[off:off + EVENT_HANDLE_BYTES])
+            if evs[idx] is not None:
+                old = evs[idx][0]
             evs[idx] = (native.runtime().event_open_handle(h), epoch)
             self.events_opened += 1
-        return evs[idx][0]
+        return evs[idx][0], old
 
     def begin_write(self, idx: int, stream=None) -> None:
         """Order the producer stream after the last consumer's pull of ``idx``
@@ -448,9 +505,10 @@ class IpcRing(RingBase):
         cid = self.released_by[idx]
         if cid < 0:
             return
-        from ..ops import native
         stream = stream or torch.cuda.current_stream(self._dev)
-        self._wait_ipc_event(stream, self._release_event(cid, idx), idx)
+        ev, old = self._release_event(cid, idx)
+        self._wait_ipc_event(stream, ev, idx)
+        self._retire(old, stream)
 
     def _wait_ipc_event(self, stream, ev: int, idx: int) -> None:
         """Order ``stream`` after an interprocess event. ROCm's IPC events can
@@ -480,10 +538,12 @@ class IpcRing(RingBase):
         from ..ops import native
         stream = stream or torch.cuda.current_stream(self._dev)
         if self.gpu_ordered:
+            old = None
             if self._wrec[idx] >= EVENT_ROTATE:
-                self._new_written_event(idx)
+                old = self._new_written_event(idx)
             native.runtime().event_record(self._wev[idx], stream.cuda_stream)
             self._wrec[idx] += 1
+            self._retire(old, stream)
         else:
             stream.synchronize()   # push completes before the slot is marked full
         self._set_valid(idx, rows)
@@ -557,18 +617,22 @@ class IpcRing(RingBase):
                 self._wopen[key] = [None] * self.num_slots    # opened on first pull
         return ptrs
 
-    def _written_event(self, key, idx: int) -> int:
-        """The producer's current "written" event of slot ``idx`` (opened on
-        first use and again whenever the producer rotated it)."""
+    def _written_event(self, key, idx: int):
+        """(event, superseded opened event or None): the producer's current
+        "written" event of slot ``idx`` (opened on first use and again
+        whenever the producer rotated it)."""
         evs = self._wopen[key]
         epoch = self.wev_epoch[idx]
+        old = None
         if evs[idx] is None or evs[idx][1] != epoch:
             from ..ops import native
             off = idx * EVENT_HANDLE_BYTES
             h = bytes(self.wev_handles[off:off + EVENT_HANDLE_BYTES])
+            if evs[idx] is not None:
+                old = evs[idx][0]
             evs[idx] = (native.runtime().event_open_handle(h), epoch)
             self.events_opened += 1
-        return evs[idx][0]
+        return evs[idx][0], old
 
     def rows_of(self, idx: int) -> int:
         return self.valid_rows(idx)[0]
@@ -589,8 +653,9 @@ class IpcRing(RingBase):
         if gpu:
             stream = torch.cuda.current_stream(dev)
             if self.gpu_ordered:
-                self._wait_ipc_event(stream, self._written_event(tuple(descriptor[:2]), idx),
-                                     idx)
+                ev, old = self._written_event(tuple(descriptor[:2]), idx)
+                self._wait_ipc_event(stream, ev, idx)
+                self._retire(old, stream)
         for t, (ph, b) in enumerate(zip(placeholders, self.valid_rows(idx))):
             if b:
                 if b > ph.shape[0] or not ph.is_contiguous():
@@ -610,6 +675,7 @@ class IpcRing(RingBase):
         if self.gpu_ordered and self._rev is not None:
             from ..ops import native
             rt = native.runtime()
+            old = None
             if self._rev[idx] is None or self._rrec[idx] >= EVENT_ROTATE:
                 # first release of this slot by this consumer, or the event
                 # reached its record budget: a new event, its handle published
@@ -619,13 +685,14 @@ class IpcRing(RingBase):
                 off = (self._cid * self.num_slots + idx) * EVENT_HANDLE_BYTES
                 self.rel_handles[off:off + len(h)] = h
                 self.rel_epoch[self._cid * self.num_slots + idx] += 1
-                self._rev[idx] = ev
+                old, self._rev[idx] = self._rev[idx], ev
                 self._rrec[idx] = 0
                 self.events_created += 1
             stream = torch.cuda.current_stream(self.consumer_device)
             rt.event_record(self._rev[idx], stream.cuda_stream)
             self._rrec[idx] += 1
             self.released_by[idx] = self._cid
+            self._retire(old, stream)
         super().release(idx)
 
     def handle_stats(self) -> dict:
@@ -633,6 +700,9 @@ class IpcRing(RingBase):
         return {"mem_handles_opened": sum(len(b) for b in self._opened_base.values()),
                 "events_opened": self.events_opened,
                 "events_created": self.events_created,
+                "events_destroyed": self.events_destroyed,
+                "events_live": self.events_created + self.events_opened
+                - self.events_destroyed,
                 "gpu_ordered_waits": self.gpu_waits,
                 "host_fallback_waits": self.stale_event_waits}
 
@@ -641,6 +711,23 @@ class IpcRing(RingBase):
         if self._ptrs is None and not self._opened and self._rev is None:
             return
         rt = native.runtime()
+        # every event this process still holds: retired ones once their
+        # markers complete, then the current created and opened ones
+        self._reap(wait_all=True)
+        if self._wev is not None or self._rev is not None or self._rel_open or self._wopen:
+            dev = self._dev if self._ptrs is not None else getattr(self, "consumer_device", None)
+            if dev is not None and dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            live = [e for e in (self._wev or []) + (self._rev or []) if e is not None]
+            for evs in list(self._rel_open.values()) + list(self._wopen.values()):
+                live += [e[0] for e in evs if e is not None]
+            for ev in live:
+                rt.event_destroy(ev)
+                self.events_destroyed += 1
+            self._wev = [None] * self.num_slots if self._wev is not None else None
+            self._rev = [None] * self.num_slots if self._rev is not None else None
+            self._rel_open = {}
+            self._wopen = {}
         for bases in self._opened_base.values():
             for base in bases:
                 rt.ipc_close_handle(base)

@@ -43,7 +43,7 @@ LATENCY_BACKLOG = int(os.environ.get("RNB_LATENCY_BACKLOG", "8"))
 CONTENDED_GET_S = float(os.environ.get("RNB_CONTENDED_GET_MS", "5")) / 1000.0
 # why a consumer-side gather ended (runner stats, BENCH JSON)
 GATHER_ENDS = ("item_cap", "row_cap", "empty", "empty_backlog", "busy_timeout", "wait_timeout",
-               "other_class")
+               "other_class", "bucket_fit")
 
 
 def _set_flag(flag, value, only_if_unset=True):
@@ -127,6 +127,14 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             prio = int(group_prio[group_idx])
         stream = torch.cuda.Stream(device=device, priority=prio)
         stream_ctx = torch.cuda.stream(stream)
+        # models running calls on streams of their own (R2P1DRunner lanes)
+        # create them at this runner's priority
+        try:
+            import inspect
+            if "stream_priority" in inspect.signature(_lc(model_module_path)).parameters:
+                model_kwargs.setdefault("stream_priority", prio)
+        except (TypeError, ValueError):
+            pass
     else:
         device = torch.device("cpu")
         stream = None
@@ -246,14 +254,29 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             # 345 videos/s against 559 for one runner with two lanes)
             adaptive_gather = False
         final_pending = []
+        # RunnerModel.on_complete(outputs): called once a call's outputs are
+        # complete on the GPU, before they are used (R2P1DRunner: the h3 range
+        # guard's full-range re-run). A non-final step whose model asks for it
+        # (``range_guarded``) then synchronises each call before publishing.
+        on_complete = getattr(model, "on_complete", None)
+        if not callable(on_complete):
+            on_complete = None
+        if on_complete is not None and getattr(model, "range_guarded", False):
+            sync_each = sync_each or stream is not None
 
-        def complete_final(limit: int) -> bool:
+        def complete_final(limit: int, done_only: bool = False) -> bool:
             """Complete in-flight final-step calls until at most ``limit`` are
-            left; False means stop the runner loop."""
+            left (``done_only``: only the leading calls whose event already
+            completed); False means stop the runner loop."""
             ok = True
             while len(final_pending) > limit:
-                ev, tc = final_pending.pop(0)
+                ev, tc, outs = final_pending[0]
+                if done_only and not ev.query():
+                    break
+                final_pending.pop(0)
                 ev.synchronize()
+                if on_complete is not None:
+                    on_complete(outs)
                 ok = finish_final(tc) and ok
             return ok
 
@@ -268,12 +291,14 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 if ev is None:
                     ev = torch.cuda.Event()
                     ev.record(stream)
-                final_pending.append((ev, time_card))
+                final_pending.append((ev, time_card, outputs))
                 return complete_final(final_depth)
             if mev is not None and stream is not None:
                 stream.wait_event(mev)      # outputs written on the model's stream
             if stream is not None and sync_each:
                 stream.synchronize()
+                if on_complete is not None and time_card is not None:
+                    on_complete(outputs)
             if time_card is None:
                 if slot is not None:
                     shared_output_ring.release(slot)    # nothing written
@@ -446,6 +471,11 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 prof[name] = prof.get(name, 0.0) + now - pclock[0]
                 pclock[0] = now
         while termination_flag.value == TerminationFlag.UNSET:
+            if final_pending:
+                # calls in flight: complete (finish time, count) the ones whose
+                # event is done now, not only when the next call pushes them out
+                if not complete_final(0, done_only=True):
+                    break
             if final_pending and not pending and backlog() == 0:
                 # nothing queued: complete the calls in flight before blocking
                 if not complete_final(0):
@@ -559,6 +589,22 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                     nxt[2].record("runner%d_start" % step_idx)
                     items.append(nxt)
                     rows += rows_of(nxt[0])
+                fit = getattr(model, "gather_fit", None)
+                if (callable(fit) and len(items) > 1
+                        and (LATENCY_BACKLOG <= 0 or backlog() >= LATENCY_BACKLOG)):
+                    # bulk regime: end the call at a graph bucket boundary
+                    # instead of padding far up to the next bucket; the
+                    # trailing items start the next call (latency phases pad)
+                    want = fit(rows)
+                    while rows > want and len(items) > 1:
+                        it = items.pop()
+                        rows -= rows_of(it[0])
+                        for tc_ in cards_of(it[2]):      # started again when taken
+                            if tc_.gpus:
+                                tc_.gpus.pop()
+                            tc_.timings.pop("runner%d_start" % step_idx, None)
+                        pending.insert(0, it)
+                        end = "bucket_fit"
                 gslot = None
                 if direct_out and getattr(model, "gather_into_output", False):
                     # batching stage: assemble the batch in the output slot itself
@@ -601,8 +647,19 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 raise RuntimeError("injected fault in runner%d at item %d"
                                    % (step_idx, count["items"]))
             if gather is not None and signal is not None:
-                call = getattr(model, "call_gathered", model)
-                outputs = call(tensor_inputs, non_tensor_inputs, time_card)
+                if gslot is None and direct_out:
+                    # the model writes its output straight into the output slot
+                    # (R2P1DRunner.call_into: a graph replay aimed at the slot)
+                    gslot = state["out_counter"] % len(shared_output_ring)
+                    if not shared_output_ring.wait_free(gslot, aborted):
+                        break
+                    shared_output_ring.begin_write(gslot, stream)
+                    tick("slot_wait")
+                    outputs = model.call_into(tensor_inputs, non_tensor_inputs, time_card,
+                                              shared_output_ring.slot_views(gslot))
+                else:
+                    call = getattr(model, "call_gathered", model)
+                    outputs = call(tensor_inputs, non_tensor_inputs, time_card)
                 tick("model")
                 if not emit(outputs, gslot):
                     break
@@ -700,11 +757,17 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 if hs is None:
                     continue
                 edge = "same_gpu" if r.producer_gpu == g_idx else "cross_gpu"
+                kind = "rccl" if getattr(r, "kind", "") == "rccl" else "ipc"
                 for k, v in hs().items():
-                    stats["ipc.%s.%s" % (edge, k)] = stats.get("ipc.%s.%s" % (edge, k), 0) + v
+                    key = "%s.%s.%s" % (kind, edge, k)
+                    stats[key] = stats.get(key, 0) + v
             for ph, st in gstats.items():
                 for k, v in st.items():
                     stats["gather.%s.%s" % (ph, k)] = v
+            mstats = getattr(model, "runtime_stats", None)
+            if callable(mstats):
+                for k, v in mstats().items():
+                    stats["model.%s" % k] = v
             result_queue.put(("ring_stats", step_idx, group_idx, instance_idx, stats))
         # ---- shutdown
         if not is_final_step:

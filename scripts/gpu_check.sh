@@ -16,6 +16,9 @@ step() {  # step <name> <timeout> <cmd...>
   return 0
 }
 step build 600 python -m rnb_amd.build
-step pytest_gpu "${PYTEST_TIMEOUT:-900}" python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread
+# TESTS: pytest targets (default: the whole GPU suite); NO_BENCH=1 skips the bench
+step pytest_gpu "${PYTEST_TIMEOUT:-900}" python -u -m pytest ${TESTS:-tests} -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench "${BENCH_TIMEOUT:-900}" python bench.py --steps "${BENCH_STEPS:-10}" --warmup 2 --json-out gpurun_out/bench.json
+if [ -z "${NO_BENCH:-}" ]; then
+  step bench "${BENCH_TIMEOUT:-900}" python bench.py --steps "${BENCH_STEPS:-10}" --warmup 2 --json-out gpurun_out/bench.json ${BENCH_ARGS:-}
+fi

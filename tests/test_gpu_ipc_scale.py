@@ -237,3 +237,135 @@ def test_ipc_ring_split_into_chunks():
     st = ring.handle_stats()
     ring.close()
     assert st["mem_handles_opened"] == 4, st
+
+
+SOAK_SLOTS = 8
+
+
+def _soak_producer(ring, ring_i, q, n, n_cons, out_q):
+    import torch
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(dev)
+    peak = 0
+    with torch.cuda.stream(s):
+        ring.producer_attach(dev)
+        desc = ring.descriptor()
+        for i in range(n):
+            idx = i % len(ring)
+            if not ring.wait_free(idx):
+                raise RuntimeError("aborted")
+            ring.begin_write(idx, s)
+            ring.slot_views(idx)[0].fill_(float(i))
+            ring.commit(idx, [1], s)
+            q.put((ring_i, idx, i, desc))
+            if i % 4096 == 0:
+                peak = max(peak, ring.handle_stats()["events_live"])
+        for _ in range(n_cons):
+            q.put(None)
+        s.synchronize()
+        st = ring.handle_stats()
+        peak = max(peak, st["events_live"])
+        out_q.put(("producer", ring_i, st, peak))
+        time.sleep(3.0)           # consumers finish their last pulls
+        ring.close()
+
+
+def _soak_consumer(rings, cid, n_prod, q, out_q):
+    import torch
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(dev)
+    B = 4096
+    buf = torch.empty((B, 1, 256), device=dev)
+    want, bad, pulls, nones, peak = [], 0, 0, 0, 0
+    with torch.cuda.stream(s):
+        for r in rings:
+            r.consumer_attach(dev, (1, 0, cid))
+        while nones < n_prod:
+            m = q.get(timeout=120)
+            if m is None:
+                nones += 1
+                continue
+            ring_i, idx, val, desc = m
+            r = rings[ring_i]
+            r.read_into(idx, [buf[len(want)]], desc)
+            r.release(idx)
+            want.append(val)
+            pulls += 1
+            if len(want) == B:
+                s.synchronize()
+                got = buf[:, 0, :]
+                exp = torch.tensor(want, dtype=torch.float32, device=dev)[:, None]
+                bad += int((got != exp).any(dim=1).sum())
+                want = []
+                peak = max(peak, sum(r.handle_stats()["events_live"] for r in rings))
+        s.synchronize()
+        if want:
+            got = buf[:len(want), 0, :]
+            exp = torch.tensor(want, dtype=torch.float32, device=dev)[:, None]
+            bad += int((got != exp).any(dim=1).sum())
+        stats = [r.handle_stats() for r in rings]
+        peak = max(peak, sum(st["events_live"] for st in stats))
+    out_q.put(("consumer", cid, stats, peak, pulls, bad))
+    time.sleep(1.0)
+    for r in rings:
+        r.close()
+
+
+def test_ipc_event_lifecycle_soak_bounded():
+    """Round-4 advice: rotated interprocess events leaked without bound.
+    2 producers x 3 consumers reuse 8-slot rings >= 200k times in total:
+    every pull sees its value, every wait stays on the GPU, and the events
+    each process holds stay bounded by a constant x slots while thousands are
+    created and destroyed (superseded events retired behind stream markers)."""
+    import multiprocessing as mp
+    import os
+    import torch
+    from rnb_amd.parallel.transport import EVENT_ROTATE, RETIRE_MAX, IpcRing
+    n_prod, n_cons = 2, 3
+    per_prod = int(os.environ.get("RNB_SOAK_REUSES", "200000")) // n_prod
+    ctx = mp.get_context("spawn")
+    rings = [IpcRing(ctx, ((1, 256),), (torch.float32,), SOAK_SLOTS, "soak%d" % k, 0)
+             for k in range(n_prod)]
+    for r in rings:
+        r.set_consumers([(1, 0, c) for c in range(n_cons)])
+    q, out_q = ctx.Queue(), ctx.Queue()
+    t0 = time.time()
+    procs = [ctx.Process(target=_soak_producer, args=(rings[k], k, q, per_prod, n_cons, out_q))
+             for k in range(n_prod)]
+    procs += [ctx.Process(target=_soak_consumer, args=(rings, c, n_prod, q, out_q))
+              for c in range(n_cons)]
+    for p in procs:
+        p.start()
+    res = [out_q.get(timeout=110) for _ in procs]
+    wall = time.time() - t0
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    prods = [r for r in res if r[0] == "producer"]
+    cons = [r for r in res if r[0] == "consumer"]
+    total = sum(c[4] for c in cons)
+    assert total == n_prod * per_prod
+    assert sum(c[5] for c in cons) == 0, "pulls with wrong data"
+    created = sum(p[2]["events_created"] for p in prods) + \
+        sum(st["events_created"] for c in cons for st in c[2])
+    destroyed = sum(p[2]["events_destroyed"] for p in prods) + \
+        sum(st["events_destroyed"] for c in cons for st in c[2])
+    for p in prods:
+        st = p[2]
+        assert st["host_fallback_waits"] == 0, st
+        # own written events + opened release events of 3 consumers + retiring
+        assert p[3] <= (1 + n_cons) * SOAK_SLOTS + RETIRE_MAX, p
+    for c in cons:
+        for st in c[2]:
+            assert st["host_fallback_waits"] == 0, st
+        # per ring: opened written events + own release events, + retiring
+        assert c[3] <= n_prod * 2 * SOAK_SLOTS + RETIRE_MAX, c
+    assert created >= n_prod * per_prod // EVENT_ROTATE, created
+    assert destroyed >= created - 2 * (n_prod + n_cons) * (SOAK_SLOTS * 4 + RETIRE_MAX)
+    print("\n[ipc-soak] %d slot reuses (%d producers x %d consumers, %d slots each) in "
+          "%.1f s: events created %d, destroyed %d; peak live per producer %s, per "
+          "consumer %s; pulls per consumer %s"
+          % (total, n_prod, n_cons, SOAK_SLOTS, wall, created, destroyed,
+             [p[3] for p in prods], [c[3] for c in cons], [c[4] for c in cons]), flush=True)

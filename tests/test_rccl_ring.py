@@ -92,3 +92,61 @@ def test_rccl_recv_times_out_instead_of_hanging(tmp_path):
     for p in procs:
         p.join(30)
     assert got["consumer"] != "returned", got
+
+
+def test_rccl_three_step_chain_both_edges_gloo(tmp_path):
+    """A middle stage that consumes one RCCL edge and produces the next: its
+    receives (main thread) and sends (sender thread) run on disjoint 2-rank
+    pair groups. Loader -> 2 runner replicas (layers 1-3) -> 1 runner (layers
+    4-5), RCCL (gloo on CPU) on both edges; the result records the world."""
+    cfg = {"video_path_iterator": IT, "defaults": SMALL, "pipeline": [
+        {"model": M + "R2P1DLoader", "queue_groups": [{"gpus": [-1], "out_queues": [0]}],
+         "num_shared_tensors": 3, "transport": "rccl"},
+        {"model": M + "R2P1DRunner", "start_index": 1, "end_index": 3,
+         "queue_groups": [{"gpus": [-1, -1], "in_queue": 0, "out_queues": [1]}],
+         "num_shared_tensors": 3, "transport": "rccl"},
+        {"model": M + "R2P1DRunner", "start_index": 4, "end_index": 5,
+         "queue_groups": [{"gpus": [-1], "in_queue": 1}]}]}
+    proc, res, _ = run_cfg(tmp_path, cfg, "-v", "8", "-mi", "0",
+                           env={"RNB_RCCL_BACKEND": "gloo"})
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    assert res["ok"] and res["videos_done"] >= 8
+    world = res["rccl_world"]
+    assert world["backend"] == "gloo" and world["world_size"] == 4
+    # loader-(2 replicas) and (2 replicas)-final: four pair groups
+    assert len(world["pair_groups"]) == 4
+    assert res["rccl_edges"]["same_gpu"]["edges"] == 4
+
+
+class _QT:
+    def __init__(self, rings):
+        self.rings = rings
+
+
+def test_rccl_replicas_on_one_gpu_get_pair_groups():
+    """Two consumer replicas on GPU 1 of a producer on GPU 0: accepted (each
+    (producer, consumer) pair is its own 2-rank RCCL group, so no communicator
+    holds two ranks of one GPU), and the pairs are as expected."""
+    import torch
+    import torch.multiprocessing as mp
+    from rnb_amd.config import parse_pipeline
+    from rnb_amd.launcher import _assign_rccl_ranks, rccl_world_summary
+    from rnb_amd.parallel.rccl_channel import RcclRing
+    cfg = {"video_path_iterator": IT, "defaults": SMALL, "pipeline": [
+        {"model": M + "R2P1DLoader",
+         "queue_groups": [{"gpus": [0, 2], "out_queues": [0]}], "transport": "rccl"},
+        {"model": M + "R2P1DRunner", "queue_groups": [{"gpus": [1, 1], "in_queue": 0}]}]}
+    spec = parse_pipeline(cfg)
+    ctx = mp.get_context("spawn")
+    rings = [[[RcclRing(ctx, ((1, 2),), (torch.float32,), 2, "r%d" % i, gpu)
+               for i, gpu in enumerate((0, 2))]]]
+    os.environ.pop("RNB_RCCL_BACKEND", None)
+    infos = _assign_rccl_ranks(spec, _QT(rings), "job")
+    world = rccl_world_summary(infos)
+    assert world["backend"] == "nccl" and world["world_size"] == 4
+    # ranks: producers (0,0,0)=0 (gpu 0), (0,0,1)=1 (gpu 2); consumers 2, 3 (gpu 1)
+    assert world["pair_groups"] == [[0, 2], [0, 3], [1, 2], [1, 3]]
+    for info in infos.values():
+        for a, b in info.pairs:
+            assert info.gpus[a] != info.gpus[b]
+    assert rings[0][0][0].producer_rank == 0 and rings[0][0][1].producer_rank == 1
