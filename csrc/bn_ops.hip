@@ -231,9 +231,10 @@ __global__ __launch_bounds__(256) void bn_seg_finalize_f32_kernel(BnSegParams p)
   }
   p.mean[(size_t)s * C + c] = mu;
   p.var[(size_t)s * C + c] = va;
-  const float sc = p.gamma[c] * rsqrtf(va + p.eps);
+  // an empty segment (a graph bucket's padding clips) maps its rows to 0
+  const float sc = rows > 0 ? p.gamma[c] * rsqrtf(va + p.eps) : 0.f;
   p.ss[(size_t)s * 2 * C + c] = sc;
-  p.ss[(size_t)s * 2 * C + C + c] = p.beta[c] - mu * sc;
+  p.ss[(size_t)s * 2 * C + C + c] = rows > 0 ? p.beta[c] - mu * sc : 0.f;
   if (p.running_mean != nullptr && rows >= 2 && c < p.channels) {
     int after = 0;                                 // segments with >= 2 rows after s
     for (int t = s + 1; t < p.nseg; ++t) after += (p.coffs[t + 1] - p.coffs[t]) * p.rpc >= 2;
@@ -266,9 +267,10 @@ __global__ __launch_bounds__(256) void bn_seg_finalize_sums_f32_kernel(BnSegPara
   }
   p.mean[(size_t)s * C + c] = mu;
   p.var[(size_t)s * C + c] = va;
-  const float sc = p.gamma[c] * rsqrtf(va + p.eps);
+  // an empty segment (a graph bucket's padding clips) maps its rows to 0
+  const float sc = rows > 0 ? p.gamma[c] * rsqrtf(va + p.eps) : 0.f;
   p.ss[(size_t)s * 2 * C + c] = sc;
-  p.ss[(size_t)s * 2 * C + C + c] = p.beta[c] - mu * sc;
+  p.ss[(size_t)s * 2 * C + C + c] = rows > 0 ? p.beta[c] - mu * sc : 0.f;
   if (p.running_mean != nullptr && rows >= 2 && c < p.channels) {
     int after = 0;
     for (int t = s + 1; t < p.nseg; ++t) after += (p.coffs[t + 1] - p.coffs[t]) * p.rpc >= 2;
@@ -318,9 +320,9 @@ __global__ __launch_bounds__(64) void bn_seg_sums_walk_f32_kernel(BnSegParams p,
       }
       p.mean[(size_t)s * C + c] = mu;
       p.var[(size_t)s * C + c] = va;
-      const float sc = g * rsqrtf(va + p.eps);
+      const float sc = rows[u] > 0 ? g * rsqrtf(va + p.eps) : 0.f;     // empty: 0
       p.ss[(size_t)s * 2 * C + c] = sc;
-      p.ss[(size_t)s * 2 * C + C + c] = b - mu * sc;
+      p.ss[(size_t)s * 2 * C + C + c] = rows[u] > 0 ? b - mu * sc : 0.f;
       if (upd && rows[u] >= 2) {
         rm = (1.f - p.momentum) * rm + p.momentum * mu;
         rv = (1.f - p.momentum) * rv +
@@ -418,9 +420,9 @@ __global__ __launch_bounds__(1024) void bn_seg_finalize_running_f32_kernel(BnSeg
     }
     p.mean[(size_t)s * C + c] = mu;
     p.var[(size_t)s * C + c] = va;
-    const float sc = p.gamma[c] * rsqrtf(va + p.eps);
+    const float sc = rows > 0 ? p.gamma[c] * rsqrtf(va + p.eps) : 0.f;    // empty: 0
     p.ss[(size_t)s * 2 * C + c] = sc;
-    p.ss[(size_t)s * 2 * C + C + c] = p.beta[c] - mu * sc;
+    p.ss[(size_t)s * 2 * C + C + c] = rows > 0 ? p.beta[c] - mu * sc : 0.f;
     if (upd && rows >= 2) {
       t1 += wts[s] * (double)mu;
       t2 += wts[s] * (double)va * ((double)rows / (double)(rows - 1));
@@ -487,9 +489,9 @@ __global__ __launch_bounds__(256) void bn_seg_walk_apply_f32_kernel(
           }
           p.mean[(size_t)s * C + c] = mu;
           p.var[(size_t)s * C + c] = va;
-          const float sc = g * rsqrtf(va + p.eps);
+          const float sc = rows[u] > 0 ? g * rsqrtf(va + p.eps) : 0.f;     // empty: 0
           p.ss[(size_t)s * 2 * C + c] = sc;
-          p.ss[(size_t)s * 2 * C + C + c] = b - mu * sc;
+          p.ss[(size_t)s * 2 * C + C + c] = rows[u] > 0 ? b - mu * sc : 0.f;
           if (upd && rows[u] >= 2) {
             rm = (1.f - p.momentum) * rm + p.momentum * mu;
             rv = (1.f - p.momentum) * rv +
@@ -528,9 +530,9 @@ __global__ __launch_bounds__(256) void bn_seg_walk_apply_f32_kernel(
             mu = (float)m;
             va = (float)fmax(a2 / (double)rows - m * m, 0.0);
           }
-          const float sc = p.gamma[c] * rsqrtf(va + p.eps);
+          const float sc = rows > 0 ? p.gamma[c] * rsqrtf(va + p.eps) : 0.f;   // empty: 0
           lsc[c] = sc;
-          lsh[c] = p.beta[c] - mu * sc;
+          lsh[c] = rows > 0 ? p.beta[c] - mu * sc : 0.f;
         }
         __syncthreads();
         const long long a = max(r0, s0), b = min(r1, s1);
@@ -605,7 +607,13 @@ __global__ __launch_bounds__(256) void bn_seg_apply_f32_kernel(
   int s = -1, s_end = 0;
   float4 sc = make_float4(0.f, 0.f, 0.f, 0.f), sh = sc;
   for (int r = ra; r < rb; ++r) {
-    if (r < lo_row || r >= hi_row) continue;
+    if (r < lo_row || r >= hi_row) {
+      // rows outside every segment (a graph bucket's padding clips) are set
+      // to 0, so they stay bounded through the layers (an unnormalised
+      // padding row would grow to inf and trip the h3 range guard)
+      *(float4*)(z + (size_t)r * z_stride + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+      continue;
+    }
     if (s < 0 || r >= s_end) {
       if (s < 0) {
         int lo = 0, hi = nseg - 1;                 // last s with start(s) <= r

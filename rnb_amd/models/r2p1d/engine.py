@@ -503,6 +503,12 @@ class R2P1DEngine:
         """Pick the fastest tile per conv for ``n`` clips (GPU only)."""
         assert self.backend == "hip"
         self.fused_choices = {}
+        if self.range_guard is not None:
+            # the tuning chain feeds raw (un-normalised) conv outputs from layer
+            # to layer, which can outgrow h3's range: its launches must not
+            # write this engine's range-guard flag
+            from ...ops.native import kernels
+            kernels().h3_set_range_flag(0)
         x = torch.randn(self.input_shape(n), device=self.device).to(self.dtype)
         bufs = {"x": x}
         chosen = {}
@@ -689,6 +695,9 @@ class GraphedEngine:
                 self._capture(b)
         if self.device.type == "cuda":
             torch.cuda.empty_cache()
+        if self.engine.range_guard is not None:
+            torch.cuda.synchronize(self.device)
+            self.engine.range_guard.reset()     # serving starts with a clear flag
 
     def input_buffer(self, n: int) -> Tuple[torch.Tensor, int]:
         """Static input of the bucket for n clips (write rows [:n] in place)."""

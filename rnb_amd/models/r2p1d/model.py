@@ -210,6 +210,9 @@ class R2P1DRunner(RunnerModel):
             self.engine(tmp)
         if device.type == "cuda":
             torch.cuda.current_stream(device).synchronize()
+        for eng in self._lane_engines:
+            if getattr(eng, "range_guard", None) is not None:
+                eng.range_guard.reset()
         self._gather_ptr = None
         self._gather_buf = None
         self._check_dir = os.environ.get("RNB_CHECK_DIR") or None

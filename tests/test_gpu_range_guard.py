@@ -124,3 +124,39 @@ def test_graphed_engine_reruns_tripped_call(monkeypatch):
     torch.cuda.synchronize()
     assert not eng.range_guard.tripped()
     assert not geng.range_fallback()
+
+
+def test_bucket_padding_rows_do_not_trip_the_guard(monkeypatch):
+    """A replay of n clips in a larger bucket computes the padding clips too.
+    Their BatchNorm segment is empty: its scale / shift are 0 and the apply
+    pass zeroes rows outside every segment, so padding rows stay bounded
+    through all 72 convs of R(2+1)D-34 (round 5: they grew to inf through
+    gamma / sqrt(eps) scales and tripped the guard on every padded call)."""
+    from rnb_amd.models.r2p1d.engine import GraphedEngine, R2P1DEngine
+    from rnb_amd.models.r2p1d.model import build_network
+    from rnb_amd.ops import conv_f32
+    from rnb_amd.ops.conv_f32 import ConvLayerF32, is_h3, is_h3k
+
+    orig = ConvLayerF32._config_for
+
+    def forced(self, x_shape):
+        if conv_f32._FULL_RANGE[0]:
+            return orig(self, x_shape)
+        c = [i for i in self.candidates(x_shape) if is_h3(i) and not is_h3k(i)]
+        if self.tune_with_affine:
+            c = [i for i in c if self.affine_ok(i, x_shape)] or c
+        return c[0] if c else orig(self, x_shape)
+    monkeypatch.setattr(ConvLayerF32, "_config_for", forced)
+
+    net = build_network(1, 5, depth=34, seed=1)
+    eng = R2P1DEngine(net, DEV, backend="hip", bn_mode="batch", dtype=torch.float32)
+    geng = GraphedEngine(eng, 4, buckets=(4,), autotune=False)
+    geng.prepare()
+    static_in, _ = geng.input_buffer(1)
+    g = torch.Generator().manual_seed(0)
+    static_in.copy_((torch.randn(static_in.shape, generator=g) * 3).to(DEV))
+    for n, offs in ((1, None), (2, [0, 1, 2]), (3, None)):
+        y = geng.replay(n, clip_offsets=offs)
+        torch.cuda.synchronize()
+        assert not eng.range_guard.tripped(), n
+        assert torch.isfinite(y).all()

@@ -419,3 +419,20 @@ def test_bn_moments_from_epilogue_sums():
             continue
         assert torch.allclose(mean[s].double(), xs.mean(0), atol=1e-5)
         assert torch.allclose(var[s].double(), xs.var(0, unbiased=False), rtol=1e-5)
+
+
+def test_geometric_buckets_cover_and_bound_padding():
+    """bench.py's default graph buckets: every count 1..8, then ~12.5 % apart
+    (multiples of 4) up to max_clips; a call padded to its bucket wastes at
+    most ~25 % only below 16 clips and <= 12.5 % + 4 rows above."""
+    from rnb_amd.models.r2p1d.engine import geometric_buckets
+    b = geometric_buckets(256)
+    assert b[:8] == list(range(1, 9)) and b[-1] == 256 and len(b) == 30
+    assert all(x % 4 == 0 for x in b[8:])
+    assert b == sorted(set(b))
+    import bisect
+    for n in range(1, 257):
+        up = b[bisect.bisect_left(b, n)]
+        assert up >= n and up - n <= max(4, 0.125 * n + 4), (n, up)
+    assert geometric_buckets(15) == [1, 2, 3, 4, 5, 6, 7, 8, 12, 15]
+    assert geometric_buckets(1) == [1]
