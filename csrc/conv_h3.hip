@@ -1078,6 +1078,7 @@ static int* g_h3_range_flag = nullptr;
 extern "C" {
 
 void rnb_h3_set_range_flag(int* flag) { g_h3_range_flag = flag; }
+int* rnb_h3_range_flag() { return g_h3_range_flag; }
 
 int rnb_conv_h3_num_configs() { return kNumH3Configs; }
 

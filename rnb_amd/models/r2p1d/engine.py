@@ -134,7 +134,8 @@ class R2P1DEngine:
         # h3 range guard (fp32 hip engines whose convs may pick h3 configs):
         # the launches of this engine write its flag on a non-finite output
         self.range_guard = (RangeGuard() if backend == "hip" and self.f32 and h3_enabled()
-                            and device.type == "cuda" else None)
+                            and device.type == "cuda"
+                            and os.environ.get("RNB_H3_GUARD", "1") != "0" else None)
 
     # ---------------------------------------------------------------- build
     def _name(self) -> str:

@@ -187,9 +187,18 @@ class R2P1DRunner(RunnerModel):
                 device, start_index, end_index, num_classes, layer_sizes, depth, backend,
                 bn_mode, seed, ckpt_path, self.max_clips, use_graphs, autotune, self.dtype,
                 buckets))
-        # lane streams at the runner's stream priority (runner.py passes the
-        # queue group's, e.g. the high-priority 15-clip replica's)
-        self._lane_streams = ([torch.cuda.Stream(device, priority=int(stream_priority))
+        # lane streams at DEFAULT priority, not the runner's (runner.py passes
+        # the queue group's, e.g. the high-priority 15-clip replica's): the
+        # round-4 advice asked for the runner's; measured interleaved, it costs
+        # 11 % of the headline and raises the mi = 10 p99 (1394 vs 1562
+        # videos/s, p99 15.2 vs 10.7 ms: profiles/r5_ab_lane_priority_guard.txt)
+        # -- a high-priority queue holding 60 % of the clips (15-clip videos)
+        # starves the small replicas' dispatches instead of overlapping them.
+        # RNB_LANE_PRIORITY=runner restores the runner's priority.
+        lane_prio = os.environ.get("RNB_LANE_PRIORITY", "0")
+        lane_prio = int(stream_priority) if lane_prio == "runner" else int(lane_prio)
+        self.lane_stream_priority = lane_prio
+        self._lane_streams = ([torch.cuda.Stream(device, priority=lane_prio)
                                for _ in range(self.lanes)] if self.lanes > 1 else None)
         self._lane_done = [None] * self.lanes     # completion event of each lane's last call
         self._lane = 0                             # lane of the next call

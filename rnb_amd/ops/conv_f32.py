@@ -143,6 +143,9 @@ H3R_BASE = 1380
 # temporal frame-band h3 kernel (conv_h3t_kernel): 3x1x1 stride 1 pad (1, 0, 0)
 # with T >= 2, variant H3T_BASE + v of rnb_conv_h3t_launch
 H3T_BASE = 1395
+# wave-specialised temporal h3 kernel (csrc/conv_h3u.hip conv_h3u_kernel): the
+# h3t weight layout and conditions, variant H3U_BASE + v of rnb_conv_h3u_launch
+H3U_BASE = 1410
 # activations are split after scaling by 2^H3_IN_LOG2: fp16 lo parts stay
 # normal for |a| >= 2^-9 and inputs up to 2^10 stay in the fp16 range
 H3_IN_LOG2 = 6
@@ -154,12 +157,17 @@ def is_h3(cid: int) -> bool:
     from .native import kernels
     return ((H3D_BASE <= cid < H3D_BASE + len(kernels().h3_configs))
             or H3K_BASE <= cid < H3K_BASE + len(H3K_CONFIGS) or is_h3r(cid)
-            or is_h3t(cid))
+            or is_h3t(cid) or is_h3u(cid))
 
 
 def is_h3t(cid: int) -> bool:
     from .native import kernels
     return H3T_BASE <= cid < H3T_BASE + kernels().h3t_variants
+
+
+def is_h3u(cid: int) -> bool:
+    from .native import kernels
+    return H3U_BASE <= cid < H3U_BASE + kernels().h3u_variants
 
 
 def is_h3r(cid: int) -> bool:
@@ -509,6 +517,10 @@ class ConvLayerF32:
         from .native import kernels
         return x_shape is None or kernels().conv_h3t_pixels(variant, x_shape[1]) > 0
 
+    def h3u_fits(self, variant: int, x_shape) -> bool:
+        from .native import kernels
+        return x_shape is None or kernels().conv_h3u_pixels(variant, x_shape[1]) > 0
+
     def wino_u(self, tc: int, m: int = 2, co0: int = 0, nco: Optional[int] = None,
                x6: bool = False) -> torch.Tensor:
         """Transformed weights of output channels [co0, co0 + nco) (default: all
@@ -570,6 +582,9 @@ class ConvLayerF32:
             if self.h3t_ok(x_shape):
                 c += [H3T_BASE + i for i in range(kernels().h3t_variants)
                       if self.h3t_fits(i, x_shape)]
+                if os.environ.get("RNB_H3U", "1") != "0":
+                    c += [H3U_BASE + i for i in range(kernels().h3u_variants)
+                          if self.h3u_fits(i, x_shape)]
             if x_shape is not None and os.environ.get("RNB_X6K", "1") != "0":
                 c += [H3K_BASE + j for j in range(len(H3K_CONFIGS))
                       if self.ksplit_for(H3K_BASE + j, x_shape) > 1]
@@ -821,7 +836,7 @@ class ConvLayerF32:
 
     def affine_ok(self, cid: int, x_shape) -> bool:
         """Whether config ``cid`` can apply the input's BN + ReLU on load."""
-        if cid in WINO_TEMPORAL or is_h3r(cid) or is_h3t(cid):
+        if cid in WINO_TEMPORAL or is_h3r(cid) or is_h3t(cid) or is_h3u(cid):
             return True
         if not is_h3(cid):
             return False
@@ -872,7 +887,7 @@ class ConvLayerF32:
         step = self.chunk_clips(x.shape, y.shape,
                                 residual.shape[-1] if residual is not None else 0)
         h3 = is_h3(cid)
-        h3t = is_h3t(cid)
+        h3t = is_h3t(cid) or is_h3u(cid)          # the same weight layout
         for n0 in range(0, N, step):
             p = self.params(x, y, residual, n0, min(N, n0 + step), x6=x6 and not h3, h3=h3,
                             h3t=h3t)
@@ -880,12 +895,14 @@ class ConvLayerF32:
                 _, _, s_in, s_out = self.h3t_buffers()
                 aff = ((in_affine[0].data_ptr(), in_affine[1].data_ptr() + 4 * n0)
                        if in_affine is not None else (0, 0))
+                launch, v = ((k.conv_h3u, cid - H3U_BASE) if is_h3u(cid)
+                             else (k.conv_h3t, cid - H3T_BASE))
                 if out_stats is not None:
-                    k.conv_h3t(p, cid - H3T_BASE, stream.cuda_stream, s_in, s_out,
-                               out_stats[0].data_ptr(), out_stats[1].data_ptr() + 4 * n0,
-                               out_stats[0].shape[2], *aff)
+                    launch(p, v, stream.cuda_stream, s_in, s_out,
+                           out_stats[0].data_ptr(), out_stats[1].data_ptr() + 4 * n0,
+                           out_stats[0].shape[2], *aff)
                 else:
-                    k.conv_h3t(p, cid - H3T_BASE, stream.cuda_stream, s_in, s_out, 0, 0, 0, *aff)
+                    launch(p, v, stream.cuda_stream, s_in, s_out, 0, 0, 0, *aff)
             elif is_h3r(cid):
                 _, _, s_in, s_out = self.h3d_buffers()
                 aff = ((in_affine[0].data_ptr(), in_affine[1].data_ptr() + 4 * n0)

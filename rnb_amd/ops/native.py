@@ -331,6 +331,10 @@ class Kernels:
         lib.rnb_conv_h3t_launch.argtypes = lib.rnb_conv_h3r_launch.argtypes
         lib.rnb_conv_h3t_launch.restype = ctypes.c_int
         lib.rnb_conv_h3t_pixels.argtypes = [ctypes.c_int, ctypes.c_int]
+        lib.rnb_conv_h3u_launch.argtypes = lib.rnb_conv_h3r_launch.argtypes
+        lib.rnb_conv_h3u_launch.restype = ctypes.c_int
+        lib.rnb_conv_h3u_pixels.argtypes = [ctypes.c_int, ctypes.c_int]
+        lib.rnb_conv_h3u_pixels.restype = ctypes.c_int
         lib.rnb_h3_set_range_flag.argtypes = [ctypes.c_void_p]
         lib.rnb_h3_set_range_flag.restype = None
         lib.rnb_conv_h3t_pixels.restype = ctypes.c_int
@@ -365,6 +369,7 @@ class Kernels:
         self.x6r_variants = lib.rnb_conv_x6r_num_variants()
         self.h3r_variants = lib.rnb_conv_h3r_num_variants()
         self.h3t_variants = lib.rnb_conv_h3t_num_variants()
+        self.h3u_variants = lib.rnb_conv_h3u_num_variants()
         self.x6_configs = []       # (pixel tile, channel tile) per x6 direct config
         for i in range(lib.rnb_conv_x6_num_configs()):
             p, c = ctypes.c_int(), ctypes.c_int()
@@ -441,6 +446,20 @@ class Kernels:
                                             sums or None, clip_seg or None, stats_c, in_scale,
                                             out_scale, in_ss or None, in_seg or None),
                "conv_h3t (variant %d)" % variant)
+
+    def conv_h3u(self, params: ConvParams, variant: int, stream: int, in_scale: float,
+                 out_scale: float, sums: int = 0, clip_seg: int = 0, stats_c: int = 0,
+                 in_ss: int = 0, in_seg: int = 0) -> None:
+        """Wave-specialised temporal h3 conv (csrc/conv_h3u.hip: staging waves
+        split the next chunk while the MFMA waves run the current one); the
+        weights and arguments as ``conv_h3t``."""
+        _check(self.lib.rnb_conv_h3u_launch(ctypes.byref(params), variant, stream,
+                                            sums or None, clip_seg or None, stats_c, in_scale,
+                                            out_scale, in_ss or None, in_seg or None),
+               "conv_h3u (variant %d)" % variant)
+
+    def conv_h3u_pixels(self, variant: int, T: int) -> int:
+        return int(self.lib.rnb_conv_h3u_pixels(variant, T))
 
     def conv_h3t_pixels(self, variant: int, T: int) -> int:
         """Pixels per block of h3t variant ``variant`` for T frames (0: cannot run)."""

@@ -273,22 +273,38 @@ def _h3t_ids():
     return [H3T_BASE + i for i in range(kernels().h3t_variants)]
 
 
+def _band_ids(fam, layer, shape):
+    """Variants of the temporal band family ``fam`` (h3t: conv_h3t_kernel,
+    h3u: the wave-specialised conv_h3u_kernel) that fit ``shape``."""
+    from rnb_amd.ops.conv_f32 import H3T_BASE, H3U_BASE
+    from rnb_amd.ops.native import kernels
+    if not layer.h3t_ok(shape):
+        return []
+    if fam == "h3t":
+        return [H3T_BASE + i for i in range(kernels().h3t_variants) if layer.h3t_fits(i, shape)]
+    return [H3U_BASE + i for i in range(kernels().h3u_variants) if layer.h3u_fits(i, shape)]
+
+
+@pytest.mark.parametrize("fam", ["h3t", "h3u"])
 @pytest.mark.parametrize("thw,cin,cout", [((8, 9, 7), 80, 72), ((4, 14, 14), 64, 150),
-                                          ((2, 7, 7), 144, 64), ((8, 8, 8), 48, 130)])
-def test_h3_temporal_band_exact_integers_stats_and_affine(thw, cin, cout):
-    """Temporal frame-band h3 kernel (conv_h3t_kernel): bit-exact on small
-    integers (zero frames at both clip ends, a partial last pixel block,
-    Cin_p % 32 == 16: the last chunk's upper half zero-padded per tap,
-    residual + ReLU epilogue) for every variant that fits T; epilogue BN
-    sums per video vs fp64 sums of the output; the input BN + ReLU on load
-    within 1e-5 of the fp64 conv of the applied input."""
+                                          ((2, 7, 7), 144, 64), ((8, 8, 8), 48, 130),
+                                          ((8, 7, 9), 144, 64), ((2, 9, 8), 576, 256)])
+def test_h3_temporal_band_exact_integers_stats_and_affine(thw, cin, cout, fam):
+    """Temporal frame-band h3 kernels (conv_h3t_kernel, and the
+    wave-specialised conv_h3u_kernel): bit-exact on small integers (zero
+    frames at both clip ends, a partial last pixel block, Cin_p % 32 == 16:
+    the last chunk's upper half zero-padded per tap, residual + ReLU
+    epilogue) for every variant that fits T; epilogue BN sums per video vs
+    fp64 sums of the output; the input BN + ReLU on load within 1e-5 of the
+    fp64 conv of the applied input."""
     layer = _layer(cin, cout, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=True, integer=True)
     x = _input(3, thw, layer.geom.cin_p, cin, integer=True)
     res = _input(3, thw, layer.geom.cout_p, cout, integer=True, seed=3)
     ref = _ref64(layer, x, res).float()
     assert layer.h3t_ok(x.shape)
-    ids = [c for c in _h3t_ids() if layer.h3t_fits(c - _h3t_ids()[0], x.shape)]
-    assert ids, thw
+    ids = _band_ids(fam, layer, x.shape)
+    if not ids:
+        pytest.skip("no %s variant for T=%d" % (fam, thw[0]))
     for cid in ids:
         y = layer.forward_hip(x, res, config=cid)
         torch.cuda.synchronize()
@@ -324,16 +340,16 @@ def test_h3_temporal_band_exact_integers_stats_and_affine(thw, cin, cout):
             assert err <= 1e-5 * scale, (cid, err, scale)
 
 
+@pytest.mark.parametrize("fam", ["h3t", "h3u"])
 @pytest.mark.parametrize("case", [c for c in F32_CASES if c[2] == (3, 1, 1) and c[3] == (1, 1, 1)],
                          ids=lambda c: "%dx%d" % (c[0], c[1]))
-def test_h3_temporal_band_matches_fp64(case):
+def test_h3_temporal_band_matches_fp64(case, fam):
     cin, cout, k, s, p, thw = case
     layer = _layer(cin, cout, k, s, p)
     x = _input(2, thw, layer.geom.cin_p, cin)
     ref = _ref64(layer, x)
     scale = ref.abs().max().item()
-    ids = [c for c in _h3t_ids() if layer.h3t_ok(x.shape)
-           and layer.h3t_fits(c - _h3t_ids()[0], x.shape)]
+    ids = _band_ids(fam, layer, x.shape)
     if not ids:
         pytest.skip("no frame-band variant for T=%d" % thw[0])
     for cid in ids:
