@@ -511,6 +511,12 @@ __global__ __launch_bounds__(256) void bn_seg_walk_apply_f32_kernel(
     const long long r0 = max(b0, lo_row), r1 = min(min(b0 + rpb, M), hi_row);
     const int QL = CQ < 256 ? CQ : 256, RL = 256 / QL;   // channel-quad / row lanes
     const int ql = tid % QL, rl = tid / QL;
+    // rows outside every segment (graph-bucket padding) -> 0, as the apply kernel
+    for (long long r = b0 + rl; r < min(b0 + rpb, M); r += RL) {
+      if (r >= lo_row && r < hi_row) continue;
+      for (int q = ql; q < CQ; q += QL)
+        *(float4*)(z + (size_t)r * z_stride + q * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     if (r0 < r1) {
       int lo = 0, hi = p.nseg - 1;                 // last s with start(s) <= r0
       while (lo < hi) {
@@ -580,6 +586,33 @@ __global__ __launch_bounds__(256) void bn_seg_running_f32_kernel(BnSegParams p) 
   p.running_var[c] = (float)(decay * (double)p.running_var[c] + p.run_acc[p.channels + c]);
   p.run_acc[c] = 0.0;
   p.run_acc[p.channels + c] = 0.0;
+}
+
+// Deferred running updates of many BatchNorms in one launch (an engine
+// forward's BNs whose finalize accumulated run_acc but did not launch
+// bn_seg_running_f32_kernel: rnb_bn_seg_set_defer_running): block (x, b)
+// applies r = (1-m)^K r + acc to channels of table entry b and re-arms acc.
+// K = the segments with >= 2 rows, the same for every conv of a forward
+// (rows per clip >= 2: the non-empty videos).
+struct BnRunEntry {
+  float* running_mean;
+  float* running_var;
+  double* run_acc;          // [2][channels]
+  int channels;
+  float momentum;
+};
+__global__ __launch_bounds__(256) void bn_seg_running_batched_kernel(
+    const BnRunEntry* __restrict__ tab, const int* __restrict__ coffs, int nseg) {
+  const BnRunEntry e = tab[blockIdx.y];
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= e.channels) return;
+  int valid = 0;
+  for (int t = 0; t < nseg; ++t) valid += coffs[t + 1] > coffs[t];
+  const double decay = pow(1.0 - (double)e.momentum, (double)valid);
+  e.running_mean[c] = (float)(decay * (double)e.running_mean[c] + e.run_acc[c]);
+  e.running_var[c] = (float)(decay * (double)e.running_var[c] + e.run_acc[e.channels + c]);
+  e.run_acc[c] = 0.0;
+  e.run_acc[e.channels + c] = 0.0;
 }
 
 // RPT consecutive rows x 4 channels per thread: z = y * scale + shift of the
@@ -654,6 +687,25 @@ static int g_bn_fixed_bps = 0;     // > 0: override (experiments)
 // fused finalize + running kernel up to this many segments (larger: separate
 // finalize + running kernels); 0 = never (A/B)
 static int g_bn_fused_finalize = 32;
+// 1: the finalize paths that need a separate running-update kernel skip it
+// (the caller batches them: rnb_bn_seg_running_batched)
+static int g_bn_defer_running = 0;
+void rnb_bn_seg_set_defer_running(int on) { g_bn_defer_running = on ? 1 : 0; }
+// whether a stats call over nseg segments (from epilogue sums or not) leaves
+// its running update to the caller under the current settings
+int rnb_bn_seg_defers_running(int nseg, int from_sums) {
+  if (!g_bn_defer_running) return 0;
+  if (from_sums) return nseg > BN_WALK_MAX_SEG && nseg > g_bn_fused_finalize;
+  return nseg > g_bn_fused_finalize;
+}
+int rnb_bn_seg_running_entry_size() { return (int)sizeof(BnRunEntry); }
+int rnb_bn_seg_running_batched(const void* table, int n, int max_channels, const int* coffs,
+                               int nseg, hipStream_t stream) {
+  if (n <= 0 || max_channels <= 0) return 0;
+  hipLaunchKernelGGL(bn_seg_running_batched_kernel, dim3((max_channels + 255) / 256, n),
+                     dim3(256), 0, stream, (const BnRunEntry*)table, coffs, nseg);
+  return (int)hipGetLastError();
+}
 void rnb_bn_seg_set_fused_finalize(int max_seg) {
   g_bn_fused_finalize = max_seg < 0 ? 0 : (max_seg > BN_FR_MAX_SEG ? BN_FR_MAX_SEG : max_seg);
 }
@@ -699,7 +751,7 @@ int rnb_bn_seg_stats_f32(const float* y, const int* coffs, int nseg, int rpc, lo
   }
   hipLaunchKernelGGL(bn_seg_finalize_f32_kernel, dim3((C + 255) / 256, nseg), dim3(256), 0,
                      stream, p);
-  if (running_mean != nullptr)
+  if (running_mean != nullptr && !g_bn_defer_running)
     hipLaunchKernelGGL(bn_seg_running_f32_kernel, dim3((channels + 255) / 256), dim3(256), 0,
                        stream, p);
   return (int)hipGetLastError();
@@ -732,7 +784,7 @@ int rnb_bn_seg_stats_from_sums_f32(double* sums, int sums_c, const int* coffs, i
   }
   hipLaunchKernelGGL(bn_seg_finalize_sums_f32_kernel, dim3((C + 255) / 256, nseg), dim3(256), 0,
                      stream, p, sums, sums_c);
-  if (running_mean != nullptr)
+  if (running_mean != nullptr && !g_bn_defer_running)
     hipLaunchKernelGGL(bn_seg_running_f32_kernel, dim3((channels + 255) / 256), dim3(256), 0,
                        stream, p);
   return (int)hipGetLastError();

@@ -381,6 +381,51 @@ class R2P1DEngine:
             if hip:
                 coffs = torch.tensor(clip_offsets, dtype=torch.int32).to(x.device,
                                                                           non_blocking=True)
+        # batched running-statistics updates: the finalize kernels leave the
+        # running update of large calls (> RNB_BN_FUSED_FINALIZE videos, which
+        # would take one extra kernel per BN) to one launch at the end
+        from ...ops import bn as bn_mod
+        batch_running = (hip and self.f32 and self.bn_mode == "batch"
+                         and os.environ.get("RNB_BN_BATCH_RUNNING", "1") == "1")
+        if batch_running:
+            from ...ops.native import kernels
+            kernels().bn_seg_set_defer_running(True)
+            bn_mod._RUN_SINK[0] = []
+        try:
+            y, coffs = self._forward_ops(x, bufs, coffs, clip_offsets, hip, defer, stats_fuse,
+                                         clip_seg, packed, out_indirect)
+            if batch_running and bn_mod._RUN_SINK[0]:
+                self._running_batched(bn_mod._RUN_SINK[0], coffs)
+        finally:
+            if batch_running:
+                kernels().bn_seg_set_defer_running(False)
+                bn_mod._RUN_SINK[0] = None
+        if self.head is not None:
+            y = self.head.forward(y, out) if hip else self.head.forward_torch(y)
+        elif out is not None:
+            out.copy_(y)
+            y = out
+        return y
+
+    def _running_batched(self, bns, coffs) -> None:
+        """One launch for the running updates the forward deferred; the
+        pointer table per BN set is built once (the eager warm-up before a
+        graph capture builds it outside the capture)."""
+        from ...ops.bn import running_update_table
+        from ...ops.native import kernels
+        key = tuple(id(b) for b in bns)
+        cache = self.__dict__.setdefault("_run_tables", {})
+        tab = cache.get(key)
+        if tab is None:
+            tab = cache[key] = running_update_table(bns, self.device)
+        kernels().bn_seg_running_batched(tab.data_ptr(), len(bns), max(b.channels for b in bns),
+                                         coffs.data_ptr(), coffs.numel() - 1,
+                                         torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _forward_ops(self, x, bufs, coffs, clip_offsets, hip, defer, stats_fuse, clip_seg,
+                     packed, out_indirect):
+        """The plan's ops (forward's body); returns (the output activation,
+        the clip offsets device tensor used, if any)."""
         skip = False
         pending = None               # deferred (scale_shift, clip_seg) for the next conv
         free_after = self._free_after
@@ -451,13 +496,7 @@ class R2P1DEngine:
             del src, res
             for name in free_after[i]:
                 bufs.pop(name, None)
-        y = bufs[self.out_name]
-        if self.head is not None:
-            y = self.head.forward(y, out) if hip else self.head.forward_torch(y)
-        elif out is not None:
-            out.copy_(y)
-            y = out
-        return y
+        return bufs[self.out_name], coffs
 
     __call__ = forward
 

@@ -23,6 +23,24 @@ import torch
 WALK_APPLY_MAX_SEG = 16     # csrc/bn_ops.hip BN_WALK_MAX_SEG
 
 
+# engine forwards collect here the BNs whose running update the finalize left
+# to them (deferred running updates: one batched kernel per forward)
+_RUN_SINK = [None]
+
+
+def running_update_table(bns, device) -> torch.Tensor:
+    """Device table of csrc/bn_ops.hip BnRunEntry structs for ``bns``."""
+    import struct
+    from .native import kernels
+    size = kernels().bn_run_entry_size
+    blob = bytearray(size * len(bns))
+    for i, bn in enumerate(bns):
+        struct.pack_into("<QQQif", blob, i * size, bn.running_mean.data_ptr(),
+                         bn.running_var.data_ptr(), bn._run_acc.data_ptr(), bn.channels,
+                         float(bn.momentum))
+    return torch.frombuffer(bytes(blob), dtype=torch.uint8).to(device)
+
+
 class BatchNormBatch:
     """One BatchNorm3d applied with batch statistics to a [N, T, H, W, Cp] tensor."""
 
@@ -219,6 +237,8 @@ class BatchNormBatch:
                                self.running_var.data_ptr() if run else None,
                                mean.data_ptr(), var.data_ptr(), ss.data_ptr(), stream)
         self.mean, self.var = mean[-1], var[-1]
+        if run and _RUN_SINK[0] is not None and k.bn_seg_defers_running(nseg, sums is not None):
+            _RUN_SINK[0].append(self)
         return mean, var, ss
 
     def epilogue_sums(self, nseg: int, device) -> torch.Tensor:

@@ -582,7 +582,7 @@ class ConvLayerF32:
             if self.h3t_ok(x_shape):
                 c += [H3T_BASE + i for i in range(kernels().h3t_variants)
                       if self.h3t_fits(i, x_shape)]
-                if os.environ.get("RNB_H3U", "1") != "0":
+                if os.environ.get("RNB_H3U", "0") == "1":
                     c += [H3U_BASE + i for i in range(kernels().h3u_variants)
                           if self.h3u_fits(i, x_shape)]
             if x_shape is not None and os.environ.get("RNB_X6K", "1") != "0":

@@ -257,6 +257,12 @@ class Kernels:
             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         lib.rnb_bn_seg_apply_f32_ind.argtypes = (lib.rnb_bn_seg_apply_f32.argtypes[:-1]
                                                  + [ctypes.c_void_p, ctypes.c_void_p])
+        lib.rnb_bn_seg_set_defer_running.argtypes = [ctypes.c_int]
+        lib.rnb_bn_seg_set_defer_running.restype = None
+        lib.rnb_bn_seg_defers_running.argtypes = [ctypes.c_int, ctypes.c_int]
+        lib.rnb_bn_seg_running_batched.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        self.bn_run_entry_size = lib.rnb_bn_seg_running_entry_size()
         lib.rnb_bn_seg_walk_apply_f32.argtypes = [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
             ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
@@ -565,6 +571,18 @@ class Kernels:
             sums_ptr, sums_c, coffs_ptr, nseg, rpc, C, run_acc_ptr, gamma_ptr, beta_ptr, eps,
             momentum, channels, rmean_ptr, rvar_ptr, mean_ptr, var_ptr, ss_ptr, stream),
             "bn_seg_stats_from_sums_f32")
+
+    def bn_seg_set_defer_running(self, on: bool) -> None:
+        """Finalize paths that would launch a separate running-update kernel
+        leave it to the caller (``bn_seg_running_batched``) while on."""
+        self.lib.rnb_bn_seg_set_defer_running(1 if on else 0)
+
+    def bn_seg_defers_running(self, nseg: int, from_sums: bool) -> bool:
+        return bool(self.lib.rnb_bn_seg_defers_running(nseg, 1 if from_sums else 0))
+
+    def bn_seg_running_batched(self, table_ptr, n, max_channels, coffs_ptr, nseg, stream):
+        _check(self.lib.rnb_bn_seg_running_batched(table_ptr, n, max_channels, coffs_ptr, nseg,
+                                                   stream), "bn_seg_running_batched")
 
     def bn_seg_apply_f32(self, y_ptr, z_ptr, res_ptr, coffs_ptr, nseg, rpc, ss_ptr, relu, M, C,
                          y_stride, z_stride, res_stride, stream, zind_ptr=None):

@@ -31,6 +31,7 @@ FLOP16 = 16384
 
 FAMILIES = (
     ("h3 temporal band", r"conv_h3t_kernel"),
+    ("h3 temporal wave-specialised", r"conv_h3u_kernel"),
     ("h3 row-band 4w", r"conv_h3q_kernel"),
     ("h3 row-band", r"conv_h3r_kernel"),
     ("h3 direct", r"conv_h3_kernel"),
@@ -69,7 +70,8 @@ def main(root):
                 ctr[did][r["Counter_Name"]] = ctr[did].get(r["Counter_Name"], 0.0) + \
                     float(r["Counter_Value"])
     fam = collections.defaultdict(lambda: [0, 0.0, 0.0, 0.0, 0.0])
-    print("%-4s %-44s %9s %10s %8s %8s" % ("#", "kernel", "us", "MFMA(M)", "busy%", "TF/s"))
+    print("%-4s %-44s %9s %10s %8s %8s %6s" % ("#", "kernel", "us", "MFMA(M)", "busy%", "TF/s",
+                                              "GHz"))
     for i, (s, e, name, did) in enumerate(rows):
         c = ctr.get(did, {})
         us = (e - s) / 1e3
@@ -79,7 +81,10 @@ def main(root):
         fl = FLOP16 if re.search(r"h3|x6", name) else FLOP_PER_MFMA
         tf = mf * fl / (us * 1e-6) / 1e12 if us > 0 else 0.0
         short = re.sub(r"\(.*\)$", "", name)[:44]
-        print("%-4d %-44s %9.1f %10.2f %7.1f%% %8.1f" % (i, short, us, mf / 1e6, 100 * busy, tf))
+        # effective clock: GRBM_GUI_ACTIVE counts GPU cycles per XCD (summed over 8)
+        ghz = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0 / (us * 1e3) if us > 0 else 0.0
+        print("%-4d %-44s %9.1f %10.2f %7.1f%% %8.1f %6.2f"
+              % (i, short, us, mf / 1e6, 100 * busy, tf, ghz))
         key = next((k for k, p in FAMILIES if re.search(p, name)), "other")
         a = fam[key]
         a[0] += 1
@@ -89,16 +94,17 @@ def main(root):
         a[4] += clk
         a.append(fl)
     tot_us = sum(a[1] for a in fam.values())
-    print("\n%-16s %5s %10s %6s %10s %8s %8s" % ("family", "n", "ms", "share", "MFMA busy",
-                                                  "TF/s", "% peak"))
+    print("\n%-16s %5s %10s %6s %10s %8s %8s %6s" % ("family", "n", "ms", "share", "MFMA busy",
+                                                      "TF/s", "% peak", "GHz"))
     for k, a in sorted(fam.items(), key=lambda kv: -kv[1][1]):
         n, us, mf, b, clk = a[:5]
         fl = a[5] if len(a) > 5 else FLOP_PER_MFMA
         peak = PEAK16_TF if fl == FLOP16 else PEAK_TF
         tf = mf * fl / (us * 1e-6) / 1e12 if us else 0.0
-        print("%-16s %5d %10.3f %5.1f%% %9.1f%% %8.1f %7.1f%%"
+        ghz = clk / 1024 / (us * 1e3) if us else 0.0
+        print("%-16s %5d %10.3f %5.1f%% %9.1f%% %8.1f %7.1f%% %6.2f"
               % (k, n, us / 1e3, 100 * us / tot_us, 100 * b / clk if clk else 0.0, tf,
-                 100 * tf / peak))
+                 100 * tf / peak, ghz))
     print("\n(TF/s = matrix-core FLOP rate of the MFMAs issued; %% peak against %.0f TF/s for "
           "fp32 MFMA, %.0f for the 16-bit 16x16x32 forms)" % (PEAK_TF, PEAK16_TF))
     print("whole forward: %.3f ms" % (tot_us / 1e3))

@@ -350,3 +350,32 @@ def test_runner_lanes_match_one_lane():
         outs[name] = res
     for a, b in zip(outs["one"], outs["two"]):
         assert torch.equal(a, b)
+
+
+def test_batched_running_update_matches_per_bn_kernels(monkeypatch):
+    """Calls of > 32 videos defer every BatchNorm's running update to one
+    batched kernel at the end of the forward (RNB_BN_BATCH_RUNNING, default
+    on): outputs and running statistics must equal the per-BN kernels'."""
+    from rnb_amd.models.r2p1d.model import build_network
+    from rnb_amd.models.r2p1d.engine import R2P1DEngine
+    g = torch.Generator().manual_seed(4)
+    n = 40
+    x = torch.randn((n, 2, 14, 14, 256), generator=g).to(DEV)
+    offs = list(range(n + 1))                        # 40 one-clip videos
+    outs, runs = [], []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("RNB_BN_BATCH_RUNNING", flag)
+        eng = R2P1DEngine(build_network(5, 5, depth=18, seed=2), DEV, backend="hip",
+                          bn_mode="batch", dtype=torch.float32)
+        for _ in range(2):
+            y = eng.forward(x, clip_offsets=offs)
+        torch.cuda.synchronize()
+        outs.append(y.cpu())
+        runs.append([(op.bn.running_mean.cpu(), op.bn.running_var.cpu())
+                     for op in eng.ops if op.bn is not None])
+    assert torch.equal(outs[0], outs[1])
+    assert len(runs[0]) == len(runs[1]) > 0
+    for (m0, v0), (m1, v1) in zip(runs[0], runs[1]):
+        assert torch.allclose(m0, m1, rtol=1e-6, atol=1e-7)
+        assert torch.allclose(v0, v1, rtol=1e-6, atol=1e-7)
+        assert not torch.equal(v0, torch.ones_like(v0))    # updated at all

@@ -311,7 +311,8 @@ def test_bn_per_video_stats_f32_kernel_matches_torch(res, relu, units):
 def test_bn_segment_apply_strides_and_untouched_rows(res, relu):
     """The segment apply kernel vs a torch reference: padded y / z / residual
     strides, segments that start after row 0 and end before M (rows outside
-    them must stay untouched), an empty segment, a partial tail."""
+    them are zeroed -- graph-bucket padding rows stay bounded -- and the
+    channels past C untouched), an empty segment, a partial tail."""
     from rnb_amd.ops.native import kernels
     k = kernels()
     M, C = 3 * 1000 + 17, 88
@@ -330,6 +331,7 @@ def test_bn_segment_apply_strides_and_untouched_rows(res, relu):
                        rs if res else 0, stream)
     torch.cuda.synchronize()
     ref = torch.full((M, zs), 7.0)
+    ref[:, :C] = 0.0
     yc, sc = y.cpu(), ss.cpu()
     for s in range(nseg):
         a, b = coffs[s] * rpc, coffs[s + 1] * rpc
@@ -720,7 +722,7 @@ def test_bn_walk_apply_one_dispatch_matches_walk_plus_apply(nseg, res, relu):
     """The one-dispatch finalize + apply from epilogue sums (<= 16 videos)
     against the walk + apply pair: bit-identical output, statistics, scale /
     shift and running statistics; clip offsets (rpc > 1) with empty and
-    one-clip videos, graph-bucket padding rows left untouched, in place
+    one-clip videos, graph-bucket padding rows zeroed by both, in place
     (z is y, as the engine calls it), sums re-armed and the ticket left at
     zero (second call)."""
     import os
