@@ -143,6 +143,10 @@ def parse_args(argv=None):
                          "1..8, then ~12.5%% apart; a gathering runner ends a bulk call at a "
                          "bucket boundary instead of padding: 30 graphs per engine instead of "
                          "65 at 256 clips)")
+    ap.add_argument("--yield-ms", type=float, default=0.0,
+                    help="(--route large-small) in the latency regime a small-video replica "
+                         "holds a call back up to this long while a 15-clip call runs on its "
+                         "GPU (runner announce_busy / yield_ms; 0 = off)")
     ap.add_argument("--large-lanes", type=int, default=2,
                     help="(--route large-small) runner lanes of the 15-clip-video replicas: "
                          "two (default) let a second large video start while the first runs; "
@@ -231,10 +235,12 @@ def pipeline_config(args, n_gpus: int) -> dict:
                                         "rnb_amd.models.r2p1d.model.LargeSmallSelector"}
                                    for g in gpus]},
                  dict(runner, queue_groups=[q for g in gpus for q in (
-                     {"gpus": [g] * (args.replicas - nl), "in_queue": 2 * g},
+                     dict({"gpus": [g] * (args.replicas - nl), "in_queue": 2 * g},
+                          **({"yield_ms": args.yield_ms} if args.yield_ms > 0 else {})),
                      # 15-clip videos only: buckets of whole videos (19 graphs)
-                     {"gpus": [g] * nl, "in_queue": 2 * g + 1,
-                      "bucket_step": LARGE_CLIPS})],
+                     dict({"gpus": [g] * nl, "in_queue": 2 * g + 1,
+                           "bucket_step": LARGE_CLIPS},
+                          **({"announce_busy": True} if args.yield_ms > 0 else {})))],
                       **({"group_stream_priority": [0, -1] * n_gpus}
                          if args.large_priority else {}),
                       **({"group_lanes": [args.lanes, args.large_lanes] * n_gpus}

@@ -309,6 +309,10 @@ def run(args) -> dict:
     procs = [("client", client)]
     last = len(spec.steps) - 1
     dist_infos = _assign_rccl_ranks(spec, qt, job_id)
+    # per-GPU count of "announcing" model calls in flight (group kwarg
+    # announce_busy, e.g. the 15-clip-video replica); runners of groups with
+    # yield_ms > 0 hold a latency-regime call back while it is nonzero
+    gpu_busy = ctx.Array("i", max([0] + list(spec.gpus_used())) + 1)
     for step_idx, step in enumerate(spec.steps):
         for group_idx, group in enumerate(step.groups):
             for instance_idx, gpu in enumerate(group.gpus):
@@ -321,7 +325,7 @@ def run(args) -> dict:
                     args=(in_q, out_qs, group.queue_selector, first_final, job_id, gpu,
                           group_idx, instance_idx, counter, target, flag, step_idx,
                           sta_bar, fin_bar, step.model, step.num_segments, in_r, out_r),
-                    kwargs=dict(group.kwargs, result_queue=result_queue,
+                    kwargs=dict(group.kwargs, result_queue=result_queue, gpu_busy=gpu_busy,
                                 barrier_timeout=args.barrier_timeout,
                                 dist_info=dist_infos.get((step_idx, group_idx,
                                                           instance_idx)),

@@ -116,6 +116,17 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
     group_lanes = model_kwargs.pop("group_lanes", None)
     if group_lanes is not None and group_idx < len(group_lanes):
         model_kwargs["lanes"] = int(group_lanes[group_idx])
+    # GPU sharing between replica groups in the latency regime (launcher
+    # gpu_busy: per-GPU count of in-flight calls of "announcing" groups):
+    # ``announce_busy`` (final step, e.g. the 15-clip-video replica) counts its
+    # calls from launch to completion; ``yield_ms`` > 0 makes a replica hold a
+    # call back for up to that long while such a call runs, when few requests
+    # are queued (bulk phases never wait)
+    gpu_busy = model_kwargs.pop("gpu_busy", None)
+    announce_busy = bool(model_kwargs.pop("announce_busy", False)) and gpu_busy is not None
+    yield_s = float(model_kwargs.pop("yield_ms", 0.0) or 0.0) / 1000.0
+    if gpu_busy is None or g_idx < 0 or g_idx >= len(gpu_busy):
+        announce_busy, yield_s = False, 0.0
     if use_gpu:
         torch.cuda.set_device(g_idx)
         device = torch.device("cuda:%d" % g_idx)
@@ -264,17 +275,23 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         if on_complete is not None and getattr(model, "range_guarded", False):
             sync_each = sync_each or stream is not None
 
+        def busy_add(d: int) -> None:
+            with gpu_busy.get_lock():
+                gpu_busy[g_idx] = max(0, gpu_busy[g_idx] + d)
+
         def complete_final(limit: int, done_only: bool = False) -> bool:
             """Complete in-flight final-step calls until at most ``limit`` are
             left (``done_only``: only the leading calls whose event already
             completed); False means stop the runner loop."""
             ok = True
             while len(final_pending) > limit:
-                ev, tc, outs = final_pending[0]
+                ev, tc, outs, ann = final_pending[0]
                 if done_only and not ev.query():
                     break
                 final_pending.pop(0)
                 ev.synchronize()
+                if ann:
+                    busy_add(-1)
                 if on_complete is not None:
                     on_complete(outs)
                 ok = finish_final(tc) and ok
@@ -286,12 +303,13 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             ``seg_slots``: [(slot, rows)] of the segments it wrote (direct_seg)."""
             tensor_outputs, non_tensor_outputs, time_card = outputs
             mev = model_event() if model_event is not None else None
+            ann = state.pop("announced", False)          # this call raised gpu_busy
             if final_depth > 0 and time_card is not None:
                 ev = mev
                 if ev is None:
                     ev = torch.cuda.Event()
                     ev.record(stream)
-                final_pending.append((ev, time_card, outputs))
+                final_pending.append((ev, time_card, outputs, ann))
                 return complete_final(final_depth)
             if mev is not None and stream is not None:
                 stream.wait_event(mev)      # outputs written on the model's stream
@@ -299,6 +317,8 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 stream.synchronize()
                 if on_complete is not None and time_card is not None:
                     on_complete(outputs)
+            if ann:
+                busy_add(-1)
             if time_card is None:
                 if slot is not None:
                     shared_output_ring.release(slot)    # nothing written
@@ -647,6 +667,16 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
                 raise RuntimeError("injected fault in runner%d at item %d"
                                    % (step_idx, count["items"]))
             if gather is not None and signal is not None:
+                if (yield_s > 0 and LATENCY_BACKLOG > 0 and backlog() < LATENCY_BACKLOG
+                        and gpu_busy[g_idx] > 0):
+                    # latency regime: let the announcing group's call run alone
+                    t_yield = time.time() + yield_s
+                    while gpu_busy[g_idx] > 0 and time.time() < t_yield:
+                        time.sleep(0.0002)
+                    tick("yield")
+                if announce_busy and is_final_step:
+                    busy_add(1)
+                    state["announced"] = True
                 if gslot is None and direct_out:
                     # the model writes its output straight into the output slot
                     # (R2P1DRunner.call_into: a graph replay aimed at the slot)
