@@ -20,6 +20,14 @@ import torch  # noqa: E402
 
 # name: (cin, cout, kernel, stride, padding, (T, H, W), in_affine, out_stats)
 CASES = {
+    # stem: conv1 spatial 3 -> 83 (1x7x7, stride (1, 2, 2)) on the 112x112
+    # input (output padded to 96 channels, engine._stconv), and its temporal
+    # conv 83 -> 64 (Cin_p 96); stem45 / stemt45: the same with 45 mid channels
+    # (Cin_p 48: a half-empty last 32-channel chunk)
+    "stem": (3, 83, (1, 7, 7), (1, 2, 2), (0, 3, 3), (8, 112, 112), False, True),
+    "stemt": (83, 64, (3, 1, 1), (1, 1, 1), (1, 0, 0), (8, 56, 56), True, True),
+    "stem45": (3, 45, (1, 7, 7), (1, 2, 2), (0, 3, 3), (8, 112, 112), False, True),
+    "stemt45": (45, 64, (3, 1, 1), (1, 1, 1), (1, 0, 0), (8, 56, 56), True, True),
     "k3": (64, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1), (8, 56, 56), False, True),
     "k3a": (64, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1), (8, 56, 56), True, True),
     "k4": (144, 64, (3, 1, 1), (1, 1, 1), (1, 0, 0), (8, 56, 56), True, True),
@@ -61,7 +69,9 @@ def main():
         b = torch.zeros(cout)
         geom = ConvGeom(cin=cin, cout=cout, kernel=k, stride=s, padding=p, align=F32_ALIGN,
                         cin_pad=((cin + 15) // 16 * 16 if k == (3, 1, 1) and s == (1, 1, 1)
-                                 and cin % 16 else 0))
+                                 and cin % 16 else 0),
+                        cout_pad=(cout + 15) // 16 * 16 if name.startswith("stem") and k[0] == 1
+                        else 0)
         layer = ConvLayerF32(w, b, geom, False, dev, name)
         n = args.clips
         x = torch.randn((n, T, H, W, geom.cin_p), generator=g).to(dev)
