@@ -146,6 +146,12 @@ H3T_BASE = 1395
 # wave-specialised temporal h3 kernel (csrc/conv_h3u.hip conv_h3u_kernel): the
 # h3t weight layout and conditions, variant H3U_BASE + v of rnb_conv_h3u_launch
 H3U_BASE = 1410
+# stride-2 row-band h3 kernel (csrc/conv_h3s.hip conv_h3s_kernel): 1x3x3 stride
+# (1, 2, 2) pad (0, 1, 1) with Cin_p % 32 == 0, the h3 direct weights, variant
+# H3S_BASE + v of rnb_conv_h3s_launch
+H3S_BASE = 1420
+# output pixels per block of each h3s variant (csrc/conv_h3s.hip kH3SConfigs)
+H3S_PIXELS = (256, 128, 64, 128, 128)
 # activations are split after scaling by 2^H3_IN_LOG2: fp16 lo parts stay
 # normal for |a| >= 2^-9 and inputs up to 2^10 stay in the fp16 range
 H3_IN_LOG2 = 6
@@ -157,7 +163,7 @@ def is_h3(cid: int) -> bool:
     from .native import kernels
     return ((H3D_BASE <= cid < H3D_BASE + len(kernels().h3_configs))
             or H3K_BASE <= cid < H3K_BASE + len(H3K_CONFIGS) or is_h3r(cid)
-            or is_h3t(cid) or is_h3u(cid))
+            or is_h3t(cid) or is_h3u(cid) or is_h3s(cid))
 
 
 def is_h3t(cid: int) -> bool:
@@ -168,6 +174,11 @@ def is_h3t(cid: int) -> bool:
 def is_h3u(cid: int) -> bool:
     from .native import kernels
     return H3U_BASE <= cid < H3U_BASE + kernels().h3u_variants
+
+
+def is_h3s(cid: int) -> bool:
+    from .native import kernels
+    return H3S_BASE <= cid < H3S_BASE + kernels().h3s_variants
 
 
 def is_h3r(cid: int) -> bool:
@@ -579,6 +590,12 @@ class ConvLayerF32:
             if self.h3r_ok(x_shape):
                 c += [H3R_BASE + i for i in range(kernels().h3r_variants)
                       if self.h3r_fits(i, x_shape)]
+            # the stride-2 row-band kernel lost to the h3 direct configs on every
+            # R(2+1)D-34 stride-2 spatial conv (profiles/r5_layers_stride2_h3s_128clips.txt):
+            # left out of the autotune set (tuning time) unless RNB_H3S=1
+            if self.h3s_ok(x_shape) and os.environ.get("RNB_H3S", "0") == "1":
+                c += [H3S_BASE + i for i in range(kernels().h3s_variants)
+                      if self.h3s_fits(i, x_shape)]
             if self.h3t_ok(x_shape):
                 c += [H3T_BASE + i for i in range(kernels().h3t_variants)
                       if self.h3t_fits(i, x_shape)]
@@ -834,8 +851,30 @@ class ConvLayerF32:
             return False
         return not efficient or 2 * min(rows, H) * W >= nw * tp * 16
 
+    def h3s_ok(self, x_shape=None) -> bool:
+        """The stride-2 row-band h3 kernel takes 1x3x3 stride-(1, 2, 2)
+        pad-(0, 1, 1) convs over 32-channel chunks."""
+        g = self.geom
+        return (tuple(g.kernel) == (1, 3, 3) and tuple(g.stride) == (1, 2, 2)
+                and tuple(g.padding) == (0, 1, 1) and g.cin_p % 32 == 0)
+
+    def h3s_fits(self, variant: int, x_shape, efficient: bool = True) -> bool:
+        """Whether h3s variant ``variant``'s band fits the output frame and
+        (when ``efficient``) uses at least half of the block's pixels."""
+        if x_shape is None:
+            return True
+        from .native import kernels
+        _, T, H, W, _ = x_shape
+        _, Ho, Wo = self.geom.out_thw(T, H, W)
+        rows = kernels().conv_h3s_rows(variant, Ho, Wo)
+        if rows < 1:
+            return False
+        return not efficient or 2 * rows * Wo >= H3S_PIXELS[variant]
+
     def affine_ok(self, cid: int, x_shape) -> bool:
         """Whether config ``cid`` can apply the input's BN + ReLU on load."""
+        if is_h3s(cid):
+            return False
         if cid in WINO_TEMPORAL or is_h3r(cid) or is_h3t(cid) or is_h3u(cid):
             return True
         if not is_h3(cid):
@@ -903,6 +942,17 @@ class ConvLayerF32:
                            out_stats[0].shape[2], *aff)
                 else:
                     launch(p, v, stream.cuda_stream, s_in, s_out, 0, 0, 0, *aff)
+            elif is_h3s(cid):
+                if in_affine is not None:
+                    raise ValueError("%s: the stride-2 row-band kernel takes no input BN"
+                                     % self.name)
+                _, _, s_in, s_out = self.h3d_buffers()
+                if out_stats is not None:
+                    k.conv_h3s(p, cid - H3S_BASE, stream.cuda_stream, s_in, s_out,
+                               out_stats[0].data_ptr(), out_stats[1].data_ptr() + 4 * n0,
+                               out_stats[0].shape[2])
+                else:
+                    k.conv_h3s(p, cid - H3S_BASE, stream.cuda_stream, s_in, s_out)
             elif is_h3r(cid):
                 _, _, s_in, s_out = self.h3d_buffers()
                 aff = ((in_affine[0].data_ptr(), in_affine[1].data_ptr() + 4 * n0)

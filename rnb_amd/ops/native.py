@@ -341,6 +341,12 @@ class Kernels:
         lib.rnb_conv_h3u_launch.restype = ctypes.c_int
         lib.rnb_conv_h3u_pixels.argtypes = [ctypes.c_int, ctypes.c_int]
         lib.rnb_conv_h3u_pixels.restype = ctypes.c_int
+        lib.rnb_conv_h3s_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_int, ctypes.c_float, ctypes.c_float]
+        lib.rnb_conv_h3s_launch.restype = ctypes.c_int
+        lib.rnb_conv_h3s_rows.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        lib.rnb_conv_h3s_rows.restype = ctypes.c_int
         lib.rnb_h3_set_range_flag.argtypes = [ctypes.c_void_p]
         lib.rnb_h3_set_range_flag.restype = None
         lib.rnb_conv_h3t_pixels.restype = ctypes.c_int
@@ -376,6 +382,7 @@ class Kernels:
         self.h3r_variants = lib.rnb_conv_h3r_num_variants()
         self.h3t_variants = lib.rnb_conv_h3t_num_variants()
         self.h3u_variants = lib.rnb_conv_h3u_num_variants()
+        self.h3s_variants = lib.rnb_conv_h3s_num_variants()
         self.x6_configs = []       # (pixel tile, channel tile) per x6 direct config
         for i in range(lib.rnb_conv_x6_num_configs()):
             p, c = ctypes.c_int(), ctypes.c_int()
@@ -463,6 +470,20 @@ class Kernels:
                                             sums or None, clip_seg or None, stats_c, in_scale,
                                             out_scale, in_ss or None, in_seg or None),
                "conv_h3u (variant %d)" % variant)
+
+    def conv_h3s(self, params: ConvParams, variant: int, stream: int, in_scale: float,
+                 out_scale: float, sums: int = 0, clip_seg: int = 0, stats_c: int = 0) -> None:
+        """h3 stride-2 row-band halo conv (csrc/conv_h3s.hip: 1x3x3 stride
+        (1, 2, 2) pad (0, 1, 1), Cin_p % 32 == 0, the h3 direct weights); the
+        arguments as ``conv_h3`` (no input BN on load)."""
+        _check(self.lib.rnb_conv_h3s_launch(ctypes.byref(params), variant, stream,
+                                            sums or None, clip_seg or None, stats_c, in_scale,
+                                            out_scale),
+               "conv_h3s (variant %d)" % variant)
+
+    def conv_h3s_rows(self, variant: int, Ho: int, Wo: int) -> int:
+        """Output rows per band of h3s variant ``variant`` (0: cannot run)."""
+        return int(self.lib.rnb_conv_h3s_rows(variant, Ho, Wo))
 
     def conv_h3u_pixels(self, variant: int, T: int) -> int:
         return int(self.lib.rnb_conv_h3u_pixels(variant, T))

@@ -14,7 +14,7 @@ import sys
 
 
 def family(n):
-    return ("h3 row-band" if ("conv_h3q" in n or "conv_h3r" in n) else
+    return ("h3 row-band" if ("conv_h3q" in n or "conv_h3r" in n or "conv_h3s" in n) else
             "h3 temporal band" if "conv_h3t" in n else
             "h3 direct" if "conv_h3_kernel" in n else
             "split-K reduce" if "splitk_reduce" in n else

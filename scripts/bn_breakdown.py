@@ -21,6 +21,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 FAMILIES = (
     ("h3 temporal band", r"conv_h3t_kernel"),
     ("h3 temporal wave-specialised", r"conv_h3u_kernel"),
+    ("h3 stride-2 row-band", r"conv_h3s_kernel"),
     ("h3 row-band 4-wave", r"conv_h3q_kernel"),
     ("h3 row-band", r"conv_h3r_kernel"),
     ("h3 direct", r"conv_h3_kernel"),

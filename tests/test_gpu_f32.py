@@ -779,7 +779,7 @@ def test_bn_walk_apply_one_dispatch_matches_walk_plus_apply(nseg, res, relu):
     for i, (a, b) in enumerate(zip(outs[0][1:], outs[1][1:])):
         assert torch.allclose(a, b, rtol=1e-6, atol=1e-7), (i, (a - b).abs().max().item())
     zc = outs[0][0].reshape(M, C)
-    assert torch.equal(zc[offs[-1] * rpc:], y0.reshape(M, C)[offs[-1] * rpc:].cpu())
+    assert torch.all(zc[offs[-1] * rpc:] == 0), "graph-bucket padding rows must be zeroed"
     # the apply itself against fp64
     yc = yd.cpu()
     for i in range(nseg):

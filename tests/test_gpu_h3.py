@@ -357,3 +357,67 @@ def test_h3_temporal_band_matches_fp64(case, fam):
         torch.cuda.synchronize()
         err = (y[..., :cout].double().cpu() - ref).abs().max().item()
         assert err <= 1e-5 * scale, (cid, err, scale)
+
+
+def _h3s_ids(layer, shape, efficient=False):
+    from rnb_amd.ops.conv_f32 import H3S_BASE
+    from rnb_amd.ops.native import kernels
+    if not layer.h3s_ok(shape):
+        return []
+    return [H3S_BASE + i for i in range(kernels().h3s_variants)
+            if layer.h3s_fits(i, shape, efficient=efficient)]
+
+
+@pytest.mark.parametrize("cin,cout,thw", [(64, 230, (2, 56, 56)), (128, 150, (3, 28, 28)),
+                                          (64, 72, (2, 13, 15)), (256, 140, (2, 14, 14)),
+                                          (32, 40, (1, 7, 9))])
+def test_h3s_stride2_rowband_exact_integers(cin, cout, thw):
+    """Stride-2 row-band h3 kernel (csrc/conv_h3s.hip): every variant that
+    fits the frame bit-exact on small integers -- parity-split patch columns,
+    odd frame sizes (the last input row / column of an odd frame is never a
+    centre tap), bands clipped at the frame end, padded Cout, residual +
+    ReLU epilogue."""
+    layer = _layer(cin, cout, (1, 3, 3), (1, 2, 2), (0, 1, 1), relu=True, integer=True)
+    x = _input(2, thw, layer.geom.cin_p, cin, integer=True)
+    oshape = layer.out_shape(x.shape)
+    res = _input(2, oshape[1:4], layer.geom.cout_p, cout, integer=True, seed=3)
+    ref = _ref64(layer, x, res).float()
+    ids = _h3s_ids(layer, x.shape)
+    assert ids, "no h3s variant fits %s" % (thw,)
+    for cid in ids:
+        y = layer.forward_hip(x, res, config=cid)
+        torch.cuda.synchronize()
+        assert torch.equal(y[..., :cout].cpu(), ref), cid
+        assert torch.all(y[..., cout:] == 0), cid
+
+
+@pytest.mark.parametrize("case", [c for c in F32_CASES if c[2] == (1, 3, 3) and c[3] == (1, 2, 2)],
+                         ids=lambda c: "%dx%d" % (c[0], c[1]))
+def test_h3s_matches_fp64_and_stats(case):
+    """The R(2+1)D stride-2 spatial convs (K5 / K11 / K17 shapes) within 1e-5
+    of the fp64 conv on every fitting variant, and the per-video BN sums of
+    the epilogue against fp64 sums of the stored output (two videos)."""
+    cin, cout, k, s, p, thw = case
+    layer = _layer(cin, cout, k, s, p)
+    x = _input(3, thw, layer.geom.cin_p, cin)
+    ref = _ref64(layer, x)
+    scale = ref.abs().max().item()
+    seg = torch.tensor([0, 0, 1], dtype=torch.int32, device=DEV)
+    ids = _h3s_ids(layer, x.shape)
+    assert ids
+    for cid in ids:
+        sums = torch.zeros((2, 2, layer.geom.cout_p), dtype=torch.float64, device=DEV)
+        y = layer.forward_hip(x, config=cid, out_stats=(sums, seg))
+        torch.cuda.synchronize()
+        assert torch.all(y[..., cout:] == 0), cid
+        err = (y[..., :cout].double().cpu() - ref).abs().max().item()
+        assert err <= 1e-5 * scale, (cid, err, scale)
+        yd = y[..., :cout].double().cpu()
+        for v, (a, b) in enumerate([(0, 2), (2, 3)]):
+            # fp32 lane partials and DPP row sums, fp64 after (the bound of
+            # test_h3_epilogue_stats_match_fp64_sums)
+            part = yd[a:b].reshape(-1, cout)
+            got = sums[v, :, :cout].cpu()
+            tol1 = 1e-6 * part.abs().sum(0) + 1e-9
+            assert ((got[0] - part.sum(0)).abs() <= tol1).all(), (cid, v)
+            assert torch.allclose(got[1], (part * part).sum(0), rtol=1e-6, atol=1e-9), (cid, v)
