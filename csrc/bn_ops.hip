@@ -594,17 +594,71 @@ __global__ __launch_bounds__(256) void bn_seg_running_f32_kernel(BnSegParams p) 
 // applies r = (1-m)^K r + acc to channels of table entry b and re-arms acc.
 // K = the segments with >= 2 rows, the same for every conv of a forward
 // (rows per clip >= 2: the non-empty videos).
+// An entry with ``sums`` set is a BN whose apply computed its scale / shift
+// from the producer epilogue's sums itself (bn_seg_apply_sums_f32_kernel, no
+// finalize kernel): its running statistics come from those sums here, the
+// segments walked in order (the reference's per-video EMA steps, as
+// bn_seg_sums_walk_f32_kernel), and the sums of every segment are re-armed
+// (null running_mean: re-arm only).
 struct BnRunEntry {
   float* running_mean;
   float* running_var;
   double* run_acc;          // [2][channels]
   int channels;
   float momentum;
+  double* sums;             // [nseg][2][sums_c] or null
+  int sums_c;
+  int rpc;                  // rows per clip of the BN's tensor
 };
 __global__ __launch_bounds__(256) void bn_seg_running_batched_kernel(
     const BnRunEntry* __restrict__ tab, const int* __restrict__ coffs, int nseg) {
   const BnRunEntry e = tab[blockIdx.y];
   const int c = blockIdx.x * 256 + threadIdx.x;
+  if (e.sums != nullptr) {
+    if (c >= e.sums_c) return;
+    const bool upd = e.running_mean != nullptr && c < e.channels;
+    // the formulas of the finalize paths this replaces: <= BN_WALK_MAX_SEG
+    // videos the in-order fp32 EMA of bn_seg_sums_walk_f32_kernel, more the
+    // closed form in fp64 of bn_seg_finalize_sums_f32_kernel + running
+    const bool walk = nseg <= BN_WALK_MAX_SEG;
+    const double m1 = 1.0 - (double)e.momentum;
+    int valid = 0;
+    if (!walk)
+      for (int t = 0; t < nseg; ++t) valid += (coffs[t + 1] - coffs[t]) * e.rpc >= 2;
+    float rm = upd ? e.running_mean[c] : 0.f, rv = upd ? e.running_var[c] : 0.f;
+    double am = 0.0, av = 0.0;
+    int after = valid;
+    for (int s = 0; s < nseg; ++s) {
+      double* sp = e.sums + (size_t)s * 2 * e.sums_c;
+      const int rows = (coffs[s + 1] - coffs[s]) * e.rpc;
+      if (upd && rows >= 2) {
+        const double m = sp[c] / (double)rows;
+        const float mu = (float)m;
+        const float va = (float)fmax(sp[e.sums_c + c] / (double)rows - m * m, 0.0);
+        if (walk) {
+          rm = (1.f - e.momentum) * rm + e.momentum * mu;
+          rv = (1.f - e.momentum) * rv + e.momentum * va * ((float)rows / (float)(rows - 1));
+        } else {
+          --after;                                   // valid segments after s
+          const double w = (double)e.momentum * pow(m1, (double)after);
+          am += w * (double)mu;
+          av += w * (double)va * ((double)rows / (double)(rows - 1));
+        }
+      }
+      sp[c] = 0.0;
+      sp[e.sums_c + c] = 0.0;
+    }
+    if (upd) {
+      if (!walk) {
+        const double decay = pow(m1, (double)valid);
+        rm = (float)(decay * (double)rm + am);
+        rv = (float)(decay * (double)rv + av);
+      }
+      e.running_mean[c] = rm;
+      e.running_var[c] = rv;
+    }
+    return;
+  }
   if (c >= e.channels) return;
   int valid = 0;
   for (int t = 0; t < nseg; ++t) valid += coffs[t + 1] > coffs[t];
@@ -676,6 +730,133 @@ __global__ __launch_bounds__(256) void bn_seg_apply_f32_kernel(
   }
 }
 
+// bn_seg_apply_f32_kernel with the scale / shift computed from the producer
+// epilogue's fp64 sums [nseg][2][sums_c] (the finalize kernels' formulas, so
+// the output is bit-identical to finalize + apply): no finalize dispatch
+// before a block-output apply. The sums are only read here; the batched
+// running update (BnRunEntry.sums) walks them and re-arms them afterwards.
+static __device__ __forceinline__ void bn_ss4_from_sums(const double* __restrict__ sp, int sums_c,
+                                                        int c, int rows,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float eps,
+                                                        float4& sc, float4& sh) {
+  float scv[4], shv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float mu = 0.f, va = 0.f;
+    if (rows > 0) {
+      const double m = sp[c + k] / (double)rows;
+      mu = (float)m;
+      va = (float)fmax(sp[sums_c + c + k] / (double)rows - m * m, 0.0);
+    }
+    // an empty segment (a graph bucket's padding clips) maps its rows to 0
+    scv[k] = rows > 0 ? gamma[c + k] * rsqrtf(va + eps) : 0.f;
+    shv[k] = rows > 0 ? beta[c + k] - mu * scv[k] : 0.f;
+  }
+  sc = make_float4(scv[0], scv[1], scv[2], scv[3]);
+  sh = make_float4(shv[0], shv[1], shv[2], shv[3]);
+}
+
+// segment of row r (coffs[s] rpc <= r < coffs[s + 1] rpc), binary search
+static __device__ __forceinline__ int bn_seg_of_row(const int* __restrict__ coffs, int nseg,
+                                                    int rpc, int r) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (coffs[mid] * rpc <= r) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// A block covers 1024 / (C / 4) consecutive rows x all C channels; when they
+// lie in at most BN_AS_SEGS segments (the common case: a video's rows run to
+// thousands) the block's threads first compute those segments' scale / shift
+// into LDS, one (segment, channel) each, then every thread applies from LDS
+// -- the fp64 moments once per block instead of once per thread (which slowed
+// the apply 30 %). Otherwise each thread computes its own, as
+// bn_seg_apply_f32_kernel reads them.
+#define BN_AS_SEGS 2
+#define BN_AS_MAX_C 512
+__global__ __launch_bounds__(256) void bn_seg_apply_sums_f32_kernel(
+    const float* __restrict__ y, float* __restrict__ z, const float* __restrict__ res,
+    const int* __restrict__ coffs, int nseg, int rpc, const double* __restrict__ sums, int sums_c,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, int relu,
+    long long M, int C, int y_stride, int z_stride, int res_stride,
+    float* const* __restrict__ zind) {
+  __shared__ float lss[BN_AS_SEGS][2][BN_AS_MAX_C];
+  if (zind != nullptr) z = *zind;
+  const int cq = C / 4;
+  const long long groups = (M + BN_APPLY_RPT - 1) / BN_APPLY_RPT;
+  const int lo_row = coffs[0] * rpc, hi_row = coffs[nseg] * rpc;
+  // the block's valid rows and their segments (uniform)
+  const long long i0 = (long long)blockIdx.x * 256;
+  const long long g0 = i0 / cq, g1 = min((i0 + 255) / cq, groups - 1);
+  const int rlo = max((int)(g0 * BN_APPLY_RPT), lo_row);
+  const int rhi = min((int)min((g1 + 1) * BN_APPLY_RPT, M), hi_row) - 1;
+  int s_lo = 0, nblk_seg = 0;
+  if (rlo <= rhi) {
+    s_lo = bn_seg_of_row(coffs, nseg, rpc, rlo);
+    nblk_seg = bn_seg_of_row(coffs, nseg, rpc, rhi) - s_lo + 1;
+  }
+  const bool shared_ss = nblk_seg > 0 && nblk_seg <= BN_AS_SEGS && C <= BN_AS_MAX_C;
+  if (shared_ss) {
+    for (int t = threadIdx.x; t < nblk_seg * C; t += 256) {
+      const int k = t / C, c = t - k * C, sg = s_lo + k;
+      const int rows = (coffs[sg + 1] - coffs[sg]) * rpc;
+      const double* sp = sums + (size_t)sg * 2 * sums_c;
+      float mu = 0.f, va = 0.f;
+      if (rows > 0) {
+        const double m = sp[c] / (double)rows;
+        mu = (float)m;
+        va = (float)fmax(sp[sums_c + c] / (double)rows - m * m, 0.0);
+      }
+      const float scv = rows > 0 ? gamma[c] * rsqrtf(va + eps) : 0.f;
+      lss[k][0][c] = scv;
+      lss[k][1][c] = rows > 0 ? beta[c] - mu * scv : 0.f;
+    }
+    __syncthreads();
+  }
+  const long long i = i0 + threadIdx.x;
+  if (i >= groups * cq) return;
+  const long long g = i / cq;
+  const int c = (int)(i - g * cq) * 4;
+  const int ra = (int)(g * BN_APPLY_RPT);
+  const int rb = (int)min((long long)ra + BN_APPLY_RPT, M);
+  int s = -1, s_end = 0;
+  float4 sc = make_float4(0.f, 0.f, 0.f, 0.f), sh = sc;
+  for (int r = ra; r < rb; ++r) {
+    if (r < lo_row || r >= hi_row) {
+      *(float4*)(z + (size_t)r * z_stride + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+      continue;
+    }
+    if (s < 0 || r >= s_end) {
+      if (s < 0) s = bn_seg_of_row(coffs, nseg, rpc, r);
+      while (r >= coffs[s + 1] * rpc) ++s;
+      s_end = coffs[s + 1] * rpc;
+      if (shared_ss) {
+        const int k = s - s_lo;
+        sc = *(const float4*)&lss[k][0][c];
+        sh = *(const float4*)&lss[k][1][c];
+      } else {
+        bn_ss4_from_sums(sums + (size_t)s * 2 * sums_c, sums_c, c, s_end - coffs[s] * rpc, gamma,
+                         beta, eps, sc, sh);
+      }
+    }
+    const float4 v = *(const float4*)(y + (size_t)r * y_stride + c);
+    float o[4] = {fmaf(v.x, sc.x, sh.x), fmaf(v.y, sc.y, sh.y), fmaf(v.z, sc.z, sh.z),
+                  fmaf(v.w, sc.w, sh.w)};
+    if (res) {
+      const float4 rv = *(const float4*)(res + (size_t)r * res_stride + c);
+      o[0] += rv.x; o[1] += rv.y; o[2] += rv.z; o[3] += rv.w;
+    }
+    if (relu) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = fmaxf(o[k], 0.f);
+    }
+    *(float4*)(z + (size_t)r * z_stride + c) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 extern "C" {
 
 // Blocks per segment: a fixed 32, so the split of a video's rows -- and with
@@ -702,6 +883,7 @@ int rnb_bn_seg_running_entry_size() { return (int)sizeof(BnRunEntry); }
 int rnb_bn_seg_running_batched(const void* table, int n, int max_channels, const int* coffs,
                                int nseg, hipStream_t stream) {
   if (n <= 0 || max_channels <= 0) return 0;
+  // (max_channels: the largest channels or sums_c of the table's entries)
   hipLaunchKernelGGL(bn_seg_running_batched_kernel, dim3((max_channels + 255) / 256, n),
                      dim3(256), 0, stream, (const BnRunEntry*)table, coffs, nseg);
   return (int)hipGetLastError();
@@ -831,6 +1013,26 @@ int rnb_bn_seg_apply_f32_ind(const float* y, float* z, const float* res, const i
   hipLaunchKernelGGL(bn_seg_apply_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      stream, y, z, res, coffs, nseg, rpc, ss, relu, M, C, y_stride, z_stride,
                      res_stride, zind);
+  return (int)hipGetLastError();
+}
+
+// the apply from the producer epilogue's sums (bn_seg_apply_sums_f32_kernel);
+// the caller re-arms the sums (rnb_bn_seg_running_batched, BnRunEntry.sums)
+int rnb_bn_seg_apply_sums_f32(const float* y, float* z, const float* res, const int* coffs,
+                              int nseg, int rpc, const double* sums, int sums_c,
+                              const float* gamma, const float* beta, float eps, int relu,
+                              long long M, int C, int y_stride, int z_stride, int res_stride,
+                              float* const* zind, hipStream_t stream) {
+  if (M <= 0 || C <= 0 || nseg <= 0) return 0;
+  if (C % 4 || y_stride % 4 || z_stride % 4 || (res && res_stride % 4) || rpc <= 0 ||
+      sums_c < C || !sums)
+    return -2;
+  if (zind != nullptr && ((uintptr_t)zind % 8) != 0) return -2;
+  const long long n = (M + BN_APPLY_RPT - 1) / BN_APPLY_RPT * (C / 4);
+  if (M > 0x7FFFFFFFLL) return -3;
+  hipLaunchKernelGGL(bn_seg_apply_sums_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     stream, y, z, res, coffs, nseg, rpc, sums, sums_c, gamma, beta, eps, relu, M,
+                     C, y_stride, z_stride, res_stride, zind);
   return (int)hipGetLastError();
 }
 

@@ -411,14 +411,14 @@ class R2P1DEngine:
         """One launch for the running updates the forward deferred; the
         pointer table per BN set is built once (the eager warm-up before a
         graph capture builds it outside the capture)."""
-        from ...ops.bn import running_update_table
+        from ...ops.bn import running_table_channels, running_table_key, running_update_table
         from ...ops.native import kernels
-        key = tuple(id(b) for b in bns)
+        key = running_table_key(bns)
         cache = self.__dict__.setdefault("_run_tables", {})
         tab = cache.get(key)
         if tab is None:
             tab = cache[key] = running_update_table(bns, self.device)
-        kernels().bn_seg_running_batched(tab.data_ptr(), len(bns), max(b.channels for b in bns),
+        kernels().bn_seg_running_batched(tab.data_ptr(), len(bns), running_table_channels(bns),
                                          coffs.data_ptr(), coffs.numel() - 1,
                                          torch.cuda.current_stream(self.device).cuda_stream)
 
@@ -475,8 +475,17 @@ class R2P1DEngine:
                         pending = (op.bn.scale_shift_f32(y, coffs, sums, rpc=thw), clip_seg)
                     else:
                         ind = out_indirect if i == len(self.ops) - 1 else None
-                        y = op.bn.forward_hip(y, res, op.bn_relu, out=y, segments=coffs,
-                                              sums=sums, rpc=thw, out_ind=ind)
+                        from ...ops import bn as bn_mod
+                        if (sums is not None and bn_mod._RUN_SINK[0] is not None
+                                and os.environ.get("RNB_BN_APPLY_SUMS", "1") != "0"):
+                            # scale / shift inside the apply, from the epilogue
+                            # sums: no finalize dispatch; the batched running
+                            # update walks and re-arms the sums at the end
+                            y = op.bn.apply_from_sums(y, res, op.bn_relu, out=y, segments=coffs,
+                                                      sums=sums, rpc=thw, out_ind=ind)
+                        else:
+                            y = op.bn.forward_hip(y, res, op.bn_relu, out=y, segments=coffs,
+                                                  sums=sums, rpc=thw, out_ind=ind)
                 else:
                     y = op.layer.forward_torch(src, None, out_dtype=self.dtype)
                     y = op.bn.forward_torch(y, res, op.bn_relu, out_dtype=self.dtype,
@@ -677,12 +686,25 @@ class GraphedEngine:
     def _tune_here(self, b: int) -> bool:
         """fp32 engines time tiles at a few batch sizes only (the largest bucket
         and the power-of-two buckets); the other buckets take the nearest tuned
-        size's tiles (ops/tuning.nearest). bf16 engines tune every bucket."""
+        size's tiles (ops/tuning.nearest). bf16 engines tune every bucket.
+        RNB_TUNE_SNAP=1 also tunes, per power of two that is not a bucket, the
+        smallest bucket holding it (geometric buckets have no 128: 140 is
+        tuned) -- +30 s of setup for no measured gain
+        (profiles/r5_ab_tune_snap_20steps.txt), so off by default."""
         if not self.autotune:
             return False
         if not self.engine.f32:
             return True
-        return b == self.buckets[-1] or (b & (b - 1)) == 0
+        if b == self.buckets[-1] or (b & (b - 1)) == 0:
+            return True
+        if os.environ.get("RNB_TUNE_SNAP", "0") != "1":
+            return False
+        k = 1
+        while k < b:
+            k *= 2
+        # b is the smallest bucket >= some power of two k / 2 .. that is not a bucket
+        half = k // 2
+        return half > 0 and half not in self.buckets and self.bucket_for(half) == b
 
     def _capture(self, b: int):
         t0 = time.time()

@@ -292,8 +292,9 @@ class R2P1DRunner(RunnerModel):
         return (max(1, self.max_batch_videos), self.max_clips, self.batch_wait_s)
 
     # trim a gathered call to a bucket boundary when padding up to the next
-    # bucket would add more than this fraction of rows (runner.py gather)
-    FIT_PAD_FRAC = 0.03
+    # bucket would add more than this fraction of rows (runner.py gather;
+    # RNB_FIT_PAD_FRAC overrides, >= 1 never trims)
+    FIT_PAD_FRAC = float(os.environ.get("RNB_FIT_PAD_FRAC", "0.03"))
 
     def gather_fit(self, rows: int) -> int:
         """Rows a gathered call of ``rows`` should keep: ``rows`` when padding

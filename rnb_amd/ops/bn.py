@@ -28,17 +28,45 @@ WALK_APPLY_MAX_SEG = 16     # csrc/bn_ops.hip BN_WALK_MAX_SEG
 _RUN_SINK = [None]
 
 
-def running_update_table(bns, device) -> torch.Tensor:
-    """Device table of csrc/bn_ops.hip BnRunEntry structs for ``bns``."""
+def _entry(e):
+    """(bn, sums or None, rpc) of a sink entry (a bare BN: finalize-accumulated)."""
+    return e if isinstance(e, tuple) else (e, None, 0)
+
+
+def running_update_table(entries, device) -> torch.Tensor:
+    """Device table of csrc/bn_ops.hip BnRunEntry structs: a BN whose finalize
+    accumulated its running terms (``run_acc``), or (bn, sums, rpc) for a BN
+    applied from its epilogue sums (the kernel walks and re-arms them)."""
     import struct
     from .native import kernels
     size = kernels().bn_run_entry_size
-    blob = bytearray(size * len(bns))
-    for i, bn in enumerate(bns):
-        struct.pack_into("<QQQif", blob, i * size, bn.running_mean.data_ptr(),
-                         bn.running_var.data_ptr(), bn._run_acc.data_ptr(), bn.channels,
-                         float(bn.momentum))
-    return torch.frombuffer(bytes(blob), dtype=torch.uint8).to(device)
+    blob = bytearray(size * len(entries))
+    for i, e in enumerate(entries):
+        bn, sums, rpc = _entry(e)
+        run = bn.update_running
+        acc = getattr(bn, "_run_acc", None)
+        struct.pack_into("<QQQifQii", blob, i * size,
+                         bn.running_mean.data_ptr() if run else 0,
+                         bn.running_var.data_ptr() if run else 0,
+                         acc.data_ptr() if acc is not None else 0, bn.channels,
+                         float(bn.momentum), sums.data_ptr() if sums is not None else 0,
+                         sums.shape[2] if sums is not None else 0, int(rpc))
+    return torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(device)
+
+
+def running_table_key(entries):
+    """Cache key of a sink's table (BN identities, sums buffers, rows per clip)."""
+    key = []
+    for e in entries:
+        bn, sums, rpc = _entry(e)
+        key.append((id(bn), sums.data_ptr() if sums is not None else 0, int(rpc)))
+    return tuple(key)
+
+
+def running_table_channels(entries) -> int:
+    """Threads per table entry the batched kernel needs (channels, or sums_c)."""
+    return max(max(_entry(e)[0].channels, _entry(e)[1].shape[2] if _entry(e)[1] is not None
+                   else 0) for e in entries)
 
 
 class BatchNormBatch:
@@ -136,6 +164,36 @@ class BatchNormBatch:
                            M, C, Cs, z.shape[-1],
                            residual.shape[-1] if residual is not None else 0, stream,
                            out_ind.data_ptr() if out_ind is not None else None)
+        return z
+
+    def apply_from_sums(self, y: torch.Tensor, residual: Optional[torch.Tensor], relu: bool,
+                        out: torch.Tensor, segments: torch.Tensor, sums: torch.Tensor,
+                        rpc: int, out_ind: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The apply with its per-video scale / shift computed from the producer
+        epilogue's fp64 ``sums`` inside the apply kernel (no finalize
+        dispatch; output bit-identical to finalize + apply). Needs an engine
+        forward's running sink: the batched running update walks the sums in
+        video order afterwards and re-arms them."""
+        from .native import kernels
+        if _RUN_SINK[0] is None:
+            raise RuntimeError("apply_from_sums needs the batched running update (engine forward)")
+        N, T, H, W, Cs = y.shape
+        M, C = N * T * H * W, self.channels_p
+        nseg = segments.numel() - 1
+        if (sums.dtype != torch.float64 or not sums.is_contiguous() or sums.dim() != 3
+                or sums.shape[0] < nseg or sums.shape[1] != 2 or sums.shape[2] < C):
+            raise ValueError("epilogue sums %s do not match %d segments x %d channels"
+                             % (tuple(sums.shape), nseg, C))
+        z = out
+        if M > 0:
+            stream = torch.cuda.current_stream(y.device).cuda_stream
+            kernels().bn_seg_apply_sums_f32(
+                y.data_ptr(), z.data_ptr(), residual.data_ptr() if residual is not None else None,
+                segments.data_ptr(), nseg, rpc, sums.data_ptr(), sums.shape[2],
+                self.gamma.data_ptr(), self.beta.data_ptr(), self.eps, 1 if relu else 0, M, C, Cs,
+                z.shape[-1], residual.shape[-1] if residual is not None else 0, stream,
+                out_ind.data_ptr() if out_ind is not None else None)
+        _RUN_SINK[0].append((self, sums, rpc))
         return z
 
     def _walk_apply_f32(self, y, residual, relu, z, segments, sums, rpc):

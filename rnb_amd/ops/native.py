@@ -257,6 +257,11 @@ class Kernels:
             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         lib.rnb_bn_seg_apply_f32_ind.argtypes = (lib.rnb_bn_seg_apply_f32.argtypes[:-1]
                                                  + [ctypes.c_void_p, ctypes.c_void_p])
+        lib.rnb_bn_seg_apply_sums_f32.argtypes = [
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+            ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_float, ctypes.c_int, ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
+            ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         lib.rnb_bn_seg_set_defer_running.argtypes = [ctypes.c_int]
         lib.rnb_bn_seg_set_defer_running.restype = None
         lib.rnb_bn_seg_defers_running.argtypes = [ctypes.c_int, ctypes.c_int]
@@ -613,6 +618,18 @@ class Kernels:
                                                  ss_ptr, relu, M, C, y_stride, z_stride,
                                                  res_stride, zind_ptr or None, stream),
                "bn_seg_apply_f32")
+
+    def bn_seg_apply_sums_f32(self, y_ptr, z_ptr, res_ptr, coffs_ptr, nseg, rpc, sums_ptr,
+                              sums_c, gamma_ptr, beta_ptr, eps, relu, M, C, y_stride, z_stride,
+                              res_stride, stream, zind_ptr=None):
+        """The apply with its scale / shift computed from the producer
+        epilogue's fp64 sums (no finalize kernel); the sums are left for the
+        batched running update to walk and re-arm."""
+        _check(self.lib.rnb_bn_seg_apply_sums_f32(y_ptr, z_ptr, res_ptr, coffs_ptr, nseg, rpc,
+                                                  sums_ptr, sums_c, gamma_ptr, beta_ptr, eps,
+                                                  relu, M, C, y_stride, z_stride, res_stride,
+                                                  zind_ptr or None, stream),
+               "bn_seg_apply_sums_f32")
 
     def bn_seg_walk_apply_f32(self, sums_ptr, sums_c, ticket_ptr, coffs_ptr, nseg, rpc, C,
                               gamma_ptr, beta_ptr, eps, momentum, channels, rmean_ptr, rvar_ptr,

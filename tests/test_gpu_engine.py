@@ -379,3 +379,37 @@ def test_batched_running_update_matches_per_bn_kernels(monkeypatch):
         assert torch.allclose(m0, m1, rtol=1e-6, atol=1e-7)
         assert torch.allclose(v0, v1, rtol=1e-6, atol=1e-7)
         assert not torch.equal(v0, torch.ones_like(v0))    # updated at all
+
+
+@pytest.mark.parametrize("n,per_video", [(40, 1), (6, 2)])
+def test_apply_from_sums_matches_finalize_path(monkeypatch, n, per_video):
+    """Block-output BatchNorms apply their scale / shift straight from the
+    producer epilogue's sums (no finalize dispatch, RNB_BN_APPLY_SUMS, default
+    on), the batched running update walking the sums afterwards: outputs
+    bit-identical to finalize + apply, running statistics equal to the
+    finalize paths' (in-order walk up to 16 videos, closed form above), the
+    epilogue sums re-armed to zero for the next call."""
+    from rnb_amd.models.r2p1d.model import build_network
+    from rnb_amd.models.r2p1d.engine import R2P1DEngine
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn((n, 2, 14, 14, 256), generator=g).to(DEV)
+    offs = list(range(0, n + 1, per_video))
+    outs, runs = [], []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("RNB_BN_APPLY_SUMS", flag)
+        eng = R2P1DEngine(build_network(5, 5, depth=18, seed=2), DEV, backend="hip",
+                          bn_mode="batch", dtype=torch.float32)
+        for _ in range(2):
+            y = eng.forward(x, clip_offsets=offs)
+        torch.cuda.synchronize()
+        outs.append(y.cpu())
+        runs.append([(op.bn.running_mean.cpu(), op.bn.running_var.cpu())
+                     for op in eng.ops if op.bn is not None])
+        for op in eng.ops:
+            s = getattr(op.bn, "_esums", None) if op.bn is not None else None
+            if s is not None:
+                assert float(s.abs().sum()) == 0.0, "epilogue sums must be re-armed"
+    assert torch.equal(outs[0], outs[1])
+    for (m0, v0), (m1, v1) in zip(runs[0], runs[1]):
+        assert torch.allclose(m0, m1, rtol=1e-6, atol=1e-7)
+        assert torch.allclose(v0, v1, rtol=1e-6, atol=1e-7)
