@@ -158,9 +158,11 @@ def parse_args(argv=None):
     ap.add_argument("--lanes", type=int, default=None,
                     help="graphed engines per runner process, calls rotating over their "
                          "streams (R2P1DRunner lanes: one-video calls overlap on the GPU). "
-                         "Default: 2 when a GPU hosts one runner replica (literal config #2: "
-                         "356 -> 554-566 videos/s, profiles/r4_ab_literal2_lanes.txt), else 1 "
-                         "(with several replicas lanes lose, r4_ab_whole_pipeline_lanes.txt)")
+                         "Default: 3 when a GPU hosts one runner replica (literal config #2: "
+                         "356 -> 554-566 videos/s with 2, profiles/r4_ab_literal2_lanes.txt; "
+                         "526 / 634 / 621 with 2 / 3 / 4, profiles/r5_ab_lanes_whole.txt), "
+                         "else 1 (with several replicas lanes lose, "
+                         "r4_ab_whole_pipeline_lanes.txt)")
     ap.add_argument("--batch-wait-ms", type=float, default=0.0,
                     help="how long a runner waits for more queued videos to batch")
     ap.add_argument("--slots", type=int, default=None,
@@ -203,7 +205,7 @@ def parse_args(argv=None):
     if args.replicas is None:
         args.replicas = 4 if args.pipeline == "whole" else 3
     if args.lanes is None:
-        args.lanes = 2 if args.replicas == 1 else 1
+        args.lanes = 3 if args.replicas == 1 else 1
     return args
 
 
@@ -637,8 +639,8 @@ def run_literal_extras(args) -> dict:
              "--steps", "2", "--warmup", "1", "--videos-per-step", "128",
              "--latency-mi", "90", "--latency-load", "0", "--latency-seconds", "4", "--no-check"]
     # (1 loader + 1 runner, one video per model call; the runner's default
-    # two lanes keep two calls in flight on two streams; the one-lane run is
-    # the round-3 form, kept for comparison)
+    # three lanes keep three calls in flight on three streams; the one-lane
+    # run is the round-3 form, kept for comparison)
     runs = [("config2_whole", whole),
             ("config2_whole_one_lane", whole + ["--lanes", "1"]),
             # its numerics (re-joined segment videos) join the headline's strata
