@@ -152,6 +152,11 @@ H3U_BASE = 1410
 H3S_BASE = 1420
 # output pixels per block of each h3s variant (csrc/conv_h3s.hip kH3SConfigs)
 H3S_PIXELS = (256, 128, 64, 128, 128)
+# stem h3 kernel (csrc/conv_h3stem.hip conv_h3stem_kernel): 1x7x7 stride (1, 2, 2)
+# pad (0, 3, 3) with Cin_p 4 and K-permuted weights (h3stem_buffers), variant
+# H3STEM_BASE + v of rnb_conv_h3stem_launch; output pixels per block per variant
+H3STEM_BASE = 1430
+H3STEM_PIXELS = (256, 128, 448)
 # activations are split after scaling by 2^H3_IN_LOG2: fp16 lo parts stay
 # normal for |a| >= 2^-9 and inputs up to 2^10 stay in the fp16 range
 H3_IN_LOG2 = 6
@@ -163,7 +168,7 @@ def is_h3(cid: int) -> bool:
     from .native import kernels
     return ((H3D_BASE <= cid < H3D_BASE + len(kernels().h3_configs))
             or H3K_BASE <= cid < H3K_BASE + len(H3K_CONFIGS) or is_h3r(cid)
-            or is_h3t(cid) or is_h3u(cid) or is_h3s(cid))
+            or is_h3t(cid) or is_h3u(cid) or is_h3s(cid) or is_h3stem(cid))
 
 
 def is_h3t(cid: int) -> bool:
@@ -174,6 +179,11 @@ def is_h3t(cid: int) -> bool:
 def is_h3u(cid: int) -> bool:
     from .native import kernels
     return H3U_BASE <= cid < H3U_BASE + kernels().h3u_variants
+
+
+def is_h3stem(cid: int) -> bool:
+    from .native import kernels
+    return H3STEM_BASE <= cid < H3STEM_BASE + kernels().h3stem_variants
 
 
 def is_h3s(cid: int) -> bool:
@@ -442,6 +452,7 @@ class ConvLayerF32:
         self._x6d = None                     # (split weights, bias) for the x6 direct kernel
         self._h3d = None                     # (weights, bias, in_scale, out_scale) for h3
         self._h3t = None                     # h3d_buffers in the per-tap padded K layout (h3t)
+        self._h3stem = None                  # h3d_buffers in the stem kernel's K order
         self._x6k_ws: Dict[int, torch.Tensor] = {}
 
     def ksplit_for(self, cid: int, x_shape) -> int:
@@ -596,6 +607,9 @@ class ConvLayerF32:
             if self.h3s_ok(x_shape) and os.environ.get("RNB_H3S", "0") == "1":
                 c += [H3S_BASE + i for i in range(kernels().h3s_variants)
                       if self.h3s_fits(i, x_shape)]
+            if self.h3stem_ok(x_shape):
+                c += [H3STEM_BASE + i for i in range(kernels().h3stem_variants)
+                      if self.h3stem_fits(i, x_shape)]
             if self.h3t_ok(x_shape):
                 c += [H3T_BASE + i for i in range(kernels().h3t_variants)
                       if self.h3t_fits(i, x_shape)]
@@ -851,6 +865,40 @@ class ConvLayerF32:
             return False
         return not efficient or 2 * min(rows, H) * W >= nw * tp * 16
 
+    def h3stem_ok(self, x_shape=None) -> bool:
+        """The stem h3 kernel takes 1x7x7 stride-(1, 2, 2) pad-(0, 3, 3) convs of
+        a 4-channel (3 + pad) input."""
+        g = self.geom
+        return (tuple(g.kernel) == (1, 7, 7) and tuple(g.stride) == (1, 2, 2)
+                and tuple(g.padding) == (0, 3, 3) and g.cin_p == 4)
+
+    def h3stem_fits(self, variant: int, x_shape, efficient: bool = True) -> bool:
+        if x_shape is None:
+            return True
+        from .native import kernels
+        _, T, H, W, _ = x_shape
+        _, Ho, Wo = self.geom.out_thw(T, H, W)
+        rows = kernels().conv_h3stem_rows(variant, Ho, Wo)
+        if rows < 1:
+            return False
+        return not efficient or 2 * rows * Wo >= H3STEM_PIXELS[variant]
+
+    def h3stem_buffers(self):
+        """h3 split weights of the stem kernel's K order: step dy (a kernel
+        row) holds k = dx * 4 + c for dx 0..6 and a zero tap (K_pad 224)."""
+        if self._h3stem is None:
+            rows = self.geom.cout_p + X6_ROW_SLACK
+            w = torch.zeros(rows, 7 * 32, dtype=torch.float32)
+            src = self.wmat[:self.geom.cout, :self.k_total].cpu()
+            for dy in range(7):
+                w[:self.geom.cout, dy * 32:dy * 32 + 28] = src[:, dy * 28:(dy + 1) * 28]
+            b = torch.zeros(rows, dtype=torch.float32)
+            b[:self.geom.cout] = self.bias[:self.geom.cout].cpu()
+            sw = h3_weight_scale_log2(w)
+            self._h3stem = (h3_direct_weights(w, sw).to(self.device), b.to(self.device),
+                            float(2.0 ** H3_IN_LOG2), float(2.0 ** -(H3_IN_LOG2 + sw)))
+        return self._h3stem
+
     def h3s_ok(self, x_shape=None) -> bool:
         """The stride-2 row-band h3 kernel takes 1x3x3 stride-(1, 2, 2)
         pad-(0, 1, 1) convs over 32-channel chunks."""
@@ -873,7 +921,7 @@ class ConvLayerF32:
 
     def affine_ok(self, cid: int, x_shape) -> bool:
         """Whether config ``cid`` can apply the input's BN + ReLU on load."""
-        if is_h3s(cid):
+        if is_h3s(cid) or is_h3stem(cid):
             return False
         if cid in WINO_TEMPORAL or is_h3r(cid) or is_h3t(cid) or is_h3u(cid):
             return True
@@ -942,6 +990,18 @@ class ConvLayerF32:
                            out_stats[0].shape[2], *aff)
                 else:
                     launch(p, v, stream.cuda_stream, s_in, s_out, 0, 0, 0, *aff)
+            elif is_h3stem(cid):
+                if in_affine is not None:
+                    raise ValueError("%s: the stem kernel takes no input BN" % self.name)
+                wx, bx, s_in, s_out = self.h3stem_buffers()
+                p.w, p.bias = wx.data_ptr(), bx.data_ptr()
+                p.K_pad, p.w_rows = 7 * 32, bx.shape[0]
+                if out_stats is not None:
+                    k.conv_h3stem(p, cid - H3STEM_BASE, stream.cuda_stream, s_in, s_out,
+                                  out_stats[0].data_ptr(), out_stats[1].data_ptr() + 4 * n0,
+                                  out_stats[0].shape[2])
+                else:
+                    k.conv_h3stem(p, cid - H3STEM_BASE, stream.cuda_stream, s_in, s_out)
             elif is_h3s(cid):
                 if in_affine is not None:
                     raise ValueError("%s: the stride-2 row-band kernel takes no input BN"

@@ -352,6 +352,10 @@ class Kernels:
         lib.rnb_conv_h3s_launch.restype = ctypes.c_int
         lib.rnb_conv_h3s_rows.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         lib.rnb_conv_h3s_rows.restype = ctypes.c_int
+        lib.rnb_conv_h3stem_launch.argtypes = lib.rnb_conv_h3s_launch.argtypes
+        lib.rnb_conv_h3stem_launch.restype = ctypes.c_int
+        lib.rnb_conv_h3stem_rows.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        lib.rnb_conv_h3stem_rows.restype = ctypes.c_int
         lib.rnb_h3_set_range_flag.argtypes = [ctypes.c_void_p]
         lib.rnb_h3_set_range_flag.restype = None
         lib.rnb_conv_h3t_pixels.restype = ctypes.c_int
@@ -388,6 +392,7 @@ class Kernels:
         self.h3t_variants = lib.rnb_conv_h3t_num_variants()
         self.h3u_variants = lib.rnb_conv_h3u_num_variants()
         self.h3s_variants = lib.rnb_conv_h3s_num_variants()
+        self.h3stem_variants = lib.rnb_conv_h3stem_num_variants()
         self.x6_configs = []       # (pixel tile, channel tile) per x6 direct config
         for i in range(lib.rnb_conv_x6_num_configs()):
             p, c = ctypes.c_int(), ctypes.c_int()
@@ -485,6 +490,19 @@ class Kernels:
                                             sums or None, clip_seg or None, stats_c, in_scale,
                                             out_scale),
                "conv_h3s (variant %d)" % variant)
+
+    def conv_h3stem(self, params: ConvParams, variant: int, stream: int, in_scale: float,
+                    out_scale: float, sums: int = 0, clip_seg: int = 0, stats_c: int = 0) -> None:
+        """h3 stem conv (csrc/conv_h3stem.hip: 1x7x7 stride (1, 2, 2) pad (0, 3, 3),
+        Cin_p 4, K-permuted weights -- ConvLayerF32.h3stem_buffers); the
+        arguments as ``conv_h3s``."""
+        _check(self.lib.rnb_conv_h3stem_launch(ctypes.byref(params), variant, stream,
+                                               sums or None, clip_seg or None, stats_c, in_scale,
+                                               out_scale),
+               "conv_h3stem (variant %d)" % variant)
+
+    def conv_h3stem_rows(self, variant: int, Ho: int, Wo: int) -> int:
+        return int(self.lib.rnb_conv_h3stem_rows(variant, Ho, Wo))
 
     def conv_h3s_rows(self, variant: int, Ho: int, Wo: int) -> int:
         """Output rows per band of h3s variant ``variant`` (0: cannot run)."""

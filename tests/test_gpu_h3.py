@@ -421,3 +421,59 @@ def test_h3s_matches_fp64_and_stats(case):
             tol1 = 1e-6 * part.abs().sum(0) + 1e-9
             assert ((got[0] - part.sum(0)).abs() <= tol1).all(), (cid, v)
             assert torch.allclose(got[1], (part * part).sum(0), rtol=1e-6, atol=1e-9), (cid, v)
+
+
+def _h3stem_ids(layer, shape, efficient=False):
+    from rnb_amd.ops.conv_f32 import H3STEM_BASE
+    from rnb_amd.ops.native import kernels
+    if not layer.h3stem_ok(shape):
+        return []
+    return [H3STEM_BASE + i for i in range(kernels().h3stem_variants)
+            if layer.h3stem_fits(i, shape, efficient=efficient)]
+
+
+@pytest.mark.parametrize("thw,cout", [((2, 112, 112), 83), ((1, 19, 17), 72), ((2, 30, 112), 40)])
+def test_h3stem_exact_integers(thw, cout):
+    """Stem h3 kernel (csrc/conv_h3stem.hip): 1x7x7 stride 2 over a
+    3-channel input, every fitting variant bit-exact on small integers --
+    parity-split patch columns, 3-pixel padding on every side, odd frames,
+    bands clipped at the frame end, the K-permuted weight steps (7 taps + a
+    zero tap per kernel row)."""
+    layer = _layer(3, cout, (1, 7, 7), (1, 2, 2), (0, 3, 3), relu=True, integer=True)
+    x = _input(2, thw, layer.geom.cin_p, 3, integer=True)
+    ref = _ref64(layer, x).float()
+    ids = _h3stem_ids(layer, x.shape)
+    assert ids, "no stem variant fits %s" % (thw,)
+    for cid in ids:
+        y = layer.forward_hip(x, config=cid)
+        torch.cuda.synchronize()
+        assert torch.equal(y[..., :cout].cpu(), ref), cid
+        assert torch.all(y[..., cout:] == 0), cid
+
+
+def test_h3stem_matches_fp64_and_stats():
+    """The R(2+1)D-34 stem (3 -> 83, 8 x 112 x 112) within 1e-5 of fp64 on
+    every fitting variant, with the per-video BN sums of the epilogue."""
+    case = F32_CASES[0]
+    cin, cout, k, s, p, thw = case
+    assert k == (1, 7, 7) and cin == 3
+    layer = _layer(cin, cout, k, s, p)
+    x = _input(3, thw, layer.geom.cin_p, cin)
+    ref = _ref64(layer, x)
+    scale = ref.abs().max().item()
+    seg = torch.tensor([0, 1, 1], dtype=torch.int32, device=DEV)
+    ids = _h3stem_ids(layer, x.shape)
+    assert ids
+    for cid in ids:
+        sums = torch.zeros((2, 2, layer.geom.cout_p), dtype=torch.float64, device=DEV)
+        y = layer.forward_hip(x, config=cid, out_stats=(sums, seg))
+        torch.cuda.synchronize()
+        err = (y[..., :cout].double().cpu() - ref).abs().max().item()
+        assert err <= 1e-5 * scale, (cid, err, scale)
+        yd = y[..., :cout].double().cpu()
+        for v, (a, b) in enumerate([(0, 1), (1, 3)]):
+            part = yd[a:b].reshape(-1, cout)
+            got = sums[v, :, :cout].cpu()
+            tol1 = 1e-6 * part.abs().sum(0) + 1e-9
+            assert ((got[0] - part.sum(0)).abs() <= tol1).all(), (cid, v)
+            assert torch.allclose(got[1], (part * part).sum(0), rtol=1e-6, atol=1e-9), (cid, v)
