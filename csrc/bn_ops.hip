@@ -280,6 +280,32 @@ __global__ __launch_bounds__(256) void bn_seg_finalize_sums_f32_kernel(BnSegPara
   }
 }
 
+// Scale / shift (and moments) only, from the producer epilogue's sums, for a
+// BN whose running update the batched kernel takes from the same sums at the
+// end of the forward (BnRunEntry.sums): no fp64 pow, no walk over the
+// segments, no atomics and no re-arm here -- a short kernel on the path to
+// the consuming conv. Formulas as bn_seg_finalize_sums_f32_kernel.
+__global__ __launch_bounds__(256) void bn_seg_ss_from_sums_f32_kernel(BnSegParams p,
+                                                                      const double* sums,
+                                                                      int sums_c) {
+  const int s = blockIdx.y, C = p.C;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const int rows = (p.coffs[s + 1] - p.coffs[s]) * p.rpc;
+  const double* sp = sums + (size_t)s * 2 * sums_c;
+  float mu = 0.f, va = 0.f;
+  if (rows > 0) {
+    const double m = sp[c] / (double)rows;
+    mu = (float)m;
+    va = (float)fmax(sp[sums_c + c] / (double)rows - m * m, 0.0);
+  }
+  p.mean[(size_t)s * C + c] = mu;
+  p.var[(size_t)s * C + c] = va;
+  const float sc = rows > 0 ? p.gamma[c] * rsqrtf(va + p.eps) : 0.f;
+  p.ss[(size_t)s * 2 * C + c] = sc;
+  p.ss[(size_t)s * 2 * C + C + c] = rows > 0 ? p.beta[c] - mu * sc : 0.f;
+}
+
 // Finalize-from-sums and the running update in ONE kernel: thread per
 // channel walks the segments in order (the reference's per-video EMA steps,
 // exact order), the sums of 8 segments in flight at a time. One dispatch
@@ -969,6 +995,22 @@ int rnb_bn_seg_stats_from_sums_f32(double* sums, int sums_c, const int* coffs, i
   if (running_mean != nullptr && !g_bn_defer_running)
     hipLaunchKernelGGL(bn_seg_running_f32_kernel, dim3((channels + 255) / 256), dim3(256), 0,
                        stream, p);
+  return (int)hipGetLastError();
+}
+
+// scale / shift (+ moments) from the epilogue sums only; the sums stay armed
+// for the batched running update (BnRunEntry.sums), which re-arms them
+int rnb_bn_seg_ss_from_sums_f32(const double* sums, int sums_c, const int* coffs, int nseg,
+                                int rpc, int C, const float* gamma, const float* beta, float eps,
+                                float* mean, float* var, float* ss, hipStream_t stream) {
+  if (nseg <= 0 || C <= 0) return 0;
+  if (sums_c < C || rpc <= 0 || !sums) return -2;
+  BnSegParams p = {};
+  p.coffs = coffs; p.nseg = nseg; p.rpc = rpc; p.C = C; p.stride = C; p.bps = 1;
+  p.gamma = gamma; p.beta = beta; p.eps = eps;
+  p.mean = mean; p.var = var; p.ss = ss;
+  hipLaunchKernelGGL(bn_seg_ss_from_sums_f32_kernel, dim3((C + 255) / 256, nseg), dim3(256), 0,
+                     stream, p, sums, sums_c);
   return (int)hipGetLastError();
 }
 

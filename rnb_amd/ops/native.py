@@ -262,6 +262,10 @@ class Kernels:
             ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_float, ctypes.c_int, ctypes.c_longlong, ctypes.c_int, ctypes.c_int,
             ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        lib.rnb_bn_seg_ss_from_sums_f32.argtypes = [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+            ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         lib.rnb_bn_seg_set_defer_running.argtypes = [ctypes.c_int]
         lib.rnb_bn_seg_set_defer_running.restype = None
         lib.rnb_bn_seg_defers_running.argtypes = [ctypes.c_int, ctypes.c_int]
@@ -636,6 +640,14 @@ class Kernels:
                                                  ss_ptr, relu, M, C, y_stride, z_stride,
                                                  res_stride, zind_ptr or None, stream),
                "bn_seg_apply_f32")
+
+    def bn_seg_ss_from_sums_f32(self, sums_ptr, sums_c, coffs_ptr, nseg, rpc, C, gamma_ptr,
+                                beta_ptr, eps, mean_ptr, var_ptr, ss_ptr, stream):
+        """Scale / shift (+ moments) from epilogue sums, no running update and
+        no re-arm (the batched running update does both)."""
+        _check(self.lib.rnb_bn_seg_ss_from_sums_f32(sums_ptr, sums_c, coffs_ptr, nseg, rpc, C,
+                                                    gamma_ptr, beta_ptr, eps, mean_ptr, var_ptr,
+                                                    ss_ptr, stream), "bn_seg_ss_from_sums_f32")
 
     def bn_seg_apply_sums_f32(self, y_ptr, z_ptr, res_ptr, coffs_ptr, nseg, rpc, sums_ptr,
                               sums_c, gamma_ptr, beta_ptr, eps, relu, M, C, y_stride, z_stride,

@@ -21,6 +21,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 FAMILIES = (
     ("h3 temporal band", r"conv_h3t_kernel"),
     ("h3 temporal wave-specialised", r"conv_h3u_kernel"),
+    ("h3 stem", r"conv_h3stem_kernel"),
     ("h3 stride-2 row-band", r"conv_h3s_kernel"),
     ("h3 row-band 4-wave", r"conv_h3q_kernel"),
     ("h3 row-band", r"conv_h3r_kernel"),
@@ -34,7 +35,7 @@ FAMILIES = (
     ("conv direct", r"conv_f32_kernel"),
     ("bn walk+apply", r"bn_seg_walk_apply"),
     ("bn sums", r"bn_seg_sums"),
-    ("bn finalize", r"bn_seg_finalize"),
+    ("bn finalize", r"bn_seg_finalize|bn_seg_ss_from_sums"),
     ("bn running", r"bn_seg_running"),
     ("bn apply", r"bn_seg_apply"),
     ("split-K reduce", r"x6d_splitk_reduce"),

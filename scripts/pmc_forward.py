@@ -32,6 +32,7 @@ FLOP16 = 16384
 FAMILIES = (
     ("h3 temporal band", r"conv_h3t_kernel"),
     ("h3 temporal wave-specialised", r"conv_h3u_kernel"),
+    ("h3 stem", r"conv_h3stem_kernel"),
     ("h3 stride-2 row-band", r"conv_h3s_kernel"),
     ("h3 row-band 4w", r"conv_h3q_kernel"),
     ("h3 row-band", r"conv_h3r_kernel"),

@@ -381,23 +381,25 @@ def test_batched_running_update_matches_per_bn_kernels(monkeypatch):
         assert not torch.equal(v0, torch.ones_like(v0))    # updated at all
 
 
+@pytest.mark.parametrize("env", ["RNB_BN_APPLY_SUMS", "RNB_BN_SS_ONLY"])
 @pytest.mark.parametrize("n,per_video", [(40, 1), (6, 2)])
-def test_apply_from_sums_matches_finalize_path(monkeypatch, n, per_video):
+def test_apply_from_sums_matches_finalize_path(monkeypatch, n, per_video, env):
     """Block-output BatchNorms apply their scale / shift straight from the
-    producer epilogue's sums (no finalize dispatch, RNB_BN_APPLY_SUMS, default
-    on), the batched running update walking the sums afterwards: outputs
-    bit-identical to finalize + apply, running statistics equal to the
-    finalize paths' (in-order walk up to 16 videos, closed form above), the
-    epilogue sums re-armed to zero for the next call."""
+    producer epilogue's sums (no finalize dispatch, RNB_BN_APPLY_SUMS), and
+    the deferred BatchNorms' finalize computes scale / shift only
+    (RNB_BN_SS_ONLY), both defaults: the batched running update walks the sums
+    afterwards. Outputs bit-identical to the finalize paths, running
+    statistics equal to theirs (in-order walk up to 16 videos, closed form
+    above), the epilogue sums re-armed to zero for the next call."""
     from rnb_amd.models.r2p1d.model import build_network
     from rnb_amd.models.r2p1d.engine import R2P1DEngine
     g = torch.Generator().manual_seed(5)
-    x = torch.randn((n, 2, 14, 14, 256), generator=g).to(DEV)
+    x = torch.randn((n, 4, 28, 28, 128), generator=g).to(DEV)
     offs = list(range(0, n + 1, per_video))
     outs, runs = [], []
     for flag in ("0", "1"):
-        monkeypatch.setenv("RNB_BN_APPLY_SUMS", flag)
-        eng = R2P1DEngine(build_network(5, 5, depth=18, seed=2), DEV, backend="hip",
+        monkeypatch.setenv(env, flag)
+        eng = R2P1DEngine(build_network(4, 5, depth=18, seed=2), DEV, backend="hip",
                           bn_mode="batch", dtype=torch.float32)
         for _ in range(2):
             y = eng.forward(x, clip_offsets=offs)
