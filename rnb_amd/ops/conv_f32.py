@@ -157,6 +157,11 @@ H3S_PIXELS = (256, 128, 64, 128, 128)
 # H3STEM_BASE + v of rnb_conv_h3stem_launch; output pixels per block per variant
 H3STEM_BASE = 1430
 H3STEM_PIXELS = (256, 128, 448)
+# pixel-major persistent temporal h3 kernel (csrc/conv_h3p.hip conv_h3p_kernel):
+# 3x1x1 stride 1 pad (1, 0, 0) at T 8 with Cin_p <= 160 and Cout_p <= 64, the
+# h3t weights; id H3P_BASE + v launches H3P_BPC[v] persistent blocks per CU
+H3P_BASE = 1440
+H3P_BPC = (1, 2)
 # activations are split after scaling by 2^H3_IN_LOG2: fp16 lo parts stay
 # normal for |a| >= 2^-9 and inputs up to 2^10 stay in the fp16 range
 H3_IN_LOG2 = 6
@@ -168,7 +173,11 @@ def is_h3(cid: int) -> bool:
     from .native import kernels
     return ((H3D_BASE <= cid < H3D_BASE + len(kernels().h3_configs))
             or H3K_BASE <= cid < H3K_BASE + len(H3K_CONFIGS) or is_h3r(cid)
-            or is_h3t(cid) or is_h3u(cid) or is_h3s(cid) or is_h3stem(cid))
+            or is_h3t(cid) or is_h3u(cid) or is_h3s(cid) or is_h3stem(cid) or is_h3p(cid))
+
+
+def is_h3p(cid: int) -> bool:
+    return H3P_BASE <= cid < H3P_BASE + len(H3P_BPC)
 
 
 def is_h3t(cid: int) -> bool:
@@ -539,6 +548,17 @@ class ConvLayerF32:
         from .native import kernels
         return x_shape is None or kernels().conv_h3t_pixels(variant, x_shape[1]) > 0
 
+    def h3p_ok(self, x_shape=None) -> bool:
+        """The pixel-major temporal h3 kernel: h3t's conditions with T 8,
+        H * W % 16 == 0, Cin_p <= 160 and Cout_p <= 64 (its weights in LDS)."""
+        if not self.h3t_ok(x_shape) or os.environ.get("RNB_H3P", "1") == "0":
+            return False
+        from .native import kernels
+        if x_shape is None:
+            return kernels().conv_h3p_ok(8, 16, 16, self.geom.cin_p, self.geom.cout_p)
+        _, T, H, W, _ = x_shape
+        return kernels().conv_h3p_ok(T, H, W, self.geom.cin_p, self.geom.cout_p)
+
     def h3u_fits(self, variant: int, x_shape) -> bool:
         from .native import kernels
         return x_shape is None or kernels().conv_h3u_pixels(variant, x_shape[1]) > 0
@@ -613,6 +633,8 @@ class ConvLayerF32:
             if self.h3t_ok(x_shape):
                 c += [H3T_BASE + i for i in range(kernels().h3t_variants)
                       if self.h3t_fits(i, x_shape)]
+                if self.h3p_ok(x_shape):
+                    c += [H3P_BASE + i for i in range(len(H3P_BPC))]
                 if os.environ.get("RNB_H3U", "0") == "1":
                     c += [H3U_BASE + i for i in range(kernels().h3u_variants)
                           if self.h3u_fits(i, x_shape)]
@@ -923,7 +945,8 @@ class ConvLayerF32:
         """Whether config ``cid`` can apply the input's BN + ReLU on load."""
         if is_h3s(cid) or is_h3stem(cid):
             return False
-        if cid in WINO_TEMPORAL or is_h3r(cid) or is_h3t(cid) or is_h3u(cid):
+        if (cid in WINO_TEMPORAL or is_h3r(cid) or is_h3t(cid) or is_h3u(cid)
+                or is_h3p(cid)):
             return True
         if not is_h3(cid):
             return False
@@ -974,7 +997,7 @@ class ConvLayerF32:
         step = self.chunk_clips(x.shape, y.shape,
                                 residual.shape[-1] if residual is not None else 0)
         h3 = is_h3(cid)
-        h3t = is_h3t(cid) or is_h3u(cid)          # the same weight layout
+        h3t = is_h3t(cid) or is_h3u(cid) or is_h3p(cid)    # the same weight layout
         for n0 in range(0, N, step):
             p = self.params(x, y, residual, n0, min(N, n0 + step), x6=x6 and not h3, h3=h3,
                             h3t=h3t)
@@ -983,6 +1006,7 @@ class ConvLayerF32:
                 aff = ((in_affine[0].data_ptr(), in_affine[1].data_ptr() + 4 * n0)
                        if in_affine is not None else (0, 0))
                 launch, v = ((k.conv_h3u, cid - H3U_BASE) if is_h3u(cid)
+                             else (k.conv_h3p, H3P_BPC[cid - H3P_BASE]) if is_h3p(cid)
                              else (k.conv_h3t, cid - H3T_BASE))
                 if out_stats is not None:
                     launch(p, v, stream.cuda_stream, s_in, s_out,

@@ -360,6 +360,13 @@ class Kernels:
         lib.rnb_conv_h3stem_launch.restype = ctypes.c_int
         lib.rnb_conv_h3stem_rows.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         lib.rnb_conv_h3stem_rows.restype = ctypes.c_int
+        lib.rnb_conv_h3p_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                            ctypes.c_void_p, ctypes.c_void_p]
+        lib.rnb_conv_h3p_launch.restype = ctypes.c_int
+        lib.rnb_conv_h3p_ok.argtypes = [ctypes.c_int] * 5
+        lib.rnb_conv_h3p_ok.restype = ctypes.c_int
         lib.rnb_h3_set_range_flag.argtypes = [ctypes.c_void_p]
         lib.rnb_h3_set_range_flag.restype = None
         lib.rnb_conv_h3t_pixels.restype = ctypes.c_int
@@ -504,6 +511,21 @@ class Kernels:
                                                sums or None, clip_seg or None, stats_c, in_scale,
                                                out_scale),
                "conv_h3stem (variant %d)" % variant)
+
+    def conv_h3p(self, params: ConvParams, blocks_per_cu: int, stream: int, in_scale: float,
+                 out_scale: float, sums: int = 0, clip_seg: int = 0, stats_c: int = 0,
+                 in_ss: int = 0, in_seg: int = 0) -> None:
+        """Pixel-major persistent temporal h3 conv (csrc/conv_h3p.hip: 3x1x1
+        stride 1 pad (1, 0, 0), T 8, Cin_p <= 160, Cout_p <= 64, all weights
+        in LDS; ``blocks_per_cu`` persistent blocks per CU); the weights and
+        the other arguments as ``conv_h3t``."""
+        _check(self.lib.rnb_conv_h3p_launch(ctypes.byref(params), blocks_per_cu, stream,
+                                            sums or None, clip_seg or None, stats_c, in_scale,
+                                            out_scale, in_ss or None, in_seg or None),
+               "conv_h3p (%d blocks per CU)" % blocks_per_cu)
+
+    def conv_h3p_ok(self, T: int, H: int, W: int, Cin_p: int, Cout_p: int) -> bool:
+        return bool(self.lib.rnb_conv_h3p_ok(T, H, W, Cin_p, Cout_p))
 
     def conv_h3stem_rows(self, variant: int, Ho: int, Wo: int) -> int:
         return int(self.lib.rnb_conv_h3stem_rows(variant, Ho, Wo))

@@ -14,10 +14,11 @@ import sys
 
 
 def family(n):
-    return ("h3 row-band" if ("conv_h3q" in n or "conv_h3r" in n or "conv_h3s" in n) else
+    return ("h3 stem" if "conv_h3stem" in n else
+            "h3 row-band" if ("conv_h3q" in n or "conv_h3r" in n or "conv_h3s" in n) else
             "h3 temporal band" if "conv_h3t" in n else
             "h3 direct" if "conv_h3_kernel" in n else
-            "h3 stem" if "conv_h3stem" in n else
+            "h3 pixel-major temporal" if "conv_h3p_kernel" in n else
             "split-K reduce" if "splitk_reduce" in n else
             "conv_x6" if "conv_x6" in n else "wino" if "wino" in n else
             "bn" if "bn_" in n else

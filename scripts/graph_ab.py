@@ -4,6 +4,9 @@ second engine reads the first's tuning cache):
 
     python scripts/graph_ab.py --env RNB_BN_APPLY_SUMS --a 0 --b 1 --clips 128 1
 
+With ``--retune`` each side tunes its own tiles (for a switch that changes
+the candidate set, e.g. RNB_H3P).
+
 Prints per clip count the mean replay time of each side over alternating
 rounds (events around --reps replays) and the difference.
 """
@@ -23,10 +26,14 @@ def main():
     ap.add_argument("--clips", type=int, nargs="+", default=[128, 1])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--retune", action="store_true",
+                    help="tune each side separately (its own cache)")
     args = ap.parse_args()
-    os.environ.setdefault("RNB_TUNE_CACHE", os.path.join(tempfile.mkdtemp(), "tune.json"))
+    tmp = tempfile.mkdtemp()
+    os.environ.setdefault("RNB_TUNE_CACHE", os.path.join(tmp, "tune.json"))
     import torch
     from rnb_amd.models.r2p1d.model import build_engine
+    from rnb_amd.ops import tuning
     dev = torch.device("cuda:0")
     for b in args.clips:
         videos = max(1, round(b / 2.27))
@@ -37,6 +44,9 @@ def main():
         engines = {}
         for side, val in (("a", args.a), ("b", args.b)):
             os.environ[args.env] = val
+            if args.retune:
+                os.environ["RNB_TUNE_CACHE"] = os.path.join(tmp, "tune_%s_%d.json" % (side, b))
+                tuning.clear()
             g = build_engine(dev, depth=34, bn_mode="batch", dtype="fp32", max_clips=b,
                              buckets=[b], autotune=True)
             g.prepare()

@@ -33,6 +33,7 @@ FAMILIES = (
     ("h3 temporal band", r"conv_h3t_kernel"),
     ("h3 temporal wave-specialised", r"conv_h3u_kernel"),
     ("h3 stem", r"conv_h3stem_kernel"),
+    ("h3 pixel-major temporal", r"conv_h3p_kernel"),
     ("h3 stride-2 row-band", r"conv_h3s_kernel"),
     ("h3 row-band 4w", r"conv_h3q_kernel"),
     ("h3 row-band", r"conv_h3r_kernel"),

@@ -267,6 +267,20 @@ def test_h3_rowband_matches_fp64(case):
         assert err <= 1e-5 * scale, (cid, err, scale)
 
 
+def _tlayer(cin, cout, relu=True, integer=False):
+    """A 3x1x1 stride-1 temporal layer with Cin_p padded to 16 channels, as
+    the engine builds the stem's temporal conv (83 -> Cin_p 96)."""
+    from rnb_amd.ops.conv import ConvGeom
+    from rnb_amd.ops.conv_f32 import F32_ALIGN, ConvLayerF32
+    lay = _layer(cin, cout, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=relu, integer=integer)
+    if cin % 16 == 0:
+        return lay
+    geom = ConvGeom(cin=cin, cout=cout, kernel=(3, 1, 1), stride=(1, 1, 1), padding=(1, 0, 0),
+                    align=F32_ALIGN, cin_pad=(cin + 15) // 16 * 16)
+    return ConvLayerF32(lay.w_ref[:cout, :cin].cpu(), lay.b_ref.cpu(), geom, relu, DEV,
+                        "f32test16")
+
+
 def _h3t_ids():
     from rnb_amd.ops.conv_f32 import H3T_BASE
     from rnb_amd.ops.native import kernels
@@ -282,26 +296,34 @@ def _band_ids(fam, layer, shape):
         return []
     if fam == "h3t":
         return [H3T_BASE + i for i in range(kernels().h3t_variants) if layer.h3t_fits(i, shape)]
+    if fam == "h3p":
+        from rnb_amd.ops.conv_f32 import H3P_BASE, H3P_BPC
+        return [H3P_BASE + i for i in range(len(H3P_BPC))] if layer.h3p_ok(shape) else []
     return [H3U_BASE + i for i in range(kernels().h3u_variants) if layer.h3u_fits(i, shape)]
 
 
-@pytest.mark.parametrize("fam", ["h3t", "h3u"])
+@pytest.mark.parametrize("fam", ["h3t", "h3u", "h3p"])
 @pytest.mark.parametrize("thw,cin,cout", [((8, 9, 7), 80, 72), ((4, 14, 14), 64, 150),
                                           ((2, 7, 7), 144, 64), ((8, 8, 8), 48, 130),
-                                          ((8, 7, 9), 144, 64), ((2, 9, 8), 576, 256)])
+                                          ((8, 7, 9), 144, 64), ((2, 9, 8), 576, 256),
+                                          ((8, 4, 4), 144, 64), ((8, 8, 8), 83, 64),
+                                          ((8, 4, 8), 80, 48)])
 def test_h3_temporal_band_exact_integers_stats_and_affine(thw, cin, cout, fam):
-    """Temporal frame-band h3 kernels (conv_h3t_kernel, and the
-    wave-specialised conv_h3u_kernel): bit-exact on small integers (zero
-    frames at both clip ends, a partial last pixel block, Cin_p % 32 == 16:
-    the last chunk's upper half zero-padded per tap, residual + ReLU
-    epilogue) for every variant that fits T; epilogue BN sums per video vs
-    fp64 sums of the output; the input BN + ReLU on load within 1e-5 of the
-    fp64 conv of the applied input."""
-    layer = _layer(cin, cout, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=True, integer=True)
+    """Temporal h3 kernels (the frame-band conv_h3t_kernel, the
+    wave-specialised conv_h3u_kernel, the pixel-major conv_h3p_kernel):
+    bit-exact on small integers (zero frames at both clip ends, a partial
+    last pixel block, Cin_p % 32 == 16: the last chunk's upper half
+    zero-padded per tap, residual + ReLU epilogue) for every variant that
+    fits the shape; epilogue BN sums per video vs fp64 sums of the output;
+    the input BN + ReLU on load within 1e-5 of the fp64 conv of the applied
+    input."""
+    layer = _tlayer(cin, cout, relu=True, integer=True)
     x = _input(3, thw, layer.geom.cin_p, cin, integer=True)
     res = _input(3, thw, layer.geom.cout_p, cout, integer=True, seed=3)
     ref = _ref64(layer, x, res).float()
     assert layer.h3t_ok(x.shape)
+    if fam == "h3p" and thw == (8, 4, 4):
+        assert layer.h3p_ok(x.shape)
     ids = _band_ids(fam, layer, x.shape)
     if not ids:
         pytest.skip("no %s variant for T=%d" % (fam, thw[0]))
@@ -310,7 +332,7 @@ def test_h3_temporal_band_exact_integers_stats_and_affine(thw, cin, cout, fam):
         torch.cuda.synchronize()
         assert torch.equal(y[..., :cout].cpu(), ref), cid
         assert torch.all(y[..., cout:] == 0), cid
-    lay2 = _layer(cin, cout, (3, 1, 1), (1, 1, 1), (1, 0, 0), relu=False)
+    lay2 = _tlayer(cin, cout, relu=False)
     xf = _input(3, thw, lay2.geom.cin_p, cin)
     seg = torch.tensor([0, 2, 2], dtype=torch.int32, device=DEV)
     g = torch.Generator().manual_seed(11)
@@ -340,12 +362,12 @@ def test_h3_temporal_band_exact_integers_stats_and_affine(thw, cin, cout, fam):
             assert err <= 1e-5 * scale, (cid, err, scale)
 
 
-@pytest.mark.parametrize("fam", ["h3t", "h3u"])
+@pytest.mark.parametrize("fam", ["h3t", "h3u", "h3p"])
 @pytest.mark.parametrize("case", [c for c in F32_CASES if c[2] == (3, 1, 1) and c[3] == (1, 1, 1)],
                          ids=lambda c: "%dx%d" % (c[0], c[1]))
 def test_h3_temporal_band_matches_fp64(case, fam):
     cin, cout, k, s, p, thw = case
-    layer = _layer(cin, cout, k, s, p)
+    layer = _tlayer(cin, cout, relu=True)
     x = _input(2, thw, layer.geom.cin_p, cin)
     ref = _ref64(layer, x)
     scale = ref.abs().max().item()
@@ -357,6 +379,53 @@ def test_h3_temporal_band_matches_fp64(case, fam):
         torch.cuda.synchronize()
         err = (y[..., :cout].double().cpu() - ref).abs().max().item()
         assert err <= 1e-5 * scale, (cid, err, scale)
+
+
+@pytest.mark.parametrize("cin,cout", [(144, 64), (83, 64)])
+def test_h3p_many_tasks_per_wave_cross_video(monkeypatch, cin, cout):
+    """conv_h3p_kernel with a forced single block (4 waves, each a run of
+    tasks over several clips and videos: the per-wave BN sums flushed on
+    every video change, the register double buffer carried across tasks):
+    bit-exact on small integers, epilogue sums per video vs fp64 sums, and
+    the input BN on load vs the fp64 conv of the applied input."""
+    from rnb_amd.ops import conv_f32
+    monkeypatch.setattr(conv_f32, "H3P_BPC", (-1, -3))
+    layer = _tlayer(cin, cout, relu=True, integer=True)
+    n, thw = 5, (8, 12, 8)
+    x = _input(n, thw, layer.geom.cin_p, cin, integer=True)
+    res = _input(n, thw, layer.geom.cout_p, cout, integer=True, seed=3)
+    ref = _ref64(layer, x, res).float()
+    ids = _band_ids("h3p", layer, x.shape)
+    assert ids
+    for cid in ids:
+        y = layer.forward_hip(x, res, config=cid)
+        torch.cuda.synchronize()
+        assert torch.equal(y[..., :cout].cpu(), ref), cid
+    lay2 = _tlayer(cin, cout, relu=False)
+    xf = _input(n, thw, lay2.geom.cin_p, cin)
+    seg = torch.tensor([0, 0, 1, 3, 3], dtype=torch.int32, device=DEV)
+    g = torch.Generator().manual_seed(5)
+    cp = lay2.geom.cin_p
+    ss = torch.empty((4, 2, cp), dtype=torch.float32)
+    ss[:, 0] = torch.rand((4, cp), generator=g) + 0.5
+    ss[:, 1] = torch.randn((4, cp), generator=g) * 0.5
+    ss = ss.to(DEV)
+    xa = torch.relu(xf * ss[seg.long(), 0][:, None, None, None, :] +
+                    ss[seg.long(), 1][:, None, None, None, :])
+    ref_a = _ref64(lay2, xa)
+    scale = ref_a.abs().max().item()
+    for cid in ids:
+        sums = torch.zeros((4, 2, lay2.geom.cout_p), dtype=torch.float64, device=DEV)
+        ya = lay2.forward_hip(xf, config=cid, in_affine=(ss, seg), out_stats=(sums, seg))
+        torch.cuda.synchronize()
+        yd = ya[..., :cout].double().cpu()
+        err = (yd - ref_a).abs().max().item()
+        assert err <= 1e-5 * scale, (cid, err, scale)
+        for v, (a, b) in enumerate([(0, 2), (2, 3), (3, 3), (3, 5)]):
+            part = yd[a:b].reshape(-1, cout)
+            got = sums[v, :, :cout].cpu()
+            assert ((got[0] - part.sum(0)).abs() <= 1e-6 * part.abs().sum(0) + 1e-9).all(), cid
+            assert torch.allclose(got[1], (part * part).sum(0), rtol=1e-6, atol=1e-9), cid
 
 
 def _h3s_ids(layer, shape, efficient=False):
