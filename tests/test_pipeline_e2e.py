@@ -311,6 +311,36 @@ def test_conv21_fits_checks_the_clip_count():
     assert not k.conv21_fits(4, 8, 56, 57 + 64)    # too wide for the kernel
 
 
+def test_h3p_shape_contract_and_candidates():
+    """The pixel-major temporal kernel (csrc/conv_h3p.hip) is offered only for
+    the shapes it was written for: 3x1x1 stride 1 at 8 frames, H * W % 16 == 0,
+    32 < Cin_p <= 160, Cout_p <= 64 (every weight in LDS)."""
+    import torch
+    from rnb_amd.ops import native
+    if not native.available():
+        pytest.skip("native library not built")
+    from rnb_amd.ops.conv_f32 import H3P_BASE, ConvLayerF32, f32_geom, is_h3p
+    k = native.kernels()
+    assert k.conv_h3p_ok(8, 56, 56, 144, 64) and k.conv_h3p_ok(8, 56, 56, 96, 64)
+    assert not k.conv_h3p_ok(4, 56, 56, 144, 64)          # T != 8
+    assert not k.conv_h3p_ok(8, 7, 7, 144, 64)            # 49 pixels: no 16-pixel tasks
+    assert not k.conv_h3p_ok(8, 56, 56, 176, 64)          # weights past the LDS
+    assert not k.conv_h3p_ok(8, 56, 56, 144, 128)
+    assert not k.conv_h3p_ok(8, 56, 56, 32, 64)           # one chunk: not instantiated
+
+    def layer(cin, cout):
+        w = torch.randn(cout, cin, 3, 1, 1)
+        return ConvLayerF32(w, torch.zeros(cout), f32_geom(cin, cout, (3, 1, 1), (1, 1, 1),
+                                                            (1, 0, 0)), True,
+                            torch.device("cpu"), "h3p_contract")
+    lay = layer(144, 64)
+    assert lay.h3p_ok((128, 8, 56, 56, 144))
+    assert any(is_h3p(c) for c in lay.candidates((128, 8, 56, 56, 144)))
+    assert H3P_BASE in lay.candidates((2, 8, 56, 56, 144))
+    assert not lay.h3p_ok((128, 4, 28, 28, 144))
+    assert not any(is_h3p(c) for c in layer(288, 128).candidates((16, 4, 28, 28, 288)))
+
+
 def test_segments_through_batching_runner_rejoined_by_aggregator(tmp_path):
     """Segment parallelism with consumer-side batching: segments of different
     videos share a runner call; the aggregator splits the batch by the rows
