@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: the RNB_H3P_PF switch was removed after this A/B, profiles/r5_h3p_touch_prefetch_ab.txt)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
