@@ -44,8 +44,11 @@ __device__ __forceinline__ void h3p_unroll(std::integer_sequence<int, I...>, F&&
 }
 
 // NCK = ceil(Cin_p / 32) chunks per tap (compile-time: the task loop body is
-// straight-line code)
-template <int T, int TC, int NCK, bool ST, bool AFF>
+// straight-line code). A task is TP consecutive 16-pixel tiles (linear over
+// clips) x T frames; a block keeps the weights of one C_TILE-channel slice
+// (p.n_ctiles slices: blocks b, b + 8, b + 16, ... -- one XCD, one L2 -- take
+// the slices of the same pixel range, so the input is read from HBM once).
+template <int T, int TC, int TP, int NCK, bool ST, bool AFF>
 __global__ __launch_bounds__(64 * H3P_NW, 1)
 void conv_h3p_kernel(const ConvF32Params p, const X6DStats st) {
   constexpr int C_TILE = TC * 16;
@@ -60,14 +63,22 @@ void conv_h3p_kernel(const ConvF32Params p, const X6DStats st) {
   const int frow = lane & 15, fq = lane >> 4;
   const int HW = p.H * p.W;
   constexpr int nstep = 3 * NCK;
+  // block -> (pixel range r, channel slice): id = ((r / 8) * nct + slice) * 8 + r % 8
+  const int nct = p.n_ctiles;
+  const int q8 = (int)blockIdx.x >> 3;
+  const int ctile = q8 % nct;
+  const int prange = (q8 / nct) * 8 + ((int)blockIdx.x & 7);
+  const int nprange = (int)gridDim.x / nct;
+  const int c0 = ctile * C_TILE;
 
-  // every step's weights once: step s = tap * NCK + chunk, rows 0 .. C_TILE
+  // every step's weights once: step s = tap * NCK + chunk, rows c0 .. c0 + C_TILE
   {
     const x6d_u32x4 wr = x6d_rsrc(p.w, (uint32_t)(p.K_pad / 32) * (uint32_t)p.w_rows * 128u);
     const int per_step = STEP_BYTES / 1024;
     for (int ins = wave; ins < nstep * per_step; ins += H3P_NW) {
       const int s = ins / per_step, part = ins - s * per_step;
-      x6d_dma16(wr, ((uint32_t)s * (uint32_t)p.w_rows) * 128u + (uint32_t)(part * 1024 + lane * 16),
+      x6d_dma16(wr, ((uint32_t)s * (uint32_t)p.w_rows + (uint32_t)c0) * 128u +
+                        (uint32_t)(part * 1024 + lane * 16),
                 wl_lds + s * STEP_BYTES + part * 1024);
     }
     x6d_wait_vm<0>();
@@ -78,14 +89,16 @@ void conv_h3p_kernel(const ConvF32Params p, const X6DStats st) {
   }
   // the bias (scaled to the accumulator) in LDS: a global load inside the task
   // loop would make the wave wait for every prefetch load issued before it
-  for (int i = threadIdx.x; i < C_TILE; i += 64 * H3P_NW) bias_lds[i] = p.bias[i] * st.acc_scale;
+  for (int i = threadIdx.x; i < C_TILE; i += 64 * H3P_NW)
+    bias_lds[i] = p.bias[c0 + i] * st.acc_scale;
   x6d_barrier();
 
-  // this wave's tasks (16 pixels x T frames of one clip), a contiguous range
+  // this wave's tasks (TP 16-pixel tiles x T frames), a contiguous range
   const int G = HW / 16;
-  const int ntask = p.N * G;
-  const int nwave = gridDim.x * H3P_NW;
-  const int gw = blockIdx.x * H3P_NW + wave;
+  const int ntile = p.N * G;
+  const int ntask = (ntile + TP - 1) / TP;
+  const int nwave = nprange * H3P_NW;
+  const int gw = prange * H3P_NW + wave;
   const int per = (ntask + nwave - 1) / nwave;
   const int t_begin = min(gw * per, ntask), t_end = min(t_begin + per, ntask);
 
@@ -106,30 +119,38 @@ void conv_h3p_kernel(const ConvF32Params p, const X6DStats st) {
   // (with AFF, the chunk's input BN scale / shift: ssr[set][0..3] = scale
   // lo, shift lo, scale hi, shift hi, loaded with the fragments -- a load
   // issued after the prefetch and waited for before it would serialise them)
-  x6f32x4 raw[2][T][2];
-  x6f32x4 ssr[AFF ? 2 : 1][4];
+  x6f32x4 raw[2][TP][T][2];
+  x6f32x4 ssr[AFF ? 2 : 1][TP][4];
   const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(AFF ? st.in_ss : p.x), (short)0, 0x7FFFFFF0u, 0x00020000);
   auto load = [&](auto set_c, int task, int c, bool live) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_c)::value;
-    const int n = task / G, px = (task - n * G) * 16 + frow;
-    const bool hi_ok = live && c * 32 + 16 < p.Cin_p;
-    if constexpr (AFF) {
-      const int sg = h3p_sload(st.in_seg, n);
-      const uint32_t so = (uint32_t)(((sg * 2) * p.Cin_p + c * 32 + fq * 4) * 4);
-      const uint32_t hb = (uint32_t)p.Cin_p * 4u;
-      ssr[SET][0] = __builtin_amdgcn_raw_buffer_load_b128(sr, live ? so : X6D_INVALID, 0, 0);
-      ssr[SET][1] = __builtin_amdgcn_raw_buffer_load_b128(sr, live ? so + hb : X6D_INVALID, 0, 0);
-      ssr[SET][2] = __builtin_amdgcn_raw_buffer_load_b128(sr, hi_ok ? so + 64u : X6D_INVALID, 0, 0);
-      ssr[SET][3] = __builtin_amdgcn_raw_buffer_load_b128(sr, hi_ok ? so + hb + 64u : X6D_INVALID,
-                                                          0, 0);
-    }
 #pragma unroll
-    for (int f = 0; f < T; ++f) {
-      const uint32_t o = (uint32_t)((((n * T + f) * HW + px) * p.Cin_p + c * 32 + fq * 4) * 4);
-      raw[SET][f][0] = __builtin_amdgcn_raw_buffer_load_b128(xr, live ? o : X6D_INVALID, 0, 0);
-      raw[SET][f][1] = __builtin_amdgcn_raw_buffer_load_b128(xr, hi_ok ? o + 64u : X6D_INVALID,
-                                                              0, 0);
+    for (int tp = 0; tp < TP; ++tp) {
+      const int g = task * TP + tp;
+      const bool ok = live && g < ntile;
+      const int gc = ok ? g : 0;
+      const int n = gc / G, px = (gc - n * G) * 16 + frow;
+      const bool hi_ok = ok && c * 32 + 16 < p.Cin_p;
+      if constexpr (AFF) {
+        const int sg = h3p_sload(st.in_seg, n);
+        const uint32_t so = (uint32_t)(((sg * 2) * p.Cin_p + c * 32 + fq * 4) * 4);
+        const uint32_t hb = (uint32_t)p.Cin_p * 4u;
+        ssr[SET][tp][0] = __builtin_amdgcn_raw_buffer_load_b128(sr, ok ? so : X6D_INVALID, 0, 0);
+        ssr[SET][tp][1] =
+            __builtin_amdgcn_raw_buffer_load_b128(sr, ok ? so + hb : X6D_INVALID, 0, 0);
+        ssr[SET][tp][2] =
+            __builtin_amdgcn_raw_buffer_load_b128(sr, hi_ok ? so + 64u : X6D_INVALID, 0, 0);
+        ssr[SET][tp][3] =
+            __builtin_amdgcn_raw_buffer_load_b128(sr, hi_ok ? so + hb + 64u : X6D_INVALID, 0, 0);
+      }
+#pragma unroll
+      for (int f = 0; f < T; ++f) {
+        const uint32_t o = (uint32_t)((((n * T + f) * HW + px) * p.Cin_p + c * 32 + fq * 4) * 4);
+        raw[SET][tp][f][0] = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? o : X6D_INVALID, 0, 0);
+        raw[SET][tp][f][1] =
+            __builtin_amdgcn_raw_buffer_load_b128(xr, hi_ok ? o + 64u : X6D_INVALID, 0, 0);
+      }
     }
   };
 
@@ -141,9 +162,9 @@ void conv_h3p_kernel(const ConvF32Params p, const X6DStats st) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (acc_seg >= 0) {
         for (int i = lane; i < C_TILE; i += 64) {
-          if (i < p.Cout_p) {
-            atomicAdd(st.sums + ((size_t)acc_seg * 2) * st.stats_c + i, red[wave][0][i]);
-            atomicAdd(st.sums + ((size_t)acc_seg * 2 + 1) * st.stats_c + i, red[wave][1][i]);
+          if (c0 + i < p.Cout_p) {
+            atomicAdd(st.sums + ((size_t)acc_seg * 2) * st.stats_c + c0 + i, red[wave][0][i]);
+            atomicAdd(st.sums + ((size_t)acc_seg * 2 + 1) * st.stats_c + c0 + i, red[wave][1][i]);
           }
           red[wave][0][i] = 0.0;
           red[wave][1][i] = 0.0;
@@ -152,7 +173,7 @@ void conv_h3p_kernel(const ConvF32Params p, const X6DStats st) {
     }
   };
 
-  x6f32x4 acc[T][TC];
+  x6f32x4 acc[TP][T][TC];
   // chunk C of ``task`` on register set SET (compile-time: a runtime index
   // into the raw[] sets would put them in scratch), after issuing the next
   // chunk's loads -- this task's chunk C + 1, or chunk 0 of the wave's next
@@ -172,25 +193,28 @@ void conv_h3p_kernel(const ConvF32Params p, const X6DStats st) {
     // them next to their first use to save registers)
     __builtin_amdgcn_sched_barrier(0);
     // BN + ReLU of the input on load, scale, split
-    H3B bf[T];
+    H3B bf[TP][T];
 #pragma unroll
-    for (int f = 0; f < T; ++f) {
-      x6f32x4 a0 = raw[SET][f][0], a1 = raw[SET][f][1];
-      if constexpr (AFF) {
+    for (int tp = 0; tp < TP; ++tp) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          a0[j] = fmaxf(fmaf(a0[j], ssr[SET][0][j], ssr[SET][1][j]), 0.f) * in_scale;
-          a1[j] = fmaxf(fmaf(a1[j], ssr[SET][2][j], ssr[SET][3][j]), 0.f) * in_scale;
+      for (int f = 0; f < T; ++f) {
+        x6f32x4 a0 = raw[SET][tp][f][0], a1 = raw[SET][tp][f][1];
+        if constexpr (AFF) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            a0[j] = fmaxf(fmaf(a0[j], ssr[SET][tp][0][j], ssr[SET][tp][1][j]), 0.f) * in_scale;
+            a1[j] = fmaxf(fmaf(a1[j], ssr[SET][tp][2][j], ssr[SET][tp][3][j]), 0.f) * in_scale;
+          }
+        } else {
+          a0 *= in_scale;
+          a1 *= in_scale;
         }
-      } else {
-        a0 *= in_scale;
-        a1 *= in_scale;
+        uint32_t h[4], l[4];
+        h3_split4(a0, h, l);
+        h3_split4(a1, h + 2, l + 2);
+        bf[tp][f].h = (wu32x4){h[0], h[1], h[2], h[3]};
+        bf[tp][f].l = (wu32x4){l[0], l[1], l[2], l[3]};
       }
-      uint32_t h[4], l[4];
-      h3_split4(a0, h, l);
-      h3_split4(a1, h + 2, l + 2);
-      bf[f].h = (wu32x4){h[0], h[1], h[2], h[3]};
-      bf[f].l = (wu32x4){l[0], l[1], l[2], l[3]};
     }
 #pragma unroll
     for (int tc = 0; tc < TC; ++tc) {
@@ -202,14 +226,17 @@ void conv_h3p_kernel(const ConvF32Params p, const X6DStats st) {
         al[k] = *(const wu32x4*)(wrow + w_ll);
       }
 #pragma unroll
-      for (int f = 0; f < T; ++f) {
+      for (int tp = 0; tp < TP; ++tp) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const int t = f - k + 1;                        // output frame fed by tap k
-          if (t < 0 || t >= T) continue;
-          acc[t][tc] = h3_mma(al[k], bf[f].h, acc[t][tc]);
-          acc[t][tc] = h3_mma(ah[k], bf[f].l, acc[t][tc]);
-          acc[t][tc] = h3_mma(ah[k], bf[f].h, acc[t][tc]);
+        for (int f = 0; f < T; ++f) {
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const int t = f - k + 1;                      // output frame fed by tap k
+            if (t < 0 || t >= T) continue;
+            acc[tp][t][tc] = h3_mma(al[k], bf[tp][f].h, acc[tp][t][tc]);
+            acc[tp][t][tc] = h3_mma(ah[k], bf[tp][f].l, acc[tp][t][tc]);
+            acc[tp][t][tc] = h3_mma(ah[k], bf[tp][f].h, acc[tp][t][tc]);
+          }
         }
       }
     }
@@ -223,54 +250,60 @@ void conv_h3p_kernel(const ConvF32Params p, const X6DStats st) {
     // stores would push the vmcnt past its 63 limit and the compiler's wait
     // would then cover most of the stores as well
     __builtin_amdgcn_s_waitcnt(0x0F70);                 // vmcnt(0)
-    const int n = task / G, px = (task - n * G) * 16 + frow;
-    if constexpr (ST) {
-      const int sg = h3p_sload(st.clip_seg, n);
-      if (sg != acc_seg) {
-        flush();
-        acc_seg = sg;
+#pragma unroll
+    for (int tp = 0; tp < TP; ++tp) {
+      const int g = task * TP + tp;
+      const bool gok = g < ntile;
+      const int gc = gok ? g : 0;
+      const int n = gc / G, px = (gc - n * G) * 16 + frow;
+      if constexpr (ST) {
+        const int sg = h3p_sload(st.clip_seg, n);
+        if (gok && sg != acc_seg) {
+          flush();
+          acc_seg = sg;
+        }
       }
-    }
 #pragma unroll
-    for (int tc = 0; tc < TC; ++tc) {
-      const int cl = tc * 16 + 4 * fq;
-      const bool cok = cl < p.Cout_p;
-      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int tc = 0; tc < TC; ++tc) {
+        const int cl = tc * 16 + 4 * fq;
+        const bool cok = gok && c0 + cl < p.Cout_p;
+        float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int t = 0; t < T; ++t) {
-        const int m = (n * T + t) * HW + px;
-        x6f32x4 v = acc[t][tc] * out_scale;
-        if (has_res) {
-          const x6f32x4 r = __builtin_amdgcn_raw_buffer_load_b128(
-              rr, cok ? (uint32_t)(m * p.res_stride + cl) * 4u : X6D_INVALID, 0, 0);
-          v += r;
-        }
-        if (st.oflag != nullptr && cok) bad |= x6d_nonfinite(v);
-        if (p.relu) {
+        for (int t = 0; t < T; ++t) {
+          const int m = (n * T + t) * HW + px;
+          x6f32x4 v = acc[tp][t][tc] * out_scale;
+          if (has_res) {
+            const x6f32x4 r = __builtin_amdgcn_raw_buffer_load_b128(
+                rr, cok ? (uint32_t)(m * p.res_stride + c0 + cl) * 4u : X6D_INVALID, 0, 0);
+            v += r;
+          }
+          if (st.oflag != nullptr && cok) bad |= x6d_nonfinite(v);
+          if (p.relu) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(
-            v, yr, cok ? (uint32_t)(m * p.y_stride + cl) * 4u : X6D_INVALID, 0, 0);
-        if (ST && cok) {
+            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(
+              v, yr, cok ? (uint32_t)(m * p.y_stride + c0 + cl) * 4u : X6D_INVALID, 0, 0);
+          if (ST && cok) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            s1[j] += v[j];
-            s2[j] = fmaf(v[j], v[j], s2[j]);
+            for (int j = 0; j < 4; ++j) {
+              s1[j] += v[j];
+              s2[j] = fmaf(v[j], v[j], s2[j]);
+            }
           }
         }
-      }
-      if constexpr (ST) {
+        if constexpr (ST) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          s1[j] = x6d_row16_sum(s1[j]);
-          s2[j] = x6d_row16_sum(s2[j]);
-        }
-        if (frow == 0 && cok) {
+          for (int j = 0; j < 4; ++j) {
+            s1[j] = x6d_row16_sum(s1[j]);
+            s2[j] = x6d_row16_sum(s2[j]);
+          }
+          if (frow == 0 && cok) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {             // this wave's region only: no atomics
-            red[wave][0][cl + j] += (double)s1[j];
-            red[wave][1][cl + j] += (double)s2[j];
+            for (int j = 0; j < 4; ++j) {           // this wave's region only: no atomics
+              red[wave][0][cl + j] += (double)s1[j];
+              red[wave][1][cl + j] += (double)s2[j];
+            }
           }
         }
       }
@@ -284,7 +317,9 @@ void conv_h3p_kernel(const ConvF32Params p, const X6DStats st) {
     for (int b = 0; b < TC; ++b) {
       const x6f32x4 bv = *(const x6f32x4*)(bias_lds + b * 16 + 4 * fq);
 #pragma unroll
-      for (int a = 0; a < T; ++a) acc[a][b] = bv;
+      for (int tp = 0; tp < TP; ++tp)
+#pragma unroll
+        for (int a = 0; a < T; ++a) acc[tp][a][b] = bv;
     }
     h3p_unroll(std::make_integer_sequence<int, NCK>(), [&](auto c_c) __attribute__((always_inline)) {
       constexpr int C = decltype(c_c)::value;
@@ -301,7 +336,7 @@ void conv_h3p_kernel(const ConvF32Params p, const X6DStats st) {
     // the loop's vector-memory shape on entry too: T * TC stores that store
     // nothing after the first loads (see ``chunk``)
 #pragma unroll
-    for (int i = 0; i < T * TC; ++i)
+    for (int i = 0; i < TP * T * TC; ++i)
       __builtin_amdgcn_raw_buffer_store_b128((x6f32x4){0.f, 0.f, 0.f, 0.f}, yr, X6D_INVALID, 0, 0);
   }
   // an odd chunk count flips the set parity from one task to the next
@@ -336,11 +371,17 @@ static int h3p_num_cus() {
 extern "C" {
 
 // whether the pixel-major kernel can run this layer: 3x1x1 stride 1 pad
-// (1, 0, 0), T == 8, Cout_p <= 64, 32 < Cin_p <= 160 (every weight in LDS),
-// H W a multiple of 16
+// (1, 0, 0), H W a multiple of 16, and one of the two instantiated forms
+// (every weight of the block's channel slice in LDS):
+//   T == 8, 32 < Cin_p <= 160, Cout_p <= 64 (conv2 / stem temporal: one
+//   64-channel slice, 1 tile per task);
+//   T == 4, 256 < Cin_p <= 288, Cout_p % 32 == 0, Cout_p <= 256 (conv3
+//   temporal: 32-channel slices, 2 tiles per task)
 int rnb_conv_h3p_ok(int T, int H, int W, int Cin_p, int Cout_p) {
-  return T == 8 && (H * W) % 16 == 0 && Cin_p % 16 == 0 && Cin_p > 32 &&
-         Cin_p <= 32 * H3P_NCK_MAX && Cout_p <= 64 && Cout_p % 4 == 0;
+  if ((H * W) % 16 != 0 || Cin_p % 16 != 0 || Cout_p % 4 != 0) return 0;
+  if (T == 8) return Cin_p > 32 && Cin_p <= 32 * H3P_NCK_MAX && Cout_p <= 64;
+  if (T == 4) return Cin_p > 256 && Cin_p <= 288 && Cout_p % 32 == 0 && Cout_p <= 256;
+  return 0;
 }
 
 int rnb_conv_h3p_launch(const ConvF32Params* pp, int blocks_per_cu, hipStream_t stream,
@@ -360,17 +401,26 @@ int rnb_conv_h3p_launch(const ConvF32Params* pp, int blocks_per_cu, hipStream_t 
   const long long xb = (long long)p.N * p.T * p.H * p.W * p.Cin_p * 4;
   if (xb > 0x7FFFFF00LL || (long long)p.M * p.y_stride * 4 > 0x7FFFFF00LL) return -5;
   if (p.res && (long long)p.M * p.res_stride * 4 > 0x7FFFFF00LL) return -6;
-  if (p.w_rows < 64 || (long long)(p.K_pad / 32) * p.w_rows * 128 > 0x7FFFFF00LL) return -11;
+  const bool t8 = p.T == 8;
+  const int c_tile = t8 ? 64 : 32, tp = t8 ? 1 : 2;
+  const int nct = t8 ? 1 : p.Cout_p / 32;
+  if (p.w_rows < nct * c_tile || (long long)(p.K_pad / 32) * p.w_rows * 128 > 0x7FFFFF00LL)
+    return -11;
   if (!(in_scale > 0.f) || !(out_scale > 0.f)) return -15;
   if (in_ss && !in_seg) return -16;
   if (sums && (!clip_seg || stats_c < p.Cout_p)) return -12;
   p.x_bytes = (uint32_t)xb;
+  p.n_ctiles = nct;
   const int cus = h3p_num_cus();
-  const long long ntask = (long long)p.N * (p.H * p.W / 16);
-  // blocks_per_cu < 0: exactly -blocks_per_cu blocks (tests: many tasks per wave)
-  const long long blocks = min(blocks_per_cu < 0 ? (long long)-blocks_per_cu
-                                                 : (long long)cus * max(blocks_per_cu, 1),
-                               (ntask + H3P_NW - 1) / H3P_NW);
+  const long long ntask = ((long long)p.N * (p.H * p.W / 16) + tp - 1) / tp;
+  // pixel ranges (blocks per channel slice); with several slices a multiple
+  // of 8 (the block -> (range, slice) map keeps a range's slices on one XCD).
+  // blocks_per_cu < 0: exactly -blocks_per_cu ranges (tests: many tasks per wave)
+  long long nr = blocks_per_cu < 0 ? (long long)-blocks_per_cu
+                                   : (long long)cus * max(blocks_per_cu, 1) / nct;
+  nr = max(1LL, min(nr, (ntask + H3P_NW - 1) / H3P_NW));
+  if (nct > 1) nr = (nr + 7) / 8 * 8;
+  const long long blocks = nr * nct;
   X6DStats st;
   st.sums = sums;
   st.clip_seg = clip_seg;
@@ -384,13 +434,17 @@ int rnb_conv_h3p_launch(const ConvF32Params* pp, int blocks_per_cu, hipStream_t 
   st.in_seg = in_seg;
   st.oflag = rnb_h3_range_flag();
   using KFn = void (*)(const ConvF32Params, const X6DStats);
-  static const KFn kTab[4][2][2] = {
-#define H3P_K(N) {{conv_h3p_kernel<8, 4, N, false, false>, conv_h3p_kernel<8, 4, N, false, true>}, \
-                  {conv_h3p_kernel<8, 4, N, true, false>, conv_h3p_kernel<8, 4, N, true, true>}}
+  static const KFn kTab8[4][2][2] = {
+#define H3P_K(N) {{conv_h3p_kernel<8, 4, 1, N, false, false>, conv_h3p_kernel<8, 4, 1, N, false, true>}, \
+                  {conv_h3p_kernel<8, 4, 1, N, true, false>, conv_h3p_kernel<8, 4, 1, N, true, true>}}
       H3P_K(2), H3P_K(3), H3P_K(4), H3P_K(5)
 #undef H3P_K
   };
-  const KFn k = kTab[nck - 2][sums != nullptr][in_ss != nullptr];
+  static const KFn kTab4[2][2] = {
+      {conv_h3p_kernel<4, 2, 2, 9, false, false>, conv_h3p_kernel<4, 2, 2, 9, false, true>},
+      {conv_h3p_kernel<4, 2, 2, 9, true, false>, conv_h3p_kernel<4, 2, 2, 9, true, true>}};
+  const KFn k = t8 ? kTab8[nck - 2][sums != nullptr][in_ss != nullptr]
+                   : kTab4[sums != nullptr][in_ss != nullptr];
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * H3P_NW), 0, stream, p, st);
   return (int)hipGetLastError();
 }

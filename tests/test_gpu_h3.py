@@ -307,7 +307,8 @@ def _band_ids(fam, layer, shape):
                                           ((2, 7, 7), 144, 64), ((8, 8, 8), 48, 130),
                                           ((8, 7, 9), 144, 64), ((2, 9, 8), 576, 256),
                                           ((8, 4, 4), 144, 64), ((8, 8, 8), 83, 64),
-                                          ((8, 4, 8), 80, 48)])
+                                          ((8, 4, 8), 80, 48), ((4, 4, 8), 288, 128),
+                                          ((4, 4, 4), 288, 64)])
 def test_h3_temporal_band_exact_integers_stats_and_affine(thw, cin, cout, fam):
     """Temporal h3 kernels (the frame-band conv_h3t_kernel, the
     wave-specialised conv_h3u_kernel, the pixel-major conv_h3p_kernel):
@@ -381,17 +382,20 @@ def test_h3_temporal_band_matches_fp64(case, fam):
         assert err <= 1e-5 * scale, (cid, err, scale)
 
 
-@pytest.mark.parametrize("cin,cout", [(144, 64), (83, 64)])
-def test_h3p_many_tasks_per_wave_cross_video(monkeypatch, cin, cout):
-    """conv_h3p_kernel with a forced single block (4 waves, each a run of
-    tasks over several clips and videos: the per-wave BN sums flushed on
-    every video change, the register double buffer carried across tasks):
-    bit-exact on small integers, epilogue sums per video vs fp64 sums, and
-    the input BN on load vs the fp64 conv of the applied input."""
+@pytest.mark.parametrize("cin,cout,thw", [(144, 64, (8, 12, 8)), (83, 64, (8, 12, 8)),
+                                          (288, 128, (4, 12, 12))])
+def test_h3p_many_tasks_per_wave_cross_video(monkeypatch, cin, cout, thw):
+    """conv_h3p_kernel with a forced single pixel range (4 waves per channel
+    slice, each a run of tasks over several clips and videos: the per-wave
+    BN sums flushed on every video change, the register double buffer
+    carried across tasks; the T = 4 form's 2-tile tasks straddle clips, 9
+    tiles per clip, and its last task is half empty): bit-exact on small
+    integers, epilogue sums per video vs fp64 sums, and the input BN on load
+    vs the fp64 conv of the applied input."""
     from rnb_amd.ops import conv_f32
     monkeypatch.setattr(conv_f32, "H3P_BPC", (-1, -3))
     layer = _tlayer(cin, cout, relu=True, integer=True)
-    n, thw = 5, (8, 12, 8)
+    n = 5
     x = _input(n, thw, layer.geom.cin_p, cin, integer=True)
     res = _input(n, thw, layer.geom.cout_p, cout, integer=True, seed=3)
     ref = _ref64(layer, x, res).float()

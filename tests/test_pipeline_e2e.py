@@ -313,8 +313,9 @@ def test_conv21_fits_checks_the_clip_count():
 
 def test_h3p_shape_contract_and_candidates():
     """The pixel-major temporal kernel (csrc/conv_h3p.hip) is offered only for
-    the shapes it was written for: 3x1x1 stride 1 at 8 frames, H * W % 16 == 0,
-    32 < Cin_p <= 160, Cout_p <= 64 (every weight in LDS)."""
+    the shapes it was written for: 3x1x1 stride 1, H * W % 16 == 0, and 8
+    frames with 32 < Cin_p <= 160, Cout_p <= 64, or 4 frames with 256 < Cin_p
+    <= 288 and 32-channel output slices (every weight of a slice in LDS)."""
     import torch
     from rnb_amd.ops import native
     if not native.available():
@@ -327,6 +328,9 @@ def test_h3p_shape_contract_and_candidates():
     assert not k.conv_h3p_ok(8, 56, 56, 176, 64)          # weights past the LDS
     assert not k.conv_h3p_ok(8, 56, 56, 144, 128)
     assert not k.conv_h3p_ok(8, 56, 56, 32, 64)           # one chunk: not instantiated
+    assert k.conv_h3p_ok(4, 28, 28, 288, 128) and k.conv_h3p_ok(4, 28, 28, 288, 256)
+    assert not k.conv_h3p_ok(4, 28, 28, 288, 144)         # not whole 32-channel slices
+    assert not k.conv_h3p_ok(2, 14, 14, 576, 256)
 
     def layer(cin, cout):
         w = torch.randn(cout, cin, 3, 1, 1)
@@ -338,7 +342,8 @@ def test_h3p_shape_contract_and_candidates():
     assert any(is_h3p(c) for c in lay.candidates((128, 8, 56, 56, 144)))
     assert H3P_BASE in lay.candidates((2, 8, 56, 56, 144))
     assert not lay.h3p_ok((128, 4, 28, 28, 144))
-    assert not any(is_h3p(c) for c in layer(288, 128).candidates((16, 4, 28, 28, 288)))
+    assert any(is_h3p(c) for c in layer(288, 128).candidates((16, 4, 28, 28, 288)))
+    assert not any(is_h3p(c) for c in layer(576, 256).candidates((16, 2, 14, 14, 576)))
 
 
 def test_segments_through_batching_runner_rejoined_by_aggregator(tmp_path):
