@@ -63,12 +63,13 @@ void conv_h3p_kernel(const ConvF32Params p, const X6DStats st) {
   const int frow = lane & 15, fq = lane >> 4;
   const int HW = p.H * p.W;
   constexpr int nstep = 3 * NCK;
-  // block -> (pixel range r, channel slice): id = ((r / 8) * nct + slice) * 8 + r % 8
+  // block -> (pixel range r, channel slice): id = ((r / 8) * nct + slice) * 8 + r % 8;
+  // st.ksplit (unused otherwise) = the number of pixel ranges, blocks past it idle
   const int nct = p.n_ctiles;
   const int q8 = (int)blockIdx.x >> 3;
   const int ctile = q8 % nct;
   const int prange = (q8 / nct) * 8 + ((int)blockIdx.x & 7);
-  const int nprange = (int)gridDim.x / nct;
+  const int nprange = st.ksplit;
   const int c0 = ctile * C_TILE;
 
   // every step's weights once: step s = tap * NCK + chunk, rows c0 .. c0 + C_TILE
@@ -100,7 +101,8 @@ void conv_h3p_kernel(const ConvF32Params p, const X6DStats st) {
   const int nwave = nprange * H3P_NW;
   const int gw = prange * H3P_NW + wave;
   const int per = (ntask + nwave - 1) / nwave;
-  const int t_begin = min(gw * per, ntask), t_end = min(t_begin + per, ntask);
+  const int t_begin = prange < nprange ? min(gw * per, ntask) : ntask;
+  const int t_end = min(t_begin + per, ntask);
 
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
@@ -419,13 +421,13 @@ int rnb_conv_h3p_launch(const ConvF32Params* pp, int blocks_per_cu, hipStream_t 
   long long nr = blocks_per_cu < 0 ? (long long)-blocks_per_cu
                                    : (long long)cus * max(blocks_per_cu, 1) / nct;
   nr = max(1LL, min(nr, (ntask + H3P_NW - 1) / H3P_NW));
-  if (nct > 1) nr = (nr + 7) / 8 * 8;
-  const long long blocks = nr * nct;
+  // the grid covers whole groups of 8 ranges when there are several slices
+  const long long blocks = (nct > 1 ? (nr + 7) / 8 * 8 : nr) * nct;
   X6DStats st;
   st.sums = sums;
   st.clip_seg = clip_seg;
   st.stats_c = stats_c;
-  st.ksplit = 1;
+  st.ksplit = (int)nr;                         // pixel ranges (see the kernel)
   st.ws = nullptr;
   st.in_scale = in_scale;
   st.out_scale = out_scale;
