@@ -16,6 +16,19 @@ static __device__ __forceinline__ x6f32x4 h3_mma(const wu32x4& a, const wu32x4& 
                                                 __builtin_bit_cast(h3f16x8, b), c, 0, 0, 0);
 }
 
+// the first 16-channel sub-step only (a K step whose second sub-step is past
+// Cin_p): v_mfma_f32_16x16x16_f16 on the low halves (A0, B0) of the paired
+// fragments -- lane quad q supplies channels 4q .. 4q+3 either way -- at
+// half the matrix-core time of the 32-deep form
+typedef _Float16 h3f16x4 __attribute__((ext_vector_type(4)));
+static __device__ __forceinline__ x6f32x4 h3_mma_k16(const wu32x4& a, const wu32x4& b,
+                                                     const x6f32x4& c) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 a0 = (u32x2){a[0], a[1]}, b0 = (u32x2){b[0], b[1]};
+  return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h3f16x4, a0),
+                                               __builtin_bit_cast(h3f16x4, b0), c, 0, 0, 0);
+}
+
 // a - h exactly, h the low (HI = 0) or high half of a packed fp16 pair (one
 // v_fma_mix_f32: the fp16 operand is widened exactly, a single rounding of
 // an exactly representable difference)
