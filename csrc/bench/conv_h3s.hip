@@ -23,9 +23,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "x6d_common.h"
+#include "../x6d_common.h"
 
-#include "h3_common.h"
+#include "../h3_common.h"
 
 extern "C" int* rnb_h3_range_flag();
 

@@ -34,9 +34,9 @@
 
 #include <type_traits>
 
-#include "x6d_common.h"
+#include "../x6d_common.h"
 
-#include "h3_common.h"
+#include "../h3_common.h"
 
 template <int NM, int NS, int TP, int TC, int HALO, int D, bool ST, bool AFF>
 __global__ __launch_bounds__(64 * (NM + NS), 1)

@@ -769,12 +769,6 @@ void conv_h3q_kernel(const ConvF32Params p, const X6DStats st) {
 // (the host pads each tap's weights to 32-channel chunks).
 // WB = weight buffers: 2 = the next chunk's weights DMA'd during this
 // chunk's MFMAs; 1 = after them (smaller LDS: two blocks per CU cover it).
-// H3T_EXP (experiment builds, csrc/bench/h3t_exp.hip; 0 in the product):
-// 1 = no MFMAs, 2 = no activation loads, 3 = no split / patch stores,
-// 4 = activation loads only (neither split nor MFMAs).
-#ifndef H3T_EXP
-#define H3T_EXP 0
-#endif
 template <int NW, int TP, int TC, int HALO, int WB, int MINB, bool ST, bool AFF>
 __global__ __launch_bounds__(64 * NW, MINB)
 void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
@@ -844,23 +838,12 @@ void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
       const uint32_t o = src[i] == X6D_INVALID ? X6D_INVALID : src[i] + (uint32_t)(c * 128);
-      if constexpr (H3T_EXP == 2) {
-        const float f = (float)(o & 1023) * 1e-3f;
-        raw0[i] = (x6f32x4){f, f, f, f};
-        raw1[i] = raw0[i];
-        continue;
-      }
       raw0[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0);
       raw1[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, (o == X6D_INVALID || !hi_ok) ? X6D_INVALID
                                                                                   : o + 64u, 0, 0);
     }
   };
   auto store_chunk = [&](int c) {
-    if constexpr (H3T_EXP == 3 || H3T_EXP == 4) {     // consume the loads, store nothing
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i) asm volatile("" ::"v"(raw0[i]), "v"(raw1[i]));
-      return;
-    }
     x6f32x4 sc0, sh0, sc1, sh1;
     if constexpr (AFF) {
       const bool hi_ok = c * 32 + 16 < p.Cin_p;
@@ -888,11 +871,7 @@ void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
       }
       uint32_t h[4], l[4];
       h3_split4(a0, h, l);
-      if (MINB != 2 || hi_ok) {          // (HALF_OK below)
-        h3_split4(a1, h + 2, l + 2);
-      } else {
-        h[2] = h[3] = l[2] = l[3] = 0u;
-      }
+      h3_split4(a1, h + 2, l + 2);
       char* base = lds + dst[i];
       *(wu32x4*)(base + (x6r_swz(2 * qd, e) << 4)) = (wu32x4){h[0], h[1], h[2], h[3]};
       *(wu32x4*)(base + (x6r_swz(2 * qd + 1, e) << 4)) = (wu32x4){l[0], l[1], l[2], l[3]};
@@ -930,11 +909,9 @@ void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
     al = *(const wu32x4*)(wrow + w_ll);
   };
 
-  // the chunk's 3 taps x TC channel tiles (weight buffer buf); HALF: 16
-  // channels (h3_mma_k16)
+  // the chunk's 3 taps x TC channel tiles (weight buffer buf)
   int buf = 0;
-  auto taps = [&](auto half_c) {
-    constexpr bool HALF = decltype(half_c)::value;
+  auto taps = [&]() {
     H3B bf[2][TP];
     wu32x4 wh[2], wl[2];
 #pragma unroll
@@ -954,33 +931,16 @@ void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
             if (tp * TC / TP == tc && tp < TP) rd_bf(bf[(k + 1) & 1][tp], k + 1, tp);
         }
         const H3B (&b)[TP] = bf[k & 1];
-        if constexpr (H3T_EXP != 1 && H3T_EXP != 4) {
-          if constexpr (HALF) {
 #pragma unroll
-            for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma_k16(wl[cs], b[tp].h, acc[tp][tc]);
+        for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(wl[cs], b[tp].h, acc[tp][tc]);
 #pragma unroll
-            for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma_k16(wh[cs], b[tp].l, acc[tp][tc]);
+        for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(wh[cs], b[tp].l, acc[tp][tc]);
 #pragma unroll
-            for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma_k16(wh[cs], b[tp].h, acc[tp][tc]);
-          } else {
-#pragma unroll
-            for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(wl[cs], b[tp].h, acc[tp][tc]);
-#pragma unroll
-            for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(wh[cs], b[tp].l, acc[tp][tc]);
-#pragma unroll
-            for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(wh[cs], b[tp].h, acc[tp][tc]);
-          }
-        }
+        for (int tp = 0; tp < TP; ++tp) acc[tp][tc] = h3_mma(wh[cs], b[tp].h, acc[tp][tc]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
   };
-  // Cin_p % 32 == 16: the last chunk's taps run after the loop, on 16 channels
-  // (peeled: no loads in flight there, and one copy of each body). The
-  // one-block-per-CU forms keep the full-chunk path: the second body spills
-  // there (6 staging items per lane)
-  constexpr bool HALF_OK = MINB == 2;
-  const bool half_last = HALF_OK && (p.Cin_p & 31) == 16;
   issue_w(0, 0);
   load_chunk(0);
   for (int c = 0; c < nck; ++c) {
@@ -994,11 +954,7 @@ void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
       load_chunk(c + 1);
     }
     buf = WB == 2 ? (c & 1) : 0;
-    if (c + 1 == nck && half_last) break;
-    taps(std::integral_constant<bool, false>());
-  }
-  if constexpr (HALF_OK) {
-    if (half_last) taps(std::integral_constant<bool, true>());
+    taps();
   }
 
   // ---- epilogue: rows (frame, pixel) of clip n, one video (ST) ----

@@ -28,11 +28,20 @@ LIBRARIES = {
     "librnb_kernels.so": (["conv_igemm.hip", "conv_halo.hip", "conv_temporal.hip",
                            "video_ops.hip", "bn_ops.hip", "conv_halo_ws.hip", "conv21.hip",
                            "conv_f32.hip", "conv_wino_f32.hip", "conv_wino_x6.hip",
-                           "conv_x6.hip", "conv_h3.hip", "conv_h3u.hip", "conv_h3s.hip", "conv_h3stem.hip",
-                           "conv_h3p.hip"], [], []),
+                           "conv_x6.hip", "conv_h3.hip", "conv_h3stem.hip", "conv_h3p.hip"],
+                          [], []),
     "librnb_runtime.so": (["runtime.cpp"], [], []),
     "librnb_tracer.so": (["tracer.cpp"], [], ["-L%s/lib" % ROCM, "-lrocprofiler-sdk",
                                                "-Wl,-rpath,%s/lib" % ROCM]),
+}
+
+# experiment kernels measured slower than the autotune set (profiles/NOTES.md
+# round 5: the wave-specialised temporal conv_h3u and the stride-2 row-band
+# conv_h3s), kept out of the product library: ``--exp`` builds them into
+# rnb_amd/_native/exp/, where ops/native.py picks them up if present (their
+# launches then resolve the range flag from librnb_kernels.so)
+EXP_LIBRARIES = {
+    "exp/librnb_h3exp.so": (["bench/conv_h3u.hip", "bench/conv_h3s.hip"], [], []),
 }
 
 
@@ -68,7 +77,7 @@ def _compile(src: str, obj: str, flags, verbose: bool) -> str:
 
 
 def build_one(name: str, force: bool = False, verbose: bool = False, pool=None) -> str:
-    srcs, flags, libs = LIBRARIES[name]
+    srcs, flags, libs = LIBRARIES[name] if name in LIBRARIES else EXP_LIBRARIES[name]
     srcs = [os.path.join(CSRC, s) for s in srcs]
     missing = [s for s in srcs if not os.path.exists(s)]
     if missing:
@@ -87,7 +96,7 @@ def build_one(name: str, force: bool = False, verbose: bool = False, pool=None) 
     if not force and not todo and os.path.exists(target) and \
             all(os.path.getmtime(o) <= os.path.getmtime(target) for o in objs):
         return target
-    os.makedirs(OUT, exist_ok=True)
+    os.makedirs(os.path.dirname(target), exist_ok=True)
     tmp = target + ".tmp.%d" % os.getpid()
     cmd = [hipcc(), "--offload-arch=%s" % ARCH, "-fPIC", "-shared"] + objs + ["-o", tmp] + libs
     res = subprocess.run(cmd, capture_output=True, text=True)
@@ -97,10 +106,11 @@ def build_one(name: str, force: bool = False, verbose: bool = False, pool=None) 
     return target
 
 
-def build_all(force: bool = False, jobs: int = 8, verbose: bool = False):
+def build_all(force: bool = False, jobs: int = 8, verbose: bool = False, exp: bool = False):
     # one pool compiles the objects of every library; the libraries link in turn
+    names = list(LIBRARIES) + (list(EXP_LIBRARIES) if exp else [])
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        return {n: build_one(n, force, verbose, ex) for n in LIBRARIES}
+        return {n: build_one(n, force, verbose, ex) for n in names}
 
 
 def main(argv=None) -> int:
@@ -108,8 +118,10 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=8)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--exp", action="store_true",
+                    help="also build the experiment kernels (csrc/bench) into _native/exp/")
     args = ap.parse_args(argv)
-    for name, path in build_all(args.force, args.jobs, args.verbose).items():
+    for name, path in build_all(args.force, args.jobs, args.verbose, args.exp).items():
         print("built %-22s -> %s" % (name, os.path.relpath(path, ROOT)))
     return 0
 

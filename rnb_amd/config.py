@@ -101,14 +101,18 @@ class PipelineSpec:
         Groups, replica counts, queue wiring, segments and selectors are
         unchanged, so a multi-GPU configuration can be exercised end to end on
         a machine without GPUs (multi-GPU topologies without
-        GPUs). Transports fall back to host shared-memory rings.
+        GPUs). Transports fall back to host shared-memory rings, except RCCL
+        edges when ``RNB_RCCL_BACKEND=gloo``: they keep their send/recv rings
+        on the gloo backend (the RCCL claim protocol and pair groups run).
         """
         import copy
+        keep_rccl = os.environ.get("RNB_RCCL_BACKEND") == "gloo"
         spec = copy.deepcopy(self)
         for s in spec.steps:
             for g in s.groups:
                 g.gpus = [CPU_DEVICE for _ in g.gpus]
-                g.transport = "auto"
+                if not (keep_rccl and g.transport == "rccl"):
+                    g.transport = "auto"
         return spec
 
     def override_kwargs(self, overrides: Dict[str, Any]) -> "PipelineSpec":

@@ -400,6 +400,11 @@ class R2P1DEngine:
             if batch_running:
                 kernels().bn_seg_set_defer_running(False)
                 bn_mod._RUN_SINK[0] = None
+            if hip and self.range_guard is not None:
+                # the flag pointer is process-wide: launches of an unguarded
+                # engine (or tests) after this one must not write our flag
+                from ...ops.native import kernels as _k
+                _k().h3_set_range_flag(0)
         if self.head is not None:
             y = self.head.forward(y, out) if hip else self.head.forward_torch(y)
         elif out is not None:
@@ -528,8 +533,21 @@ class R2P1DEngine:
         if g is None or not g.tripped():
             return False
         g.reset()
+        # the tripped call already applied its BatchNorm running-statistics
+        # step; the re-run would apply a second one: keep the state as the
+        # call left it (one EMA step per call, as the reference's single
+        # forward). (If the tripped call's statistics were non-finite, its
+        # step already poisoned the running buffers -- the pre-call state is
+        # not kept per call.)
+        bns = [op.bn for op in self.ops
+               if op.bn is not None and getattr(op.bn, "update_running", False)
+               and hasattr(op.bn, "running_mean")]
+        snap = [(b.running_mean.clone(), b.running_var.clone()) for b in bns]
         with full_range():
             z = self.forward(x, clip_offsets=clip_offsets)
+        for b, (rm, rv) in zip(bns, snap):
+            b.running_mean.copy_(rm)
+            b.running_var.copy_(rv)
         y.copy_(z)
         torch.cuda.current_stream(self.device).synchronize()
         g.reset()
@@ -642,7 +660,8 @@ class GraphedEngine:
         self.graphs: Dict[int, Tuple[torch.cuda.CUDAGraph, torch.Tensor, torch.Tensor]] = {}
         self.pool = None
         self.capture_s = 0.0
-        self._last = None           # (bucket, n, clip offsets) of the last replay
+        self._last = None           # (bucket, n, clip offsets, replay no.) of the last replay
+        self._replays: Dict[int, int] = {}      # replays per bucket
         # intermediate stages: each bucket graph's final BN apply writes through
         # a device-held pointer (int64 [1] per bucket), so a replay can target
         # an output slot (replay(out=...)); default: the bucket's static output
@@ -658,15 +677,26 @@ class GraphedEngine:
     def range_guard(self):
         return self.engine.range_guard
 
-    def range_fallback(self, out: Optional[torch.Tensor] = None) -> bool:
-        """After the last replay completed: if the engine's h3 range guard
-        tripped, recompute that call's rows eagerly on full-range kernels (its
-        input still sits in the bucket's static input) into the bucket's
-        output, or into ``out`` (where the caller copied it); True if it did."""
+    @property
+    def last_call(self):
+        """Record of the last replay, for ``range_fallback(call=...)``."""
+        return self._last
+
+    def range_fallback(self, out: Optional[torch.Tensor] = None, call=None) -> bool:
+        """After a replay completed (``call``: its ``last_call`` record;
+        default the last replay): if the engine's h3 range guard tripped,
+        recompute that call's rows eagerly on full-range kernels (its input
+        still sits in the bucket's static input) into the bucket's output, or
+        into ``out`` (where the caller copied it); True if it did. Raises if a
+        later replay of the same bucket has overwritten the call's input."""
         g = self.engine.range_guard
-        if g is None or not g.tripped() or self._last is None:
+        call = call or self._last
+        if g is None or not g.tripped() or call is None:
             return False
-        b, n, offs = self._last
+        b, n, offs, gen = call
+        if self._replays.get(b) != gen:
+            raise RuntimeError("h3 range guard tripped, but bucket %d's input was overwritten "
+                               "by a later call (more than one call in flight per engine)" % b)
         _, static_in, static_out = self.graphs[b]
         return self.engine.range_fallback(static_in[:n], static_out[:n] if out is None else out,
                                           offs)
@@ -826,7 +856,9 @@ class GraphedEngine:
             self._set_dst(b, (out if out is not None else static_out).data_ptr())
         if self.batch_bn:
             self._set_offsets(b, n, clip_offsets)
-        self._last = (b, n, None if clip_offsets is None else [int(o) for o in clip_offsets])
+        self._replays[b] = self._replays.get(b, 0) + 1
+        self._last = (b, n, None if clip_offsets is None else [int(o) for o in clip_offsets],
+                      self._replays[b])
         # rows >= n hold stale (finite) inputs; in eval mode clip rows are
         # independent, in batch mode they sit outside every video's segment:
         # their outputs are simply not returned

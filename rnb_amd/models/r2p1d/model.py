@@ -230,7 +230,7 @@ class R2P1DRunner(RunnerModel):
         # when the runner sees them complete (on_complete), in call order
         self.range_guarded = any(getattr(e, "range_guard", None) is not None
                                  for e in self._lane_engines)
-        self._guard_calls = []           # (graphed engine, output) per call in flight
+        self._guard_calls = []           # (graphed engine, output, call record) in flight
         self.range_fallbacks = 0
         self._direct_calls = self._staged_calls = 0     # intermediate-stage outputs
 
@@ -240,14 +240,21 @@ class R2P1DRunner(RunnerModel):
         split), recompute its output on full-range kernels before it is used."""
         if not self._guard_calls:
             return
-        eng, out = self._guard_calls.pop(0)
-        if eng.range_fallback(out):
+        eng, out, call = self._guard_calls.pop(0)
+        if eng.range_fallback(out, call):
             self.range_fallbacks += 1
             print("[runner] h3 range guard: call of %d rows re-run on full-range kernels "
                   "(%d so far)" % (out.shape[0], self.range_fallbacks), flush=True)
 
     def runtime_stats(self) -> dict:
         st = {"h3_range_fallbacks": self.range_fallbacks} if self.range_guarded else {}
+        # conv shapes this process timed vs took from the tuning cache / seed
+        # table (ops/tuning.py): a replica that starts after another has tuned
+        # the same shapes should time none of them
+        from ...ops import tuning
+        ts = tuning.stats()
+        st.update({"tune_tuned": ts["tuned"], "tune_read": ts["read"],
+                   "tune_runners_tuning": int(ts["tuned"] > 0), "tune_runners": 1})
         if self.end_index < 5:
             st.update(direct_slot_calls=self._direct_calls, staged_slot_calls=self._staged_calls)
         return st
@@ -270,7 +277,7 @@ class R2P1DRunner(RunnerModel):
             offs = self._clip_offsets(time_card, x.shape[0])
             y = eng.replay(x.shape[0], clip_offsets=offs, out=slot)
             if eng.range_guard is not None:
-                self._guard_calls.append((eng, y))
+                self._guard_calls.append((eng, y, eng.last_call))
             self._direct_calls += 1
             return (y,), non_tensors, time_card
         (y,), nts, tc = self._call(tensors, non_tensors, time_card)
@@ -280,7 +287,8 @@ class R2P1DRunner(RunnerModel):
             slot[:y.shape[0]].copy_(y)
         if self._guard_calls and self._guard_calls[-1][1] is y:
             # a guard re-run of this call must land in the slot
-            self._guard_calls[-1] = (self._guard_calls[-1][0], slot[:y.shape[0]])
+            e, _, call = self._guard_calls[-1]
+            self._guard_calls[-1] = (e, slot[:y.shape[0]], call)
         self._staged_calls += 1
         return (slot[:y.shape[0]],), nts, tc
 
@@ -428,14 +436,14 @@ class R2P1DRunner(RunnerModel):
             self._gather_ptr = None
             y = eng.replay(x.shape[0], clip_offsets=offs)
             if eng.range_guard is not None:
-                self._guard_calls.append((eng, y))
+                self._guard_calls.append((eng, y, eng.last_call))
             return y
         self._gather_ptr = None
         x = _to_boundary(x, self.start_index, self.dtype)
         if isinstance(eng, GraphedEngine) and x.shape[0] > 0:
             y = eng.forward(x, clip_offsets=offs) if self.bn_mode == "batch" else eng(x)
             if eng.range_guard is not None:
-                self._guard_calls.append((eng, y))
+                self._guard_calls.append((eng, y, eng.last_call))
             return y
         if getattr(eng, "range_guard", None) is not None and x.shape[0] > 0:
             # eager hip engine: checked right here (waits for the call)

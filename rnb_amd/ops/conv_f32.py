@@ -1103,7 +1103,9 @@ class ConvLayerF32:
                                    (is_h3(cached) and h3_enabled()) or
                                    (is_x6d(cached) and not is_h3(cached) and x6_enabled())):
             self._config[tuple(x.shape[:4])] = cached
+            tuning.count("read")
             return cached
+        tuning.count("tuned")
         y = torch.empty(self.out_shape(x.shape), dtype=torch.float32, device=x.device)
         stream = torch.cuda.current_stream(x.device)
         verbose = os.environ.get("RNB_TUNE_VERBOSE") == "1"

@@ -346,17 +346,32 @@ class Kernels:
         lib.rnb_conv_h3t_launch.argtypes = lib.rnb_conv_h3r_launch.argtypes
         lib.rnb_conv_h3t_launch.restype = ctypes.c_int
         lib.rnb_conv_h3t_pixels.argtypes = [ctypes.c_int, ctypes.c_int]
-        lib.rnb_conv_h3u_launch.argtypes = lib.rnb_conv_h3r_launch.argtypes
-        lib.rnb_conv_h3u_launch.restype = ctypes.c_int
-        lib.rnb_conv_h3u_pixels.argtypes = [ctypes.c_int, ctypes.c_int]
-        lib.rnb_conv_h3u_pixels.restype = ctypes.c_int
-        lib.rnb_conv_h3s_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
-                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                            ctypes.c_int, ctypes.c_float, ctypes.c_float]
-        lib.rnb_conv_h3s_launch.restype = ctypes.c_int
-        lib.rnb_conv_h3s_rows.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
-        lib.rnb_conv_h3s_rows.restype = ctypes.c_int
-        lib.rnb_conv_h3stem_launch.argtypes = lib.rnb_conv_h3s_launch.argtypes
+        # experiment kernels (build.py --exp; absent from the product build):
+        # conv_h3u / conv_h3s report 0 variants without their library
+        self.exp = None
+        exp_path = os.path.join(NATIVE_DIR, "exp", "librnb_h3exp.so")
+        if os.path.exists(exp_path) and os.environ.get("RNB_EXP_KERNELS", "1") != "0":
+            try:
+                self.exp = ctypes.CDLL(exp_path)
+            except OSError:
+                self.exp = None
+        if self.exp is not None:
+            ex = self.exp
+            ex.rnb_conv_h3u_launch.argtypes = lib.rnb_conv_h3r_launch.argtypes
+            ex.rnb_conv_h3u_launch.restype = ctypes.c_int
+            ex.rnb_conv_h3u_pixels.argtypes = [ctypes.c_int, ctypes.c_int]
+            ex.rnb_conv_h3u_pixels.restype = ctypes.c_int
+            ex.rnb_conv_h3s_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
+                                               ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_int, ctypes.c_float,
+                                               ctypes.c_float]
+            ex.rnb_conv_h3s_launch.restype = ctypes.c_int
+            ex.rnb_conv_h3s_rows.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+            ex.rnb_conv_h3s_rows.restype = ctypes.c_int
+        lib.rnb_conv_h3stem_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
+                                               ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_int, ctypes.c_float,
+                                               ctypes.c_float]
         lib.rnb_conv_h3stem_launch.restype = ctypes.c_int
         lib.rnb_conv_h3stem_rows.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         lib.rnb_conv_h3stem_rows.restype = ctypes.c_int
@@ -401,8 +416,8 @@ class Kernels:
         self.x6r_variants = lib.rnb_conv_x6r_num_variants()
         self.h3r_variants = lib.rnb_conv_h3r_num_variants()
         self.h3t_variants = lib.rnb_conv_h3t_num_variants()
-        self.h3u_variants = lib.rnb_conv_h3u_num_variants()
-        self.h3s_variants = lib.rnb_conv_h3s_num_variants()
+        self.h3u_variants = self.exp.rnb_conv_h3u_num_variants() if self.exp else 0
+        self.h3s_variants = self.exp.rnb_conv_h3s_num_variants() if self.exp else 0
         self.h3stem_variants = lib.rnb_conv_h3stem_num_variants()
         self.x6_configs = []       # (pixel tile, channel tile) per x6 direct config
         for i in range(lib.rnb_conv_x6_num_configs()):
@@ -487,7 +502,7 @@ class Kernels:
         """Wave-specialised temporal h3 conv (csrc/conv_h3u.hip: staging waves
         split the next chunk while the MFMA waves run the current one); the
         weights and arguments as ``conv_h3t``."""
-        _check(self.lib.rnb_conv_h3u_launch(ctypes.byref(params), variant, stream,
+        _check(self.exp.rnb_conv_h3u_launch(ctypes.byref(params), variant, stream,
                                             sums or None, clip_seg or None, stats_c, in_scale,
                                             out_scale, in_ss or None, in_seg or None),
                "conv_h3u (variant %d)" % variant)
@@ -497,7 +512,7 @@ class Kernels:
         """h3 stride-2 row-band halo conv (csrc/conv_h3s.hip: 1x3x3 stride
         (1, 2, 2) pad (0, 1, 1), Cin_p % 32 == 0, the h3 direct weights); the
         arguments as ``conv_h3`` (no input BN on load)."""
-        _check(self.lib.rnb_conv_h3s_launch(ctypes.byref(params), variant, stream,
+        _check(self.exp.rnb_conv_h3s_launch(ctypes.byref(params), variant, stream,
                                             sums or None, clip_seg or None, stats_c, in_scale,
                                             out_scale),
                "conv_h3s (variant %d)" % variant)
@@ -532,10 +547,10 @@ class Kernels:
 
     def conv_h3s_rows(self, variant: int, Ho: int, Wo: int) -> int:
         """Output rows per band of h3s variant ``variant`` (0: cannot run)."""
-        return int(self.lib.rnb_conv_h3s_rows(variant, Ho, Wo))
+        return int(self.exp.rnb_conv_h3s_rows(variant, Ho, Wo)) if self.exp else 0
 
     def conv_h3u_pixels(self, variant: int, T: int) -> int:
-        return int(self.lib.rnb_conv_h3u_pixels(variant, T))
+        return int(self.exp.rnb_conv_h3u_pixels(variant, T)) if self.exp else 0
 
     def conv_h3t_pixels(self, variant: int, T: int) -> int:
         """Pixels per block of h3t variant ``variant`` for T frames (0: cannot run)."""

@@ -9,7 +9,20 @@ device), so results are cached under that key:
   R(2+1)D-34) are timed once;
 * across processes: with ``RNB_TUNE_CACHE=<path>`` (the bench and the launcher
   set one per job) results go to a JSON file guarded by an ``fcntl`` lock, so
-  the replicas of a GPU type time each shape once and the others read it.
+  the replicas of a GPU type time each shape once and the others read it. A
+  miss re-reads the file whenever its size or mtime changed since the last
+  read, so a process that waited for the ``FileLock("autotune")`` holder sees
+  every shape the holder timed (before round 6 the file was read once per
+  process, and every replica after the first re-timed its shapes serially
+  under the lock);
+* across boxes: a committed seed table (``tune_seed.json`` next to this file,
+  or ``RNB_TUNE_SEED=<path>``; ``RNB_TUNE_SEED=0`` disables it) holds the
+  picks measured on MI355X -- MIOpen's perf-db idea: a fresh box times only
+  the shapes the table does not have. Seed entries never override the job's
+  own cache file.
+
+``stats()`` counts, per process, the shapes timed here (``tuned``) and the
+ones served from the cache or the seed (``read``); runners report them.
 
 For a shape that was never timed, ``nearest`` returns the config of the
 closest timed batch of the same geometry (log distance in pixels), which is
@@ -26,11 +39,22 @@ from typing import Dict, Optional, Tuple
 
 _lock = threading.Lock()
 _mem: Dict[str, int] = {}
-_loaded_from: Optional[str] = None
+_file_sig: Optional[Tuple[str, int, int]] = None     # (path, size, mtime_ns) last read
+_seed_from: Optional[str] = None
+_stats = {"tuned": 0, "read": 0, "seeded": 0, "file_reads": 0}
+
+_SEED_DEFAULT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tune_seed.json")
 
 
 def _path() -> Optional[str]:
     return os.environ.get("RNB_TUNE_CACHE") or None
+
+
+def _seed_path() -> Optional[str]:
+    p = os.environ.get("RNB_TUNE_SEED", _SEED_DEFAULT)
+    if p in ("", "0", "none"):
+        return None
+    return p
 
 
 def make_key(family: str, geom, shape, device_name: str = "") -> str:
@@ -41,19 +65,51 @@ def make_key(family: str, geom, shape, device_name: str = "") -> str:
                                           "x".join(map(str, shape)), device_name)
 
 
+def _load_seed() -> None:
+    """Seed table entries under the cache (once per seed path)."""
+    global _seed_from
+    path = _seed_path()
+    if path is None or _seed_from == path:
+        return
+    _seed_from = path
+    try:
+        with open(path) as f:
+            data = json.load(f)
+    except (OSError, ValueError):
+        return
+    entries = data.get("entries", data) if isinstance(data, dict) else {}
+    n = 0
+    for k, v in entries.items():
+        if k not in _mem:
+            _mem[k] = int(v)
+            n += 1
+    _stats["seeded"] += n
+
+
 def _load_file() -> None:
-    global _loaded_from
+    """(Re-)read the job's cache file when it changed since the last read."""
+    global _file_sig
+    _load_seed()
     path = _path()
-    if path is None or _loaded_from == path or not os.path.exists(path):
+    if path is None:
+        return
+    try:
+        st = os.stat(path)
+    except OSError:
+        return
+    sig = (path, st.st_size, st.st_mtime_ns)
+    if sig == _file_sig:
         return
     try:
         with open(path) as f:
             fcntl.flock(f, fcntl.LOCK_SH)
+            st = os.fstat(f.fileno())
             data = json.load(f)
     except (OSError, ValueError):
         return
     _mem.update({k: int(v) for k, v in data.items()})
-    _loaded_from = path
+    _file_sig = (path, st.st_size, st.st_mtime_ns)
+    _stats["file_reads"] += 1
 
 
 def get(key: str) -> Optional[int]:
@@ -64,6 +120,7 @@ def get(key: str) -> Optional[int]:
 
 
 def put(key: str, cid: int) -> None:
+    global _file_sig
     with _lock:
         _mem[key] = int(cid)
         path = _path()
@@ -77,11 +134,26 @@ def put(key: str, cid: int) -> None:
                 data = json.loads(f.read() or "{}")
             except ValueError:
                 data = {}
+            # entries other processes wrote meanwhile come along for free
+            _mem.update({k: int(v) for k, v in data.items() if k not in _mem})
             data[key] = int(cid)
             f.seek(0)
             f.truncate()
             json.dump(data, f, indent=0, sort_keys=True)
             f.flush()
+            st = os.fstat(f.fileno())
+            _file_sig = (path, st.st_size, st.st_mtime_ns)
+
+
+def count(kind: str) -> None:
+    """Record one shape ``tuned`` (timed here) or ``read`` (cache / seed hit)."""
+    with _lock:
+        _stats[kind] = _stats.get(kind, 0) + 1
+
+
+def stats() -> Dict[str, int]:
+    with _lock:
+        return dict(_stats)
 
 
 class FileLock:
@@ -126,8 +198,18 @@ def nearest(prefix: str, pixels: int) -> Optional[int]:
         return best
 
 
+def snapshot() -> Dict[str, int]:
+    """Every entry this process knows (seed + cache file + own picks)."""
+    with _lock:
+        _load_file()
+        return dict(_mem)
+
+
 def clear() -> None:
-    global _loaded_from
+    global _file_sig, _seed_from
     with _lock:
         _mem.clear()
-        _loaded_from = None
+        _file_sig = None
+        _seed_from = None
+        for k in _stats:
+            _stats[k] = 0

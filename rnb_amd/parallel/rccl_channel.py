@@ -32,8 +32,10 @@ them, so sends and receives match. The participating runners form one world
 but there is no world communicator: every (producer, consumer) pair of an RCCL
 edge gets its own 2-rank process-group backend (``ProcessGroupNCCL`` = RCCL on
 ROCm, ``ProcessGroupGloo`` for the CPU tests) under its own store prefix,
-created by the two members in one global order (no creation deadlock), and a
-call's sends or receives are launched per pair communicator. Hence
+created and connected (one 1-element exchange, eagerly: RCCL otherwise creates a
+communicator at its first transfer) by the two members in one global order, so
+creation cannot deadlock; a call's sends or receives are launched per pair
+communicator. Hence
 
 * RCCL never sees two ranks of one communicator on one GPU, even when a GPU
   hosts several consumer replicas or producers of an edge (the launcher only
@@ -121,10 +123,33 @@ def init_dist(info: Optional[DistInfo], device: torch.device) -> None:
         else:
             raise ValueError("RCCL world backend must be 'nccl' or 'gloo', got %r"
                              % info.backend)
+        # connect now, in this global pair order: ProcessGroupNCCL creates its
+        # communicator lazily at the first send / recv, and that creation
+        # blocks until the peer joins -- left to traffic order, two producers
+        # serving claims of two consumers could each wait on a communicator
+        # the other's peer is not yet creating. A 1-element exchange per pair
+        # (lower rank sends) in sorted order always has both ends of the
+        # smallest unconnected pair ready, so it completes.
+        _connect_pair(pg, me, device)
         comms[pair[1 - me]] = (pg, 1 - me)         # peer global rank -> (pg, its rank)
     _store_barrier(store, "rnb_rccl_world_up", info.world_size)
     _state.update(rank=info.rank, world=info.world_size, backend=info.backend,
                   pairs=comms, device=device)
+
+
+def _connect_pair(pg, me: int, device: torch.device) -> None:
+    """One 1-element transfer over a fresh pair communicator (rank 0 of the
+    pair sends), waited for on the host: the communicator exists afterwards."""
+    dev = device if device.type == "cuda" else torch.device("cpu")
+    t = torch.full((1,), 7 if me == 0 else 0, dtype=torch.int32, device=dev)
+    w = pg.send([t], 1, 0) if me == 0 else pg.recv([t], 0, 0)
+    if not w.wait(_timeout()):
+        raise TimeoutError("RCCL pair communicator not connected within %s s"
+                           % _timeout().total_seconds())
+    if dev.type == "cuda":
+        torch.cuda.current_stream(dev).synchronize()
+    if me == 1 and int(t.item()) != 7:
+        raise RuntimeError("RCCL pair connect: received %d, expected 7" % int(t.item()))
 
 
 def _pair(peer: int):

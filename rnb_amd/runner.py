@@ -255,6 +255,10 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         lane_inflight = getattr(model, "inflight_calls", None)
         if is_final_step and stream is not None and callable(lane_inflight):
             final_depth = max(final_depth, int(lane_inflight()))
+            if getattr(model, "range_guarded", False):
+                # a guard re-run recomputes a call from its bucket's static
+                # input: at most one call in flight per lane engine
+                final_depth = min(final_depth, int(lane_inflight()))
         model_event = getattr(model, "completion_event", None)
         if not callable(model_event):
             model_event = None

@@ -5,8 +5,6 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 240 python scripts/h3t_exp.py --cases k4,k4c128,k8 > gpurun_out/h3t_exp.txt 2>&1 || exit $?
-cat gpurun_out/h3t_exp.txt
 timeout -k 10 1000 python scripts/ab_bench.py --rounds 2 --out gpurun_out/ab_yield.txt \
   "base||--steps 10" "y4||--steps 10 --yield-ms 4" "y8||--steps 10 --yield-ms 8"
 rc=$?; cat gpurun_out/ab_yield.txt; exit $rc

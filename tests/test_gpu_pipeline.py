@@ -49,6 +49,11 @@ def test_layer_split_ipc_gpu(tmp_path):
     proc, res, _ = checked_run(tmp_path, cfg, "-v", "30", "-mi", "5", timeout=600, depth=18,
                                bn_mode="batch", device="cuda:0", tol=5e-4, min_videos=4)
     assert res["ok"] and res["latency"]["count"] > 0
+    # the intermediate stage's graph replays write the boundary
+    # activation straight into the output slot -- no staging copy ran
+    mc = res.get("model_counters") or {}
+    assert mc.get("direct_slot_calls", 0) > 0, mc
+    assert mc.get("staged_slot_calls", -1) == 0, mc
 
 
 def test_gather_pipeline_two_runners_race_checked(tmp_path):
