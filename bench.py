@@ -545,7 +545,7 @@ def run_cross_gpu_extras(args) -> dict:
                "--loaders", str(args.loaders), "--replicas", str(args.replicas),
                # 16-clip graph buckets: a quarter of the headline's graph
                # captures in each extra's setup (4 short steps, padding cost small)
-               "--bucket-step", ("geo" if args.bucket_step == "geo"
+               "--bucket-step", (args.bucket_step if str(args.bucket_step).startswith("geo")
                                  else str(max(int(args.bucket_step), 16))),
                "--no-check", "--no-cross-gpu-extras", "--json-out", path]
         env = {k: v for k, v in os.environ.items()
@@ -774,7 +774,7 @@ def run_fused(args) -> int:
     # graph buckets every --bucket-step clips: a batch pads to the next
     # bucket (every 8 clips with arrival-order packing: 2.3 % of the clips
     # padded vs 6.2 % with power-of-two-ish buckets on the reference clip mix)
-    bstep = 8 if args.bucket_step == "geo" else max(1, int(args.bucket_step))
+    bstep = 8 if str(args.bucket_step).startswith("geo") else max(1, int(args.bucket_step))
     buckets = sorted(set(range(bstep, args.clips_per_batch + 1, bstep))
                      | {args.clips_per_batch, max_clips})
     eng = FusedR2P1D(device, depth=args.depth, replicas=args.fused_replicas,

@@ -55,19 +55,37 @@ DEFAULT_BUCKETS = (1, 2, 3, 4, 5, 6, 8, 10, 12, 15, 16, 20, 24, 30, 32, 40, 45, 
 
 
 def geometric_buckets(max_clips: int, ratio: float = 1.125, dense: int = 8,
-                      align: int = 4) -> List[int]:
+                      align: int = 4, fine_from: int = 0, fine_step: int = 8) -> List[int]:
     """Clip buckets 1..``dense`` one by one, then growing by ``ratio`` (rounded
     up to multiples of ``align``) to ``max_clips``: 30 graphs instead of 65 at
     256 clips with 4-clip steps. A gathering runner trims a call to a bucket
     boundary when padding would cost more than a few percent
     (R2P1DRunner.gather_fit), so the coarser spacing defers clips to the next
-    call instead of computing padding rows."""
+    call instead of computing padding rows. ``fine_from`` > 0: from that many
+    clips on, buckets every ``fine_step`` clips instead (where bulk calls
+    land: bucket_step "geo8" = fine_from 96, fine_step 8)."""
     out = list(range(1, min(dense, max_clips) + 1))
     s = dense
     while s < max_clips:
-        s = min(max_clips, max(s + align, -(-int(s * ratio) // align) * align))
+        if fine_from and s >= fine_from:
+            s = min(max_clips, (s // fine_step + 1) * fine_step)
+        else:
+            s = min(max_clips, max(s + align, -(-int(s * ratio) // align) * align))
         out.append(s)
     return sorted(set(out) | {max_clips})
+
+
+def parse_bucket_step(step, max_clips: int) -> Optional[List[int]]:
+    """Graph buckets of a runner's ``bucket_step``: "geo" (geometric), "geoN"
+    (geometric below 96 clips, every N clips from there), an integer step
+    (every that many clips), or None (DEFAULT_BUCKETS)."""
+    if step is None or step == "" or step == 0:
+        return None
+    if isinstance(step, str) and step.startswith("geo"):
+        fine = int(step[3:]) if step[3:] else 0
+        return geometric_buckets(max_clips, fine_from=96 if fine else 0, fine_step=fine or 8)
+    n = int(step)
+    return sorted(set(range(n, max_clips + 1, n)) | {1, max_clips})
 
 
 def boundary_channels_p(layer_idx: int, dtype=torch.bfloat16) -> int:

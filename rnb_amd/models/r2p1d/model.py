@@ -47,7 +47,7 @@ from ...video_path_provider import (DirectoryVideoPathIterator,
                                     SyntheticVideoPathIterator, VideoPathIterator)
 from .decoder import make_decoder
 from .engine import (GraphedEngine, R2P1DEngine, boundary_channels_p, boundary_shape,
-                     geometric_buckets)
+                     parse_bucket_step)
 from .network import (LAYER_INPUT_CTHW, R2Plus1DLayerWrapper, init_random_,
                       load_reference_state_dict, normalize_layer_sizes)
 from .sampler import R2P1DSampler
@@ -162,13 +162,8 @@ class R2P1DRunner(RunnerModel):
         self.bn_mode = bn_mode = default_bn_mode(bn_mode, self.dtype)
         self.max_batch_videos = int(max_batch_videos)
         self.batch_wait_s = float(batch_wait_ms) / 1000.0
-        buckets = None
-        if bucket_step == "geo":
-            # geometric spacing + bucket-aligned gathering (gather_fit)
-            buckets = geometric_buckets(self.max_clips)
-        elif bucket_step:
-            step = int(bucket_step)
-            buckets = sorted(set(range(step, self.max_clips + 1, step)) | {1, self.max_clips})
+        # "geo": geometric spacing + bucket-aligned gathering (gather_fit)
+        buckets = parse_bucket_step(bucket_step, self.max_clips)
         self.engine = build_engine(device, start_index, end_index, num_classes,
                                    layer_sizes, depth, backend, bn_mode, seed, ckpt_path,
                                    self.max_clips, use_graphs, autotune, self.dtype, buckets)

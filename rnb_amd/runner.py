@@ -802,6 +802,11 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
             if callable(mstats):
                 for k, v in mstats().items():
                     stats["model.%s" % k] = v
+                    if k == "tune_tuned":
+                        # per runner (the launcher sums the others): which
+                        # processes timed shapes
+                        stats["model.tune_tuned@%d/%d/%d" % (step_idx, group_idx,
+                                                             instance_idx)] = v
             result_queue.put(("ring_stats", step_idx, group_idx, instance_idx, stats))
         # ---- shutdown
         if not is_final_step:

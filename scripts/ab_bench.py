@@ -50,6 +50,8 @@ def run(name, env, extra, timeout, idx):
     return {"name": name, "rc": rc, "value": d.get("value"), "p50": d.get("p50_ms"),
             "p99": d.get("p99_ms"), "mi10_p50": mi.get("p50_ms"), "mi10_p99": mi.get("p99_ms"),
             "items_per_call": g.get("items_per_call"), "rows_per_call": g.get("rows_per_call"),
+            "setup_s": (d.get("timeline_s") or {}).get("headline.setup"),
+            "tuned": (d.get("model_counters") or {}).get("tune_tuned"),
             "wall_s": round(time.time() - t0, 1)}
 
 
@@ -79,16 +81,17 @@ def main():
                                                                           " ".join(BASE))]
     for name, env, extra in vs:
         lines.append("# %s: env %s, args %s" % (name, env, " ".join(extra)))
-    lines.append("%-10s %5s %9s %8s %8s %9s %9s %7s %7s" % (
-        "variant", "round", "videos/s", "p50", "p99", "mi10 p50", "mi10 p99", "items", "rows"))
+    lines.append("%-10s %5s %9s %8s %8s %9s %9s %7s %7s %7s %6s" % (
+        "variant", "round", "videos/s", "p50", "p99", "mi10 p50", "mi10 p99", "items", "rows",
+        "setup", "tuned"))
     for res in rows:
         if "value" not in res:
             lines.append("%-10s %5d  rc=%s" % (res["name"], res["round"], res["rc"]))
             continue
-        lines.append("%-10s %5d %9.1f %8.2f %8.2f %9.2f %9.2f %7s %7s" % (
+        lines.append("%-10s %5d %9.1f %8.2f %8.2f %9.2f %9.2f %7s %7s %7s %6s" % (
             res["name"], res["round"], res["value"], res["p50"], res["p99"],
             res["mi10_p50"] or 0, res["mi10_p99"] or 0, res["items_per_call"],
-            res["rows_per_call"]))
+            res["rows_per_call"], res.get("setup_s"), res.get("tuned")))
     for name, _, _ in vs:
         ok = [x for x in rows if x["name"] == name and "value" in x]
         if ok:
