@@ -138,11 +138,20 @@ def parse_args(argv=None):
                          "256 clips / 128 videos beat 128 / 64 by 4.8%% in interleaved "
                          "runs (1090 vs 1040 videos/s, profiles/r3_bench_batch_sweep.txt; "
                          "a 256-clip R(2+1)D-34 runner holds ~19 GB)")
-    ap.add_argument("--bucket-step", default="geo",
-                    help="HIP-graph clip buckets: every this many clips, or 'geo' (default: "
-                         "1..8, then ~12.5%% apart; a gathering runner ends a bulk call at a "
-                         "bucket boundary instead of padding: 30 graphs per engine instead of "
-                         "65 at 256 clips)")
+    ap.add_argument("--bucket-step", default="geo8",
+                    help="HIP-graph clip buckets: every this many clips, 'geo' (1..8, then "
+                         "~12.5%% apart; a gathering runner ends a bulk call at a bucket "
+                         "boundary instead of padding: 30 graphs per engine instead of 65 at "
+                         "256 clips) or 'geo8' (default since round 6: geometric below 96 "
+                         "clips, every 8 clips above, where bulk calls land: 42 graphs; "
+                         "interleaved A/B with the seed table, 2 rounds: 1596 vs 1543 "
+                         "videos/s, 155-165 vs 63-79 rows per bulk call, setup 14 vs 9 s, "
+                         "half-load p50 6.7 vs 6.2 ms; every 4 clips: 1613, p50 8.0 ms, setup "
+                         "20 s -- profiles/r6_ab_buckets_seeded.txt)")
+    ap.add_argument("--small-cu-frac", type=float, default=1.0,
+                    help="(--route large-small) fraction of the CUs the 1-clip-video "
+                         "replicas' streams may use (hipExtStreamCreateWithCUMask); < 1 keeps "
+                         "the rest free for 15-clip calls (1.0 = no mask)")
     ap.add_argument("--yield-ms", type=float, default=0.0,
                     help="(--route large-small) in the latency regime a small-video replica "
                          "holds a call back up to this long while a 15-clip call runs on its "
@@ -238,7 +247,8 @@ def pipeline_config(args, n_gpus: int) -> dict:
                                    for g in gpus]},
                  dict(runner, queue_groups=[q for g in gpus for q in (
                      dict({"gpus": [g] * (args.replicas - nl), "in_queue": 2 * g},
-                          **({"yield_ms": args.yield_ms} if args.yield_ms > 0 else {})),
+                          **({"yield_ms": args.yield_ms} if args.yield_ms > 0 else {}),
+                          **({"cu_frac": args.small_cu_frac} if args.small_cu_frac < 1 else {})),
                      # 15-clip videos only: buckets of whole videos (19 graphs)
                      dict({"gpus": [g] * nl, "in_queue": 2 * g + 1,
                            "bucket_step": LARGE_CLIPS},

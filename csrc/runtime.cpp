@@ -10,6 +10,7 @@
 //
 // Exposed with a C ABI and loaded through ctypes (rnb_amd/ops/native.py).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <cstring>
 #include <cstdint>
 
@@ -126,6 +127,17 @@ int rnb_stream_create(int nonblocking, int priority, void** stream) {
 }
 
 int rnb_stream_destroy(void* stream) { return (int)hipStreamDestroy((hipStream_t)stream); }
+
+// a stream whose dispatches may only use the CUs whose bits are set in
+// ``mask`` (n_words 32-bit words, CU i = bit i % 32 of word i / 32): a replica
+// group kept off part of the chip so that another group's calls find those
+// CUs free (bench.py --small-cu-frac)
+int rnb_stream_create_cumask(const uint32_t* mask, int n_words, void** stream) {
+  hipStream_t s;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, mask);
+  *stream = (void*)s;
+  return (int)e;
+}
 
 // ~cycles of busy wait on the stream (a pending record for the IPC-event tests)
 __global__ void rnb_spin_kernel(long long cycles) {

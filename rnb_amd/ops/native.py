@@ -790,6 +790,8 @@ class Runtime:
         lib.rnb_mem_get_info.argtypes = [ctypes.POINTER(sz), ctypes.POINTER(sz)]
         lib.rnb_stream_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
         lib.rnb_stream_destroy.argtypes = [vp]
+        lib.rnb_stream_create_cumask.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
+                                                 ctypes.POINTER(vp)]
         lib.rnb_spin.argtypes = [vp, ctypes.c_longlong]
         self.handle_size = lib.rnb_ipc_handle_size()
         self.event_handle_size = lib.rnb_ipc_event_handle_size()
@@ -801,6 +803,19 @@ class Runtime:
         s = ctypes.c_void_p()
         _check(self.lib.rnb_stream_create(int(nonblocking), priority, ctypes.byref(s)),
                "hipStreamCreateWithPriority")
+        return s.value
+
+    def stream_create_cumask(self, enabled_cus) -> int:
+        """A stream limited to the CUs in ``enabled_cus`` (indices) of the
+        current device (hipExtStreamCreateWithCUMask)."""
+        cus = sorted(set(int(c) for c in enabled_cus))
+        n = (max(cus) // 32 + 1) if cus else 1
+        words = (ctypes.c_uint32 * n)()
+        for c in cus:
+            words[c // 32] |= 1 << (c % 32)
+        s = ctypes.c_void_p()
+        _check(self.lib.rnb_stream_create_cumask(words, n, ctypes.byref(s)),
+               "hipExtStreamCreateWithCUMask")
         return s.value
 
     def stream_destroy(self, stream: int) -> None:

@@ -53,6 +53,28 @@ def _set_flag(flag, value, only_if_unset=True):
             flag.value = value
 
 
+
+def _cu_masked_stream(device, frac: float):
+    """An external stream on ``device`` limited to ``frac`` of its CUs (in
+    eighths); None when the runtime refuses (the replica then uses a normal
+    stream). CU i is in class ((i % 8) + (i // 8)) % 8 and the lowest classes
+    are left out: a class holds an eighth of every XCD's CUs whether the mask
+    bits go round-robin over the 8 XCDs or XCD by XCD."""
+    import torch
+    try:
+        from .ops.native import runtime
+        n = torch.cuda.get_device_properties(device).multi_processor_count
+        drop = min(7, max(0, int(round(8 * (1.0 - frac)))))
+        keep = [i for i in range(n) if ((i % 8) + (i // 8)) % 8 >= drop]
+        ptr = runtime().stream_create_cumask(keep)
+        print("[runner gpu %d] CU-masked stream: %d of %d CUs" % (device.index or 0, len(keep), n),
+              flush=True)
+        return torch.cuda.ExternalStream(ptr, device=device)
+    except Exception as err:                   # reported, never fatal
+        print("[runner] CU-masked stream refused (%s): using a normal stream" % (err,),
+              flush=True)
+        return None
+
 def runner(input_queue, output_queues, queue_selector_path, print_summary,
            job_id, g_idx, group_idx, instance_idx,
            global_inference_counter, num_videos,
@@ -123,6 +145,11 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
     # call back for up to that long while such a call runs, when few requests
     # are queued (bulk phases never wait)
     gpu_busy = model_kwargs.pop("gpu_busy", None)
+    # ``cu_frac`` < 1 (group kwarg): this replica's stream may use only that
+    # fraction of the GPU's CUs (every k-th CU left out, spread over the
+    # XCDs), so another group's calls (the 15-clip-video replica) find CUs
+    # free in the latency regime (bench.py --small-cu-frac)
+    cu_frac = float(model_kwargs.pop("cu_frac", 1.0) or 1.0)
     announce_busy = bool(model_kwargs.pop("announce_busy", False)) and gpu_busy is not None
     yield_s = float(model_kwargs.pop("yield_ms", 0.0) or 0.0) / 1000.0
     if gpu_busy is None or g_idx < 0 or g_idx >= len(gpu_busy):
@@ -136,7 +163,11 @@ def _runner_body(input_queue, output_queues, queue_selector_path, print_summary,
         prio = int(getattr(_lc(model_module_path), "stream_priority", 0))
         if group_prio is not None and group_idx < len(group_prio):
             prio = int(group_prio[group_idx])
-        stream = torch.cuda.Stream(device=device, priority=prio)
+        stream = None
+        if cu_frac < 1.0:
+            stream = _cu_masked_stream(device, cu_frac)
+        if stream is None:
+            stream = torch.cuda.Stream(device=device, priority=prio)
         stream_ctx = torch.cuda.stream(stream)
         # models running calls on streams of their own (R2P1DRunner lanes)
         # create them at this runner's priority

@@ -44,6 +44,9 @@ CASES = {
     "k14": (576, 256, (3, 1, 1), (1, 1, 1), (1, 0, 0), (2, 14, 14), True, True),
     "k17": (256, 921, (1, 3, 3), (1, 2, 2), (0, 1, 1), (2, 14, 14), False, True),
     "k19": (512, 1152, (1, 3, 3), (1, 1, 1), (0, 1, 1), (1, 7, 7), False, True),
+    "k20": (1152, 512, (3, 1, 1), (1, 1, 1), (1, 0, 0), (1, 7, 7), True, True),
+    "k12": (460, 256, (3, 1, 1), (2, 1, 1), (1, 0, 0), (4, 14, 14), True, True),
+    "k18": (921, 512, (3, 1, 1), (2, 1, 1), (1, 0, 0), (2, 7, 7), True, True),
 }
 PEAK_16 = 2517.0
 
