@@ -1073,15 +1073,6 @@ static const ConvH3Config kH3Configs[] = {
     H3CFG(1, 8, 4, 1, 3, 3),   // 10:  64 px x 128 ch, 4 waves, 3 blocks per CU (48 KB)
     H3CFG(2, 9, 8, 1, 1, 4),   // 11: config 0 with the fourth product
     H3CFG(1, 9, 8, 1, 2, 4),   // 12: config 2 with the fourth product
-    // round 6: wider per-wave tiles for the GEMM-shaped convs (conv3-5
-    // temporal, conv5 spatial): each split B fragment feeds 8 channel tiles
-    // and each weight fragment 2-4 pixel tiles (fewer LDS reads and less
-    // split VALU per MFMA than configs 9 / 10)
-    H3CFG(2, 8, 2, 2, 2, 3),   // 13:  64 px x 256 ch, 4 waves (80 KB)
-    H3CFG(4, 8, 2, 1, 2, 3),   // 14: 128 px x 128 ch, 2 waves x 64 px (64 KB)
-    H3CFG(2, 8, 4, 1, 2, 3),   // 15: 128 px x 128 ch, 4 waves x 32 px (64 KB)
-    H3CFG(4, 4, 2, 2, 2, 3),   // 16: 128 px x 128 ch, 4 waves x 64 px x 64 ch (64 KB)
-    H3CFG(2, 8, 4, 2, 1, 3),   // 17: 128 px x 256 ch, 8 waves (96 KB)
 };
 static const int kNumH3Configs = sizeof(kH3Configs) / sizeof(kH3Configs[0]);
 
