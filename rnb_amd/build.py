@@ -28,7 +28,8 @@ LIBRARIES = {
     "librnb_kernels.so": (["conv_igemm.hip", "conv_halo.hip", "conv_temporal.hip",
                            "video_ops.hip", "bn_ops.hip", "conv_halo_ws.hip", "conv21.hip",
                            "conv_f32.hip", "conv_wino_f32.hip", "conv_wino_x6.hip",
-                           "conv_x6.hip", "conv_h3.hip", "conv_h3stem.hip", "conv_h3p.hip"],
+                           "conv_x6.hip", "conv_h3.hip", "conv_h3stem.hip", "conv_h3p.hip",
+                           "conv_h3w.hip"],
                           [], []),
     "librnb_runtime.so": (["runtime.cpp"], [], []),
     "librnb_tracer.so": (["tracer.cpp"], [], ["-L%s/lib" % ROCM, "-lrocprofiler-sdk",

@@ -162,6 +162,14 @@ H3STEM_PIXELS = (256, 128, 448)
 # h3t weights; id H3P_BASE + v launches H3P_BPC[v] persistent blocks per CU
 H3P_BASE = 1440
 H3P_BPC = (1, 2)
+# Winograd F(2x2, 3x3) h3 kernel (csrc/conv_h3w.hip conv_h3w_kernel): 1x3x3
+# stride 1 pad 1 with Cin_p % 16 == 0, U = G g G^T split into fp16 hi / lo on
+# the host (h3w_weights), variant H3W_BASE + v of rnb_conv_h3w_launch (16 TC
+# output channels per work unit, TC = kernels().conv_h3w_tc(v))
+H3W_BASE = 1460
+# V = B^T d B is up to 4x the input: split after scaling by 2^4 keeps inputs
+# up to 2^10 in the fp16 range, as the direct kernels' 2^6
+H3W_IN_LOG2 = 4
 # activations are split after scaling by 2^H3_IN_LOG2: fp16 lo parts stay
 # normal for |a| >= 2^-9 and inputs up to 2^10 stay in the fp16 range
 H3_IN_LOG2 = 6
@@ -173,7 +181,18 @@ def is_h3(cid: int) -> bool:
     from .native import kernels
     return ((H3D_BASE <= cid < H3D_BASE + len(kernels().h3_configs))
             or H3K_BASE <= cid < H3K_BASE + len(H3K_CONFIGS) or is_h3r(cid)
-            or is_h3t(cid) or is_h3u(cid) or is_h3s(cid) or is_h3stem(cid) or is_h3p(cid))
+            or is_h3t(cid) or is_h3u(cid) or is_h3s(cid) or is_h3stem(cid) or is_h3p(cid)
+            or is_h3w(cid))
+
+
+def is_h3w(cid: int) -> bool:
+    from .native import kernels
+    return H3W_BASE <= cid < H3W_BASE + kernels().h3w_variants
+
+
+def h3w_enabled() -> bool:
+    """RNB_H3W=0 leaves the Winograd h3 kernel out of the autotune set."""
+    return os.environ.get("RNB_H3W", "1") != "0"
 
 
 def is_h3p(cid: int) -> bool:
@@ -320,6 +339,40 @@ def x6_direct_weights(wmat: torch.Tensor) -> torch.Tensor:
     return phys.permute(1, 0, 2, 3).contiguous().view(torch.int16)
 
 
+_WINO_SWZ = (0, 2, 3, 1)
+
+
+def h3w_weights(w: torch.Tensor, cin_p: int, cout: int, tc: int):
+    """[Cout, Cin, 1, 3, 3] weights -> (U, sw): the h3 Winograd kernel's
+    layout [Cin_p/16][n_cblocks][16 (x = 4i + j)][CT = 16 tc][4 chunks][8
+    fp16] as int16 of U = G g G^T (fp64) * 2^sw, sw putting max |U| in
+    [2^13, 2^14); per row and channel quad q the 16-B chunk (Uh[4] | Ul[4])
+    of the RNE split of the fp64 value (u = h + l to 22 bits), stored at
+    chunk q ^ _WINO_SWZ[(row % 16) >> 2] (csrc/conv_h3w.hip h3w_swz). Output
+    rows past Cout and input channels past Cin are zero."""
+    co, ci = w.shape[:2]
+    g = w.detach().double().cpu().reshape(co, ci, 3, 3)
+    G = torch.tensor(_WINO_G, dtype=torch.float64)
+    u = torch.einsum("ik,ockl,jl->ocij", G, g, G).reshape(co, ci, 16)
+    ct = 16 * tc
+    nb = (cout + ct - 1) // ct
+    full = torch.zeros(nb * ct, cin_p, 16, dtype=torch.float64)
+    full[:co, :ci] = u
+    m = float(full.abs().max()) if full.numel() else 0.0
+    sw = 0 if m == 0.0 else H3_W_TOP_LOG2 - int(math.floor(math.log2(m)))
+    a = full * (2.0 ** sw)
+    h = a.half()
+    lo = (a - h.double()).half()
+
+    def lay(t):                       # [rows, ci, 16x] -> [ci/16, nb, 16x, ct, quad, 4]
+        return t.reshape(nb, ct, cin_p // 16, 4, 4, 16).permute(2, 0, 5, 1, 3, 4)
+    logical = torch.cat([lay(h), lay(lo)], -1)                 # [..., quad, 8]
+    s = torch.tensor([_WINO_SWZ[(r % 16) >> 2] for r in range(ct)], dtype=torch.int64)
+    idx = torch.arange(4, dtype=torch.int64)[None, :] ^ s[:, None]      # [ct, 4]
+    phys = logical.gather(4, idx[None, None, None, :, :, None].expand_as(logical))
+    return phys.contiguous().view(torch.int16), sw
+
+
 def x6_enabled() -> bool:
     """RNB_X6=0 keeps the Winograd convs on the fp32 MFMA kernels."""
     return os.environ.get("RNB_X6", "1") != "0"
@@ -463,6 +516,7 @@ class ConvLayerF32:
         self._h3t = None                     # h3d_buffers in the per-tap padded K layout (h3t)
         self._h3stem = None                  # h3d_buffers in the stem kernel's K order
         self._x6k_ws: Dict[int, torch.Tensor] = {}
+        self._h3w: Dict[int, Tuple[torch.Tensor, int]] = {}   # tc -> (U, sw)
 
     def ksplit_for(self, cid: int, x_shape) -> int:
         """Blocks per tile of split-K config ``cid`` (x6 or h3) for this input:
@@ -581,6 +635,68 @@ class ConvLayerF32:
             u = self._wino_u[key] = fn(w, nco, tc, x6=x6).to(self.device)
         return u
 
+    def h3w_u(self, tc: int) -> Tuple[torch.Tensor, int]:
+        """(U, sw) of the h3 Winograd kernel with 16 tc channels per unit
+        (``h3w_weights``), built once per tc."""
+        got = self._h3w.get(tc)
+        if got is None:
+            u, sw = h3w_weights(self.w_ref, self.geom.cin_p, self.geom.cout_p, tc)
+            got = self._h3w[tc] = (u.to(self.device), sw)
+        return got
+
+    def _launch_h3w(self, x, y, residual, cid, stream, in_affine=None, out_stats=None):
+        """One h3w launch over x [N, T, H, W, Cin_p] -> y (see _launch_wino)."""
+        from .native import WinoParams, kernels
+        g = self.geom
+        N, T, H, W, C = x.shape
+        if not (self.wino_ok and x.is_contiguous() and y.is_contiguous() and C == g.cin_p
+                and tuple(y.shape[:4]) == (N, T, H, W) and y.shape[-1] >= g.cout_p
+                and (residual is None or (residual.is_contiguous()
+                                          and tuple(residual.shape[:4]) == (N, T, H, W)
+                                          and residual.shape[-1] >= g.cout_p))):
+            raise ValueError("%s: h3w operands do not match the conv geometry: x %s y %s"
+                             % (self.name, tuple(x.shape), tuple(y.shape)))
+        k = kernels()
+        variant = cid - H3W_BASE
+        u, sw = self.h3w_u(k.conv_h3w_tc(variant))
+        p = WinoParams()
+        p.x, p.u = x.data_ptr(), u.data_ptr()
+        p.bias = self.bias.data_ptr()
+        p.res = residual.data_ptr() if residual is not None else None
+        p.y = y.data_ptr()
+        p.F, p.H, p.W, p.Cin = N * T, H, W, C
+        p.Cout = g.cout_p
+        p.y_stride = y.shape[-1]
+        p.res_stride = residual.shape[-1] if residual is not None else 0
+        p.relu = 1 if self.relu else 0
+        p.clip_frames = T
+        if in_affine is not None:
+            ss, aseg = in_affine
+            if (ss.dim() != 3 or ss.shape[1:] != (2, C) or ss.dtype != torch.float32
+                    or not ss.is_contiguous() or aseg.dtype != torch.int32
+                    or aseg.numel() != N or not aseg.is_contiguous()):
+                raise ValueError("%s: input BN scale/shift %s / clip_seg %s do not match x %s"
+                                 % (self.name, tuple(ss.shape), tuple(aseg.shape),
+                                    tuple(x.shape)))
+            p.in_ss, p.clip_seg = ss.data_ptr(), aseg.data_ptr()
+        if out_stats is not None:
+            sums, clip_seg = out_stats
+            if (sums.dim() != 3 or sums.shape[1] != 2 or sums.shape[2] < g.cout_p
+                    or sums.dtype != torch.float64 or not sums.is_contiguous()
+                    or clip_seg.dtype != torch.int32 or clip_seg.numel() != N
+                    or not clip_seg.is_contiguous()
+                    or (in_affine is not None and in_affine[1].data_ptr() != clip_seg.data_ptr())):
+                raise ValueError("%s: output BN sums %s / clip_seg %s do not match y %s"
+                                 % (self.name, tuple(sums.shape), tuple(clip_seg.shape),
+                                    tuple(y.shape)))
+            p.out_stats, p.clip_seg = sums.data_ptr(), clip_seg.data_ptr()
+            p.stats_c = sums.shape[2]
+        # the activation scale is folded into the input BN's scale / shift
+        # (AFF) or applied before the split
+        in_scale = float(2.0 ** H3W_IN_LOG2)
+        out_scale = float(2.0 ** -(H3W_IN_LOG2 + sw))
+        k.conv_h3w(p, variant, stream.cuda_stream, in_scale, out_scale)
+
     def wino_parts(self, cid: int):
         """[(co0, nco, tc, variant)] launches of Winograd config ``cid``: the
         split-transform spatial variants cover a cout_p that is not a multiple
@@ -621,6 +737,8 @@ class ConvLayerF32:
             if self.h3r_ok(x_shape):
                 c += [H3R_BASE + i for i in range(kernels().h3r_variants)
                       if self.h3r_fits(i, x_shape)]
+            if self.wino_ok and h3w_enabled():
+                c += [H3W_BASE + i for i in range(kernels().h3w_variants)]
             # the stride-2 row-band kernel lost to the h3 direct configs on every
             # R(2+1)D-34 stride-2 spatial conv (profiles/r5_layers_stride2_h3s_128clips.txt):
             # left out of the autotune set (tuning time) unless RNB_H3S=1
@@ -946,7 +1064,7 @@ class ConvLayerF32:
         if is_h3s(cid) or is_h3stem(cid):
             return False
         if (cid in WINO_TEMPORAL or is_h3r(cid) or is_h3t(cid) or is_h3u(cid)
-                or is_h3p(cid)):
+                or is_h3p(cid) or is_h3w(cid)):
             return True
         if not is_h3(cid):
             return False
@@ -970,6 +1088,17 @@ class ConvLayerF32:
                 self._launch_wino(x[n0:n1], y[n0:n1],
                                   residual[n0:n1] if residual is not None else None, cid,
                                   stream, aff, ost)
+            return
+        if is_h3w(cid):
+            step = self.chunk_clips(x.shape, y.shape,
+                                    residual.shape[-1] if residual is not None else 0)
+            for n0 in range(0, N, step):
+                n1 = min(N, n0 + step)
+                aff = None if in_affine is None else (in_affine[0], in_affine[1][n0:n1])
+                ost = None if out_stats is None else (out_stats[0], out_stats[1][n0:n1])
+                self._launch_h3w(x[n0:n1], y[n0:n1],
+                                 residual[n0:n1] if residual is not None else None, cid,
+                                 stream, aff, ost)
             return
         x6 = is_x6d(cid)
         if (in_affine is not None and not is_h3(cid)) or (out_stats is not None and not x6):

@@ -382,6 +382,11 @@ class Kernels:
         lib.rnb_conv_h3p_launch.restype = ctypes.c_int
         lib.rnb_conv_h3p_ok.argtypes = [ctypes.c_int] * 5
         lib.rnb_conv_h3p_ok.restype = ctypes.c_int
+        lib.rnb_conv_h3w_launch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                            ctypes.c_float, ctypes.c_float]
+        lib.rnb_conv_h3w_launch.restype = ctypes.c_int
+        lib.rnb_conv_h3w_tc.argtypes = [ctypes.c_int]
+        lib.rnb_conv_h3w_tc.restype = ctypes.c_int
         lib.rnb_h3_set_range_flag.argtypes = [ctypes.c_void_p]
         lib.rnb_h3_set_range_flag.restype = None
         lib.rnb_conv_h3t_pixels.restype = ctypes.c_int
@@ -416,6 +421,7 @@ class Kernels:
         self.x6r_variants = lib.rnb_conv_x6r_num_variants()
         self.h3r_variants = lib.rnb_conv_h3r_num_variants()
         self.h3t_variants = lib.rnb_conv_h3t_num_variants()
+        self.h3w_variants = lib.rnb_conv_h3w_num_variants()
         self.h3u_variants = self.exp.rnb_conv_h3u_num_variants() if self.exp else 0
         self.h3s_variants = self.exp.rnb_conv_h3s_num_variants() if self.exp else 0
         self.h3stem_variants = lib.rnb_conv_h3stem_num_variants()
@@ -538,6 +544,20 @@ class Kernels:
                                             sums or None, clip_seg or None, stats_c, in_scale,
                                             out_scale, in_ss or None, in_seg or None),
                "conv_h3p (%d blocks per CU)" % blocks_per_cu)
+
+    def conv_h3w(self, params: "WinoParams", variant: int, stream: int, in_scale: float,
+                 out_scale: float) -> None:
+        """Winograd F(2x2, 3x3) h3 conv (csrc/conv_h3w.hip: 1x3x3 stride 1 pad 1,
+        Cin_p % 16 == 0, U split into fp16 hi / lo on the host --
+        ConvLayerF32.h3w_u); input BN on load when ``params.in_ss`` is set,
+        epilogue BN sums when ``params.out_stats`` is set."""
+        _check(self.lib.rnb_conv_h3w_launch(ctypes.byref(params), variant, stream, in_scale,
+                                            out_scale),
+               "conv_h3w (variant %d)" % variant)
+
+    def conv_h3w_tc(self, variant: int) -> int:
+        """16-channel groups per work unit of h3w variant ``variant``."""
+        return int(self.lib.rnb_conv_h3w_tc(variant))
 
     def conv_h3p_ok(self, T: int, H: int, W: int, Cin_p: int, Cout_p: int) -> bool:
         return bool(self.lib.rnb_conv_h3p_ok(T, H, W, Cin_p, Cout_p))

@@ -38,12 +38,15 @@ CASES = {
     "k5": (64, 230, (1, 3, 3), (1, 2, 2), (0, 1, 1), (8, 56, 56), False, True),
     "k6": (230, 128, (3, 1, 1), (2, 1, 1), (1, 0, 0), (8, 28, 28), True, True),
     "k7": (128, 288, (1, 3, 3), (1, 1, 1), (0, 1, 1), (4, 28, 28), False, True),
+    "k7a": (128, 288, (1, 3, 3), (1, 1, 1), (0, 1, 1), (4, 28, 28), True, True),
     "k8": (288, 128, (3, 1, 1), (1, 1, 1), (1, 0, 0), (4, 28, 28), True, True),
     "k11": (128, 460, (1, 3, 3), (1, 2, 2), (0, 1, 1), (4, 28, 28), False, True),
     "k13": (256, 576, (1, 3, 3), (1, 1, 1), (0, 1, 1), (2, 14, 14), False, True),
+    "k13a": (256, 576, (1, 3, 3), (1, 1, 1), (0, 1, 1), (2, 14, 14), True, True),
     "k14": (576, 256, (3, 1, 1), (1, 1, 1), (1, 0, 0), (2, 14, 14), True, True),
     "k17": (256, 921, (1, 3, 3), (1, 2, 2), (0, 1, 1), (2, 14, 14), False, True),
     "k19": (512, 1152, (1, 3, 3), (1, 1, 1), (0, 1, 1), (1, 7, 7), False, True),
+    "k19a": (512, 1152, (1, 3, 3), (1, 1, 1), (0, 1, 1), (1, 7, 7), True, True),
     "k20": (1152, 512, (3, 1, 1), (1, 1, 1), (1, 0, 0), (1, 7, 7), True, True),
     "k12": (460, 256, (3, 1, 1), (2, 1, 1), (1, 0, 0), (4, 14, 14), True, True),
     "k18": (921, 512, (3, 1, 1), (2, 1, 1), (1, 0, 0), (2, 7, 7), True, True),
