@@ -64,17 +64,48 @@ static __device__ __forceinline__ bool h3w_nonfinite(const wf32x4& v) {
          __builtin_amdgcn_classf(v[2], 0x207) | __builtin_amdgcn_classf(v[3], 0x207);
 }
 
+// B operands of one GEMM step as one 6-register tuple R = (H01 H23 L01 L23
+// H01 H23): the two MFMA B operands are the overlapping quads R[0:4] =
+// (Vh ; Vl) and R[2:6] = (Vl ; Vh), so with A = (Uh | Ul)
+//   (Uh | Ul) x (Vh ; Vl) = Uh Vh + Ul Vl,   (Uh | Ul) x (Vl ; Vh) = Uh Vl + Ul Vh
+// -- all four products, and only H is stored twice (no per-operand copies)
 struct H3WB {
-  wu32x4 hh, ll;      // (Vh ; Vh), (Vl ; Vl)
+  wu32x8 r;
 };
 
-// split 4 fp32 values (already scaled) into the two B operands
+// a - b on fp32 pairs in one v_pk_add_f32 (negated second operand; the
+// compiler splits a wf32x2 subtraction into two v_sub_f32)
+static __device__ __forceinline__ wf32x2 h3w_pk_sub(const wf32x2& a, const wf32x2& b) {
+  wf32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// sum over the 16 lanes of a DPP row (quad swaps, half-row and row mirrors;
+// as x6d_common.h x6d_row16_sum)
+static __device__ __forceinline__ float h3w_row16_sum(float v) {
+  int t, iv;
+  iv = __float_as_int(v);
+  t = __builtin_amdgcn_update_dpp(iv, iv, 0xB1, 0xF, 0xF, false);
+  v += __int_as_float(t);
+  iv = __float_as_int(v);
+  t = __builtin_amdgcn_update_dpp(iv, iv, 0x4E, 0xF, 0xF, false);
+  v += __int_as_float(t);
+  iv = __float_as_int(v);
+  t = __builtin_amdgcn_update_dpp(iv, iv, 0x141, 0xF, 0xF, false);
+  v += __int_as_float(t);
+  iv = __float_as_int(v);
+  t = __builtin_amdgcn_update_dpp(iv, iv, 0x140, 0xF, 0xF, false);
+  return v + __int_as_float(t);
+}
+
+// split 4 fp32 values (already scaled) into the B tuple
 static __device__ __forceinline__ H3WB h3w_split(const wf32x4& v) {
   uint32_t h[2], l[2];
   h3_split4(v, h, l);
+  const wu32x4 hl = (wu32x4){h[0], h[1], l[0], l[1]};
   H3WB b;
-  b.hh = (wu32x4){h[0], h[1], h[0], h[1]};
-  b.ll = (wu32x4){l[0], l[1], l[0], l[1]};
+  b.r = __builtin_shufflevector(hl, hl, 0, 1, 2, 3, 0, 1, -1, -1);   // R[6:8] unused
   return b;
 }
 
@@ -97,14 +128,18 @@ static __device__ __forceinline__ void h3w_read_a(wu32x4 (&a)[TC], const char* u
   for (int tc = 0; tc < TC; ++tc) a[tc] = *(const wu32x4*)(ub + (x * CT + tc * 16 + frow) * 64 + c);
 }
 
-// one GEMM step: the small products first, TC chains interleaved
-template <int TC>
+// one GEMM step: the cross products first, TC chains interleaved; Z = the
+// unit's first chunk (the accumulators start from the MFMA's zero operand)
+template <int TC, bool Z>
 static __device__ __forceinline__ void h3w_step(wf32x4 (&acc)[TC], const wu32x4 (&a)[TC],
                                                 const H3WB& b) {
+  const wu32x4 hl = __builtin_shufflevector(b.r, b.r, 0, 1, 2, 3);
+  const wu32x4 lh = __builtin_shufflevector(b.r, b.r, 2, 3, 4, 5);
 #pragma unroll
-  for (int tc = 0; tc < TC; ++tc) acc[tc] = h3_mma(a[tc], b.ll, acc[tc]);
+  for (int tc = 0; tc < TC; ++tc)
+    acc[tc] = h3_mma(a[tc], lh, Z ? (wf32x4){0.f, 0.f, 0.f, 0.f} : acc[tc]);
 #pragma unroll
-  for (int tc = 0; tc < TC; ++tc) acc[tc] = h3_mma(a[tc], b.hh, acc[tc]);
+  for (int tc = 0; tc < TC; ++tc) acc[tc] = h3_mma(a[tc], hl, acc[tc]);
 }
 
 // U chunk staging: a linear LDS-DMA copy of NBYTES (whole 1-KB instructions)
@@ -124,17 +159,16 @@ static __device__ __forceinline__ void h3w_issue_u(const __amdgpu_buffer_rsrc_t&
   }
 }
 
-// VALU ops per MFMA to interleave per step: split (8) + its share of the
-// transform (4) + the activation scale (2) or the input BN (8)
-#define H3W_VALU_PER_MFMA(TC, AFF) (((AFF) ? 20 : 14) + 2 * (TC) - 1) / (2 * (TC))
+// VALU ops per MFMA to interleave per step: split (8) + the B tuple (2) +
+// its share of the transform (4) + the activation scale (2) or the input BN (8)
+#define H3W_VALU_PER_MFMA(TC, AFF) ((((AFF) ? 22 : 16) + 2 * (TC) - 1) / (2 * (TC)))
 
 template <int TC, int WAVES, bool ST, bool AFF>
 __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParams p,
                                                                  const H3WExtra ex) {
   constexpr int CT = 16 * TC, NT = 16 * WAVES;
   constexpr int U_BYTES = 16 * CT * 64;                 // one chunk: 16 x CT rows of 64 B
-  static_assert(NT * (CT + 1) * 8 + 64 * WAVES * 8 * 2 <= U_BYTES,
-                "epilogue statistics scratch fits one U buffer");
+  static_assert(CT * 16 <= U_BYTES, "epilogue statistics scratch fits one U buffer");
   __shared__ __attribute__((aligned(16))) char lds[2 * U_BYTES];
 
   const int lane = threadIdx.x & 63;
@@ -156,15 +190,13 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
   int unit = lo_u + (blockIdx.x >> 3);
   if (unit >= hi_u) return;                            // more blocks than units here
 
-  // per-unit state of the lane: tile coordinates, patch row offsets (or
-  // H3W_OOB for padding rows), padding columns, and what the epilogue needs
-  // (bias, video of the tile, whether the block's tiles are one video),
-  // loaded when the unit is set so that the epilogue issues no loads behind
-  // the next unit's prefetch (vmcnt is in order)
-  int cb = 0, tb = 0, f = 0, ty = 0, tx = 0, cmask = 0, seg = 0, bseg = 0;
-  bool tvalid = false, buni = false;
-  uint32_t rowoff[4];
-  wf32x4 bias[TC];
+  // per-unit state of the lane: tile coordinates, the byte offset of each
+  // patch element (chunk 0; H3W_OOB for padding: out-of-range buffer loads
+  // give 0, and a chunk's byte offset goes into the scalar offset), and the
+  // video of the tile
+  int cb = 0, tb = 0, f = 0, ty = 0, tx = 0, seg = 0;
+  bool tvalid = false;
+  uint32_t voff[16];
   float emask[16];                                     // AFF: 1 = in-frame element
   const float* ssrow = nullptr;                        // AFF: in_ss row of the lane's video
   auto set_unit = [&](int u) {
@@ -180,49 +212,24 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
       ty = t1 - f * p.tiles_h;
     }
     const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
-    int rmask = 0;
-    cmask = 0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      rmask |= (tvalid && y0 + d >= 0 && y0 + d < p.H) ? (1 << d) : 0;
-      cmask |= (x0 + d >= 0 && x0 + d < p.W) ? (1 << d) : 0;
-    }
     const int pix0 = (f * p.H + y0) * p.W + x0;        // may be negative (padding)
+    const uint32_t base = (uint32_t)(pix0 * p.Cin * 4 + q * 16);
 #pragma unroll
-    for (int dy = 0; dy < 4; ++dy)
-      rowoff[dy] = ((rmask >> dy) & 1) ? (uint32_t)(pix0 * p.Cin * 4 + q * 16 + dy * row_bytes)
-                                       : H3W_OOB;
-    if constexpr (AFF) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e)
-        emask[e] = (((rmask >> (e >> 2)) & 1) && ((cmask >> (e & 3)) & 1)) ? 1.f : 0.f;
+    for (int e = 0; e < 16; ++e) {
+      const int dy = e >> 2, dx = e & 3;
+      const bool ok = tvalid && y0 + dy >= 0 && y0 + dy < p.H && x0 + dx >= 0 && x0 + dx < p.W;
+      voff[e] = ok ? base + (uint32_t)(dy * row_bytes) + (uint32_t)dx * cin4 : H3W_OOB;
+      if constexpr (AFF) emask[e] = ok ? 1.f : 0.f;
     }
-    if constexpr (AFF || ST) {
-      seg = tvalid ? p.clip_seg[f / p.clip_frames] : 0;
-      if constexpr (AFF) ssrow = p.in_ss + (size_t)seg * 2 * p.Cin + 4 * q;
-    }
-    if constexpr (ST) {
-      // statistics: one LDS reduction per block when its tiles are one video
-      // (first and last valid tile: clips are in video order)
-      const int ta = tb * NT, tz = min(tb * NT + NT - 1, p.n_tiles - 1);
-      const int fa = w_div(w_div(ta, p.m_tw, p.s_tw), p.m_th, p.s_th);
-      const int fz = w_div(w_div(tz, p.m_tw, p.s_tw), p.m_th, p.s_th);
-      bseg = __builtin_amdgcn_readfirstlane(p.clip_seg[fa / p.clip_frames]);
-      buni = bseg == __builtin_amdgcn_readfirstlane(p.clip_seg[fz / p.clip_frames]);
-    }
-#pragma unroll
-    for (int tc = 0; tc < TC; ++tc) {
-      const int co = min(cb * CT + tc * 16 + 4 * q, p.Cout - 4);
-      const float4 b4 = *(const float4*)(p.bias + co);
-      bias[tc] = (wf32x4){b4.x, b4.y, b4.z, b4.w};
-    }
+    if constexpr (AFF || ST) seg = tvalid ? p.clip_seg[f / p.clip_frames] : 0;
+    if constexpr (AFF) ssrow = p.in_ss + (size_t)seg * 2 * p.Cin + 4 * q;
   };
 
+  // chunk `chunk`'s element e of the lane's patch; chunk < 0: a load of
+  // nothing (out of range) that keeps the memory sequence of every chunk equal
   auto load_one = [&](int chunk, int e) -> wf32x4 {
-    const int dy = e >> 2, dx = e & 3;
-    const uint32_t off = ((cmask >> dx) & 1) ? rowoff[dy] + (uint32_t)(dx * cin4 + chunk * 64)
-                                             : H3W_OOB;
-    return __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+    const uint32_t so = chunk >= 0 ? (uint32_t)chunk * 64u : p.x_bytes;
+    return __builtin_amdgcn_raw_buffer_load_b128(xr, voff[e], so, 0);
   };
   auto issue_u = [&](int chunk, int buf) {
     const uint32_t base = ((uint32_t)chunk * (uint32_t)p.n_cblocks + (uint32_t)cb) * U_BYTES;
@@ -263,7 +270,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
       const wf32x2 b1 = (wf32x2){v[r * 4 + 1][2 * hf], v[r * 4 + 1][2 * hf + 1]};
       const wf32x2 b2 = (wf32x2){v[r * 4 + 2][2 * hf], v[r * 4 + 2][2 * hf + 1]};
       const wf32x2 b3 = (wf32x2){v[r * 4 + 3][2 * hf], v[r * 4 + 3][2 * hf + 1]};
-      const wf32x2 o[4] = {b0 - b2, b1 + b2, b2 - b1, b1 - b3};
+      const wf32x2 o[4] = {h3w_pk_sub(b0, b2), b1 + b2, h3w_pk_sub(b2, b1), h3w_pk_sub(b1, b3)};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         v[r * 4 + j][2 * hf] = o[j][0];
@@ -276,7 +283,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
     for (int hf = 0; hf < 2; ++hf) {
       const wf32x2 x = (wf32x2){a[2 * hf], a[2 * hf + 1]};
       const wf32x2 y = (wf32x2){b[2 * hf], b[2 * hf + 1]};
-      const wf32x2 z = add ? x + y : x - y;
+      const wf32x2 z = add ? x + y : h3w_pk_sub(x, y);
       dst[2 * hf] = z[0];
       dst[2 * hf + 1] = z[1];
     }
@@ -315,14 +322,15 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
   // GEMM steps in V-row order 0, 2, 1, 3: the next chunk's refill loads go out
   // in that order, so it starts on V row 0 (patch rows 0 and 2) while rows 1 /
   // 3 are in flight. Pipelined one step ahead: step k+1's split (VALU) and A
-  // fragments (LDS) under step k's 2 TC MFMAs.
+  // fragments (LDS) under step k's 2 TC MFMAs. V[x]'s registers are refilled
+  // with element x of chunk `next` (< 0: nothing) once step x has split it.
   constexpr int perm[16] = {0, 1, 2, 3, 8, 9, 10, 11, 4, 5, 6, 7, 12, 13, 14, 15};
-  auto gemm = [&](const char* ub, wf32x4 (&v)[16], int next, auto refill) {
-    constexpr bool RF = decltype(refill)::value;
+  auto gemm = [&](const char* ub, wf32x4 (&v)[16], int next, auto first) {
+    constexpr bool Z = decltype(first)::value;
     wu32x4 af[2][TC];
     H3WB bf[2];
     bf[0] = split(v[0]);
-    if constexpr (RF) v[0] = load_one(next, 0);
+    v[0] = load_one(next, 0);
     h3w_read_a<TC>(af[0], ub, 0, frow, q);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -331,10 +339,10 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
         const int xn = perm[k + 1];
         if (k + 1 == 4) transform_b(v);
         bf[(k + 1) & 1] = split(v[xn]);
-        if constexpr (RF) v[xn] = load_one(next, xn);
+        v[xn] = load_one(next, xn);
         h3w_read_a<TC>(af[(k + 1) & 1], ub, xn, frow, q);
       }
-      h3w_step<TC>(acc[x], af[k & 1], bf[k & 1]);
+      h3w_step<TC, Z>(acc[x], af[k & 1], bf[k & 1]);
       if (k + 1 < 16) {
 #pragma unroll
         for (int i = 0; i < 2 * TC; ++i) {
@@ -342,7 +350,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
           if (i < TC) __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);              // DS read
           __builtin_amdgcn_sched_group_barrier(0x0002, H3W_VALU_PER_MFMA(TC, AFF), 0); // VALU
         }
-        if constexpr (RF) __builtin_amdgcn_sched_group_barrier(0x0020, 1, 0);          // VMEM read
+        __builtin_amdgcn_sched_group_barrier(0x0020, 1, 0);                            // VMEM read
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -357,22 +365,24 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
 #pragma unroll
   for (int e = 0; e < 16; ++e) d[e] = load_one(0, e);
   while (true) {
-#pragma unroll
-    for (int x = 0; x < 16; ++x)
-#pragma unroll
-      for (int c = 0; c < TC; ++c) acc[x][c] = (wf32x4){0.f, 0.f, 0.f, 0.f};
     // the unit's chunk 0 (U DMA, scale / shift, patch) was issued before the
     // previous unit's epilogue (or just above)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int c = 0; c + 1 < nchunks; ++c) {
+    // chunk 0 peeled (its MFMAs start from zero accumulators); the last
+    // chunk refills nothing (out-of-range loads): the accumulators stay in
+    // place, no copies at a loop exit
+    auto chunk = [&](int c, auto first) {
       const int cur = g & 1;
-      issue_u(c + 1, cur ^ 1);
-      if constexpr (AFF) load_ss(c + 1, scn, shn);
+      const bool more = c + 1 < nchunks;             // uniform
+      if (more) {
+        issue_u(c + 1, cur ^ 1);
+        if constexpr (AFF) load_ss(c + 1, scn, shn);
+      }
       // keep the U DMA (and scale / shift) ahead of the patch loads in issue order
       asm volatile("" ::: "memory");
       transform_a(d);
-      gemm(lds + cur * U_BYTES, d, c + 1, std::true_type{});
+      gemm(lds + cur * U_BYTES, d, more ? c + 1 : -1, first);
       ++g;
       if constexpr (AFF) {
         sc = scn;
@@ -381,20 +391,34 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
       // U of chunk c+1 landed; the 16 younger patch loads may stay in flight
       asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       __syncthreads();
-    }
-    transform_a(d);
-    gemm(lds + (g & 1) * U_BYTES, d, -1, std::false_type{});
-    ++g;
-    // every wave is done with this unit's last U buffer: it holds the
-    // epilogue's statistics scratch; the next unit's chunk 0 goes to the other
-    __syncthreads();
+    };
+    chunk(0, std::true_type{});
+    for (int c = 1; c < nchunks; ++c) chunk(c, std::false_type{});
+    // every wave is done with this unit's last U buffer (the barrier above):
+    // it holds the epilogue's statistics; the next unit's chunk 0 goes to the other
     const int nxt = unit + per_x;
-    // this unit's state for its epilogue, before set_unit moves on
-    const int e_cb = cb, e_f = f, e_ty = ty, e_tx = tx, e_seg = seg, e_bseg = bseg;
-    const bool e_valid = tvalid, e_buni = buni;
-    wf32x4 e_bias[TC];
+    const int e_cb = cb, e_f = f, e_ty = ty, e_tx = tx, e_seg = seg, e_tb = tb;
+    const bool e_valid = tvalid;
+    // the epilogue's own loads (bias, videos) before the next unit's prefetch:
+    // waiting for them does not wait for the prefetch (vmcnt is in order)
+    wf32x4 bias[TC];
 #pragma unroll
-    for (int tc = 0; tc < TC; ++tc) e_bias[tc] = bias[tc];
+    for (int tc = 0; tc < TC; ++tc) {
+      const int co = min(e_cb * CT + tc * 16 + 4 * q, p.Cout - 4);
+      const float4 b4 = *(const float4*)(p.bias + co);
+      bias[tc] = (wf32x4){b4.x, b4.y, b4.z, b4.w};
+    }
+    int bseg = 0;
+    bool buni = false;
+    if constexpr (ST) {
+      // one LDS reduction per block when its tiles are one video (first and
+      // last valid tile: clips are in video order)
+      const int ta = e_tb * NT, tz = min(e_tb * NT + NT - 1, p.n_tiles - 1);
+      const int fa = w_div(w_div(ta, p.m_tw, p.s_tw), p.m_th, p.s_th);
+      const int fz = w_div(w_div(tz, p.m_tw, p.s_tw), p.m_th, p.s_th);
+      bseg = __builtin_amdgcn_readfirstlane(p.clip_seg[fa / p.clip_frames]);
+      buni = bseg == __builtin_amdgcn_readfirstlane(p.clip_seg[fz / p.clip_frames]);
+    }
     if (nxt < hi_u) {
       set_unit(nxt);
       issue_u(0, g & 1);
@@ -403,20 +427,30 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
 #pragma unroll
       for (int e = 0; e < 16; ++e) d[e] = load_one(0, e);
     }
-    char* scratch = lds + ((g - 1) & 1) * U_BYTES;
+    double* red = (double*)(lds + ((g - 1) & 1) * U_BYTES);   // [CT][2] block sums
+    if constexpr (ST) {
+      if (buni) {
+        for (int i = threadIdx.x; i < CT * 2; i += 64 * WAVES) red[i] = 0.0;
+        __syncthreads();
+      }
+    }
 
     // ---- epilogue: Y = A^T M A, * out_scale + bias (+ residual) (ReLU),
-    // range guard, stores, per-video BN sums ----
+    // range guard, stores, per-video BN sums (fp32 over the lane's 2x2
+    // pixels and the 16 tiles of a DPP row, fp64 from there) ----
     const int oy = 2 * e_ty, ox = 2 * e_tx;
     const bool has_res = p.res != nullptr;
     bool bad = false;
-    double s1[TC][4], s2[TC][4];
+    bool wmixed = false;
+    if constexpr (ST) {
+      const int s0 = __builtin_amdgcn_readfirstlane(e_seg);
+      wmixed = __ballot(e_valid && e_seg != s0) != 0;
+    }
 #pragma unroll
     for (int tc = 0; tc < TC; ++tc) {
       const int co = e_cb * CT + tc * 16 + 4 * q;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) s1[tc][k] = s2[tc][k] = 0.0;
       const bool live = co < p.Cout && e_valid;
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
       if (live) {
         wf32x4 t0[4], t1[4];
 #pragma unroll
@@ -425,10 +459,10 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
           t1[j] = acc[1 * 4 + j][tc] - acc[2 * 4 + j][tc] - acc[3 * 4 + j][tc];
         }
         wf32x4 o[2][2];
-        o[0][0] = (t0[0] + t0[1] + t0[2]) * ex.out_scale + e_bias[tc];
-        o[0][1] = (t0[1] - t0[2] - t0[3]) * ex.out_scale + e_bias[tc];
-        o[1][0] = (t1[0] + t1[1] + t1[2]) * ex.out_scale + e_bias[tc];
-        o[1][1] = (t1[1] - t1[2] - t1[3]) * ex.out_scale + e_bias[tc];
+        o[0][0] = (t0[0] + t0[1] + t0[2]) * ex.out_scale + bias[tc];
+        o[0][1] = (t0[1] - t0[2] - t0[3]) * ex.out_scale + bias[tc];
+        o[1][0] = (t1[0] + t1[1] + t1[2]) * ex.out_scale + bias[tc];
+        o[1][1] = (t1[1] - t1[2] - t1[3]) * ex.out_scale + bias[tc];
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -449,18 +483,56 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
             if constexpr (ST) {
 #pragma unroll
               for (int k = 0; k < 4; ++k) {
-                s1[tc][k] += (double)val[k];
-                s2[tc][k] += (double)val[k] * (double)val[k];
+                s1[k] += val[k];
+                s2[k] = fmaf(val[k], val[k], s2[k]);
               }
             }
           }
       }
       if constexpr (ST) {
-        if (!e_buni) w_commit_stats(p, lane, live, e_seg, co, s1[tc], s2[tc]);
+        if (!wmixed) {
+          // the wave's tiles are one video: 16-lane DPP sums (a DPP row = the
+          // 16 tiles of channel quad q), one lane per row commits
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            s1[k] = h3w_row16_sum(s1[k]);
+            s2[k] = h3w_row16_sum(s2[k]);
+          }
+          if (frow == 0 && co < p.Cout) {
+            if (buni) {
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                atomicAdd(red + (tc * 16 + 4 * q + k) * 2, (double)s1[k]);
+                atomicAdd(red + (tc * 16 + 4 * q + k) * 2 + 1, (double)s2[k]);
+              }
+            } else {
+              const int s0 = __builtin_amdgcn_readfirstlane(e_seg);
+              double* dst = p.out_stats + (size_t)s0 * 2 * p.stats_c + co;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                atomicAdd(dst + k, (double)s1[k]);
+                atomicAdd(dst + p.stats_c + k, (double)s2[k]);
+              }
+            }
+          }
+        } else if (live) {
+          double* dst = p.out_stats + (size_t)e_seg * 2 * p.stats_c + co;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            atomicAdd(dst + k, (double)s1[k]);
+            atomicAdd(dst + p.stats_c + k, (double)s2[k]);
+          }
+        }
       }
     }
     if constexpr (ST) {
-      if (e_buni) w_block_stats<TC, WAVES>(p, scratch, wave, tl, q, e_cb, e_bseg, s1, s2);
+      if (buni) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < CT * 2; i += 64 * WAVES) {
+          const int co = e_cb * CT + (i >> 1);
+          if (co < p.Cout) atomicAdd(p.out_stats + ((size_t)bseg * 2 + (i & 1)) * p.stats_c + co, red[i]);
+        }
+      }
     }
     if (bad) *ex.oflag = 1;
 
