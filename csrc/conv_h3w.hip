@@ -56,6 +56,7 @@ struct H3WExtra {
   float in_scale;     // power-of-two scale of the activations before the split
   float out_scale;    // 2^-(in + weight scale): accumulators -> conv output
   int* oflag;         // range guard (host-coherent word) or null
+  const int* out_seg; // ST: video of each clip for the output sums (p.clip_seg: the input BN's)
 };
 
 // true when any element of v is +-inf or NaN (v_cmp_class)
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
   // patch element (chunk 0; H3W_OOB for padding: out-of-range buffer loads
   // give 0, and a chunk's byte offset goes into the scalar offset), and the
   // video of the tile
-  int cb = 0, tb = 0, f = 0, ty = 0, tx = 0, seg = 0;
+  int cb = 0, tb = 0, f = 0, ty = 0, tx = 0, seg = 0, sseg = 0;
   bool tvalid = false;
   uint32_t voff[16];
   float emask[16];                                     // AFF: 1 = in-frame element
@@ -221,8 +222,11 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
       voff[e] = ok ? base + (uint32_t)(dy * row_bytes) + (uint32_t)dx * cin4 : H3W_OOB;
       if constexpr (AFF) emask[e] = ok ? 1.f : 0.f;
     }
-    if constexpr (AFF || ST) seg = tvalid ? p.clip_seg[f / p.clip_frames] : 0;
-    if constexpr (AFF) ssrow = p.in_ss + (size_t)seg * 2 * p.Cin + 4 * q;
+    if constexpr (AFF) {
+      seg = tvalid ? p.clip_seg[f / p.clip_frames] : 0;
+      ssrow = p.in_ss + (size_t)seg * 2 * p.Cin + 4 * q;
+    }
+    if constexpr (ST) sseg = tvalid ? ex.out_seg[f / p.clip_frames] : 0;
   };
 
   // chunk `chunk`'s element e of the lane's patch; chunk < 0: a load of
@@ -397,7 +401,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
     // every wave is done with this unit's last U buffer (the barrier above):
     // it holds the epilogue's statistics; the next unit's chunk 0 goes to the other
     const int nxt = unit + per_x;
-    const int e_cb = cb, e_f = f, e_ty = ty, e_tx = tx, e_seg = seg, e_tb = tb;
+    const int e_cb = cb, e_f = f, e_ty = ty, e_tx = tx, e_seg = sseg, e_tb = tb;
     const bool e_valid = tvalid;
     // the epilogue's own loads (bias, videos) before the next unit's prefetch:
     // waiting for them does not wait for the prefetch (vmcnt is in order)
@@ -416,8 +420,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
       const int ta = e_tb * NT, tz = min(e_tb * NT + NT - 1, p.n_tiles - 1);
       const int fa = w_div(w_div(ta, p.m_tw, p.s_tw), p.m_th, p.s_th);
       const int fz = w_div(w_div(tz, p.m_tw, p.s_tw), p.m_th, p.s_th);
-      bseg = __builtin_amdgcn_readfirstlane(p.clip_seg[fa / p.clip_frames]);
-      buni = bseg == __builtin_amdgcn_readfirstlane(p.clip_seg[fz / p.clip_frames]);
+      bseg = __builtin_amdgcn_readfirstlane(ex.out_seg[fa / p.clip_frames]);
+      buni = bseg == __builtin_amdgcn_readfirstlane(ex.out_seg[fz / p.clip_frames]);
     }
     if (nxt < hi_u) {
       set_unit(nxt);
@@ -594,10 +598,10 @@ int rnb_conv_h3w_tc(int variant) {
 // Spatial F(2x2, 3x3) h3 conv, stride 1, pad 1: p.F = N T frames of H x W.
 // U layout [Cin/16][n_cblocks][16 x][16 TC rows][4 x 16-B chunks (Uh | Ul)
 // of a channel quad, chunk q at h3w_swz(q, row)] (ops/conv_f32.h3w_weights).
-// AFF when p.in_ss is set (with p.clip_seg, p.clip_frames = frames per
-// clip), ST when p.out_stats is set.
+// AFF when p.in_ss is set (videos of the clips in p.clip_seg), ST when
+// p.out_stats is set (videos in out_seg); p.clip_frames = frames per clip.
 int rnb_conv_h3w_launch(const WinoParams* pp, int variant, hipStream_t stream, float in_scale,
-                        float out_scale) {
+                        float out_scale, const int* out_seg) {
   if (variant < 0 || variant >= rnb_conv_h3w_num_variants()) return -1;
   WinoParams p = *pp;
   const int TC = kH3WTC[variant], CT = 16 * TC;
@@ -607,7 +611,9 @@ int rnb_conv_h3w_launch(const WinoParams* pp, int variant, hipStream_t stream, f
     return -2;
   if (p.Cout > p.y_stride || (p.res && p.Cout > p.res_stride)) return -3;
   if (!(in_scale > 0.f) || !(out_scale > 0.f)) return -15;
-  if ((p.in_ss || p.out_stats) && (!p.clip_seg || p.clip_frames <= 0)) return -16;
+  if ((p.in_ss && !p.clip_seg) || (p.out_stats && !out_seg) ||
+      ((p.in_ss || p.out_stats) && p.clip_frames <= 0))
+    return -16;
   if (p.out_stats && p.stats_c < p.Cout) return -12;
   const long long xb = (long long)p.F * p.H * p.W * p.Cin * 4;
   if (xb > 0x7FFFFF00LL) return -5;
@@ -631,6 +637,7 @@ int rnb_conv_h3w_launch(const WinoParams* pp, int variant, hipStream_t stream, f
   ex.in_scale = in_scale;
   ex.out_scale = out_scale;
   ex.oflag = rnb_h3_range_flag();
+  ex.out_seg = out_seg;
   switch (TC) {
     case 2: h3w_dispatch<2>(p, ex, stream); break;
     default: h3w_dispatch<3>(p, ex, stream); break;

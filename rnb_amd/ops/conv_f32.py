@@ -679,23 +679,23 @@ class ConvLayerF32:
                                  % (self.name, tuple(ss.shape), tuple(aseg.shape),
                                     tuple(x.shape)))
             p.in_ss, p.clip_seg = ss.data_ptr(), aseg.data_ptr()
+        out_seg = 0
         if out_stats is not None:
             sums, clip_seg = out_stats
             if (sums.dim() != 3 or sums.shape[1] != 2 or sums.shape[2] < g.cout_p
                     or sums.dtype != torch.float64 or not sums.is_contiguous()
                     or clip_seg.dtype != torch.int32 or clip_seg.numel() != N
-                    or not clip_seg.is_contiguous()
-                    or (in_affine is not None and in_affine[1].data_ptr() != clip_seg.data_ptr())):
+                    or not clip_seg.is_contiguous()):
                 raise ValueError("%s: output BN sums %s / clip_seg %s do not match y %s"
                                  % (self.name, tuple(sums.shape), tuple(clip_seg.shape),
                                     tuple(y.shape)))
-            p.out_stats, p.clip_seg = sums.data_ptr(), clip_seg.data_ptr()
+            p.out_stats, out_seg = sums.data_ptr(), clip_seg.data_ptr()
             p.stats_c = sums.shape[2]
         # the activation scale is folded into the input BN's scale / shift
         # (AFF) or applied before the split
         in_scale = float(2.0 ** H3W_IN_LOG2)
         out_scale = float(2.0 ** -(H3W_IN_LOG2 + sw))
-        k.conv_h3w(p, variant, stream.cuda_stream, in_scale, out_scale)
+        k.conv_h3w(p, variant, stream.cuda_stream, in_scale, out_scale, out_seg)
 
     def wino_parts(self, cid: int):
         """[(co0, nco, tc, variant)] launches of Winograd config ``cid``: the

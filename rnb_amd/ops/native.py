@@ -383,7 +383,7 @@ class Kernels:
         lib.rnb_conv_h3p_ok.argtypes = [ctypes.c_int] * 5
         lib.rnb_conv_h3p_ok.restype = ctypes.c_int
         lib.rnb_conv_h3w_launch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
-                                            ctypes.c_float, ctypes.c_float]
+                                            ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
         lib.rnb_conv_h3w_launch.restype = ctypes.c_int
         lib.rnb_conv_h3w_tc.argtypes = [ctypes.c_int]
         lib.rnb_conv_h3w_tc.restype = ctypes.c_int
@@ -546,13 +546,14 @@ class Kernels:
                "conv_h3p (%d blocks per CU)" % blocks_per_cu)
 
     def conv_h3w(self, params: "WinoParams", variant: int, stream: int, in_scale: float,
-                 out_scale: float) -> None:
+                 out_scale: float, out_seg: int = 0) -> None:
         """Winograd F(2x2, 3x3) h3 conv (csrc/conv_h3w.hip: 1x3x3 stride 1 pad 1,
         Cin_p % 16 == 0, U split into fp16 hi / lo on the host --
         ConvLayerF32.h3w_u); input BN on load when ``params.in_ss`` is set,
-        epilogue BN sums when ``params.out_stats`` is set."""
+        epilogue BN sums when ``params.out_stats`` is set (videos of the clips in
+        ``out_seg``; ``params.clip_seg``: the input BN's)."""
         _check(self.lib.rnb_conv_h3w_launch(ctypes.byref(params), variant, stream, in_scale,
-                                            out_scale),
+                                            out_scale, out_seg or None),
                "conv_h3w (variant %d)" % variant)
 
     def conv_h3w_tc(self, variant: int) -> int:

@@ -188,3 +188,43 @@ def test_h3w_in_autotune_set_and_affine():
     assert all(lay.affine_ok(cid, shape) for cid in c)
     s2 = _layer(64, 144, (1, 3, 3), (1, 2, 2), (0, 1, 1))
     assert not any(is_h3w(cid) for cid in s2.candidates((4, 8, 56, 56, 64)))
+
+
+def test_h3w_separate_input_and_output_video_maps():
+    """The input BN's video map and the output sums' video map are separate
+    tensors (the autotuner passes two, and they may differ): scale / shift by
+    one map, sums by the other."""
+    layer = _layer(64, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False)
+    n = 4
+    x = _input(n, (2, 14, 14), 64, 64)
+    aseg = torch.tensor([0, 0, 1, 1], dtype=torch.int32, device=DEV)
+    oseg = torch.tensor([0, 1, 1, 2], dtype=torch.int32, device=DEV)
+    ss = _ss(2, 64, 7)
+    xa = torch.relu(x * ss[aseg.long(), 0][:, None, None, None, :] +
+                    ss[aseg.long(), 1][:, None, None, None, :])
+    ref = _ref64(layer, xa)
+    scale = ref.abs().max().item()
+    for cid in _ids():
+        sums = torch.zeros((3, 2, layer.geom.cout_p), dtype=torch.float64, device=DEV)
+        y = layer.forward_hip(x, config=cid, in_affine=(ss, aseg), out_stats=(sums, oseg))
+        torch.cuda.synchronize()
+        yd = y[..., :144].double().cpu()
+        assert (yd - ref).abs().max().item() <= 1e-5 * scale, cid
+        for v in range(3):
+            part = yd[oseg.cpu() == v].reshape(-1, 144)
+            got = sums[v, :, :144].cpu()
+            assert ((got[0] - part.sum(0)).abs() <= 1e-6 * part.abs().sum(0) + 1e-9).all(), (cid, v)
+
+
+def test_h3w_autotune_with_stats_and_affine(monkeypatch, tmp_path):
+    """The forward's tuning mode for a spatial conv after a deferred BN
+    (statistics and input BN on, separate video maps): every candidate,
+    h3w included, runs."""
+    monkeypatch.setenv("RNB_TUNE_CACHE", str(tmp_path / "tune.json"))
+    monkeypatch.setenv("RNB_TUNE_SEED", "0")
+    layer = _layer(64, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1), relu=False)
+    layer.tune_with_stats = True
+    layer.tune_with_affine = True
+    x = _input(2, (2, 14, 14), 64, 64)
+    cid = layer.autotune(x, reps=1)
+    assert layer.affine_ok(cid, x.shape)
