@@ -19,7 +19,10 @@ device), so results are cached under that key:
   or ``RNB_TUNE_SEED=<path>``; ``RNB_TUNE_SEED=0`` disables it) holds the
   picks measured on MI355X -- MIOpen's perf-db idea: a fresh box times only
   the shapes the table does not have. Seed entries never override the job's
-  own cache file.
+  own cache file. A seed entry serves any device of the seed's arch: the
+  device-name field of a key (a marketing name, which depends on how the
+  runtime resolves it -- under rocprofv3 a seeded run re-timed every shape)
+  is ignored for seed lookups.
 
 ``stats()`` counts, per process, the shapes timed here (``tuned``) and the
 ones served from the cache or the seed (``read``); runners report them.
@@ -41,6 +44,9 @@ _lock = threading.Lock()
 _mem: Dict[str, int] = {}
 _file_sig: Optional[Tuple[str, int, int]] = None     # (path, size, mtime_ns) last read
 _seed_from: Optional[str] = None
+_seed: Dict[str, int] = {}                     # seed entries by key without the device field
+_seed_arch: Optional[str] = None
+_arch: list = [None, False]                    # (gfx arch of the current device, resolved)
 _stats = {"tuned": 0, "read": 0, "seeded": 0, "file_reads": 0}
 
 _SEED_DEFAULT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tune_seed.json")
@@ -65,9 +71,34 @@ def make_key(family: str, geom, shape, device_name: str = "") -> str:
                                           "x".join(map(str, shape)), device_name)
 
 
+def _dev_free(key: str) -> Optional[str]:
+    """A make_key key without its device-name field (None: not such a key)."""
+    parts = key.split("|")
+    return "|".join(parts[:-1]) if len(parts) == 7 else None
+
+
+def _current_arch() -> Optional[str]:
+    """gfx arch of the current GPU (None without one)."""
+    if not _arch[1]:
+        _arch[1] = True
+        try:
+            import torch
+            if torch.cuda.is_available():
+                props = torch.cuda.get_device_properties(torch.cuda.current_device())
+                _arch[0] = str(getattr(props, "gcnArchName", "")).split(":")[0] or None
+        except Exception:
+            _arch[0] = None
+    return _arch[0]
+
+
+def _seed_ok() -> bool:
+    cur = _current_arch()
+    return _seed_arch is None or cur is None or cur == _seed_arch
+
+
 def _load_seed() -> None:
     """Seed table entries under the cache (once per seed path)."""
-    global _seed_from
+    global _seed_from, _seed_arch
     path = _seed_path()
     if path is None or _seed_from == path:
         return
@@ -78,11 +109,15 @@ def _load_seed() -> None:
     except (OSError, ValueError):
         return
     entries = data.get("entries", data) if isinstance(data, dict) else {}
+    _seed_arch = data.get("arch") if isinstance(data, dict) and "entries" in data else None
     n = 0
     for k, v in entries.items():
         if k not in _mem:
             _mem[k] = int(v)
             n += 1
+        df = _dev_free(k)
+        if df is not None:
+            _seed.setdefault(df, int(v))
     _stats["seeded"] += n
 
 
@@ -116,6 +151,10 @@ def get(key: str) -> Optional[int]:
     with _lock:
         if key not in _mem:
             _load_file()
+        if key not in _mem:
+            df = _dev_free(key)
+            if df is not None and df in _seed and _seed_ok():
+                _mem[key] = _seed[df]            # the seed under another device name
         return _mem.get(key)
 
 
@@ -195,6 +234,17 @@ def nearest(prefix: str, pixels: int) -> Optional[int]:
             d = abs(math.log(max(n, 1)) - math.log(max(pixels, 1)))
             if best_d is None or d < best_d:
                 best, best_d = cid, d
+        if best is None and _seed_ok():
+            for key, cid in _seed.items():            # seed keys without the device field
+                parts = key.split("|")
+                if parts[:5] != [fam, geo, k, s, p]:
+                    continue
+                n = 1
+                for x in parts[5].split("x"):
+                    n *= int(x)
+                d = abs(math.log(max(n, 1)) - math.log(max(pixels, 1)))
+                if best_d is None or d < best_d:
+                    best, best_d = cid, d
         return best
 
 
@@ -206,10 +256,12 @@ def snapshot() -> Dict[str, int]:
 
 
 def clear() -> None:
-    global _file_sig, _seed_from
+    global _file_sig, _seed_from, _seed_arch
     with _lock:
         _mem.clear()
+        _seed.clear()
         _file_sig = None
         _seed_from = None
+        _seed_arch = None
         for k in _stats:
             _stats[k] = 0

@@ -113,3 +113,29 @@ def test_committed_seed_parses():
     assert entries
     for k, v in entries.items():
         assert len(k.split("|")) == 7 and int(v) >= 0
+
+
+def test_seed_serves_other_device_names_of_its_arch(tmp_path, monkeypatch):
+    """A seed entry keyed under one device name serves the same shape on a
+    device reported under another name (the marketing name depends on how
+    the runtime resolves it), but not on another arch; nearest() falls back
+    to seed entries too."""
+    from rnb_amd.ops import tuning
+    seed = tmp_path / "seed.json"
+    k_a = "f32st|64x144|k1x3x3|s1x1x1|p0x1x1|16x8x56x56|Name A"
+    seed.write_text(json.dumps({"arch": "gfx950", "entries": {k_a: 1387}}))
+    monkeypatch.setenv("RNB_TUNE_SEED", str(seed))
+    monkeypatch.setenv("RNB_TUNE_CACHE", str(tmp_path / "cache.json"))
+    k_b = k_a.replace("Name A", "Name B")
+    tuning.clear()
+    try:
+        monkeypatch.setattr(tuning, "_arch", ["gfx950", True])
+        assert tuning.get(k_b) == 1387
+        assert tuning.nearest(k_b.replace("16x8x56x56", "20x8x56x56").rsplit("|", 1)[0]
+                              .rsplit("|", 1)[0] + "|20x8x56x56|Name C", 20 * 8 * 56 * 56) == 1387
+        tuning.clear()
+        monkeypatch.setattr(tuning, "_arch", ["gfx942", True])
+        assert tuning.get(k_b) is None
+        assert tuning.get(k_a) == 1387             # exact keys still served
+    finally:
+        tuning.clear()
