@@ -336,6 +336,17 @@ class R2P1DEngine:
     def conv_layers(self) -> List[ConvLayer]:
         return [op.layer for op in self.ops if op.kind == "conv"]
 
+    def uses_h3(self) -> bool:
+        """True when a conv of this engine picked an h3 config for any input
+        shape seen so far (tuned, captured or run): only those launches can
+        trip the range guard."""
+        from ...ops.conv_f32 import is_h3
+        for layer in self.conv_layers():
+            cfg = getattr(layer, "_config", None)
+            if isinstance(cfg, dict) and any(is_h3(c) for c in cfg.values()):
+                return True
+        return False
+
     # -------------------------------------------------------------- forward
     @property
     def supports_out_indirect(self) -> bool:
@@ -694,6 +705,9 @@ class GraphedEngine:
     @property
     def range_guard(self):
         return self.engine.range_guard
+
+    def uses_h3(self) -> bool:
+        return self.engine.uses_h3()
 
     @property
     def last_call(self):

@@ -222,9 +222,14 @@ class R2P1DRunner(RunnerModel):
         self._check_dir = os.environ.get("RNB_CHECK_DIR") or None
         self._checked = {}               # samples written per stratum
         # h3 range guard (ops/conv_f32.RangeGuard): graphed calls are checked
-        # when the runner sees them complete (on_complete), in call order
-        self.range_guarded = any(getattr(e, "range_guard", None) is not None
-                                 for e in self._lane_engines)
+        # when the runner sees them complete (on_complete), in call order. An
+        # engine whose convs picked no h3 config (RNB_H3=0, full-range picks)
+        # cannot trip it: then a non-final stage need not synchronise each
+        # call before publishing (runner.py)
+        self.range_guarded = any(
+            getattr(e, "range_guard", None) is not None
+            and (not callable(getattr(e, "uses_h3", None)) or e.uses_h3())
+            for e in self._lane_engines)
         self._guard_calls = []           # (graphed engine, output, call record) in flight
         self.range_fallbacks = 0
         self._direct_calls = self._staged_calls = 0     # intermediate-stage outputs

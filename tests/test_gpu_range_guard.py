@@ -160,3 +160,28 @@ def test_bucket_padding_rows_do_not_trip_the_guard(monkeypatch):
         torch.cuda.synchronize()
         assert not eng.range_guard.tripped(), n
         assert torch.isfinite(y).all()
+
+
+def test_engine_uses_h3_reflects_its_picks():
+    """R2P1DEngine.uses_h3 (which decides whether a range-guarded non-final
+    pipeline stage must synchronise each call): true after a
+    forward that picked h3 configs, false once no conv holds an h3 pick."""
+    from rnb_amd.models.r2p1d.engine import R2P1DEngine
+    from rnb_amd.models.r2p1d.model import build_network
+    from rnb_amd.ops.conv_f32 import H3D_BASE
+    eng = R2P1DEngine(build_network(1, 2, depth=18, seed=0), DEV, backend="hip",
+                      bn_mode="batch", dtype=torch.float32)
+    x = torch.randn((2, 8, 112, 112, 4), device=DEV)
+    x[..., 3:] = 0
+    for layer in eng.conv_layers():
+        layer._config.clear()
+    eng.forward(x, clip_offsets=[0, 2])
+    torch.cuda.synchronize()
+    for layer in eng.conv_layers():
+        for k in list(layer._config):
+            layer._config[k] = H3D_BASE           # force an h3 pick
+    assert eng.uses_h3()
+    for layer in eng.conv_layers():
+        for k in list(layer._config):
+            layer._config[k] = 0                  # fp32-MFMA direct config
+    assert not eng.uses_h3()
