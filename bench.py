@@ -156,6 +156,10 @@ def parse_args(argv=None):
                     help="(--route large-small) in the latency regime a small-video replica "
                          "holds a call back up to this long while a 15-clip call runs on its "
                          "GPU (runner announce_busy / yield_ms; 0 = off)")
+    ap.add_argument("--large-overflow", type=int, default=0,
+                    help="(--route large-small) a 15-clip video goes to the 1-clip-video "
+                         "replicas while this many wait for the 15-clip replica already "
+                         "(LargeSmallSelector, RNB_LARGE_OVERFLOW; 0 = never)")
     ap.add_argument("--large-lanes", type=int, default=2,
                     help="(--route large-small) runner lanes of the 15-clip-video replicas: "
                          "two (default) let a second large video start while the first runs; "
@@ -381,6 +385,8 @@ def main(argv=None) -> int:
         return 2
     if args.pipeline == "fused":
         return run_fused(args)
+    if args.large_overflow > 0:
+        os.environ["RNB_LARGE_OVERFLOW"] = str(args.large_overflow)   # loaders' LargeSmallSelector
     store = _rank_store(rank, world) if world > 1 else None
     rc, line = 0, None
     if rank == 0:
@@ -439,6 +445,7 @@ def main(argv=None) -> int:
                                       % (args.loaders, args.replicas),
                        "pipeline": args.pipeline, "launcher_config": res.get("config_path"),
                        "route": args.route, "lanes": args.lanes,
+                       "large_overflow": args.large_overflow,
                        "bn": ("eval (folded into the convs in fp64)" if args.bn == "eval" else
                               "batch (training-mode BN as the reference, per-video "
                               "statistics)"),

@@ -689,14 +689,34 @@ class R2P1DAggregator(RunnerModel):
 
 
 class LargeSmallSelector(QueueSelector):
-    """Routes 15-clip videos to queue 1 and everything else to queue 0."""
+    """Routes 15-clip videos to queue 1 and everything else to queue 0
+    (reference config/rnb.json, models/r2p1d/model.py:288-296).
 
-    def __init__(self, num_queues, large_clips: int = 15):
+    ``RNB_LARGE_OVERFLOW=k`` (> 0): a 15-clip video goes to queue 0 instead
+    while k or more are already waiting in queue 1 -- the one 15-clip replica
+    of a GPU cannot drain a burst of them alone, and the 1-clip replicas'
+    buckets take whole 15-clip videos too (work-conserving overflow; the
+    runner passes the queues to selectors that accept them)."""
+
+    def __init__(self, num_queues, large_clips: int = 15, queues=None):
         if num_queues != 2:
             raise ValueError("LargeSmallSelector needs exactly 2 out queues")
         super().__init__(num_queues)
         self.large_clips = large_clips
+        self.queues = queues
+        self.overflow = int(os.environ.get("RNB_LARGE_OVERFLOW", "0") or 0)
+        self.overflowed = 0
 
     def select(self, tensors, non_tensors, time_card):
         n = getattr(time_card, "num_clips", None)
-        return 1 if n is not None and n >= self.large_clips else 0
+        if n is None or n < self.large_clips:
+            return 0
+        if self.overflow > 0 and self.queues is not None:
+            try:
+                backlog = self.queues[1].qsize()
+            except (NotImplementedError, AttributeError, OSError):
+                backlog = 0
+            if backlog >= self.overflow:
+                self.overflowed += 1
+                return 0
+        return 1

@@ -443,3 +443,33 @@ def test_bench_default_topology_is_per_gpu():
             feeds.setdefault(q, set()).update(grp["gpus"])
     for grp in runner["queue_groups"]:
         assert feeds[grp["in_queue"]] == set(grp["gpus"]), grp
+
+
+def test_large_small_selector_overflow(monkeypatch):
+    """RNB_LARGE_OVERFLOW=k: 15-clip videos go to the 15-clip queue until k
+    wait there, then to the 1-clip queue; 1-clip videos always to queue 0;
+    without queues (the reference signature) the plain routing."""
+    from rnb_amd.models.r2p1d.model import LargeSmallSelector
+
+    class Card:
+        def __init__(self, n):
+            self.num_clips = n
+
+    class Q:
+        def __init__(self, n):
+            self.n = n
+
+        def qsize(self):
+            return self.n
+
+    monkeypatch.setenv("RNB_LARGE_OVERFLOW", "2")
+    qs = [Q(0), Q(1)]
+    sel = LargeSmallSelector(2, queues=qs)
+    assert sel.select(None, None, Card(1)) == 0
+    assert sel.select(None, None, Card(15)) == 1
+    qs[1].n = 2
+    assert sel.select(None, None, Card(15)) == 0 and sel.overflowed == 1
+    assert sel.select(None, None, Card(1)) == 0
+    assert LargeSmallSelector(2).select(None, None, Card(15)) == 1
+    monkeypatch.setenv("RNB_LARGE_OVERFLOW", "0")
+    assert LargeSmallSelector(2, queues=qs).select(None, None, Card(15)) == 1
