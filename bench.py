@@ -423,7 +423,8 @@ def main(argv=None) -> int:
                 "p50_ms": round(mi_phase.get("p50_ms", float("nan")), 3),
                 "p99_ms": round(mi_phase.get("p99_ms", float("nan")), 3),
                 "mean_ms": round(mi_phase.get("mean_ms", float("nan")), 3),
-                "requests": mi_phase.get("count", 0)},
+                "requests": mi_phase.get("count", 0),
+                "tail_breakdown": mi_phase.get("tail_breakdown")},
             "stale_event_waits": res.get("stale_event_waits"),
             # consumer-side gathering per phase: items / rows per model call and
             # why each gather ended (runner.py GATHER_ENDS)
