@@ -15,6 +15,8 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+#include "bn_tail.h"
+
 static __device__ __forceinline__ float bn_lo(uint32_t u) { return __uint_as_float(u << 16); }
 static __device__ __forceinline__ float bn_hi(uint32_t u) { return __uint_as_float(u & 0xFFFF0000u); }
 static __device__ __forceinline__ uint32_t bn_pack(float a, float b) {
@@ -883,6 +885,23 @@ __global__ __launch_bounds__(256) void bn_seg_apply_sums_f32_kernel(
   }
 }
 
+// ---- BN tail (bn_tail.h): the finalize armed by the host for the next
+// producer launch that supports it, taken (and disarmed) by that launch ----
+static BnTail g_bn_tail = {};
+static int g_bn_tail_taken = 0;
+
+BnTail bn_tail_take(long long waves) {
+  BnTail t = g_bn_tail;
+  if (t.ticket == nullptr || waves <= 0 || waves > 0x7FFFFFFF) {
+    t.ticket = nullptr;
+    return t;
+  }
+  t.expect = (int)waves;
+  g_bn_tail.ticket = nullptr;
+  g_bn_tail_taken = 1;
+  return t;
+}
+
 extern "C" {
 
 // Blocks per segment: a fixed 32, so the split of a video's rows -- and with
@@ -996,6 +1015,29 @@ int rnb_bn_seg_stats_from_sums_f32(double* sums, int sums_c, const int* coffs, i
     hipLaunchKernelGGL(bn_seg_running_f32_kernel, dim3((channels + 255) / 256), dim3(256), 0,
                        stream, p);
   return (int)hipGetLastError();
+}
+
+// Arms the BN tail for the next supporting producer launch (bn_tail.h):
+// ticket = device int, zero before the first launch (the tail leaves it zero).
+int rnb_bn_tail_arm(int* ticket, const double* sums, int sums_c, const int* coffs, int nseg,
+                    int rpc, int C, const float* gamma, const float* beta, float eps, float* ss) {
+  if (!ticket || !sums || !coffs || !gamma || !beta || !ss) return -1;
+  if (nseg <= 0 || C <= 0 || sums_c < C || rpc <= 0) return -2;
+  BnTail t = {};
+  t.ticket = ticket;
+  t.nseg = nseg; t.C = C; t.sums_c = sums_c; t.rpc = rpc;
+  t.sums = sums; t.coffs = coffs; t.gamma = gamma; t.beta = beta; t.eps = eps; t.ss = ss;
+  g_bn_tail = t;
+  g_bn_tail_taken = 0;
+  return 0;
+}
+void rnb_bn_tail_disarm() { g_bn_tail.ticket = nullptr; }
+// 1 when a launch took the tail armed last (then its scale / shift rows are
+// written by that launch); resets
+int rnb_bn_tail_taken() {
+  const int t = g_bn_tail_taken;
+  g_bn_tail_taken = 0;
+  return t;
 }
 
 // scale / shift (+ moments) from the epilogue sums only; the sums stay armed

@@ -67,6 +67,10 @@ __device__ unsigned long long* h3_phase_buf;
 #define H3_PHASE(k) do {} while (0)
 #endif
 
+// split-K fix-up in the kernel (X6DStats.tick) for configs with at most this
+// many accumulator tiles per wave (the split-K set; bigger tiles would spill)
+#define H3_FIXUP_MAX_TILES 18
+
 // input BatchNorm on load (AFF): per stage, the scale / shift of the step's
 // 32 channels for each clip the tile touches, [clip][sub][scale, shift][16]
 // (256 B per clip), DMA'd with the step's activations
@@ -337,10 +341,52 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
           *(x6f32x4*)(st.ws + ((size_t)kidx * p.M + m) * p.Cout_p + c) = acc[tp][tc];
       }
     }
-    return;
+    // x6d_splitk_reduce_kernel finishes (or, TP x TC > 18, the fix-up would
+    // cost the non-split form of this config registers: not built)
+    if (st.tick == nullptr || TP * TC > H3_FIXUP_MAX_TILES) return;
+    // serial fix-up: the tile's last-arriving block (of its ksplit, all on
+    // one XCD: consecutive remapped ids) sums the partials in split order --
+    // the reduce kernel's order -- and runs the epilogue
+    __threadfence();                           // this block's partial: performed
+    __syncthreads();
+    int* flag = (int*)lds;                     // no DMA in flight (loop's last wait)
+    if (threadIdx.x == 0) *flag = atomicAdd(st.tick + wgid, 1) == ksplit - 1;
+    __syncthreads();
+    const bool last = *flag != 0;
+    __syncthreads();                           // every wave read the flag (the epilogue reuses lds)
+    if (!last) {
+      bn_tail_run(st.tail);
+      return;
+    }
+    __threadfence();                           // the other blocks' partials: visible
+    if (threadIdx.x == 0) atomicExch(st.tick + wgid, 0);   // re-armed for the next launch
+#pragma unroll
+    for (int tc = 0; tc < TC; ++tc) {
+      const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
+      const float4 b4 = *(const float4*)(p.bias + c);
+#pragma unroll
+      for (int tp = 0; tp < TP; ++tp) {
+        const int m = p0 + (wp * TP + tp) * 16 + frow;
+        x6f32x4 v = (x6f32x4){b4.x, b4.y, b4.z, b4.w};
+        if (m < p.M && c < p.Cout_p) {
+          for (int k0 = 0; k0 < ksplit; k0 += 4) {     // 4 partials in flight
+            x6f32x4 part[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              part[u] = k0 + u < ksplit
+                            ? *(const x6f32x4*)(st.ws + ((size_t)(k0 + u) * p.M + m) * p.Cout_p + c)
+                            : (x6f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v += part[u];
+          }
+        }
+        acc[tp][tc] = v;
+      }
+    }
   }
   x6d_epilogue<TP, TC, NW, C_TILE, ST>(p, st, acc, p0, p.M, p0 + P_TILE, c0, wp, wc, lane, lds,
                                        NS * BUF);
+  bn_tail_run(st.tail);
 }
 
 // ===========================================================================
@@ -1045,7 +1091,7 @@ void conv_h3t_kernel(const ConvF32Params p, const X6DStats st) {
 // host side: config table + launcher (C ABI, ctypes)
 // ---------------------------------------------------------------------------
 struct ConvH3Config {
-  int p_tile, c_tile, threads;
+  int p_tile, c_tile, threads, fixup;        // fixup: in-kernel split-K finish built
   void (*kernel)(const ConvF32Params, const X6DStats);
   void (*kernel_st)(const ConvF32Params, const X6DStats);
   void (*kernel_aff)(const ConvF32Params, const X6DStats);       // + input BN on load
@@ -1053,7 +1099,7 @@ struct ConvH3Config {
 };
 
 #define H3CFG(TP, TC, WP, WC, MINB, NPROD)                                     \
-  {WP * TP * 16, WC * TC * 16, 64 * WP * WC,                                    \
+  {WP * TP * 16, WC * TC * 16, 64 * WP * WC, (TP) * (TC) <= H3_FIXUP_MAX_TILES,  \
    conv_h3_kernel<TP, TC, WP, WC, MINB, false, NPROD, false>,                   \
    conv_h3_kernel<TP, TC, WP, WC, MINB, true, NPROD, false>,                    \
    conv_h3_kernel<TP, TC, WP, WC, MINB, false, NPROD, true>,                    \
@@ -1111,7 +1157,8 @@ int rnb_conv_h3_affine_ok(int config_id, int cin_p, int rows_per_clip) {
 
 int rnb_conv_h3_launch(const ConvF32Params* pp, int config_id, hipStream_t stream, double* sums,
                        const int* clip_seg, int stats_c, int ksplit, float* ws, float in_scale,
-                       float out_scale, const float* in_ss, const int* in_seg) {
+                       float out_scale, const float* in_ss, const int* in_seg, int* tick,
+                       int tick_cap) {
   if (config_id < 0 || config_id >= kNumH3Configs) return -1;
   ConvF32Params p = *pp;
   const ConvH3Config& cfg = kH3Configs[config_id];
@@ -1158,10 +1205,21 @@ int rnb_conv_h3_launch(const ConvF32Params* pp, int config_id, hipStream_t strea
     if (!ws || ksplit > 16) return -14;
     st.ksplit = ksplit;
     st.ws = ws;
+    if (tick && cfg.fixup) {
+      // serial fix-up in the kernel (X6DStats.tick): one dispatch
+      if (blocks > tick_cap) return -17;
+      st.tick = tick;
+      st.tail = bn_tail_take(blocks * ksplit * (cfg.threads / 64));
+      hipLaunchKernelGGL(aff ? (sums ? cfg.kernel_aff_st : cfg.kernel_aff)
+                             : (sums ? cfg.kernel_st : cfg.kernel),
+                         dim3((unsigned)(blocks * ksplit)), dim3(cfg.threads), 0, stream, p, st);
+      return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(aff ? cfg.kernel_aff : cfg.kernel, dim3((unsigned)(blocks * ksplit)),
                        dim3(cfg.threads), 0, stream, p, st);
     return rnb_x6d_splitk_reduce(&p, &st, stream);
   }
+  st.tail = bn_tail_take(blocks * (cfg.threads / 64));
   hipLaunchKernelGGL(aff ? (sums ? cfg.kernel_aff_st : cfg.kernel_aff)
                          : (sums ? cfg.kernel_st : cfg.kernel),
                      dim3((unsigned)blocks), dim3(cfg.threads), 0, stream, p, st);

@@ -57,6 +57,7 @@ struct H3WExtra {
   float out_scale;    // 2^-(in + weight scale): accumulators -> conv output
   int* oflag;         // range guard (host-coherent word) or null
   const int* out_seg; // ST: video of each clip for the output sums (p.clip_seg: the input BN's)
+  BnTail tail;        // ST: BN finalize folded in (bn_tail.h); ticket null = off
 };
 
 // true when any element of v is +-inf or NaN (v_cmp_class)
@@ -545,6 +546,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void conv_h3w_kernel(const WinoParam
     // the statistics scratch is the buffer chunk 1 will DMA into: the barrier
     // at the top of the loop orders them
   }
+  // blocks without a unit returned above; the launcher counts the others' waves
+  if constexpr (ST) bn_tail_run(ex.tail);
 }
 
 static int h3w_num_cus() {
@@ -566,8 +569,20 @@ static void h3w_launch(const WinoParams& p, const H3WExtra& ex, hipStream_t stre
   long long grid = h3w_num_cus();                     // one block (4 waves, one per SIMD) per CU
   if (grid > units) grid = units;
   grid = (grid + 7) / 8 * 8;
+  H3WExtra e = ex;
+  e.tail = BnTail{};
+  if (ST) {
+    // blocks with at least one unit (the kernel's per-XCD ranges) reach the tail
+    long long active = 0;
+    for (int x = 0; x < 8; ++x) {
+      const long long per_x = (grid + 7 - x) >> 3;
+      const long long span = units * (x + 1) / 8 - units * x / 8;
+      active += per_x < span ? per_x : span;
+    }
+    e.tail = bn_tail_take(active * 4);
+  }
   hipLaunchKernelGGL((conv_h3w_kernel<TC, 4, ST, AFF>), dim3((unsigned)grid), dim3(256), 0,
-                     stream, p, ex);
+                     stream, p, e);
 }
 
 template <int TC>

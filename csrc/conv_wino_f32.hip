@@ -53,7 +53,7 @@
 // steps consume them: prefetch at PF = 0's register count.
 template <int TC, int PF, bool ST = false>
 __global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f32_kernel(
-    const WinoParams p) {
+    const WinoParams p, const BnTail tail) {
   constexpr int CT = 16 * TC;
   constexpr int U_BYTES = 16 * CT * 64;                 // one chunk: 16 x CT rows of 64 B
   constexpr int U_INSTR = U_BYTES / 1024 / 4;           // DMA instructions per wave
@@ -343,6 +343,7 @@ __global__ __launch_bounds__(256, (PF == 1 || TC == 3) ? 1 : 2) void conv_wino_f
 
   // ---- output transform Y = A^T M A + epilogue (lane: tile tl, 4 channels) ----
   w_spatial_epilogue<TC, ST, 4>(p, lds, acc, tb, wave, tl, q, cb, lane, tvalid, f, ty, tx);
+  if constexpr (ST) bn_tail_run(tail);               // BN finalize folded in (bn_tail.h)
 }
 
 // ===========================================================================
@@ -550,34 +551,35 @@ int rnb_wino_f32_launch(const WinoParams* pp, int variant, hipStream_t stream) {
   const dim3 grid((unsigned)blocks), block(256);
   const bool st = p.out_stats != nullptr;
   if (st && variant < 4) return -9;             // epilogue statistics: variants 4-9
+  const BnTail tail = st ? bn_tail_take(blocks * 4) : BnTail{};
   switch (variant) {
-    case 0: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 1>), grid, block, 0, stream, p); break;
-    case 1: hipLaunchKernelGGL((conv_wino_f32_kernel<3, 1>), grid, block, 0, stream, p); break;
-    case 2: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 0>), grid, block, 0, stream, p); break;
-    case 3: hipLaunchKernelGGL((conv_wino_f32_kernel<1, 0>), grid, block, 0, stream, p); break;
+    case 0: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 1>), grid, block, 0, stream, p, tail); break;
+    case 1: hipLaunchKernelGGL((conv_wino_f32_kernel<3, 1>), grid, block, 0, stream, p, tail); break;
+    case 2: hipLaunchKernelGGL((conv_wino_f32_kernel<2, 0>), grid, block, 0, stream, p, tail); break;
+    case 3: hipLaunchKernelGGL((conv_wino_f32_kernel<1, 0>), grid, block, 0, stream, p, tail); break;
     case 4:
-      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<1, 2, true>), grid, block, 0, stream, p);
-      else hipLaunchKernelGGL((conv_wino_f32_kernel<1, 2>), grid, block, 0, stream, p);
+      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<1, 2, true>), grid, block, 0, stream, p, tail);
+      else hipLaunchKernelGGL((conv_wino_f32_kernel<1, 2>), grid, block, 0, stream, p, tail);
       break;
     case 5:
-      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<2, 2, true>), grid, block, 0, stream, p);
-      else hipLaunchKernelGGL((conv_wino_f32_kernel<2, 2>), grid, block, 0, stream, p);
+      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<2, 2, true>), grid, block, 0, stream, p, tail);
+      else hipLaunchKernelGGL((conv_wino_f32_kernel<2, 2>), grid, block, 0, stream, p, tail);
       break;
     case 6:
-      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<3, 2, true>), grid, block, 0, stream, p);
-      else hipLaunchKernelGGL((conv_wino_f32_kernel<3, 2>), grid, block, 0, stream, p);
+      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<3, 2, true>), grid, block, 0, stream, p, tail);
+      else hipLaunchKernelGGL((conv_wino_f32_kernel<3, 2>), grid, block, 0, stream, p, tail);
       break;
     case 7:
-      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<1, 3, true>), grid, block, 0, stream, p);
-      else hipLaunchKernelGGL((conv_wino_f32_kernel<1, 3>), grid, block, 0, stream, p);
+      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<1, 3, true>), grid, block, 0, stream, p, tail);
+      else hipLaunchKernelGGL((conv_wino_f32_kernel<1, 3>), grid, block, 0, stream, p, tail);
       break;
     case 8:
-      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<2, 3, true>), grid, block, 0, stream, p);
-      else hipLaunchKernelGGL((conv_wino_f32_kernel<2, 3>), grid, block, 0, stream, p);
+      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<2, 3, true>), grid, block, 0, stream, p, tail);
+      else hipLaunchKernelGGL((conv_wino_f32_kernel<2, 3>), grid, block, 0, stream, p, tail);
       break;
     default:
-      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<3, 3, true>), grid, block, 0, stream, p);
-      else hipLaunchKernelGGL((conv_wino_f32_kernel<3, 3>), grid, block, 0, stream, p);
+      if (st) hipLaunchKernelGGL((conv_wino_f32_kernel<3, 3, true>), grid, block, 0, stream, p, tail);
+      else hipLaunchKernelGGL((conv_wino_f32_kernel<3, 3>), grid, block, 0, stream, p, tail);
       break;
   }
   return (int)hipGetLastError();

@@ -626,7 +626,7 @@ __global__ __launch_bounds__(512, 1) void conv_wino_x6h_kernel(const WinoParams 
 // optional BN + ReLU of the input on load. U per chunk: 6 x CT rows of 128 B.
 template <int TC, int WAVES, bool ST = false>
 __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : 2) void conv_winot_x6_kernel(
-    const WinoParams p) {
+    const WinoParams p, const BnTail tail) {
   constexpr int CT = 16 * TC, NT = 16 * WAVES;
   constexpr int U_BYTES = 6 * CT * 128;
   __shared__ __attribute__((aligned(16))) char lds[2 * U_BYTES];
@@ -762,6 +762,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 1 : 2) void conv_winot_x6_
   gemm(lds + ((nchunks - 1) & 1) * U_BYTES, d, -1, std::false_type{});
   __syncthreads();
   w_temporal_epilogue<TC, ST, WAVES>(p, lds, acc, tb, wave, tl, q, cb, lane, tvalid, n, tt, hw);
+  if constexpr (ST) bn_tail_run(tail);               // BN finalize folded in (bn_tail.h)
 }
 
 // ---------------------------------------------------------------------------
@@ -791,8 +792,10 @@ static int x6_prepare(WinoParams& p, int tile_h, int tile_w_div, int CT, int NT,
 
 template <typename K>
 static void x6_launch(K kernel, const WinoParams& p, int threads, hipStream_t stream) {
-  hipLaunchKernelGGL(kernel, dim3((unsigned)(p.n_tblocks * p.n_cblocks)), dim3(threads), 0, stream,
-                     p);
+  const long long blocks = (long long)p.n_tblocks * p.n_cblocks;
+  // the BN tail (bn_tail.h) rides on a launch that writes output sums
+  const BnTail tail = p.out_stats != nullptr ? bn_tail_take(blocks * (threads / 64)) : BnTail{};
+  hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(threads), 0, stream, p, tail);
 }
 
 // compute units of the current device (cached per device)

@@ -325,24 +325,25 @@ __global__ __launch_bounds__(512) void x6d_splitk_reduce_kernel(const ConvF32Par
   if (!stats) return;
   if (!uni) {
     if (cok) flush();
-    return;
-  }
+  } else {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    red[ty][tx][j] = s1[j];
-    red[ty][tx][4 + j] = s2[j];
-  }
-  __syncthreads();
-  if (ty == 0 && cok) {
-    const int sg = st.clip_seg[rb / rows_per_clip];
+    for (int j = 0; j < 4; ++j) {
+      red[ty][tx][j] = s1[j];
+      red[ty][tx][4 + j] = s2[j];
+    }
+    __syncthreads();
+    if (ty == 0 && cok) {
+      const int sg = st.clip_seg[rb / rows_per_clip];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      double t = 0.0;
+      for (int j = 0; j < 8; ++j) {
+        double t = 0.0;
 #pragma unroll
-      for (int y = 0; y < 8; ++y) t += red[y][tx][j];
-      atomicAdd(st.sums + ((size_t)sg * 2 + (j >> 2)) * st.stats_c + c + (j & 3), t);
+        for (int y = 0; y < 8; ++y) t += red[y][tx][j];
+        atomicAdd(st.sums + ((size_t)sg * 2 + (j >> 2)) * st.stats_c + c + (j & 3), t);
+      }
     }
   }
+  bn_tail_run(st.tail);                 // BN finalize folded in (bn_tail.h)
 }
 
 // ===========================================================================
@@ -556,10 +557,12 @@ extern "C" {
 int rnb_x6d_splitk_reduce(const ConvF32Params* p, const X6DStats* st, hipStream_t stream) {
   const int rpt = 4;                     // rows per thread: many threads, short chains
   const int rows_per_clip = p->To * p->Ho * p->Wo;
-  hipLaunchKernelGGL(x6d_splitk_reduce_kernel,
-                     dim3((unsigned)((p->Cout_p / 4 + 63) / 64),
-                          (unsigned)((p->M + 8 * rpt - 1) / (8 * rpt))),
-                     dim3(64, 8), 0, stream, *p, *st, rpt, rows_per_clip);
+  const long long gx = (p->Cout_p / 4 + 63) / 64, gy = (p->M + 8 * rpt - 1) / (8 * rpt);
+  X6DStats s = *st;
+  // the BN tail rides on the kernel that writes the sums (8 waves per block)
+  s.tail = s.sums != nullptr ? bn_tail_take(gx * gy * 8) : BnTail{};
+  hipLaunchKernelGGL(x6d_splitk_reduce_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(64, 8), 0,
+                     stream, *p, s, rpt, rows_per_clip);
   return (int)hipGetLastError();
 }
 

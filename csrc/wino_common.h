@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bn_tail.h"
+
 typedef float wf32x4 __attribute__((ext_vector_type(4)));
 
 struct WinoParams {

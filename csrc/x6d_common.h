@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bn_tail.h"
 #include "conv_f32_common.h"
 #include "x6_common.h"
 
@@ -70,6 +71,12 @@ struct X6DStats {
   // the ReLU, which would hide a NaN) sets *oflag = 1 (a plain vector store to
   // host-coherent memory; the host re-runs the call on full-range kernels)
   int* oflag = nullptr;
+  // conv_h3.hip split-K only: per-tile arrival counters (zero between
+  // launches): the last of a tile's ksplit blocks sums the partials and runs
+  // the epilogue itself (no x6d_splitk_reduce_kernel dispatch). Null = off.
+  int* tick = nullptr;
+  // BN finalize folded into this launch (bn_tail.h); ticket null = off
+  BnTail tail = {};
 };
 
 // true when any element of v is +-inf or NaN (v_cmp_class: sNaN, qNaN, -inf, +inf)

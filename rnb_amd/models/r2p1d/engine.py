@@ -463,6 +463,11 @@ class R2P1DEngine:
         skip = False
         pending = None               # deferred (scale_shift, clip_seg) for the next conv
         free_after = self._free_after
+        from ...ops import bn as bn_mod
+        # BN tail (csrc/bn_tail.h): a deferred BN's finalize folded into its
+        # producer conv when videos x channels <= this (the last wave walks
+        # them 512 at a time); 0 = a separate finalize dispatch per BN
+        tail_max = int(os.environ.get("RNB_BN_TAIL_MAX", "2048")) if hip else 0
         for i, op in enumerate(self.ops):
             if skip:                      # temporal half of a fused pair
                 skip = False
@@ -494,19 +499,43 @@ class R2P1DEngine:
                         nvid = 1 if coffs is None else coffs.numel() - 1
                         sums = op.bn.epilogue_sums(nvid, x.device)
                         kw["out_stats"] = (sums, clip_seg)
-                    y = op.layer.forward_hip(src, None, **kw)
-                    # segments in clip units: the BN kernels scale the clip
-                    # offsets by the layer's rows per clip (T*H*W)
-                    thw = y.shape[1] * y.shape[2] * y.shape[3]
                     if coffs is None and self.f32:
                         coffs = torch.tensor([0, x.shape[0]], dtype=torch.int32,
                                              device=x.device)
-                    if (defer and self._defer_ok[i] and self.f32
-                            and self.ops[i + 1].layer.accepts_input_affine(y.shape)):
+                    tail_ss = None
+                    if sums is not None and tail_max > 0 and bn_mod._RUN_SINK[0] is not None:
+                        yshape = tuple(op.layer.out_shape(src.shape))
+                        if (defer and self._defer_ok[i]
+                                and self.ops[i + 1].layer.accepts_input_affine(yshape)
+                                and (coffs.numel() - 1) * op.bn.channels_p <= tail_max):
+                            # the finalize rides on the producer's last launch (BN tail)
+                            tail_ss, kw["bn_tail"] = op.bn.tail_args(
+                                coffs, sums, yshape[1] * yshape[2] * yshape[3])
+                    y = op.layer.forward_hip(src, None, **kw)
+                    if tail_ss is not None:
+                        from ...ops.native import kernels as _kn
+                        if tuple(y.shape) != yshape:
+                            raise RuntimeError("%s: output %s, predicted %s" % (
+                                op.layer.name, tuple(y.shape), yshape))
+                        if not _kn().bn_tail_taken():
+                            _kn().bn_tail_disarm()     # this config's kernel has no tail
+                            tail_ss = None
+                        else:
+                            self.bn_tails = getattr(self, "bn_tails", 0) + 1
+                    # segments in clip units: the BN kernels scale the clip
+                    # offsets by the layer's rows per clip (T*H*W)
+                    thw = y.shape[1] * y.shape[2] * y.shape[3]
+                    deferred = (defer and self._defer_ok[i] and self.f32
+                                and self.ops[i + 1].layer.accepts_input_affine(y.shape))
+                    if deferred:
                         # statistics now; normalise + ReLU inside the next conv
                         if clip_seg is None:
                             clip_seg = self._clip_segments(coffs, x.shape[0], x.device)
-                        pending = (op.bn.scale_shift_f32(y, coffs, sums, rpc=thw), clip_seg)
+                        if tail_ss is not None:
+                            bn_mod._RUN_SINK[0].append((op.bn, sums, thw))
+                            pending = (tail_ss, clip_seg)
+                        else:
+                            pending = (op.bn.scale_shift_f32(y, coffs, sums, rpc=thw), clip_seg)
                     else:
                         ind = out_indirect if i == len(self.ops) - 1 else None
                         from ...ops import bn as bn_mod

@@ -315,6 +315,27 @@ class BatchNormBatch:
             _RUN_SINK[0].append(self)
         return mean, var, ss
 
+    def tail_args(self, segments: torch.Tensor, sums: torch.Tensor, rpc: int):
+        """(scale/shift [nseg, 2, Cp] fp32, ``kernels().bn_tail_arm`` arguments):
+        the finalize of ``_stats_ss``'s sums path folded into the producing
+        conv's last launch (csrc/bn_tail.h) -- the producer's last wave writes
+        the rows; no bn_seg_ss_from_sums dispatch. The caller checks
+        ``bn_tail_taken`` after the conv and appends (self, sums, rpc) to the
+        forward's running sink as the ss-only path does (moments ``mean`` /
+        ``var`` are not kept)."""
+        nseg, C = segments.numel() - 1, self.channels_p
+        if (sums.dtype != torch.float64 or not sums.is_contiguous() or sums.dim() != 3
+                or sums.shape[0] < nseg or sums.shape[1] != 2 or sums.shape[2] < C):
+            raise ValueError("epilogue sums %s do not match %d segments x %d channels"
+                             % (tuple(sums.shape), nseg, C))
+        t = getattr(self, "_tail_ticket", None)
+        if t is None or t.device != sums.device:
+            t = self._tail_ticket = torch.zeros(1, dtype=torch.int32, device=sums.device)
+        ss = torch.empty((nseg, 2, C), dtype=torch.float32, device=sums.device)
+        return ss, (t.data_ptr(), sums.data_ptr(), sums.shape[2], segments.data_ptr(), nseg,
+                    int(rpc), C, self.gamma.data_ptr(), self.beta.data_ptr(), self.eps,
+                    ss.data_ptr())
+
     def epilogue_sums(self, nseg: int, device) -> torch.Tensor:
         """fp64 [nseg, 2, Cp] per-segment (sum, sum of squares) for a producer
         conv's epilogue to accumulate into: zero on return, and zeroed again

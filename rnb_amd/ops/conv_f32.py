@@ -541,6 +541,16 @@ class ConvLayerF32:
             ws = self._x6k_ws[numel] = torch.empty(numel, dtype=torch.float32, device=self.device)
         return ws
 
+    def splitk_ticks(self, tiles: int) -> torch.Tensor:
+        """int32 per-tile arrival counters of the in-kernel split-K fix-up
+        (zero between launches: the kernel re-arms them), one persistent
+        buffer per size (graph-safe)."""
+        d = self.__dict__.setdefault("_splitk_ticks", {})
+        t = d.get(tiles)
+        if t is None:
+            t = d[tiles] = torch.zeros(tiles, dtype=torch.int32, device=self.device)
+        return t
+
     def x6d_buffers(self):
         """(split weight matrix [K16/16][rows][64] int16, bias [rows] fp32),
         rows = Cout_p + X6_ROW_SLACK, built once."""
@@ -762,7 +772,8 @@ class ConvLayerF32:
         ids = self.wino_ids if x6_enabled() else self.wino_ids - WINO_X6
         return c + sorted(ids)
 
-    def _launch_wino(self, x, y, residual, cid, stream, in_affine=None, out_stats=None):
+    def _launch_wino(self, x, y, residual, cid, stream, in_affine=None, out_stats=None,
+                     bn_tail=None):
         from .native import WinoParams, kernels
         ft = cid in WINO_TEMPORAL
         x6 = cid in WINO_X6
@@ -817,7 +828,8 @@ class ConvLayerF32:
         k = kernels()
         launch = ((k.winot_x6 if ft else k.wino_x6) if x6 else
                   (k.winot_f32 if ft else k.wino_f32))
-        for co0, nco, tc, variant in self.wino_parts(cid):
+        parts = self.wino_parts(cid)
+        for j, (co0, nco, tc, variant) in enumerate(parts):
             u = self.wino_u(tc, m, co0, nco, x6=x6)
             assert u.shape[0] * 16 == C and u.shape[1] * 16 * tc >= nco
             p.u = u.data_ptr()
@@ -827,6 +839,8 @@ class ConvLayerF32:
             p.Cout = nco
             if sums is not None:
                 p.out_stats = sums.data_ptr() + 8 * co0
+            if bn_tail is not None and j == len(parts) - 1:
+                k.bn_tail_arm(*bn_tail)            # the conv's last launch
             launch(p, variant, stream.cuda_stream)
 
     # ------------------------------------------------------------------
@@ -1074,7 +1088,11 @@ class ConvLayerF32:
         To, Ho, Wo = self.geom.out_thw(T, H, W)
         return kernels().conv_h3_affine_ok(conf, self.geom.cin_p, To * Ho * Wo)
 
-    def _launch_all(self, x, y, residual, cid, stream, in_affine=None, out_stats=None):
+    def _launch_all(self, x, y, residual, cid, stream, in_affine=None, out_stats=None,
+                    bn_tail=None):
+        """``bn_tail``: ``kernels().bn_tail_arm`` arguments, armed right before
+        the conv's LAST launch (a launch that supports it takes it; the caller
+        checks ``bn_tail_taken``)."""
         from .native import kernels
         k = kernels()
         N = x.shape[0]
@@ -1087,7 +1105,7 @@ class ConvLayerF32:
                 ost = None if out_stats is None else (out_stats[0], out_stats[1][n0:n1])
                 self._launch_wino(x[n0:n1], y[n0:n1],
                                   residual[n0:n1] if residual is not None else None, cid,
-                                  stream, aff, ost)
+                                  stream, aff, ost, bn_tail=bn_tail if n1 == N else None)
             return
         if is_h3w(cid):
             step = self.chunk_clips(x.shape, y.shape,
@@ -1096,6 +1114,8 @@ class ConvLayerF32:
                 n1 = min(N, n0 + step)
                 aff = None if in_affine is None else (in_affine[0], in_affine[1][n0:n1])
                 ost = None if out_stats is None else (out_stats[0], out_stats[1][n0:n1])
+                if bn_tail is not None and n1 == N:
+                    k.bn_tail_arm(*bn_tail)
                 self._launch_h3w(x[n0:n1], y[n0:n1],
                                  residual[n0:n1] if residual is not None else None, cid,
                                  stream, aff, ost)
@@ -1130,6 +1150,8 @@ class ConvLayerF32:
         for n0 in range(0, N, step):
             p = self.params(x, y, residual, n0, min(N, n0 + step), x6=x6 and not h3, h3=h3,
                             h3t=h3t)
+            if bn_tail is not None and n0 + step >= N:
+                k.bn_tail_arm(*bn_tail)            # the conv's last launch
             if h3t:
                 _, _, s_in, s_out = self.h3t_buffers()
                 aff = ((in_affine[0].data_ptr(), in_affine[1].data_ptr() + 4 * n0)
@@ -1180,19 +1202,26 @@ class ConvLayerF32:
                 _, _, s_in, s_out = self.h3d_buffers()
                 ks, ws = 1, None
                 conf = cid - H3D_BASE
+                tick = None
                 if is_h3k(cid):
                     conf = H3K_CONFIGS[cid - H3K_BASE]
                     ks = self.ksplit_for(cid, x[n0:min(N, n0 + step)].shape)
                     ws = self.x6k_workspace(ks * p.M * self.geom.cout_p) if ks > 1 else None
+                    if ks > 1 and os.environ.get("RNB_SPLITK_FIXUP", "1") != "0":
+                        # the last block of each tile finishes it: no reduce dispatch
+                        pt, ct = k.h3_configs[conf]
+                        tick = self.splitk_ticks(math.ceil(p.M / pt)
+                                                 * math.ceil(self.geom.cout_p / ct))
                 aff = ((in_affine[0].data_ptr(), in_affine[1].data_ptr() + 4 * n0)
                        if in_affine is not None else (0, 0))
+                tk = (tick.data_ptr(), tick.numel()) if tick is not None else (0, 0)
                 if out_stats is not None:
                     k.conv_h3(p, conf, stream.cuda_stream, s_in, s_out, out_stats[0].data_ptr(),
                               out_stats[1].data_ptr() + 4 * n0, out_stats[0].shape[2], ks,
-                              ws.data_ptr() if ws is not None else 0, *aff)
+                              ws.data_ptr() if ws is not None else 0, *aff, *tk)
                 else:
                     k.conv_h3(p, conf, stream.cuda_stream, s_in, s_out, 0, 0, 0, ks,
-                              ws.data_ptr() if ws is not None else 0, *aff)
+                              ws.data_ptr() if ws is not None else 0, *aff, *tk)
             elif is_x6r(cid):
                 if not self.wino_ok:
                     raise ValueError("%s: the row-band x6 kernel takes 1x3x3 stride-1 convs"
@@ -1302,7 +1331,7 @@ class ConvLayerF32:
 
     def forward_hip(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                     out: Optional[torch.Tensor] = None, config: Optional[int] = None,
-                    in_affine=None, out_stats=None):
+                    in_affine=None, out_stats=None, bn_tail=None):
         """``in_affine`` = (scale_shift [nseg, 2, Cin], clip_seg int32 [N]): x is
         the raw output of a conv whose BatchNorm + ReLU (per video) is applied
         here on load (temporal Winograd configs only). ``out_stats`` = (sums
@@ -1324,7 +1353,7 @@ class ConvLayerF32:
             return y
         cid = self.config_for(x.shape) if config is None else config
         self._launch_all(x, y, residual, cid, torch.cuda.current_stream(x.device), in_affine,
-                         out_stats)
+                         out_stats, bn_tail)
         return y
 
     def forward_torch(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,

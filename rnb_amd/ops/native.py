@@ -334,8 +334,17 @@ class Kernels:
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.c_float, ctypes.c_float, ctypes.c_void_p,
-                                           ctypes.c_void_p]
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         lib.rnb_conv_h3_launch.restype = ctypes.c_int
+        lib.rnb_bn_tail_arm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+                                        ctypes.c_void_p]
+        lib.rnb_bn_tail_arm.restype = ctypes.c_int
+        lib.rnb_bn_tail_disarm.argtypes = []
+        lib.rnb_bn_tail_disarm.restype = None
+        lib.rnb_bn_tail_taken.argtypes = []
+        lib.rnb_bn_tail_taken.restype = ctypes.c_int
         lib.rnb_conv_h3_affine_ok.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         lib.rnb_conv_h3_affine_ok.restype = ctypes.c_int
         lib.rnb_conv_h3r_launch.argtypes = [ctypes.POINTER(ConvParams), ctypes.c_int,
@@ -464,18 +473,35 @@ class Kernels:
 
     def conv_h3(self, params: ConvParams, config_id: int, stream: int, in_scale: float,
                 out_scale: float, sums: int = 0, clip_seg: int = 0, stats_c: int = 0,
-                ksplit: int = 1, ws: int = 0, in_ss: int = 0, in_seg: int = 0) -> None:
+                ksplit: int = 1, ws: int = 0, in_ss: int = 0, in_seg: int = 0,
+                tick: int = 0, tick_cap: int = 0) -> None:
         """h3 direct conv (fp32 products as fp16 hi/lo products, csrc/conv_h3.hip):
         ``params.w`` = split weights scaled by 2^sw, ``in_scale`` = 2^sa applied
         to the activations, ``out_scale`` = 2^-(sa + sw); sums / ksplit / ws as
         ``conv_x6``; ``in_ss`` (fp32 [nseg][2][Cin_p] scale/shift) with
         ``in_seg`` (int32 [N] video per clip): the input's BatchNorm + ReLU
-        applied on load."""
+        applied on load. ``tick`` (split-K): int32 [>= tiles] zeroed arrival
+        counters (``tick_cap`` entries): the last block of each tile finishes
+        it in the same dispatch instead of a reduce kernel."""
         _check(self.lib.rnb_conv_h3_launch(ctypes.byref(params), config_id, stream,
                                            sums or None, clip_seg or None, stats_c, ksplit,
                                            ws or None, in_scale, out_scale, in_ss or None,
-                                           in_seg or None),
+                                           in_seg or None, tick or None, tick_cap),
                "conv_h3 (config %d, ksplit %d)" % (config_id, ksplit))
+
+    def bn_tail_arm(self, ticket, sums, sums_c, coffs, nseg, rpc, C, gamma, beta, eps,
+                    ss) -> None:
+        """Arms the BN finalize (scale / shift rows into ``ss``) for the next
+        conv launch that supports it (csrc/bn_tail.h); see ``bn_tail_taken``."""
+        _check(self.lib.rnb_bn_tail_arm(ticket, sums, sums_c, coffs, nseg, rpc, C, gamma, beta,
+                                        eps, ss), "bn_tail_arm")
+
+    def bn_tail_disarm(self) -> None:
+        self.lib.rnb_bn_tail_disarm()
+
+    def bn_tail_taken(self) -> bool:
+        """True when a launch took the last armed BN tail (resets)."""
+        return bool(self.lib.rnb_bn_tail_taken())
 
     def h3_set_range_flag(self, dev_ptr: int) -> None:
         """Range-guard flag (device address of host-coherent memory, 0 = none)
