@@ -5,11 +5,16 @@
 // between the two convs (a one-clip forward carried 46 of them, ~4.7 us
 // each, profiles/r6_bnbreak_1clips.txt).
 //
-// Every wave of the launch, after its last sums atomic, releases (agent-scope
-// fence) and adds 1 to the BN's ticket; the wave that brings it to `expect`
-// (the launch's wave count) acquires, computes scale / shift for all nseg x C
+// Every wave of the launch, once its sums atomics are performed (s_waitcnt
+// vmcnt(0): agent-scope fp64 atomics, done beyond the XCD's L2), adds 1 to
+// the BN's ticket; the wave that brings it to `expect` (the launch's wave
+// count) reads the sums with sc1 loads (L1 bypassed, no stale line: the
+// atomics left none in any L2), computes scale / shift for all nseg x C
 // (segment, channel) pairs with the formulas of bn_seg_ss_from_sums_f32_kernel
-// and re-arms the ticket to 0 for the next launch (stream-ordered). The
+// and re-arms the ticket to 0 for the next launch (stream-ordered). No
+// agent-scope fence: __threadfence() writes back and invalidates the XCD's L2
+// in every wave that runs it -- a first build with it ran the one-clip
+// forward at 4.3 ms instead of 2.3 (profiles/r6_bn_tail_threadfence.txt). The
 // producer's launcher takes the tail that the host armed (rnb_bn_tail_arm)
 // for the LAST launch of the conv only, so when that wave runs every sums
 // atomic of the conv has been performed. Sums stay in place: the forward's
@@ -34,11 +39,16 @@ struct BnTail {
 // ticket null when none is armed). Defined in bn_ops.hip.
 BnTail bn_tail_take(long long waves);
 
+// sc1 load (global_load_dwordx2 ... sc1): bypasses this CU's L1
+static __device__ __forceinline__ double bn_tail_load(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Called by every wave of a producer launch after its epilogue (all lanes
 // converged; the wave's sums atomics issued).
 static __device__ __forceinline__ void bn_tail_run(const BnTail& t) {
   if (t.ticket == nullptr) return;
-  __threadfence();                                  // this wave's sums: performed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sums atomics: performed
   const unsigned long long live = __ballot(1);
   const int leader = __ffsll((long long)live) - 1;
   const int lane = threadIdx.x & 63;
@@ -46,7 +56,6 @@ static __device__ __forceinline__ void bn_tail_run(const BnTail& t) {
   if (lane == leader) old = atomicAdd(t.ticket, 1);
   old = __shfl(old, leader, 64);
   if (old != t.expect - 1) return;
-  __threadfence();                                  // every wave's sums: visible
   const int total = t.nseg * t.C;
   for (int i0 = 0; i0 < total; i0 += 8 * 64) {
     // eight (segment, channel) pairs per lane in flight
@@ -58,8 +67,8 @@ static __device__ __forceinline__ void bn_tail_run(const BnTail& t) {
       sg[u] = i < total ? i / t.C : 0;
       ch[u] = i < total ? i - sg[u] * t.C : -1;
       const double* sp = t.sums + (size_t)sg[u] * 2 * t.sums_c;
-      a1[u] = ch[u] >= 0 ? sp[ch[u]] : 0.0;
-      a2[u] = ch[u] >= 0 ? sp[t.sums_c + ch[u]] : 0.0;
+      a1[u] = ch[u] >= 0 ? bn_tail_load(sp + ch[u]) : 0.0;
+      a2[u] = ch[u] >= 0 ? bn_tail_load(sp + t.sums_c + ch[u]) : 0.0;
       rows[u] = ch[u] >= 0 ? (t.coffs[sg[u] + 1] - t.coffs[sg[u]]) * t.rpc : 0;
     }
 #pragma unroll

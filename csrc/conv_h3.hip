@@ -70,6 +70,9 @@ __device__ unsigned long long* h3_phase_buf;
 // split-K fix-up in the kernel (X6DStats.tick) for configs with at most this
 // many accumulator tiles per wave (the split-K set; bigger tiles would spill)
 #define H3_FIXUP_MAX_TILES 18
+// cache-policy bits of a buffer load / store: sc1 (bypass L1; stores write
+// through and leave no line in the XCD's L2)
+#define H3_SC1 16
 
 // input BatchNorm on load (AFF): per stage, the scale / shift of the step's
 // 32 channels for each clip the tile touches, [clip][sub][scale, shift][16]
@@ -331,23 +334,35 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
 #pragma unroll
     for (int tc = 0; tc < TC; ++tc) acc[tp][tc] *= out_scale;     // exact: a power of two
   if (ksplit > 1) {                 // raw partial sums -> ws[kidx][m][c]
+    // in-kernel finish (st.tick): the partials go out sc1 (write-through,
+    // no line left in this XCD's L2) for the tile's last block to read sc1
+    // from any XCD -- the counter form of the inter-workgroup hand-off
+    // without an agent-scope fence (the guide's split-K recipe)
+    const bool fix = st.tick != nullptr && TP * TC <= H3_FIXUP_MAX_TILES;
+    const uint32_t ws_bytes = (uint32_t)min((long long)ksplit * p.M * p.Cout_p * 4, 0x7FFFFF00LL);
+    const __amdgpu_buffer_rsrc_t wsr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)st.ws, (short)0, ws_bytes, 0x00020000);
 #pragma unroll
     for (int tp = 0; tp < TP; ++tp) {
       const int m = p0 + (wp * TP + tp) * 16 + frow;
 #pragma unroll
       for (int tc = 0; tc < TC; ++tc) {
         const int c = c0 + (wc * TC + tc) * 16 + 4 * fq;
-        if (m < p.M && c < p.Cout_p)
-          *(x6f32x4*)(st.ws + ((size_t)kidx * p.M + m) * p.Cout_p + c) = acc[tp][tc];
+        const uint32_t off = (m < p.M && c < p.Cout_p)
+                                 ? (uint32_t)((((long long)kidx * p.M + m) * p.Cout_p + c) * 4)
+                                 : X6D_INVALID;
+        if (fix)
+          __builtin_amdgcn_raw_buffer_store_b128(acc[tp][tc], wsr, off, 0, H3_SC1);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(acc[tp][tc], wsr, off, 0, 0);
       }
     }
     // x6d_splitk_reduce_kernel finishes (or, TP x TC > 18, the fix-up would
     // cost the non-split form of this config registers: not built)
-    if (st.tick == nullptr || TP * TC > H3_FIXUP_MAX_TILES) return;
-    // serial fix-up: the tile's last-arriving block (of its ksplit, all on
-    // one XCD: consecutive remapped ids) sums the partials in split order --
-    // the reduce kernel's order -- and runs the epilogue
-    __threadfence();                           // this block's partial: performed
+    if (!fix) return;
+    // serial fix-up: the tile's last-arriving block sums the partials in
+    // split order -- the reduce kernel's order -- and runs the epilogue
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's partial: performed
     __syncthreads();
     int* flag = (int*)lds;                     // no DMA in flight (loop's last wait)
     if (threadIdx.x == 0) *flag = atomicAdd(st.tick + wgid, 1) == ksplit - 1;
@@ -358,7 +373,6 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
       bn_tail_run(st.tail);
       return;
     }
-    __threadfence();                           // the other blocks' partials: visible
     if (threadIdx.x == 0) atomicExch(st.tick + wgid, 0);   // re-armed for the next launch
 #pragma unroll
     for (int tc = 0; tc < TC; ++tc) {
@@ -374,7 +388,9 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
 #pragma unroll
             for (int u = 0; u < 4; ++u)
               part[u] = k0 + u < ksplit
-                            ? *(const x6f32x4*)(st.ws + ((size_t)(k0 + u) * p.M + m) * p.Cout_p + c)
+                            ? __builtin_amdgcn_raw_buffer_load_b128(
+                                  wsr, (uint32_t)((((long long)(k0 + u) * p.M + m) * p.Cout_p + c) * 4),
+                                  0, H3_SC1)
                             : (x6f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int u = 0; u < 4; ++u) v += part[u];
