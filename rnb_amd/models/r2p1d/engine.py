@@ -467,7 +467,9 @@ class R2P1DEngine:
         # BN tail (csrc/bn_tail.h): a deferred BN's finalize folded into its
         # producer conv when videos x channels <= this (the last wave walks
         # them 512 at a time); 0 = a separate finalize dispatch per BN
-        tail_max = int(os.environ.get("RNB_BN_TAIL_MAX", "2048")) if hip else 0
+        # (opt-in: per-wave tickets on one address serialise at the memory
+        # side, +0.46 ms per one-clip forward, profiles/r6_ab_bn_tail_fixup.txt)
+        tail_max = int(os.environ.get("RNB_BN_TAIL_MAX", "0")) if hip else 0
         for i, op in enumerate(self.ops):
             if skip:                      # temporal half of a fused pair
                 skip = False

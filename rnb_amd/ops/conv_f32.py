@@ -1207,8 +1207,11 @@ class ConvLayerF32:
                     conf = H3K_CONFIGS[cid - H3K_BASE]
                     ks = self.ksplit_for(cid, x[n0:min(N, n0 + step)].shape)
                     ws = self.x6k_workspace(ks * p.M * self.geom.cout_p) if ks > 1 else None
-                    if ks > 1 and os.environ.get("RNB_SPLITK_FIXUP", "1") != "0":
-                        # the last block of each tile finishes it: no reduce dispatch
+                    if ks > 1 and os.environ.get("RNB_SPLITK_FIXUP", "0") == "1":
+                        # the last block of each tile finishes it: no reduce
+                        # dispatch (opt-in: one block reading up to 16 slabs
+                        # of 32 KB is slower than the parallel reduce kernel,
+                        # +0.39 ms per one-clip forward, profiles/r6_ab_bn_tail_fixup.txt)
                         pt, ct = k.h3_configs[conf]
                         tick = self.splitk_ticks(math.ceil(p.M / pt)
                                                  * math.ceil(self.geom.cout_p / ct))

@@ -138,8 +138,9 @@ def test_splitk_fixup_matches_reduce_kernel(monkeypatch, k, s, p, thw, cin):
 @pytest.mark.parametrize("n,offs", [(1, [0, 1]), (2, [0, 1, 2]), (4, [0, 3, 4, 4])])
 def test_engine_bn_tail_matches_separate_finalize(monkeypatch, n, offs):
     """A one- to four-clip R(2+1)D-34 forward with every deferred BN
-    finalized in its producer (default) against the separate finalize
-    dispatches (RNB_BN_TAIL_MAX=0): logits and running statistics agree."""
+    finalized in its producer (opt-in) against the separate finalize
+    dispatches (RNB_BN_TAIL_MAX=0, the default): logits and running
+    statistics agree."""
     from rnb_amd.models.r2p1d.model import build_network
     from rnb_amd.models.r2p1d.engine import R2P1DEngine
     g = torch.Generator().manual_seed(7)

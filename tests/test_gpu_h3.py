@@ -83,12 +83,14 @@ def test_h3_temporal_tap_skip_and_stem_exact(k, s, p, thw):
 @pytest.mark.parametrize("k,s,p,thw,cin", [((1, 3, 3), (1, 1, 1), (0, 1, 1), (1, 7, 7), 64),
                                            ((3, 1, 1), (1, 1, 1), (1, 0, 0), (2, 7, 7), 256),
                                            ((1, 3, 3), (1, 2, 2), (0, 1, 1), (2, 14, 14), 64)])
-def test_h3_splitk_exact_integers_and_stats(k, s, p, thw, cin):
+@pytest.mark.parametrize("fixup", ["0", "1"])
+def test_h3_splitk_exact_integers_and_stats(monkeypatch, fixup, k, s, p, thw, cin):
     """Split-K h3 configs (partials scaled back per split, finished by the
     tile's last block in the kernel -- default -- or by the shared x6 reduce
     kernel): bit-exact on small integers; per-video sums vs fp64 (the
     in-kernel finish sums in the direct epilogue's fp32-then-fp64 order)."""
     from rnb_amd.ops.conv_f32 import H3K_BASE, H3K_CONFIGS
+    monkeypatch.setenv("RNB_SPLITK_FIXUP", fixup)
     layer = _layer(cin, 150, k, s, p, relu=True, integer=True)
     x = _input(3, thw, cin, cin, integer=True)
     oshape = layer.out_shape(x.shape)
