@@ -885,9 +885,151 @@ __global__ __launch_bounds__(256) void bn_seg_apply_sums_f32_kernel(
   }
 }
 
+// Block-tiled apply (the default for both applies): a block owns R
+// consecutive rows x all C channels (R C 4 <= 128 KB, R <= 3 rows-per-clip
+// so the rows span at most 4 videos), and pays its prologue -- the videos'
+// row offsets into LDS, the segments of its rows, their scale / shift (from
+// the epilogue sums, or the finalize's rows) into LDS -- once per block.
+// bn_seg_apply_sums_f32_kernel gives each 256 threads 16 KB and re-walks
+// three binary searches of dependent global loads per block and thread: at
+// conv2's 64 channels and 128 videos it ran at 0.65 TB/s (0.49 ms per apply,
+// profiles/pmc/r5_forward_128clips_per_dispatch_h3p.txt). Each thread then
+// streams (row, channel quad) items 4 at a time, loads first.
+#define BN_AB_MAX_SEG 256
+#define BN_AB_SEGS 4
+template <bool FROM_SUMS>
+__global__ __launch_bounds__(256) void bn_seg_apply_blk_f32_kernel(
+    const float* __restrict__ y, float* z, const float* __restrict__ res,
+    const int* __restrict__ coffs, int nseg, int rpc, const float* __restrict__ ss,
+    const double* __restrict__ sums, int sums_c, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, int relu, long long M, int C, int y_stride,
+    int z_stride, int res_stride, int R, float* const* __restrict__ zind) {
+  __shared__ int loffs[BN_AB_MAX_SEG + 1];
+  __shared__ float lss[BN_AB_SEGS][2][BN_AS_MAX_C];
+  if (zind != nullptr) z = *zind;
+  const int tid = threadIdx.x;
+  for (int i = tid; i <= nseg; i += 256) loffs[i] = coffs[i] * rpc;
+  __syncthreads();
+  const long long r0 = (long long)blockIdx.x * R;
+  const long long r1 = min(r0 + R, M);
+  const long long lo_row = loffs[0], hi_row = loffs[nseg];
+  const long long va = max(r0, lo_row), vb = min(r1, hi_row);
+  auto seg_of = [&](long long r) {                 // last s with start(s) <= r
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (loffs[mid] <= r) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
+  int s_lo = 0, s_n = 0;
+  if (va < vb) {
+    s_lo = seg_of(va);
+    s_n = seg_of(vb - 1) - s_lo + 1;
+  }
+  const bool lds_ss = s_n <= BN_AB_SEGS && C <= BN_AS_MAX_C;
+  if (lds_ss) {
+    for (int t = tid; t < s_n * C; t += 256) {
+      const int k = t / C, c = t - k * C, sg = s_lo + k;
+      float scv, shv;
+      if constexpr (FROM_SUMS) {
+        const int rows = loffs[sg + 1] - loffs[sg];
+        const double* sp = sums + (size_t)sg * 2 * sums_c;
+        float mu = 0.f, va2 = 0.f;
+        if (rows > 0) {
+          const double m = sp[c] / (double)rows;
+          mu = (float)m;
+          va2 = (float)fmax(sp[sums_c + c] / (double)rows - m * m, 0.0);
+        }
+        scv = rows > 0 ? gamma[c] * rsqrtf(va2 + eps) : 0.f;   // empty video: rows -> 0
+        shv = rows > 0 ? beta[c] - mu * scv : 0.f;
+      } else {
+        scv = ss[(size_t)sg * 2 * C + c];
+        shv = ss[(size_t)sg * 2 * C + C + c];
+      }
+      lss[k][0][c] = scv;
+      lss[k][1][c] = shv;
+    }
+    __syncthreads();
+  }
+  // the block's segment boundaries (uniform), for the per-item segment pick
+  const long long b1 = s_n > 1 ? loffs[s_lo + 1] : hi_row, b2 = s_n > 2 ? loffs[s_lo + 2] : hi_row,
+                  b3 = s_n > 3 ? loffs[s_lo + 3] : hi_row;
+  const int cq = C >> 2;
+  const int n = (int)(r1 - r0) * cq;                 // <= 8192: R C <= 32768
+  for (int base = tid; base < n; base += 4 * 256) {
+    float4 v[4], rv[4];
+    long long rr[4];
+    int cc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int it = base + u * 256;
+      rr[u] = -1;
+      if (it < n) {
+        const int rl = it / cq;
+        rr[u] = r0 + rl;
+        cc[u] = (int)(it - rl * cq) * 4;
+        if (rr[u] >= lo_row && rr[u] < hi_row) {
+          v[u] = *(const float4*)(y + (size_t)rr[u] * y_stride + cc[u]);
+          if (res) rv[u] = *(const float4*)(res + (size_t)rr[u] * res_stride + cc[u]);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (rr[u] < 0) continue;
+      const long long r = rr[u];
+      const int c = cc[u];
+      if (r < lo_row || r >= hi_row) {
+        // rows outside every video (a graph bucket's padding clips): 0, so
+        // they stay bounded through the layers
+        *(float4*)(z + (size_t)r * z_stride + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+        continue;
+      }
+      float4 sc, sh;
+      if (lds_ss) {
+        const int k = (r >= b1) + (r >= b2) + (r >= b3);
+        sc = *(const float4*)&lss[k][0][c];
+        sh = *(const float4*)&lss[k][1][c];
+      } else {
+        const int sg = seg_of(r);
+        if constexpr (FROM_SUMS) {
+          bn_ss4_from_sums(sums + (size_t)sg * 2 * sums_c, sums_c, c, loffs[sg + 1] - loffs[sg],
+                           gamma, beta, eps, sc, sh);
+        } else {
+          sc = *(const float4*)(ss + (size_t)sg * 2 * C + c);
+          sh = *(const float4*)(ss + (size_t)sg * 2 * C + C + c);
+        }
+      }
+      float o[4] = {fmaf(v[u].x, sc.x, sh.x), fmaf(v[u].y, sc.y, sh.y), fmaf(v[u].z, sc.z, sh.z),
+                    fmaf(v[u].w, sc.w, sh.w)};
+      if (res) {
+        o[0] += rv[u].x; o[1] += rv[u].y; o[2] += rv[u].z; o[3] += rv[u].w;
+      }
+      if (relu) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = fmaxf(o[k], 0.f);
+      }
+      *(float4*)(z + (size_t)r * z_stride + c) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+// rows per block of the block-tiled apply: <= 128 KB of output, <= 3 rows per
+// clip (<= 4 videos per block), and >= ~1024 blocks where M allows
+static int bn_apply_rows_per_block(long long M, int C, int rpc) {
+  long long R = 32768 / C;
+  if (R > 3LL * rpc) R = 3LL * rpc;
+  const long long want = (M + 1023) / 1024;
+  if (R > want) R = want;
+  return (int)(R < 1 ? 1 : R);
+}
+
 // ---- BN tail (bn_tail.h): the finalize armed by the host for the next
 // producer launch that supports it, taken (and disarmed) by that launch ----
 static BnTail g_bn_tail = {};
+// block-tiled applies (bn_seg_apply_blk_f32_kernel); 0: the per-thread-row kernels
+static int g_bn_apply_blk = 1;
 static int g_bn_tail_taken = 0;
 
 BnTail bn_tail_take(long long waves) {
@@ -1032,6 +1174,7 @@ int rnb_bn_tail_arm(int* ticket, const double* sums, int sums_c, const int* coff
   return 0;
 }
 void rnb_bn_tail_disarm() { g_bn_tail.ticket = nullptr; }
+void rnb_bn_set_apply_blk(int on) { g_bn_apply_blk = on; }
 // 1 when a launch took the tail armed last (then its scale / shift rows are
 // written by that launch); resets
 int rnb_bn_tail_taken() {
@@ -1094,6 +1237,13 @@ int rnb_bn_seg_apply_f32_ind(const float* y, float* z, const float* res, const i
   if (zind != nullptr && ((uintptr_t)zind % 8) != 0) return -2;
   const long long n = (M + BN_APPLY_RPT - 1) / BN_APPLY_RPT * (C / 4);
   if (M > 0x7FFFFFFFLL) return -3;
+  if (nseg <= BN_AB_MAX_SEG && g_bn_apply_blk) {
+    const int R = bn_apply_rows_per_block(M, C, rpc);
+    hipLaunchKernelGGL(bn_seg_apply_blk_f32_kernel<false>, dim3((unsigned)((M + R - 1) / R)),
+                       dim3(256), 0, stream, y, z, res, coffs, nseg, rpc, ss, nullptr, 0, nullptr,
+                       nullptr, 0.f, relu, M, C, y_stride, z_stride, res_stride, R, zind);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(bn_seg_apply_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      stream, y, z, res, coffs, nseg, rpc, ss, relu, M, C, y_stride, z_stride,
                      res_stride, zind);
@@ -1114,6 +1264,13 @@ int rnb_bn_seg_apply_sums_f32(const float* y, float* z, const float* res, const 
   if (zind != nullptr && ((uintptr_t)zind % 8) != 0) return -2;
   const long long n = (M + BN_APPLY_RPT - 1) / BN_APPLY_RPT * (C / 4);
   if (M > 0x7FFFFFFFLL) return -3;
+  if (nseg <= BN_AB_MAX_SEG && g_bn_apply_blk) {
+    const int R = bn_apply_rows_per_block(M, C, rpc);
+    hipLaunchKernelGGL(bn_seg_apply_blk_f32_kernel<true>, dim3((unsigned)((M + R - 1) / R)),
+                       dim3(256), 0, stream, y, z, res, coffs, nseg, rpc, nullptr, sums, sums_c,
+                       gamma, beta, eps, relu, M, C, y_stride, z_stride, res_stride, R, zind);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(bn_seg_apply_sums_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      stream, y, z, res, coffs, nseg, rpc, sums, sums_c, gamma, beta, eps, relu, M,
                      C, y_stride, z_stride, res_stride, zind);

@@ -233,6 +233,11 @@ class Kernels:
         if os.environ.get("RNB_BN_BPS"):
             # fixed BN statistics blocks per segment (batch-invariant split)
             lib.rnb_bn_seg_set_bps(int(os.environ["RNB_BN_BPS"]))
+        lib.rnb_bn_set_apply_blk.argtypes = [ctypes.c_int]
+        lib.rnb_bn_set_apply_blk.restype = None
+        if "RNB_BN_APPLY_BLK" in os.environ:
+            # block-tiled BN applies (default 1; 0: the per-thread-row kernels)
+            lib.rnb_bn_set_apply_blk(int(os.environ["RNB_BN_APPLY_BLK"]))
         lib.rnb_bn_seg_set_fused_finalize.argtypes = [ctypes.c_int]
         if os.environ.get("RNB_BN_FUSED_FINALIZE"):
             # fused finalize + running-update kernel up to this many videos
@@ -495,6 +500,10 @@ class Kernels:
         conv launch that supports it (csrc/bn_tail.h); see ``bn_tail_taken``."""
         _check(self.lib.rnb_bn_tail_arm(ticket, sums, sums_c, coffs, nseg, rpc, C, gamma, beta,
                                         eps, ss), "bn_tail_arm")
+
+    def bn_set_apply_blk(self, on: bool) -> None:
+        """Block-tiled BN applies (bn_seg_apply_blk_f32_kernel) on / off."""
+        self.lib.rnb_bn_set_apply_blk(1 if on else 0)
 
     def bn_tail_disarm(self) -> None:
         self.lib.rnb_bn_tail_disarm()
