@@ -885,18 +885,22 @@ __global__ __launch_bounds__(256) void bn_seg_apply_sums_f32_kernel(
   }
 }
 
-// Block-tiled apply (the default for both applies): a block owns R
-// consecutive rows x all C channels (R C 4 <= 128 KB, R <= 3 rows-per-clip
+// Block-tiled apply (both applies, tensors <= BN_AB_MAX_ELEMS): a block owns
+// R consecutive rows x all C channels (R C 4 <= 128 KB, R <= 3 rows-per-clip
 // so the rows span at most 4 videos), and pays its prologue -- the videos'
 // row offsets into LDS, the segments of its rows, their scale / shift (from
-// the epilogue sums, or the finalize's rows) into LDS -- once per block.
+// the epilogue sums, or the finalize's rows) into LDS -- once per block;
 // bn_seg_apply_sums_f32_kernel gives each 256 threads 16 KB and re-walks
-// three binary searches of dependent global loads per block and thread: at
-// conv2's 64 channels and 128 videos it ran at 0.65 TB/s (0.49 ms per apply,
-// profiles/pmc/r5_forward_128clips_per_dispatch_h3p.txt). Each thread then
-// streams (row, channel quad) items 4 at a time, loads first.
+// three binary searches of dependent global loads per block and thread. Each
+// thread streams (row, channel quad) items 4 at a time, loads first.
 #define BN_AB_MAX_SEG 256
 #define BN_AB_SEGS 4
+// Large tensors keep the per-thread-row kernels: on conv2's 822 MB block
+// outputs both forms stream at ~5.2 TB/s (the apply is HBM-bound there, 2.5
+// GB per call, scripts/apply_bench.py) and the graphed 128-clip forward was
+// 0.3 ms slower block-tiled; one- to 16-clip forwards 0.03-0.05 ms faster
+// (profiles/r6_ab_bn_apply_blk.txt)
+#define BN_AB_MAX_ELEMS (8LL << 20)
 template <bool FROM_SUMS>
 __global__ __launch_bounds__(256) void bn_seg_apply_blk_f32_kernel(
     const float* __restrict__ y, float* z, const float* __restrict__ res,
@@ -1237,7 +1241,7 @@ int rnb_bn_seg_apply_f32_ind(const float* y, float* z, const float* res, const i
   if (zind != nullptr && ((uintptr_t)zind % 8) != 0) return -2;
   const long long n = (M + BN_APPLY_RPT - 1) / BN_APPLY_RPT * (C / 4);
   if (M > 0x7FFFFFFFLL) return -3;
-  if (nseg <= BN_AB_MAX_SEG && g_bn_apply_blk) {
+  if (nseg <= BN_AB_MAX_SEG && g_bn_apply_blk && M * C <= BN_AB_MAX_ELEMS) {
     const int R = bn_apply_rows_per_block(M, C, rpc);
     hipLaunchKernelGGL(bn_seg_apply_blk_f32_kernel<false>, dim3((unsigned)((M + R - 1) / R)),
                        dim3(256), 0, stream, y, z, res, coffs, nseg, rpc, ss, nullptr, 0, nullptr,
@@ -1264,7 +1268,7 @@ int rnb_bn_seg_apply_sums_f32(const float* y, float* z, const float* res, const 
   if (zind != nullptr && ((uintptr_t)zind % 8) != 0) return -2;
   const long long n = (M + BN_APPLY_RPT - 1) / BN_APPLY_RPT * (C / 4);
   if (M > 0x7FFFFFFFLL) return -3;
-  if (nseg <= BN_AB_MAX_SEG && g_bn_apply_blk) {
+  if (nseg <= BN_AB_MAX_SEG && g_bn_apply_blk && M * C <= BN_AB_MAX_ELEMS) {
     const int R = bn_apply_rows_per_block(M, C, rpc);
     hipLaunchKernelGGL(bn_seg_apply_blk_f32_kernel<true>, dim3((unsigned)((M + R - 1) / R)),
                        dim3(256), 0, stream, y, z, res, coffs, nseg, rpc, nullptr, sums, sums_c,
