@@ -79,13 +79,10 @@ __device__ unsigned long long* h3_phase_buf;
 // (256 B per clip), DMA'd with the step's activations
 #define H3_AFF_CLIPS 8
 
-// NS: LDS stages -- 2 (one step's DMAs in flight during a step's MFMAs) or 3
-// (two steps ahead: the wait at the end of a step leaves the newest stage in
-// flight)
-template <int TP, int TC, int WP, int WC, int MINB, bool ST, int NPROD, bool AFF, int NS = 2>
+template <int TP, int TC, int WP, int WC, int MINB, bool ST, int NPROD, bool AFF>
 __global__ __launch_bounds__(64 * WP * WC, MINB)
 void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
-  static_assert(NS == 2 || NS == 3, "LDS stages");
+  constexpr int NS = 2;
   constexpr int NW = WP * WC;
   constexpr int P_TILE = WP * TP * 16, C_TILE = WC * TC * 16;
   constexpr int PLANE = P_TILE * 64;               // one 16-channel sub-step, 64-B rows
@@ -307,35 +304,14 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
     t_begin = a;
     t_end = b;
   }
-  // DMA instructions this wave issues per stage (AFF: waves 0 / 1 one more)
-  const bool vm_plus = AFF && wave < 2;
-  auto wait_newest_in_flight = [&]() {       // every stage but the newest landed
-    if (vm_plus) x6d_wait_vm<VM_STAGE + 1>(); else x6d_wait_vm<VM_STAGE>();
-  };
   if (t_begin < t_end) issue(t_begin, 0);
-  if constexpr (NS == 3) {
-    if (t_begin + 1 < t_end) {
-      issue(t_begin + 1, 1);
-      wait_newest_in_flight();
-    } else {
-      x6d_wait_vm<0>();
-    }
-  }
   if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);    // as conv_x6_kernel
-  if constexpr (NS == 2) x6d_wait_vm<0>();
+  x6d_wait_vm<0>();
   x6d_barrier();
   for (int t = t_begin; t < t_end; ++t) {
     const int it = t - t_begin;
-    const int slot = NS == 2 ? (it & 1) : it % 3;
-    // NS 2: slot (it + 1) & 1 was read in step t - 1, finished by every wave;
-    // NS 3: slot (it + 2) % 3 likewise
-    bool ahead = false;
-    if constexpr (NS == 2) {
-      if (t + 1 < t_end) issue(t + 1, (it + 1) & 1);
-    } else {
-      ahead = t + 2 < t_end;
-      if (ahead) issue(t + 2, (it + 2) % 3);
-    }
+    // slot (it + 1) & 1 was read in step t - 1, finished by every wave
+    if (t + 1 < t_end) issue(t + 1, (it + 1) & 1);
     if constexpr (AFF) {
       // the tap of sub-steps 2t, 2t + 1: quad 0's gather-table requirement
       const __attribute__((address_space(4))) int* tab =
@@ -345,13 +321,10 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
     }
     H3B bf[TP];
 #pragma unroll
-    for (int tp = 0; tp < TP; ++tp) bf[tp] = load_b(slot, tp);
+    for (int tp = 0; tp < TP; ++tp) bf[tp] = load_b(it & 1, tp);
 #pragma unroll
-    for (int tc = 0; tc < TC; ++tc) mma_tc(slot, tc, bf);
-    if (NS == 3 && ahead)
-      wait_newest_in_flight();                 // step t + 1 landed, t + 2 may fly
-    else
-      x6d_wait_vm<0>();
+    for (int tc = 0; tc < TC; ++tc) mma_tc(it & 1, tc, bf);
+    x6d_wait_vm<0>();
     x6d_barrier();
   }
 
@@ -1141,13 +1114,12 @@ struct ConvH3Config {
   void (*kernel_aff_st)(const ConvF32Params, const X6DStats);
 };
 
-#define H3CFGS(TP, TC, WP, WC, MINB, NPROD, NS)                                \
+#define H3CFG(TP, TC, WP, WC, MINB, NPROD)                                     \
   {WP * TP * 16, WC * TC * 16, 64 * WP * WC, (TP) * (TC) <= H3_FIXUP_MAX_TILES,  \
-   conv_h3_kernel<TP, TC, WP, WC, MINB, false, NPROD, false, NS>,               \
-   conv_h3_kernel<TP, TC, WP, WC, MINB, true, NPROD, false, NS>,                \
-   conv_h3_kernel<TP, TC, WP, WC, MINB, false, NPROD, true, NS>,                \
-   conv_h3_kernel<TP, TC, WP, WC, MINB, true, NPROD, true, NS>}
-#define H3CFG(TP, TC, WP, WC, MINB, NPROD) H3CFGS(TP, TC, WP, WC, MINB, NPROD, 2)
+   conv_h3_kernel<TP, TC, WP, WC, MINB, false, NPROD, false>,                   \
+   conv_h3_kernel<TP, TC, WP, WC, MINB, true, NPROD, false>,                    \
+   conv_h3_kernel<TP, TC, WP, WC, MINB, false, NPROD, true>,                    \
+   conv_h3_kernel<TP, TC, WP, WC, MINB, true, NPROD, true>}
 // LDS per block = 2 stages x (P_TILE x 128 + C_TILE x 128) bytes
 static const ConvH3Config kH3Configs[] = {
     H3CFG(2, 9, 8, 1, 1, 3),   //  0: 256 px x 144 ch (100 KB)
@@ -1163,12 +1135,6 @@ static const ConvH3Config kH3Configs[] = {
     H3CFG(1, 8, 4, 1, 3, 3),   // 10:  64 px x 128 ch, 4 waves, 3 blocks per CU (48 KB)
     H3CFG(2, 9, 8, 1, 1, 4),   // 11: config 0 with the fourth product
     H3CFG(1, 9, 8, 1, 2, 4),   // 12: config 2 with the fourth product
-    // three LDS stages (two K steps in flight) for the small-tile configs
-    // that carry the temporal / stride-2 / conv5 convs
-    H3CFGS(1, 8, 4, 1, 2, 3, 3),   // 13: config 10, 3 stages (78 KB), 2 blocks per CU
-    H3CFGS(2, 4, 4, 2, 1, 3, 3),   // 14: config 9, 3 stages (102 KB)
-    H3CFGS(1, 8, 8, 1, 1, 3, 3),   // 15: config 4, 3 stages (102 KB)
-    H3CFGS(2, 4, 8, 1, 1, 3, 3),   // 16: config 5, 3 stages (126 KB)
 };
 static const int kNumH3Configs = sizeof(kH3Configs) / sizeof(kH3Configs[0]);
 
