@@ -417,8 +417,8 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
 // with the weights streamed per tap group (LDS-DMA, double-buffered): the
 // gathered activation traffic of the direct kernel drops 9x and the split
 // runs once per input value instead of once per tap.
-template <int NW, int TP, int TC, int HALO_PX, int G, bool ST, bool AFF>
-__global__ __launch_bounds__(64 * NW, 1)
+template <int NW, int TP, int TC, int HALO_PX, int G, bool ST, bool AFF, int MINB = 1>
+__global__ __launch_bounds__(64 * NW, MINB)
 void conv_h3r_kernel(const ConvF32Params p, const X6DStats st) {
   constexpr int P_TILE = NW * TP * 16, C_TILE = TC * 16;
   constexpr int HALO_BYTES = HALO_PX * 128;
@@ -486,7 +486,8 @@ void conv_h3r_kernel(const ConvF32Params p, const X6DStats st) {
   // spatial conv ran 1.68-1.85 ms with BN on load vs 1.40 ms without)
   // (AFF: 3 items' loads in flight at 4 tiles per wave, every item at 3:
   // the largest batches that compile without scratch)
-  constexpr int SB = AFF ? (NW > 8 ? 1 : (TP >= 4 ? 3 : ITEMS)) : ITEMS;
+  // (four waves per SIMD, MINB 4: 128 registers a lane, one item at a time)
+  constexpr int SB = MINB >= 4 ? 1 : AFF ? (NW > 8 ? 1 : (TP >= 4 ? 3 : ITEMS)) : ITEMS;
   auto stage = [&](int chunk) {
     x6f32x4 sc0, sh0, sc1, sh1;
     if constexpr (AFF) {
@@ -1255,11 +1256,12 @@ struct ConvH3RConfig {
   void (*kernel_aff)(const ConvF32Params, const X6DStats);
   void (*kernel_aff_st)(const ConvF32Params, const X6DStats);
 };
-#define H3RCFG(NW, TP, HALO, G)                                                    \
-  {NW, TP, HALO, 0, conv_h3r_kernel<NW, TP, 9, HALO, G, false, false>,             \
-   conv_h3r_kernel<NW, TP, 9, HALO, G, true, false>,                               \
-   conv_h3r_kernel<NW, TP, 9, HALO, G, false, true>,                               \
-   conv_h3r_kernel<NW, TP, 9, HALO, G, true, true>}
+#define H3RCFGM(NW, TP, HALO, G, MINB)                                             \
+  {NW, TP, HALO, 0, conv_h3r_kernel<NW, TP, 9, HALO, G, false, false, MINB>,       \
+   conv_h3r_kernel<NW, TP, 9, HALO, G, true, false, MINB>,                         \
+   conv_h3r_kernel<NW, TP, 9, HALO, G, false, true, MINB>,                         \
+   conv_h3r_kernel<NW, TP, 9, HALO, G, true, true, MINB>}
+#define H3RCFG(NW, TP, HALO, G) H3RCFGM(NW, TP, HALO, G, 1)
 // one wave per SIMD (conv_h3q_kernel): 4 waves x TP tiles
 #define H3QCFG(NW, TP, HALO, G, MINB)                                             \
   {NW, TP, HALO, 1, conv_h3q_kernel<NW, TP, HALO, G, MINB, false, false>,          \
@@ -1277,6 +1279,10 @@ static const ConvH3RConfig kH3RConfigs[] = {
     // 8: 8 waves x 4 tiles = 512 px (two waves per SIMD: one wave issues an
     // MFMA every ~16.5 cycles, two together every ~8.5, profiles/r3_mfma_split.txt)
     H3QCFG(8, 4, 640, 2, 1),
+    // 9: 7 waves x 2 tiles = 224 px (4 rows of W = 56 without padding pixels),
+    // one tap per barrier, 82 KB: two blocks per CU, so one block's patch
+    // staging (no MFMAs in flight) overlaps the other's taps
+    H3RCFGM(7, 2, 352, 1, 4),
 };
 
 int rnb_conv_h3r_num_variants() { return (int)(sizeof(kH3RConfigs) / sizeof(kH3RConfigs[0])); }
