@@ -1279,10 +1279,10 @@ static const ConvH3RConfig kH3RConfigs[] = {
     // 8: 8 waves x 4 tiles = 512 px (two waves per SIMD: one wave issues an
     // MFMA every ~16.5 cycles, two together every ~8.5, profiles/r3_mfma_split.txt)
     H3QCFG(8, 4, 640, 2, 1),
-    // 9: 7 waves x 2 tiles = 224 px (4 rows of W = 56 without padding pixels),
-    // one tap per barrier, 82 KB: two blocks per CU, so one block's patch
-    // staging (no MFMAs in flight) overlaps the other's taps
-    H3RCFGM(7, 2, 352, 1, 4),
+    // (7 waves x 2 tiles = 224 px, one tap per barrier, 82 KB, four waves per
+    // SIMD so two blocks share a CU: no faster on conv2 spatial, 1.62 vs 1.57
+    // ms for variant 7, a tie on conv4 spatial;
+    // profiles/r6_layers_h3r_224px_two_blocks_128clips.txt -- not kept)
 };
 
 int rnb_conv_h3r_num_variants() { return (int)(sizeof(kH3RConfigs) / sizeof(kH3RConfigs[0])); }

@@ -1009,10 +1009,9 @@ class ConvLayerF32:
             return True
         _, T, H, W, _ = x_shape
         # csrc/conv_h3.hip kH3RConfigs: 0-5 conv_h3r_kernel (x 2 barrier
-        # groupings), 6 / 7 / 8 conv_h3q_kernel (4 waves x 7 / 4 tiles, 8 x 4),
-        # 9 conv_h3r_kernel (7 waves x 2 tiles, two blocks per CU)
+        # groupings), 6 / 7 / 8 conv_h3q_kernel (4 waves x 7 / 4 tiles, 8 x 4)
         nw, tp, halo = ((7, 4, 600), (14, 2, 600), (7, 3, 480))[variant % 3] if variant < 6 \
-            else ((4, 7, 600), (4, 4, 344), (8, 4, 640), (7, 2, 352))[variant - 6]
+            else ((4, 7, 600), (4, 4, 344), (8, 4, 640))[variant - 6]
         rows = nw * tp * 16 // W
         # conv_h3q_kernel rows hold W + 1 entries (one shared zero column) + 1
         q = 6 <= variant <= 8
