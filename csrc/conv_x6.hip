@@ -30,7 +30,6 @@
 // which would make hipcc wait vmcnt(0)).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 #include "conv_f32_common.h"
 #include "x6_common.h"
@@ -556,13 +555,7 @@ static const int kNumX6Configs = sizeof(kX6Configs) / sizeof(kX6Configs[0]);
 extern "C" {
 
 int rnb_x6d_splitk_reduce(const ConvF32Params* p, const X6DStats* st, hipStream_t stream) {
-  // rows per thread: a thread's rows run one after another, each a round trip
-  // for its ksplit partials. Small outputs (the one-video calls' conv4 / conv5
-  // splits: 49-392 rows) get one row per thread -- more blocks, one round
-  // trip; big ones four (RNB_SPLITK_RPT overrides)
-  static const int rpt_env = getenv("RNB_SPLITK_RPT") ? atoi(getenv("RNB_SPLITK_RPT")) : 0;
-  const int rpt = rpt_env > 0 ? rpt_env
-                              : ((long long)p->M * p->Cout_p <= (1LL << 20) ? 1 : 4);
+  const int rpt = 4;                     // rows per thread: many threads, short chains
   const int rows_per_clip = p->To * p->Ho * p->Wo;
   const long long gx = (p->Cout_p / 4 + 63) / 64, gy = (p->M + 8 * rpt - 1) / (8 * rpt);
   X6DStats s = *st;
