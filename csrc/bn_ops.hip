@@ -1034,6 +1034,11 @@ static int bn_apply_rows_per_block(long long M, int C, int rpc) {
 static BnTail g_bn_tail = {};
 // block-tiled applies (bn_seg_apply_blk_f32_kernel); 0: the per-thread-row kernels
 static int g_bn_apply_blk = 1;
+// consumer-side scale / shift from sums (bn_tail.h BnAffSums); ss null = off
+static BnAffSums g_bn_aff = {};
+static int g_bn_aff_used = 0;
+const BnAffSums* bn_aff_armed() { return g_bn_aff.ss != nullptr ? &g_bn_aff : nullptr; }
+void bn_aff_mark_used() { g_bn_aff_used = 1; }
 static int g_bn_tail_taken = 0;
 
 BnTail bn_tail_take(long long waves) {
@@ -1179,6 +1184,26 @@ int rnb_bn_tail_arm(int* ticket, const double* sums, int sums_c, const int* coff
 }
 void rnb_bn_tail_disarm() { g_bn_tail.ticket = nullptr; }
 void rnb_bn_set_apply_blk(int on) { g_bn_apply_blk = on; }
+// Arms consumer-side scale / shift (bn_tail.h BnAffSums) for the launches of
+// the next conv whose input BN rows are `ss`; disarm after them.
+int rnb_bn_aff_arm(const double* sums, int sums_c, const int* coffs, int nseg, int rpc, int C,
+                   const float* gamma, const float* beta, float eps, float* ss) {
+  if (!sums || !coffs || !gamma || !beta || !ss) return -1;
+  if (nseg <= 0 || C <= 0 || sums_c < C || rpc <= 0) return -2;
+  BnAffSums a = {};
+  a.sums = sums; a.sums_c = sums_c; a.nseg = nseg; a.rpc = rpc; a.coffs = coffs;
+  a.gamma = gamma; a.beta = beta; a.eps = eps; a.ss = ss;
+  g_bn_aff = a;
+  g_bn_aff_used = 0;
+  return 0;
+}
+void rnb_bn_aff_disarm() { g_bn_aff.ss = nullptr; }
+// 1 when a launch computed the armed rows since the last call (resets)
+int rnb_bn_aff_used() {
+  const int u = g_bn_aff_used;
+  g_bn_aff_used = 0;
+  return u;
+}
 // 1 when a launch took the tail armed last (then its scale / shift rows are
 // written by that launch); resets
 int rnb_bn_tail_taken() {

@@ -88,3 +88,24 @@ static __device__ __forceinline__ void bn_tail_run(const BnTail& t) {
   }
   if (lane == leader) atomicExch(t.ticket, 0);
 }
+
+// BN scale / shift computed by the CONSUMING conv from the producer's epilogue
+// sums (the h3 direct kernel's input BN on load, X6DStats.aff_*): every block
+// writes the rows of all nseg videos into `ss` (identical values from every
+// block), drains its stores and then DMAs them as it does a finalize's rows --
+// the finalize dispatch is gone and its latency overlaps the consumer's start.
+// Armed by the host around the consumer's launches (rnb_bn_aff_arm); a launch
+// whose in_ss is the armed `ss` computes them.
+struct BnAffSums {
+  const double* sums;        // [nseg][2][sums_c]
+  int sums_c, nseg, rpc;
+  const int* coffs;          // [nseg + 1] clip offsets
+  const float* gamma;
+  const float* beta;
+  float eps;
+  float* ss;                 // [nseg][2][C] out (C = the consumer's Cin_p)
+};
+// host: the armed descriptor, or null; a launch that uses it marks it (defined
+// in bn_ops.hip)
+const BnAffSums* bn_aff_armed();
+void bn_aff_mark_used();

@@ -137,6 +137,33 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
   // split weights [K_pad / 32][w_rows][128 B]
   const x6d_u32x4 wr = x6d_rsrc(p.w, (uint32_t)(p.K_pad / 32) * (uint32_t)p.w_rows * 128u);
 
+  // AFF from sums (st.aff_sums): the scale / shift rows of every video, as
+  // bn_seg_ss_from_sums_f32_kernel computes them, into st.in_ss before this
+  // block DMAs any (every block writes the same values; its own stores are
+  // drained and ordered before its reads)
+  if constexpr (AFF) {
+    if (st.aff_sums != nullptr) {
+      const int E = st.aff_nseg * p.Cin_p;
+      float* ssw = const_cast<float*>(st.in_ss);
+      for (int i = threadIdx.x; i < E; i += 64 * NW) {
+        const int v = i / p.Cin_p, c = i - v * p.Cin_p;
+        const int rows = (st.aff_coffs[v + 1] - st.aff_coffs[v]) * st.aff_rpc;
+        const double* sp = st.aff_sums + (size_t)v * 2 * st.aff_sums_c;
+        float mu = 0.f, va = 0.f;
+        if (rows > 0) {
+          const double m = sp[c] / (double)rows;
+          mu = (float)m;
+          va = (float)fmax(sp[st.aff_sums_c + c] / (double)rows - m * m, 0.0);
+        }
+        const float sc = rows > 0 ? st.aff_gamma[c] * rsqrtf(va + st.aff_eps) : 0.f;
+        ssw[(size_t)v * 2 * p.Cin_p + c] = sc;
+        ssw[(size_t)v * 2 * p.Cin_p + p.Cin_p + c] = rows > 0 ? st.aff_beta[c] - mu * sc : 0.f;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
   // AFF: clips of the tile (clip_lo .. clip_lo + 7), the scale/shift DMA
   // lane's clip / sub-step / row (scale or shift) / quad, and its video
   const int rows_per_clip = p.To * p.Ho * p.Wo;
@@ -1218,6 +1245,20 @@ int rnb_conv_h3_launch(const ConvF32Params* pp, int config_id, hipStream_t strea
   const bool aff = in_ss != nullptr;
   if (aff && (!in_seg || !rnb_conv_h3_affine_ok(config_id, p.Cin_p, p.To * p.Ho * p.Wo)))
     return -16;
+  if (const BnAffSums* a = aff ? bn_aff_armed() : nullptr) {
+    if (a->ss == in_ss) {                      // this conv computes its input BN rows
+      if (a->sums_c < p.Cin_p) return -18;
+      st.aff_sums = a->sums;
+      st.aff_sums_c = a->sums_c;
+      st.aff_nseg = a->nseg;
+      st.aff_rpc = a->rpc;
+      st.aff_coffs = a->coffs;
+      st.aff_gamma = a->gamma;
+      st.aff_beta = a->beta;
+      st.aff_eps = a->eps;
+      bn_aff_mark_used();
+    }
+  }
   if (ksplit > 1) {
     if (!ws || ksplit > 16) return -14;
     st.ksplit = ksplit;

@@ -77,6 +77,14 @@ struct X6DStats {
   int* tick = nullptr;
   // BN finalize folded into this launch (bn_tail.h); ticket null = off
   BnTail tail = {};
+  // conv_h3.hip AFF only: the input BN's scale / shift rows computed here into
+  // in_ss from the producer's sums (bn_tail.h BnAffSums); null = off
+  const double* aff_sums = nullptr;
+  int aff_sums_c = 0, aff_nseg = 0, aff_rpc = 0;
+  const int* aff_coffs = nullptr;
+  const float* aff_gamma = nullptr;
+  const float* aff_beta = nullptr;
+  float aff_eps = 0.f;
 };
 
 // true when any element of v is +-inf or NaN (v_cmp_class: sNaN, qNaN, -inf, +inf)

@@ -470,6 +470,31 @@ class R2P1DEngine:
         # (opt-in: per-wave tickets on one address serialise at the memory
         # side, +0.46 ms per one-clip forward, profiles/r6_ab_bn_tail_fixup.txt)
         tail_max = int(os.environ.get("RNB_BN_TAIL_MAX", "0")) if hip else 0
+        # consumer-side scale / shift (csrc/bn_tail.h BnAffSums): a deferred BN
+        # whose consumer is an h3 direct config with BN on load, videos x
+        # channels <= this, has its rows computed by that conv from the sums
+        # (no finalize dispatch); 0 = off
+        aff_max = int(os.environ.get("RNB_BN_AFF_SUMS_MAX", "2304")) if hip else 0
+        pending_aff = None           # bn_aff_arm arguments for pending's consumer
+        from ...ops.native import kernels as _kn
+
+        def consume(fn):
+            """Run the conv consuming ``pending`` (armed for it when its rows
+            come from the sums)."""
+            nonlocal pending_aff
+            if pending_aff is None:
+                return fn()
+            _kn().bn_aff_arm(*pending_aff)
+            try:
+                out = fn()
+                if not _kn().bn_aff_used():
+                    raise RuntimeError("a deferred BN's rows were left to a conv that did not "
+                                       "compute them from the sums")
+                return out
+            finally:
+                _kn().bn_aff_disarm()
+                pending_aff = None
+
         for i, op in enumerate(self.ops):
             if skip:                      # temporal half of a fused pair
                 skip = False
@@ -513,7 +538,7 @@ class R2P1DEngine:
                             # the finalize rides on the producer's last launch (BN tail)
                             tail_ss, kw["bn_tail"] = op.bn.tail_args(
                                 coffs, sums, yshape[1] * yshape[2] * yshape[3])
-                    y = op.layer.forward_hip(src, None, **kw)
+                    y = consume(lambda: op.layer.forward_hip(src, None, **kw))
                     if tail_ss is not None:
                         from ...ops.native import kernels as _kn
                         if tuple(y.shape) != yshape:
@@ -536,6 +561,14 @@ class R2P1DEngine:
                         if tail_ss is not None:
                             bn_mod._RUN_SINK[0].append((op.bn, sums, thw))
                             pending = (tail_ss, clip_seg)
+                        elif (sums is not None and aff_max > 0 and bn_mod._RUN_SINK[0] is not None
+                              and (coffs.numel() - 1) * op.bn.channels_p <= aff_max
+                              and self.ops[i + 1].layer.takes_sums_affine(y.shape)):
+                            # the consuming h3 direct conv computes the rows
+                            ss, pending_aff = op.bn.aff_args(coffs, sums, thw)
+                            bn_mod._RUN_SINK[0].append((op.bn, sums, thw))
+                            pending = (ss, clip_seg)
+                            self.bn_aff_sums = getattr(self, "bn_aff_sums", 0) + 1
                         else:
                             pending = (op.bn.scale_shift_f32(y, coffs, sums, rpc=thw), clip_seg)
                     else:
@@ -560,7 +593,8 @@ class R2P1DEngine:
                      else op.layer.forward_torch(src, res, prepacked=True))
             elif hip:
                 if pending is not None:           # the producer's deferred BN + ReLU
-                    y = op.layer.forward_hip(src, res, in_affine=pending)
+                    aff = pending
+                    y = consume(lambda: op.layer.forward_hip(src, res, in_affine=aff))
                     pending = None
                 else:
                     y = op.layer.forward_hip(src, res)

@@ -336,6 +336,21 @@ class BatchNormBatch:
                     int(rpc), C, self.gamma.data_ptr(), self.beta.data_ptr(), self.eps,
                     ss.data_ptr())
 
+    def aff_args(self, segments: torch.Tensor, sums: torch.Tensor, rpc: int):
+        """(scale/shift [nseg, 2, Cp] fp32, ``kernels().bn_aff_arm`` arguments):
+        the consuming h3 direct conv computes these rows from the producer's
+        sums itself (csrc/bn_tail.h BnAffSums) -- no finalize dispatch. The
+        caller arms them around the consumer's launches and appends (self,
+        sums, rpc) to the forward's running sink as the ss-only path does."""
+        nseg, C = segments.numel() - 1, self.channels_p
+        if (sums.dtype != torch.float64 or not sums.is_contiguous() or sums.dim() != 3
+                or sums.shape[0] < nseg or sums.shape[1] != 2 or sums.shape[2] < C):
+            raise ValueError("epilogue sums %s do not match %d segments x %d channels"
+                             % (tuple(sums.shape), nseg, C))
+        ss = torch.empty((nseg, 2, C), dtype=torch.float32, device=sums.device)
+        return ss, (sums.data_ptr(), sums.shape[2], segments.data_ptr(), nseg, int(rpc), C,
+                    self.gamma.data_ptr(), self.beta.data_ptr(), self.eps, ss.data_ptr())
+
     def epilogue_sums(self, nseg: int, device) -> torch.Tensor:
         """fp64 [nseg, 2, Cp] per-segment (sum, sum of squares) for a producer
         conv's epilogue to accumulate into: zero on return, and zeroed again

@@ -1327,6 +1327,16 @@ class ConvLayerF32:
         cid = self.config_for(x_shape)
         return cid in WINO_ALL or is_x6d(cid)
 
+    def takes_sums_affine(self, x_shape) -> bool:
+        """True when this conv's kernel for ``x_shape`` is an h3 direct config
+        that applies its input BatchNorm on load and can compute the scale /
+        shift rows itself from the producer's sums (``kernels().bn_aff_arm``)."""
+        cid = self.config_for(x_shape)
+        if not is_h3(cid) or is_h3w(cid) or is_h3t(cid) or is_h3u(cid) or is_h3p(cid) \
+                or is_h3stem(cid) or is_h3s(cid) or is_h3r(cid):
+            return False
+        return self.affine_ok(cid, x_shape)
+
     def accepts_input_affine(self, x_shape) -> bool:
         """True when this conv's kernel for ``x_shape`` can apply its input's
         BatchNorm + ReLU on load (``forward_hip(in_affine=...)``): temporal

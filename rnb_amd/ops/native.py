@@ -233,6 +233,14 @@ class Kernels:
         if os.environ.get("RNB_BN_BPS"):
             # fixed BN statistics blocks per segment (batch-invariant split)
             lib.rnb_bn_seg_set_bps(int(os.environ["RNB_BN_BPS"]))
+        lib.rnb_bn_aff_arm.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p]
+        lib.rnb_bn_aff_arm.restype = ctypes.c_int
+        lib.rnb_bn_aff_disarm.argtypes = []
+        lib.rnb_bn_aff_disarm.restype = None
+        lib.rnb_bn_aff_used.argtypes = []
+        lib.rnb_bn_aff_used.restype = ctypes.c_int
         lib.rnb_bn_set_apply_blk.argtypes = [ctypes.c_int]
         lib.rnb_bn_set_apply_blk.restype = None
         if "RNB_BN_APPLY_BLK" in os.environ:
@@ -500,6 +508,19 @@ class Kernels:
         conv launch that supports it (csrc/bn_tail.h); see ``bn_tail_taken``."""
         _check(self.lib.rnb_bn_tail_arm(ticket, sums, sums_c, coffs, nseg, rpc, C, gamma, beta,
                                         eps, ss), "bn_tail_arm")
+
+    def bn_aff_arm(self, sums, sums_c, coffs, nseg, rpc, C, gamma, beta, eps, ss) -> None:
+        """The next h3 direct launches whose input BN rows are ``ss`` compute
+        them from the producer's fp64 ``sums`` (csrc/bn_tail.h BnAffSums)."""
+        _check(self.lib.rnb_bn_aff_arm(sums, sums_c, coffs, nseg, rpc, C, gamma, beta, eps, ss),
+               "bn_aff_arm")
+
+    def bn_aff_disarm(self) -> None:
+        self.lib.rnb_bn_aff_disarm()
+
+    def bn_aff_used(self) -> bool:
+        """True when a launch computed the armed rows since the last call."""
+        return bool(self.lib.rnb_bn_aff_used())
 
     def bn_set_apply_blk(self, on: bool) -> None:
         """Block-tiled BN applies (bn_seg_apply_blk_f32_kernel) on / off."""

@@ -12,6 +12,10 @@ forward with the tail against the separate-finalize path.
 The split-K fix-up: the last-arriving block of a tile sums the partials in
 split order and runs the epilogue -- outputs bit-identical to the reduce
 kernel's, tick counters back at zero, BN sums within fp32 class of fp64.
+
+Consumer-side rows (csrc/bn_tail.h BnAffSums): an h3 direct conv with its
+input BN on load computes the scale / shift rows from the producer's sums
+itself; checked per config against the finalize kernel's rows, and end to end.
 """
 import pytest
 import torch
@@ -159,6 +163,92 @@ def test_engine_bn_tail_matches_separate_finalize(monkeypatch, n, offs):
                      for op in eng.ops if op.bn is not None])
     scale = outs[0].abs().max().item()
     assert (outs[0] - outs[1]).abs().max().item() <= 1e-5 * scale + 1e-6
+    for (m0, v0), (m1, v1) in zip(runs[0], runs[1]):
+        assert torch.allclose(m0, m1, rtol=1e-5, atol=1e-6)
+        assert torch.allclose(v0, v1, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("cin,cout,k,p,thw", [
+    (144, 64, (3, 1, 1), (1, 0, 0), (4, 14, 14)),      # temporal
+    (576, 256, (3, 1, 1), (1, 0, 0), (2, 14, 14)),     # conv4 temporal (split-K territory)
+    (64, 144, (1, 3, 3), (0, 1, 1), (4, 14, 14)),      # spatial
+])
+def test_h3_input_bn_rows_from_sums_match_finalize(cin, cout, k, p, thw):
+    """Consumer-side input BN (csrc/bn_tail.h BnAffSums): every h3 direct
+    config that applies its input BN on load, with the scale / shift rows
+    computed by the conv itself from the producer's sums, against the same
+    conv fed the finalize kernel's rows: rows and outputs agree."""
+    from rnb_amd.ops.bn import BatchNormBatch
+    from rnb_amd.ops import conv_f32 as cf
+    from rnb_amd.ops.native import kernels
+    kn = kernels()
+    layer = _layer(cin, cout, k, (1, 1, 1), p, relu=True)
+    x = _input(3, thw, layer.geom.cin_p, cin)
+    bnm = torch.nn.BatchNorm3d(cin)
+    with torch.no_grad():
+        bnm.weight.uniform_(0.5, 1.5)
+        bnm.bias.uniform_(-0.2, 0.2)
+    bn = BatchNormBatch(bnm, layer.geom.cin_p, DEV)
+    coffs = torch.tensor([0, 2, 3], dtype=torch.int32, device=DEV)
+    seg = torch.tensor([0, 0, 1], dtype=torch.int32, device=DEV)
+    rpc = thw[0] * thw[1] * thw[2]
+    sums = torch.zeros((2, 2, layer.geom.cin_p), dtype=torch.float64, device=DEV)
+    for v, (a, b) in enumerate([(0, 2), (2, 3)]):
+        xd = x[a:b].double().reshape(-1, layer.geom.cin_p)
+        sums[v, 0] = xd.sum(0)
+        sums[v, 1] = (xd * xd).sum(0)
+    stream = torch.cuda.current_stream().cuda_stream
+    ref_ss = torch.empty((2, 2, layer.geom.cin_p), device=DEV)
+    mean = torch.empty((2, layer.geom.cin_p), device=DEV)
+    var = torch.empty_like(mean)
+    kn.bn_seg_ss_from_sums_f32(sums.data_ptr(), sums.shape[2], coffs.data_ptr(), 2, rpc,
+                               layer.geom.cin_p, bn.gamma.data_ptr(), bn.beta.data_ptr(), bn.eps,
+                               mean.data_ptr(), var.data_ptr(), ref_ss.data_ptr(), stream)
+    ids = [c for c in layer.candidates(x.shape)
+           if cf.is_h3(c) and not (cf.is_h3w(c) or cf.is_h3t(c) or cf.is_h3p(c) or cf.is_h3r(c)
+                                   or cf.is_h3stem(c) or cf.is_h3s(c) or cf.is_h3u(c))
+           and layer.affine_ok(c, x.shape)]
+    assert ids
+    for cid in ids:
+        y_ref = layer.forward_hip(x, config=cid, in_affine=(ref_ss, seg))
+        ss, args = bn.aff_args(coffs, sums, rpc)
+        ss.fill_(float("nan"))
+        kn.bn_aff_arm(*args)
+        try:
+            y = layer.forward_hip(x, config=cid, in_affine=(ss, seg))
+            assert kn.bn_aff_used(), cid
+        finally:
+            kn.bn_aff_disarm()
+        torch.cuda.synchronize()
+        assert torch.allclose(ss, ref_ss, rtol=1e-6, atol=1e-7), cid
+        scale = y_ref.abs().max().item()
+        assert (y - y_ref).abs().max().item() <= 1e-6 * scale + 1e-7, cid
+
+
+@pytest.mark.parametrize("n,offs", [(1, [0, 1]), (2, [0, 1, 2]), (4, [0, 3, 4, 4])])
+def test_engine_input_bn_rows_from_sums(monkeypatch, n, offs):
+    """A one- to four-clip R(2+1)D-34 forward whose h3 direct consumers
+    compute their input BN rows from the sums (default) against the finalize
+    dispatches (RNB_BN_AFF_SUMS_MAX=0): logits and running statistics agree."""
+    from rnb_amd.models.r2p1d.model import build_network
+    from rnb_amd.models.r2p1d.engine import R2P1DEngine
+    g = torch.Generator()
+    net = build_network(1, 5, depth=34, seed=2)
+    outs, runs = [], []
+    for cap in ("0", "2304"):
+        monkeypatch.setenv("RNB_BN_AFF_SUMS_MAX", cap)
+        eng = R2P1DEngine(net, DEV, backend="hip", bn_mode="batch", dtype=torch.float32)
+        x = torch.randn(eng.input_shape(n), generator=g.manual_seed(11)).to(DEV)
+        for _ in range(2):
+            y = eng.forward(x, clip_offsets=offs)
+        torch.cuda.synchronize()
+        outs.append((y.cpu(), getattr(eng, "bn_aff_sums", 0)))
+        runs.append([(op.bn.running_mean.cpu(), op.bn.running_var.cpu())
+                     for op in eng.ops if op.bn is not None])
+    (y0, c0), (y1, c1) = outs
+    assert c0 == 0
+    scale = y0.abs().max().item()
+    assert (y0 - y1).abs().max().item() <= 1e-5 * scale + 1e-6
     for (m0, v0), (m1, v1) in zip(runs[0], runs[1]):
         assert torch.allclose(m0, m1, rtol=1e-5, atol=1e-6)
         assert torch.allclose(v0, v1, rtol=1e-5, atol=1e-6)
