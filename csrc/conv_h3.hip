@@ -137,33 +137,6 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
   // split weights [K_pad / 32][w_rows][128 B]
   const x6d_u32x4 wr = x6d_rsrc(p.w, (uint32_t)(p.K_pad / 32) * (uint32_t)p.w_rows * 128u);
 
-  // AFF from sums (st.aff_sums): the scale / shift rows of every video, as
-  // bn_seg_ss_from_sums_f32_kernel computes them, into st.in_ss before this
-  // block DMAs any (every block writes the same values; its own stores are
-  // drained and ordered before its reads)
-  if constexpr (AFF) {
-    if (st.aff_sums != nullptr) {
-      const int E = st.aff_nseg * p.Cin_p;
-      float* ssw = const_cast<float*>(st.in_ss);
-      for (int i = threadIdx.x; i < E; i += 64 * NW) {
-        const int v = i / p.Cin_p, c = i - v * p.Cin_p;
-        const int rows = (st.aff_coffs[v + 1] - st.aff_coffs[v]) * st.aff_rpc;
-        const double* sp = st.aff_sums + (size_t)v * 2 * st.aff_sums_c;
-        float mu = 0.f, va = 0.f;
-        if (rows > 0) {
-          const double m = sp[c] / (double)rows;
-          mu = (float)m;
-          va = (float)fmax(sp[st.aff_sums_c + c] / (double)rows - m * m, 0.0);
-        }
-        const float sc = rows > 0 ? st.aff_gamma[c] * rsqrtf(va + st.aff_eps) : 0.f;
-        ssw[(size_t)v * 2 * p.Cin_p + c] = sc;
-        ssw[(size_t)v * 2 * p.Cin_p + p.Cin_p + c] = rows > 0 ? st.aff_beta[c] - mu * sc : 0.f;
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  }
-
   // AFF: clips of the tile (clip_lo .. clip_lo + 7), the scale/shift DMA
   // lane's clip / sub-step / row (scale or shift) / quad, and its video
   const int rows_per_clip = p.To * p.Ho * p.Wo;
@@ -182,7 +155,7 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
     }
   }
 
-  auto issue = [&](int t, int slot) {
+  auto issue = [&](int t, int slot, bool with_ss = true) {
     // the 8 gather-table entries of sub-steps 2t, 2t + 1 (scalar loads)
     const __attribute__((address_space(4))) int* tab =
         (const __attribute__((address_space(4))) int*)(p.ktab + t * 8);
@@ -216,7 +189,7 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
     }
     if constexpr (AFF) {
       // the input channels of sub-step 2t + ss_sub (Cin_p % 16 == 0: one tap)
-      if (wave < 2) {
+      if (wave < 2 && with_ss) {
         const int cb = ((2 * t + ss_sub) * 16) % p.Cin_p;
         x6d_dma16(sr, ss_off == X6D_INVALID ? X6D_INVALID : ss_off + (uint32_t)(cb * 4),
                   base + ACT_BYTES + W_BYTES + wave * 1024);
@@ -331,7 +304,54 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
     t_begin = a;
     t_end = b;
   }
-  if (t_begin < t_end) issue(t_begin, 0);
+  // AFF from sums (st.aff_sums): this conv computes the input BN's scale /
+  // shift rows from the producer's sums itself, with the formulas of
+  // bn_seg_ss_from_sums_f32_kernel -- every video's rows into st.in_ss (each
+  // block writes the same values; the wait below drains them before step 1's
+  // DMA reads them) and step 0's rows straight into its LDS stage, while step
+  // 0's activation and weight DMAs are in flight
+  const bool sums_mode = AFF && st.aff_sums != nullptr;
+  if (t_begin < t_end) issue(t_begin, 0, !sums_mode);
+  if constexpr (AFF) {
+    if (sums_mode) {
+      auto ss_of = [&](int v, int c, float& sc, float& sh) {
+        const int rows = (st.aff_coffs[v + 1] - st.aff_coffs[v]) * st.aff_rpc;
+        const double* sp = st.aff_sums + (size_t)v * 2 * st.aff_sums_c;
+        float mu = 0.f, va = 0.f;
+        if (rows > 0) {
+          const double m = sp[c] / (double)rows;
+          mu = (float)m;
+          va = (float)fmax(sp[st.aff_sums_c + c] / (double)rows - m * m, 0.0);
+        }
+        sc = rows > 0 ? st.aff_gamma[c] * rsqrtf(va + st.aff_eps) : 0.f;
+        sh = rows > 0 ? st.aff_beta[c] - mu * sc : 0.f;
+      };
+      const int E = st.aff_nseg * p.Cin_p;
+      float* ssw = const_cast<float*>(st.in_ss);
+      for (int i = threadIdx.x; i < E; i += 64 * NW) {
+        const int v = i / p.Cin_p, c = i - v * p.Cin_p;
+        float sc, sh;
+        ss_of(v, c, sc, sh);
+        ssw[(size_t)v * 2 * p.Cin_p + c] = sc;
+        ssw[(size_t)v * 2 * p.Cin_p + p.Cin_p + c] = sh;
+      }
+      if (t_begin < t_end) {
+        // step 0's stage: [clip slot][sub-step][scale, shift][16 channels], as the DMA lays it
+        float* l0 = (float*)(lds + ACT_BYTES + W_BYTES);
+        for (int i = threadIdx.x; i < H3_AFF_CLIPS * 64; i += 64 * NW) {
+          const int ci = i >> 6, sub = (i >> 5) & 1, which = (i >> 4) & 1, ch = i & 15;
+          const int clip = clip_lo + ci;
+          float v = 0.f;
+          if (clip < p.N && clip * rows_per_clip < p0 + P_TILE) {
+            float sc, sh;
+            ss_of(st.in_seg[clip], ((2 * t_begin + sub) * 16) % p.Cin_p + ch, sc, sh);
+            v = which ? sh : sc;
+          }
+          l0[i] = v;
+        }
+      }
+    }
+  }
   if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);    // as conv_x6_kernel
   x6d_wait_vm<0>();
   x6d_barrier();
