@@ -67,6 +67,10 @@ __device__ unsigned long long* h3_phase_buf;
 #define H3_PHASE(k) do {} while (0)
 #endif
 
+// consumer-side input BN rows (X6DStats.aff_sums): at most this many videos x
+// channels (the host's RNB_BN_AFF_SUMS_MAX cap)
+#define H3_AFF_SUMS_MAX 2304
+
 // split-K fix-up in the kernel (X6DStats.tick) for configs with at most this
 // many accumulator tiles per wave (the split-K set; bigger tiles would spill)
 #define H3_FIXUP_MAX_TILES 18
@@ -314,40 +318,67 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
   if (t_begin < t_end) issue(t_begin, 0, !sums_mode);
   if constexpr (AFF) {
     if (sums_mode) {
-      auto ss_of = [&](int v, int c, float& sc, float& sh) {
-        const int rows = (st.aff_coffs[v + 1] - st.aff_coffs[v]) * st.aff_rpc;
-        const double* sp = st.aff_sums + (size_t)v * 2 * st.aff_sums_c;
-        float mu = 0.f, va = 0.f;
-        if (rows > 0) {
-          const double m = sp[c] / (double)rows;
-          mu = (float)m;
-          va = (float)fmax(sp[st.aff_sums_c + c] / (double)rows - m * m, 0.0);
-        }
-        sc = rows > 0 ? st.aff_gamma[c] * rsqrtf(va + st.aff_eps) : 0.f;
-        sh = rows > 0 ? st.aff_beta[c] - mu * sc : 0.f;
-      };
+      // entries of this thread: global rows i = tid + k NT (k < KG) of the
+      // nseg x Cin_p table, then step 0's LDS entries j = tid + k NT (k < KL);
+      // every load first (one round trip under step 0's DMAs), then the math
+      constexpr int NT = 64 * NW;
+      constexpr int KG = (H3_AFF_SUMS_MAX + NT - 1) / NT;
+      constexpr int KL = (H3_AFF_CLIPS * 64 + NT - 1) / NT;
       const int E = st.aff_nseg * p.Cin_p;
-      float* ssw = const_cast<float*>(st.in_ss);
-      for (int i = threadIdx.x; i < E; i += 64 * NW) {
-        const int v = i / p.Cin_p, c = i - v * p.Cin_p;
-        float sc, sh;
-        ss_of(v, c, sc, sh);
-        ssw[(size_t)v * 2 * p.Cin_p + c] = sc;
-        ssw[(size_t)v * 2 * p.Cin_p + p.Cin_p + c] = sh;
-      }
-      if (t_begin < t_end) {
-        // step 0's stage: [clip slot][sub-step][scale, shift][16 channels], as the DMA lays it
-        float* l0 = (float*)(lds + ACT_BYTES + W_BYTES);
-        for (int i = threadIdx.x; i < H3_AFF_CLIPS * 64; i += 64 * NW) {
-          const int ci = i >> 6, sub = (i >> 5) & 1, which = (i >> 4) & 1, ch = i & 15;
-          const int clip = clip_lo + ci;
-          float v = 0.f;
-          if (clip < p.N && clip * rows_per_clip < p0 + P_TILE) {
-            float sc, sh;
-            ss_of(st.in_seg[clip], ((2 * t_begin + sub) * 16) % p.Cin_p + ch, sc, sh);
-            v = which ? sh : sc;
+      double a1[KG + KL], a2[KG + KL];
+      float gm[KG + KL], bt[KG + KL];
+      int rows[KG + KL], dst[KG + KL];            // dst: < 0 none; global index, or ~LDS index
+#pragma unroll
+      for (int k = 0; k < KG + KL; ++k) {
+        int v = -1, c = 0;
+        dst[k] = -1;
+        if (k < KG) {
+          const int i = threadIdx.x + k * NT;
+          if (i < E) {
+            v = i / p.Cin_p;
+            c = i - v * p.Cin_p;
+            dst[k] = i;
           }
-          l0[i] = v;
+        } else if (t_begin < t_end) {
+          const int j = threadIdx.x + (k - KG) * NT;
+          const int ci = j >> 6, sub = (j >> 5) & 1, ch = j & 15;
+          const int clip = clip_lo + ci;
+          if (j < H3_AFF_CLIPS * 64) {
+            dst[k] = ~j;
+            if (clip < p.N && clip * rows_per_clip < p0 + P_TILE) {
+              v = st.in_seg[clip];
+              c = ((2 * t_begin + sub) * 16) % p.Cin_p + ch;
+            }
+          }
+        }
+        const double* sp = st.aff_sums + (size_t)(v < 0 ? 0 : v) * 2 * st.aff_sums_c;
+        a1[k] = v >= 0 ? sp[c] : 0.0;
+        a2[k] = v >= 0 ? sp[st.aff_sums_c + c] : 0.0;
+        gm[k] = v >= 0 ? st.aff_gamma[c] : 0.f;
+        bt[k] = v >= 0 ? st.aff_beta[c] : 0.f;
+        rows[k] = v >= 0 ? (st.aff_coffs[v + 1] - st.aff_coffs[v]) * st.aff_rpc : 0;
+      }
+      float* ssw = const_cast<float*>(st.in_ss);
+      float* l0 = (float*)(lds + ACT_BYTES + W_BYTES);    // step 0's stage (slot 0)
+#pragma unroll
+      for (int k = 0; k < KG + KL; ++k) {
+        if (dst[k] == -1) continue;
+        // formulas of bn_seg_ss_from_sums_f32_kernel; no video: 0
+        float mu = 0.f, va = 0.f;
+        if (rows[k] > 0) {
+          const double m = a1[k] / (double)rows[k];
+          mu = (float)m;
+          va = (float)fmax(a2[k] / (double)rows[k] - m * m, 0.0);
+        }
+        const float sc = rows[k] > 0 ? gm[k] * rsqrtf(va + st.aff_eps) : 0.f;
+        const float sh = rows[k] > 0 ? bt[k] - mu * sc : 0.f;
+        if (dst[k] >= 0) {
+          const int v = dst[k] / p.Cin_p, c = dst[k] - v * p.Cin_p;
+          ssw[(size_t)v * 2 * p.Cin_p + c] = sc;
+          ssw[(size_t)v * 2 * p.Cin_p + p.Cin_p + c] = sh;
+        } else {
+          const int j = ~dst[k];
+          l0[j] = ((j >> 4) & 1) ? sh : sc;
         }
       }
     }
@@ -1267,7 +1298,7 @@ int rnb_conv_h3_launch(const ConvF32Params* pp, int config_id, hipStream_t strea
     return -16;
   if (const BnAffSums* a = aff ? bn_aff_armed() : nullptr) {
     if (a->ss == in_ss) {                      // this conv computes its input BN rows
-      if (a->sums_c < p.Cin_p) return -18;
+      if (a->sums_c < p.Cin_p || (long long)a->nseg * p.Cin_p > H3_AFF_SUMS_MAX) return -18;
       st.aff_sums = a->sums;
       st.aff_sums_c = a->sums_c;
       st.aff_nseg = a->nseg;

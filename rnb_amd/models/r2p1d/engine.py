@@ -474,7 +474,8 @@ class R2P1DEngine:
         # whose consumer is an h3 direct config with BN on load, videos x
         # channels <= this, has its rows computed by that conv from the sums
         # (no finalize dispatch); 0 = off
-        aff_max = int(os.environ.get("RNB_BN_AFF_SUMS_MAX", "2304")) if hip else 0
+        # (<= csrc/conv_h3.hip H3_AFF_SUMS_MAX)
+        aff_max = min(2304, int(os.environ.get("RNB_BN_AFF_SUMS_MAX", "2304"))) if hip else 0
         pending_aff = None           # bn_aff_arm arguments for pending's consumer
         from ...ops.native import kernels as _kn
 
