@@ -327,7 +327,7 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
       const int E = st.aff_nseg * p.Cin_p;
       double a1[KG + KL], a2[KG + KL];
       float gm[KG + KL], bt[KG + KL];
-      int rows[KG + KL], dst[KG + KL];            // dst: < 0 none; global index, or ~LDS index
+      int rows[KG + KL], dst[KG + KL];            // dst: -1 none; global index; -2 - LDS index
 #pragma unroll
       for (int k = 0; k < KG + KL; ++k) {
         int v = -1, c = 0;
@@ -344,7 +344,7 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
           const int ci = j >> 6, sub = (j >> 5) & 1, ch = j & 15;
           const int clip = clip_lo + ci;
           if (j < H3_AFF_CLIPS * 64) {
-            dst[k] = ~j;
+            dst[k] = -2 - j;
             if (clip < p.N && clip * rows_per_clip < p0 + P_TILE) {
               v = st.in_seg[clip];
               c = ((2 * t_begin + sub) * 16) % p.Cin_p + ch;
@@ -377,7 +377,7 @@ void conv_h3_kernel(const ConvF32Params p, const X6DStats st) {
           ssw[(size_t)v * 2 * p.Cin_p + c] = sc;
           ssw[(size_t)v * 2 * p.Cin_p + p.Cin_p + c] = sh;
         } else {
-          const int j = ~dst[k];
+          const int j = -2 - dst[k];
           l0[j] = ((j >> 4) & 1) ? sh : sc;
         }
       }
