@@ -474,8 +474,12 @@ class R2P1DEngine:
         # whose consumer is an h3 direct config with BN on load, videos x
         # channels <= this, has its rows computed by that conv from the sums
         # (no finalize dispatch); 0 = off
-        # (<= csrc/conv_h3.hip H3_AFF_SUMS_MAX)
+        # (<= csrc/conv_h3.hip H3_AFF_SUMS_MAX), for calls of at most
+        # RNB_BN_AFF_SUMS_VIDEOS videos: per graphed forward 2.165 vs 2.185 ms at
+        # one clip / video, 2.99 vs 2.955 at four clips / two videos, equal at 16
+        # (profiles/r6_ab_bn_aff_sums.txt): one-video calls only by default
         aff_max = min(2304, int(os.environ.get("RNB_BN_AFF_SUMS_MAX", "2304"))) if hip else 0
+        aff_videos = int(os.environ.get("RNB_BN_AFF_SUMS_VIDEOS", "1"))
         pending_aff = None           # bn_aff_arm arguments for pending's consumer
         from ...ops.native import kernels as _kn
 
@@ -563,6 +567,7 @@ class R2P1DEngine:
                             bn_mod._RUN_SINK[0].append((op.bn, sums, thw))
                             pending = (tail_ss, clip_seg)
                         elif (sums is not None and aff_max > 0 and bn_mod._RUN_SINK[0] is not None
+                              and coffs.numel() - 1 <= aff_videos
                               and (coffs.numel() - 1) * op.bn.channels_p <= aff_max
                               and self.ops[i + 1].layer.takes_sums_affine(y.shape)):
                             # the consuming h3 direct conv computes the rows

@@ -228,13 +228,15 @@ def test_h3_input_bn_rows_from_sums_match_finalize(cin, cout, k, p, thw):
 @pytest.mark.parametrize("n,offs", [(1, [0, 1]), (2, [0, 1, 2]), (4, [0, 3, 4, 4])])
 def test_engine_input_bn_rows_from_sums(monkeypatch, n, offs):
     """A one- to four-clip R(2+1)D-34 forward whose h3 direct consumers
-    compute their input BN rows from the sums (default) against the finalize
+    compute their input BN rows from the sums (default for one-video calls,
+    here up to four) against the finalize
     dispatches (RNB_BN_AFF_SUMS_MAX=0): logits and running statistics agree."""
     from rnb_amd.models.r2p1d.model import build_network
     from rnb_amd.models.r2p1d.engine import R2P1DEngine
     g = torch.Generator()
     net = build_network(1, 5, depth=34, seed=2)
     outs, runs = [], []
+    monkeypatch.setenv("RNB_BN_AFF_SUMS_VIDEOS", "4")
     for cap in ("0", "2304"):
         monkeypatch.setenv("RNB_BN_AFF_SUMS_MAX", cap)
         eng = R2P1DEngine(net, DEV, backend="hip", bn_mode="batch", dtype=torch.float32)
