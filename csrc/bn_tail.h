@@ -95,7 +95,9 @@ static __device__ __forceinline__ void bn_tail_run(const BnTail& t) {
 // block), drains its stores and then DMAs them as it does a finalize's rows --
 // the finalize dispatch is gone and its latency overlaps the consumer's start.
 // Armed by the host around the consumer's launches (rnb_bn_aff_arm); a launch
-// whose in_ss is the armed `ss` computes them.
+// whose in_ss is the armed `ss` computes them. The armed state (like the BN
+// tail's) is process-global: the host thread that arms it launches the conv
+// (runner lanes launch from the runner's one thread).
 struct BnAffSums {
   const double* sums;        // [nseg][2][sums_c]
   int sums_c, nseg, rpc;
